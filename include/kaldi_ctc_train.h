@@ -1,0 +1,101 @@
+/*
+ * kaldi_ctc_train.h -- C ABI of the native nnet2 CTC trainer (csrc/nnet.cpp).
+ *
+ * The C++ side mirrors the reference's nnet2 classes on device buffers
+ * (kctc::nnet2::{Component, SpliceComponent, CuDNNRecurrentComponent,
+ * ClipGradientComponent, AffineComponent, Nnet, NnetCtcUpdater}); this ABI is
+ * what a ctypes/cgo/JNI host binds.  Each entry names the reference function it
+ * replaces:
+ *   kctc_nnet_create        <- nnet-init / Nnet::Init from component config lines
+ *                              (src/nnet2/nnet-nnet.cc; line format of
+ *                              egs/wsj/s5/steps/ctc/nnet2/components.py:73-102)
+ *   kctc_nnet_train_step    <- DoBackprop(nnet, egs, &formatted, nnet, &acc)
+ *                              == NnetCtcUpdater::ComputeForMinibatch + SGD
+ *                              (src/ctc/ctc-nnet-update.cc:94-128, 447-463)
+ *   kctc_nnet_compute_objf  <- ComputeNnetObjf (no backprop; nnet2-ctc-compute-prob,
+ *                              src/ctc/ctc-nnet-update.cc:426-431)
+ *   kctc_nnet_get/set_params<- UpdatableComponent::Vectorize / UnVectorize
+ *   kctc_nnet_write/read    <- Nnet::Write / Read (text form, component tokens of
+ *                              nnet-cudnn-component.cc:673-837, nnet-component.cc:1228-1262)
+ *   kctc_format_input       <- FormatNnetInput (src/ctc/ctc-nnet-update.cc:351-424)
+ *   kctc_nnet_enable_dp     <- (new) data parallelism: RCCL all-reduce of the
+ *                              weight gradients over xGMI; replaces the recipe's
+ *                              per-iteration model averaging (nnet-am-average)
+ * Features are device pointers in the time-major [T_max*N][dim] layout of
+ * FormatNnetInput; labels/lengths are host arrays.  Return 0 on success,
+ * non-zero on error (kctc_last_error() describes it).
+ */
+#ifndef KALDI_CTC_AMD_KALDI_CTC_TRAIN_H_
+#define KALDI_CTC_AMD_KALDI_CTC_TRAIN_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+struct ihipStream_t;
+typedef struct kctcNnetImpl *kctcNnet_t;
+
+const char *kctc_last_error(void);
+
+/* config: newline-separated component lines ("<Type> key=value ...").
+ * seed: weight-init RNG seed.  device: HIP device ordinal. */
+int kctc_nnet_create(kctcNnet_t *nnet, const char *config, unsigned long long seed, int device);
+int kctc_nnet_destroy(kctcNnet_t nnet);
+int kctc_nnet_num_components(kctcNnet_t nnet);
+/* writes "<Type> dim info" of component c into buf */
+int kctc_nnet_component_info(kctcNnet_t nnet, int c, char *buf, size_t buflen);
+long kctc_nnet_num_params(kctcNnet_t nnet, int c);
+int kctc_nnet_get_params(kctcNnet_t nnet, int c, float *host, long n);
+int kctc_nnet_set_params(kctcNnet_t nnet, int c, const float *host, long n);
+int kctc_nnet_set_learning_rate(kctcNnet_t nnet, float lr);
+/* ClipGradientComponent counters of component c: num_clipped, count */
+int kctc_nnet_clip_stats(kctcNnet_t nnet, int c, double *num_clipped, double *count);
+/* RNG stream for the self-repair draws (glibc rand() in the reference) */
+int kctc_nnet_set_repair_seed(kctcNnet_t nnet, unsigned long long seed);
+
+/* One SGD minibatch.  feats_dev [T_max*N][input_dim] (device, zero padded).
+ * Outputs: sum of CTC costs, accuracy numerator (sum L - edits), weight (sum L). */
+int kctc_nnet_train_step(kctcNnet_t nnet, const float *feats_dev, int T_max, int N,
+                         const int *num_frames, const int *flat_labels, const int *label_lengths,
+                         double *tot_objf, double *tot_accuracy, double *tot_weight);
+int kctc_nnet_compute_objf(kctcNnet_t nnet, const float *feats_dev, int T_max, int N,
+                           const int *num_frames, const int *flat_labels,
+                           const int *label_lengths, double *tot_objf, double *tot_accuracy,
+                           double *tot_weight);
+/* The stream the trainer's kernels run on (for host-side event timing). */
+struct ihipStream_t *kctc_nnet_stream(kctcNnet_t nnet);
+/* Per-launch device time of the last step's kernels, by kernel family (ms):
+ * filled only when profiling is enabled with kctc_nnet_set_profiling(nnet, 1). */
+int kctc_nnet_set_profiling(kctcNnet_t nnet, int on);
+int kctc_nnet_profile(kctcNnet_t nnet, const char *family, double *ms_total, int *launches);
+
+int kctc_nnet_write(kctcNnet_t nnet, const char *path);
+int kctc_nnet_read(kctcNnet_t *nnet, const char *path, int device);
+
+/* Data parallelism over RCCL (one process per GPU).  uid: 128-byte
+ * ncclUniqueId from kctc_dp_unique_id on rank 0, broadcast by the launcher. */
+int kctc_dp_unique_id(void *uid128);
+int kctc_nnet_enable_dp(kctcNnet_t nnet, const void *uid128, int rank, int world_size);
+
+/* FormatNnetInput: pack per-utterance [T_n][dim] host matrices (concatenated
+ * in `feats`, row offsets by num_frames) into [T_max*N][dim], row t*N+n,
+ * zero padded.  out must hold T_max*N*dim floats (host). */
+int kctc_format_input(const float *feats, const int *num_frames, int N, int dim, int T_max,
+                      float *out);
+
+/* Synthetic minibatch of the BASELINE.md §2 generator (splitmix64 + Box-Muller,
+ * seed = 20161015 + 1000*rank + step): features N(0,1) already formatted
+ * [T_max*N][dim] (host), T_n = T_max - floor(u*0.1*T_max) (n=0 gets T_max),
+ * L_n = floor(T_n*label_ratio) clamped to <= 639 and <= (T_n-1)/2, labels
+ * uniform in [1, A-1] without consecutive repeats.  flat_labels capacity
+ * >= N*639.  Returns the total number of labels. */
+long kctc_synth_minibatch(unsigned long long seed, int T_max, int N, int dim, int A,
+                          double label_ratio, float *feats, int *num_frames, int *flat_labels,
+                          int *label_lengths);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KALDI_CTC_AMD_KALDI_CTC_TRAIN_H_ */

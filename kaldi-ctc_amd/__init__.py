@@ -1,0 +1,236 @@
+"""kaldi-ctc_amd -- MI355X-native CTC acoustic-model training path.
+
+Host-side mirror of the reference's interfaces over the C-ABI HIP library
+libkaldictc_amd.so (built from csrc/ by the Makefile next to this file):
+
+  * warp-ctc ABI (include/ctc.h): compute_ctc_loss / get_workspace_size /
+    ctcGetStatusString -- replaces warp-ctc at src/ctc/ctc-nnet-update.cc:211-243.
+  * cuDNN-shaped RNN ABI (include/kaldi_rnn.h) -- replaces the
+    kaldi::cudnn::Recurrent* shim of src/cudamatrix/cudnn-recurrent.h.
+  * nnet2 trainer ABI (include/kaldi_ctc_train.h) -- the NnetCtcUpdater /
+    TrainNnetSimple step (src/ctc/ctc-nnet-update.cc:94-128,
+    src/ctc/ctc-nnet-train.cc:181-284) on device buffers.
+
+torch is used only as plumbing (device memory, streams, torch.distributed
+rendezvous).  Every entry point fails loudly when the HIP library is missing;
+there is no CPU fallback.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libkaldictc_amd.so")
+
+CTC_CPU, CTC_GPU = 0, 1
+CTC_STATUS = {0: "CTC_STATUS_SUCCESS", 1: "CTC_STATUS_MEMOPS_FAILED", 2: "CTC_STATUS_INVALID_VALUE",
+              3: "CTC_STATUS_EXECUTION_FAILED", 4: "CTC_STATUS_UNKNOWN_ERROR"}
+
+_lib = None
+
+
+class CtcOptions(ctypes.Structure):
+    """struct ctcOptions { ctcComputeLocation loc; union { unsigned num_threads;
+    hipStream_t stream; }; int blank_label; }  (include/ctc.h)"""
+    _fields_ = [("loc", ctypes.c_int), ("stream", ctypes.c_void_p), ("blank_label", ctypes.c_int)]
+
+
+class CtcError(RuntimeError):
+    def __init__(self, status, where):
+        msg = lib().ctcGetStatusString(status).decode()
+        super().__init__(f"ctcStatus_t {status} : \"{msg}\" returned from '{where}'")
+        self.status = status
+
+
+class KctcError(RuntimeError):
+    pass
+
+
+def build(verbose=False):
+    import subprocess
+    subprocess.run(["make", "-s" if not verbose else "-j8", "-j8", "-C", HERE], check=True)
+
+
+def lib():
+    """Load libkaldictc_amd.so; raises if it has not been built (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise KctcError(f"{LIB_PATH} is missing: run `make -C {HERE}` (or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, ip, sz = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_size_t
+    L.get_warpctc_version.restype = ctypes.c_int
+    L.ctcGetStatusString.argtypes = [ctypes.c_int]
+    L.ctcGetStatusString.restype = ctypes.c_char_p
+    L.compute_ctc_loss.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, CtcOptions]
+    L.compute_ctc_loss.restype = ctypes.c_int
+    L.get_workspace_size.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, CtcOptions,
+                                     ctypes.POINTER(sz)]
+    L.get_workspace_size.restype = ctypes.c_int
+    L.mictc_compute_ctc_loss_async.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int,
+                                               vp, vp, vp, ctypes.c_int]
+    L.mictc_compute_ctc_loss_async.restype = ctypes.c_int
+    _bind_optional(L)
+    _lib = L
+    return L
+
+
+def _bind_optional(L):
+    """Bindings for the RNN / trainer ABIs (added as those layers land)."""
+    from . import _bindings  # noqa: F401  (relative import when loaded as a package)
+    _bindings.bind(L)
+
+
+def exported_symbols():
+    """Symbols declared by include/*.h (checked by tests/test_abi.py)."""
+    import re
+    inc = os.path.join(os.path.dirname(HERE), "include")
+    names = []
+    for fn in sorted(os.listdir(inc)):
+        if fn.endswith(".h"):
+            txt = open(os.path.join(inc, fn)).read()
+            txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+            names += re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b([a-zA-Z_]\w*)\s*\([^;{]*\)\s*;",
+                                txt, flags=re.M)
+    return sorted(set(n for n in names if n not in ("if", "while", "for", "return")))
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    raise TypeError(type(x))
+
+
+def _stream_handle(stream):
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+
+def ctc_workspace_size(label_lengths, input_lengths, alphabet_size):
+    ll = np.ascontiguousarray(label_lengths, dtype=np.int32)
+    il = np.ascontiguousarray(input_lengths, dtype=np.int32)
+    opts = CtcOptions(CTC_GPU, None, 0)
+    out = ctypes.c_size_t()
+    st = lib().get_workspace_size(ll.ctypes.data, il.ctypes.data, int(alphabet_size), len(ll),
+                                  opts, ctypes.byref(out))
+    if st != 0:
+        raise CtcError(st, "get_workspace_size")
+    return out.value
+
+
+def compute_ctc_loss(acts, flat_labels, label_lengths, input_lengths, want_grad=True, blank=0,
+                     stream=None, workspace=None):
+    """warp-ctc compute_ctc_loss on a torch CUDA tensor acts [T, N, A] (float32).
+    Returns (costs np.float32 [N], grads tensor or None)."""
+    import torch
+    assert acts.is_cuda and acts.dtype == torch.float32 and acts.is_contiguous()
+    T, N, A = acts.shape
+    fl = np.ascontiguousarray(flat_labels, dtype=np.int32)
+    if fl.size == 0:
+        fl = np.zeros(1, np.int32)
+    ll = np.ascontiguousarray(label_lengths, dtype=np.int32)
+    il = np.ascontiguousarray(input_lengths, dtype=np.int32)
+    if workspace is None:
+        workspace = torch.empty(ctc_workspace_size(ll, il, A), dtype=torch.uint8, device=acts.device)
+    grads = torch.empty_like(acts) if want_grad else None
+    costs = np.zeros(N, np.float32)
+    opts = CtcOptions(CTC_GPU, _stream_handle(stream), blank)
+    st = lib().compute_ctc_loss(acts.data_ptr(), _ptr(grads), fl.ctypes.data, ll.ctypes.data,
+                                il.ctypes.data, A, N, costs.ctypes.data, workspace.data_ptr(), opts)
+    if st != 0:
+        raise CtcError(st, "compute_ctc_loss")
+    return costs, grads
+
+
+class RnnError(RuntimeError):
+    pass
+
+
+def _krnn_check(st, where):
+    if st != 0:
+        raise RnnError(f"{where}: {lib().krnnGetStatusString(st).decode()} ({st})")
+
+
+class Rnn:
+    """Thin Python view of the cuDNN-shaped RNN ABI (include/kaldi_rnn.h).
+
+    Mirrors how CuDNNRecurrentComponent drives cudnn-recurrent.h: buffers are
+    owned by the caller (torch CUDA tensors here), every call is stream-ordered.
+    """
+    RELU, TANH, LSTM, GRU = 0, 1, 2, 3
+
+    def __init__(self, mode, input_dim, hidden_dim, num_layers=1, bidirectional=True):
+        self.mode, self.D, self.H, self.L = mode, input_dim, hidden_dim, num_layers
+        self.dirs = 2 if bidirectional else 1
+        h = ctypes.c_void_p()
+        _krnn_check(lib().krnnCreate(ctypes.byref(h), mode, input_dim, hidden_dim, num_layers,
+                                     1 if bidirectional else 0), "krnnCreate")
+        self.h = h
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().krnnDestroy(self.h)
+        except Exception:
+            pass
+
+    @property
+    def num_params(self):
+        return lib().krnnGetParamsSize(self.h) // 4
+
+    def lin_offset(self, pseudo_layer, lin_id, is_bias):
+        dims = (ctypes.c_int * 2)()
+        off = lib().krnnGetLinLayerOffset(self.h, pseudo_layer, lin_id, is_bias, dims)
+        if off < 0:
+            raise RnnError("bad lin layer")
+        return off, (dims[0], dims[1])
+
+    def sizes(self, T, N):
+        return (lib().krnnGetWorkspaceSize(self.h, T, N), lib().krnnGetTrainingReserveSize(self.h, T, N))
+
+    def forward_training(self, x, w, y, workspace, reserve, stream=None):
+        T, N = x.shape[0], x.shape[1]
+        _krnn_check(lib().krnnForwardTraining(self.h, _stream_handle(stream), T, N, _ptr(x), _ptr(w),
+                                              _ptr(y), _ptr(workspace), workspace.numel(),
+                                              _ptr(reserve), reserve.numel()), "krnnForwardTraining")
+
+    def forward_inference(self, x, w, y, workspace, stream=None):
+        T, N = x.shape[0], x.shape[1]
+        _krnn_check(lib().krnnForwardInference(self.h, _stream_handle(stream), T, N, _ptr(x), _ptr(w),
+                                               _ptr(y), _ptr(workspace), workspace.numel()),
+                    "krnnForwardInference")
+
+    def backward_data(self, y, dy, w, dx, workspace, reserve, stream=None):
+        T, N = y.shape[0], y.shape[1]
+        _krnn_check(lib().krnnBackwardData(self.h, _stream_handle(stream), T, N, _ptr(y), _ptr(dy),
+                                           _ptr(w), _ptr(dx), _ptr(workspace), workspace.numel(),
+                                           _ptr(reserve), reserve.numel()), "krnnBackwardData")
+
+    def backward_weights(self, x, y, dw, workspace, reserve, stream=None):
+        T, N = x.shape[0], x.shape[1]
+        _krnn_check(lib().krnnBackwardWeights(self.h, _stream_handle(stream), T, N, _ptr(x), _ptr(y),
+                                              _ptr(workspace), workspace.numel(), _ptr(dw),
+                                              _ptr(reserve), reserve.numel()), "krnnBackwardWeights")
+
+    def device_status(self, stream=None):
+        return lib().krnnGetDeviceStatus(self.h, _stream_handle(stream))
+
+
+def add_mat_mat(C, A, B, transA=False, transB=False, alpha=1.0, beta=0.0, stream=None):
+    """C = alpha op(A) op(B) + beta C on 2-D row-major torch CUDA tensors."""
+    M, N = C.shape
+    K = A.shape[0] if transA else A.shape[1]
+    st = lib().kcm_add_mat_mat(_stream_handle(stream), int(transA), int(transB), M, N, K, alpha,
+                               _ptr(A), A.stride(0), _ptr(B), B.stride(0), beta, _ptr(C), C.stride(0))
+    if st != 0:
+        raise KctcError(f"kcm_add_mat_mat failed ({st})")

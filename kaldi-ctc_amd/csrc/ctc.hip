@@ -1,0 +1,515 @@
+// ctc.hip -- CTC loss and gradient for MI355X (gfx950), behind the warp-ctc C ABI
+// (include/ctc.h).  Replaces warp-ctc's compute_ctc_loss as called from
+// src/ctc/ctc-nnet-update.cc:211-243 of the reference.
+//
+// Three launches per call, all stream-ordered:
+//   K1 ctc_logz        one wave per frame row: logZ[t,n] = logsumexp_a act[t,n,a]
+//                      (fully parallel, HBM-bound: 4*A B read per row).
+//   K2 ctc_alpha_beta  one 256-thread workgroup per (utterance, direction):
+//                      log-space alpha (forward) or beta (backward) recursion,
+//                      serial over T with ONE workgroup barrier per frame.  The
+//                      extended (blank-interleaved) label sequence lives in
+//                      registers, the previous frame's column in double-buffered
+//                      LDS, the emission log-probs are prefetched PD frames ahead
+//                      into registers.  Each frame is renormalised by the max of
+//                      the previous column (wave max via DPP/shfl, then LDS) and
+//                      the running offset is kept in fp64, so exp(alpha+beta-logp)
+//                      keeps ~1e-7 relative accuracy at T=2000 (plain fp32 log
+//                      space -- warp-ctc's own arithmetic -- loses ~1e-3).  The
+//                      normalised columns are spilled to HBM (4*T*S B each).
+//   K3 ctc_grad        (utterance, 8-frame chunk) per workgroup, fully parallel:
+//                      gamma_t(k) = sum_{s: l'_s = k} exp(a~+b~+off), then
+//                      grad = softmax - gamma; padding / infeasible rows get 0.
+//                      Deterministic (fixed summation order, no atomics).
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+#include "ctc.h"
+
+namespace kctc {
+namespace ctcimpl {
+
+constexpr int kMaxLabel = 639;  // MAX_WARPCTC_LABEL_LENGTH, src/ctc/ctc-nnet-train.cc:25-26
+constexpr int kThreads = 256;
+constexpr int kSPT = (2 * kMaxLabel + 1 + kThreads - 1) / kThreads;  // states per thread (5)
+constexpr int kPD = 8;   // emission prefetch depth (frames)
+constexpr int kFR = 8;   // frames per K3 workgroup
+
+struct UttDesc {
+  int T, L, S, feasible, lab_off, pad;
+  long long ab_off;   // float offset of this utterance's alpha spill; beta follows at +T*S
+  long long off_off;  // double offset of offA[T]; offB follows at +T
+};
+
+struct Layout {
+  size_t desc, labels, costs, logz, spill, offs, total;
+  int T_max;
+  long long spill_floats, off_doubles;
+};
+
+static bool make_layout(const int *label_lengths, const int *input_lengths, int A, int N,
+                        Layout *lay, std::vector<UttDesc> *descs, bool *bad) {
+  *bad = false;
+  if (A <= 0 || N <= 0 || !label_lengths || !input_lengths) { *bad = true; return false; }
+  int T_max = 0;
+  long long nlab = 0, spill = 0, offs = 0;
+  if (descs) descs->resize(N);
+  for (int n = 0; n < N; n++) {
+    int T = input_lengths[n], L = label_lengths[n];
+    if (T < 0 || L < 0 || L > kMaxLabel) { *bad = true; return false; }
+    T_max = T > T_max ? T : T_max;
+    int S = 2 * L + 1;
+    if (descs) {
+      UttDesc &d = (*descs)[n];
+      d.T = T; d.L = L; d.S = S; d.feasible = 0; d.lab_off = (int)nlab; d.pad = 0;
+      d.ab_off = spill; d.off_off = offs;
+    }
+    nlab += L;
+    spill += 2LL * T * S;
+    offs += 2LL * T;
+  }
+  Layout &l = *lay;
+  size_t p = 0;
+  l.desc = p;   p = align_up(p + sizeof(UttDesc) * N, 256);
+  l.labels = p; p = align_up(p + sizeof(int) * (nlab > 0 ? nlab : 1), 256);
+  l.costs = p;  p = align_up(p + sizeof(double) * N, 256);
+  l.logz = p;   p = align_up(p + sizeof(float) * (size_t)T_max * N + 4, 256);
+  l.spill = p;  p = align_up(p + sizeof(float) * (size_t)spill, 256);
+  l.offs = p;   p = align_up(p + sizeof(double) * (size_t)offs, 256);
+  l.total = p;
+  l.T_max = T_max;
+  l.spill_floats = spill;
+  l.off_doubles = offs;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// K1: per-frame log normaliser.  One wave per row, 4 rows per workgroup.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void ctc_logz(const float *__restrict__ acts, int A, long rows,
+                                                float *__restrict__ logz) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float *r = acts + row * A;
+  float m = -INFINITY;
+  for (int a = lane; a < A; a += kWave) m = fmaxf(m, r[a]);
+  m = wave_max(m);
+  float s = 0.f;
+  for (int a = lane; a < A; a += kWave) s += expf(r[a] - m);
+  s = wave_sum(s);
+  if (lane == 0) logz[row] = m + logf(s);
+}
+
+// log(e^a + e^b + e^c) as max + log1p(sum of the two smaller terms): the
+// dominant term contributes exactly 1, so log1p keeps full relative precision
+// of the small ones (logf(1 + x) would round x to the ulp of 1).
+__device__ __forceinline__ float lse3(float a, float b, float c) {
+  const float m = fmaxf(a, fmaxf(b, c));
+  if (m == -INFINITY) return -INFINITY;
+  const float lo = fminf(a, fminf(b, c));
+  const float md = fmaxf(fminf(a, b), fminf(fmaxf(a, b), c));  // median, exact
+  return m + log1pf(expf(md - m) + expf(lo - m));
+}
+
+// ---------------------------------------------------------------------------
+// K2: alpha (blockIdx.x < N) and beta (blockIdx.x >= N) recursions.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void ctc_alpha_beta(
+    const float *__restrict__ acts, const float *__restrict__ logz, int N, int A, int blank,
+    UttDesc *__restrict__ descs, const int *__restrict__ labels, float *__restrict__ spill,
+    double *__restrict__ offs, double *__restrict__ costs, int write_spill) {
+  const bool is_beta = blockIdx.x >= (unsigned)N;
+  const int n = is_beta ? blockIdx.x - N : blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ float col[2][2 * kMaxLabel + 4];
+  __shared__ float wmax[2][kThreads / kWave];
+  __shared__ int sh_feasible;
+
+  UttDesc d = descs[n];
+  const int T = d.T, L = d.L, S = d.S;
+  const int *lab = labels + d.lab_off;
+  if (tid == 0) {
+    int rep = 0;
+    for (int i = 1; i < L; i++) rep += (lab[i] == lab[i - 1]);
+    sh_feasible = (T > 0 && L + rep <= T);
+  }
+  __syncthreads();
+  const int feasible = sh_feasible;
+  if (!is_beta && tid == 0) {
+    descs[n].feasible = feasible;
+    if (!feasible) costs[n] = 0.0;
+  }
+  if (!feasible) return;
+
+  // extended label of each owned state, and its skip permission
+  int ext[kSPT];
+  bool skip[kSPT];
+#pragma unroll
+  for (int i = 0; i < kSPT; i++) {
+    int s = tid + i * kThreads;
+    ext[i] = (s < S) ? ((s & 1) ? lab[(s - 1) >> 1] : blank) : blank;
+    skip[i] = false;
+    if (s < S && (s & 1)) {
+      if (!is_beta) skip[i] = (s >= 2) && (lab[(s - 1) >> 1] != lab[(s - 3) >> 1]);
+      else skip[i] = (s + 2 < S) && (lab[(s + 1) >> 1] != lab[(s - 1) >> 1]);
+    } else if (s < S && is_beta) {
+      skip[i] = false;  // blank -> blank+2 is never a skip target (l'_{s+2} is blank)
+    }
+  }
+  // beta: transition s -> s+2 allowed iff l'_{s+2} != blank and != l'_s; for
+  // odd s that is lab[(s+1)/2] != lab[(s-1)/2]; for even s, l'_{s+2} is blank.
+
+  const float *arow = acts + (long)n * A;        // + t*N*A
+  const float *zrow = logz + n;                  // + t*N
+  const long tstride = (long)N * A;
+  float *sp = spill + d.ab_off + (is_beta ? (long long)T * S : 0);
+  double *op = offs + d.off_off + (is_beta ? T : 0);
+
+  // emission prefetch ring: pf[k][i] = act[t_k, n, ext_i], pz[k] = logZ[t_k, n]
+  float pf[kPD][kSPT];
+  float pz[kPD];
+  auto tframe = [&](int k) { return is_beta ? T - 1 - k : k; };  // k-th processed frame
+#pragma unroll
+  for (int k = 0; k < kPD; k++) {
+    if (k < T) {
+      int t = tframe(k);
+#pragma unroll
+      for (int i = 0; i < kSPT; i++) pf[k][i] = arow[t * tstride + ext[i]];
+      pz[k] = zrow[(long)t * N];
+    }
+  }
+
+  double off = 0.0;
+  int cur = 0;
+  for (int k0 = 0; k0 < T; k0 += kPD) {
+#pragma unroll
+    for (int kk = 0; kk < kPD; kk++) {
+      const int k = k0 + kk;
+      if (k < T) {
+        const int t = tframe(k);
+        float ly[kSPT];
+#pragma unroll
+        for (int i = 0; i < kSPT; i++) ly[i] = pf[kk][i] - pz[kk];
+        // issue the prefetch for frame k + PD into the slot just consumed
+        if (k + kPD < T) {
+          int tn = tframe(k + kPD);
+#pragma unroll
+          for (int i = 0; i < kSPT; i++) pf[kk][i] = arow[tn * tstride + ext[i]];
+          pz[kk] = zrow[(long)tn * N];
+        }
+        float lmax = -INFINITY;
+        if (k == 0) {
+          // init: alpha_0(0)=ly(blank), alpha_0(1)=ly(l1); beta_{T-1}(S-1)=beta(S-2)=0,
+          // stored as q = beta + ly (the next step's input)
+#pragma unroll
+          for (int i = 0; i < kSPT; i++) {
+            int s = tid + i * kThreads;
+            if (s < S) {
+              float v;
+              if (!is_beta) v = (s <= 1) ? ly[i] : -INFINITY;
+              else v = (s >= S - 2) ? 0.f : -INFINITY;
+              if (write_spill) sp[(long)t * S + s] = v;
+              float q = is_beta ? v + ly[i] : v;
+              col[cur][s] = q;
+              lmax = fmaxf(lmax, q);
+            }
+          }
+        } else {
+          float mu = wmax[cur ^ 1][0];
+#pragma unroll
+          for (int w = 1; w < kThreads / kWave; w++) mu = fmaxf(mu, wmax[cur ^ 1][w]);
+          const float *pv = col[cur ^ 1];
+#pragma unroll
+          for (int i = 0; i < kSPT; i++) {
+            int s = tid + i * kThreads;
+            if (s < S) {
+              float v;
+              if (!is_beta) {
+                float a = pv[s];
+                float b = s >= 1 ? pv[s - 1] : -INFINITY;
+                float c = skip[i] ? pv[s - 2] : -INFINITY;
+                v = lse3(a - mu, b - mu, c - mu);
+                v = (v == -INFINITY) ? v : v + ly[i];
+                if (write_spill) sp[(long)t * S + s] = v;
+                col[cur][s] = v;
+                lmax = fmaxf(lmax, v);
+              } else {
+                float a = pv[s];
+                float b = s + 1 < S ? pv[s + 1] : -INFINITY;
+                float c = skip[i] ? pv[s + 2] : -INFINITY;
+                v = lse3(a - mu, b - mu, c - mu);
+                if (write_spill) sp[(long)t * S + s] = v;
+                float q = (v == -INFINITY) ? v : v + ly[i];
+                col[cur][s] = q;
+                lmax = fmaxf(lmax, q);
+              }
+            }
+          }
+          off += (double)mu;
+        }
+        lmax = wave_max(lmax);
+        if (lane == 0) wmax[cur][wid] = lmax;
+        if (tid == 0 && write_spill) op[t] = off;
+        __syncthreads();
+        cur ^= 1;
+      }
+    }
+  }
+  if (!is_beta && tid == 0) {
+    // log p = O_{T-1} + lse(alpha~_{T-1}(S-1), alpha~_{T-1}(S-2))
+    const float *pv = col[cur ^ 1];
+    float a = pv[S - 1], b = S > 1 ? pv[S - 2] : -INFINITY;
+    float m = fmaxf(a, b);
+    double lp = off + (double)m + log((double)expf(a - m) + (double)expf(b - m));
+    costs[n] = -lp;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K3: gradient.  grid (ceil(T_max/FR), N), 256 threads.
+// dynamic LDS: occ[FR][S] | next[L] | owner[A] | gblank[FR] | gtot[FR]
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void ctc_grad(
+    const float *__restrict__ acts, const float *__restrict__ logz, float *__restrict__ grads,
+    int N, int A, int T_max, int blank, const UttDesc *__restrict__ descs,
+    const int *__restrict__ labels, const float *__restrict__ spill,
+    const double *__restrict__ offs, const double *__restrict__ costs) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int n = blockIdx.y, t0 = blockIdx.x * kFR, tid = threadIdx.x;
+  const UttDesc d = descs[n];
+  const int T = d.feasible ? d.T : 0, L = d.L, S = d.S;
+  const int nf = min(kFR, T_max - t0);
+  if (t0 >= T) {  // padding or infeasible: zero rows
+    for (int it = tid; it < nf * A; it += kThreads) {
+      int f = it / A, a = it - f * A;
+      grads[((long)(t0 + f) * N + n) * A + a] = 0.f;
+    }
+    return;
+  }
+  float *occ = reinterpret_cast<float *>(smem);
+  int *nxt = reinterpret_cast<int *>(occ + kFR * S);
+  int *owner = nxt + (L > 0 ? L : 1);
+  float *gblank = reinterpret_cast<float *>(owner + A);
+  float *gtot = gblank + kFR;
+  const int *lab = labels + d.lab_off;
+  for (int a = tid; a < A; a += kThreads) owner[a] = -1;
+  __syncthreads();
+  for (int j = tid; j < L; j += kThreads) {
+    int k = lab[j], nx = -1;
+    for (int i = j + 1; i < L; i++)
+      if (lab[i] == k) { nx = i; break; }
+    nxt[j] = nx;
+    bool first = true;
+    for (int i = 0; i < j; i++)
+      if (lab[i] == k) { first = false; break; }
+    if (first) owner[k] = j;
+  }
+  const double logp = -costs[n];
+  const float *al = spill + d.ab_off;
+  const float *be = al + (long long)T * S;
+  const double *oa = offs + d.off_off, *ob = oa + T;
+  const int nreal = min(nf, T - t0);
+  for (int f = 0; f < nreal; f++) {
+    const int t = t0 + f;
+    const float Kt = (float)(oa[t] + ob[t] - logp);
+    for (int s = tid; s < S; s += kThreads) {
+      float v = al[(long)t * S + s] + be[(long)t * S + s];
+      occ[f * S + s] = (v == -INFINITY) ? 0.f : expf(v + Kt);
+    }
+  }
+  __syncthreads();
+  // blank occupancy and total occupancy: wave w sums frames w, w+4.  gamma is
+  // normalised by the frame's own total sum_s alpha_t(s) beta_t(s) (= p for
+  // every t): the alpha and beta rounding accumulated over T steps is common
+  // to every state of a frame and cancels, instead of surviving against logp.
+  {
+    const int lane = tid & 63, wid = tid >> 6;
+    for (int f = wid; f < nreal; f += kThreads / kWave) {
+      float acc = 0.f, tot = 0.f;
+      for (int s = 2 * lane; s < S; s += 2 * kWave) {
+        acc += occ[f * S + s];
+        tot += occ[f * S + s] + (s + 1 < S ? occ[f * S + s + 1] : 0.f);
+      }
+      acc = wave_sum(acc);
+      tot = wave_sum(tot);
+      if (lane == 0) { gblank[f] = acc / tot; gtot[f] = 1.f / tot; }
+    }
+  }
+  __syncthreads();
+  for (int it = tid; it < nf * A; it += kThreads) {
+    const int f = it / A, a = it - f * A, t = t0 + f;
+    const long idx = ((long)t * N + n) * A + a;
+    float g = 0.f;
+    if (t < T) {
+      float gam = 0.f;
+      if (a == blank) {
+        gam = gblank[f];
+      } else {
+        for (int j = owner[a]; j >= 0; j = nxt[j]) gam += occ[f * S + 2 * j + 1];
+        gam *= gtot[f];
+      }
+      g = expf(acts[idx] - logz[(long)t * N + n]) - gam;
+    }
+    grads[idx] = g;
+  }
+}
+
+struct Staging {
+  char *buf = nullptr;
+  size_t cap = 0;
+  hipEvent_t ev = nullptr;
+  bool pending = false;
+};
+static thread_local Staging g_stage;
+
+static char *staging_acquire(size_t bytes) {
+  Staging &s = g_stage;
+  if (s.pending) {
+    if (hipEventSynchronize(s.ev) != hipSuccess) return nullptr;
+    s.pending = false;
+  }
+  if (!s.ev && hipEventCreateWithFlags(&s.ev, hipEventDisableTiming) != hipSuccess) return nullptr;
+  if (bytes > s.cap) {
+    if (s.buf) (void)hipHostFree(s.buf);
+    size_t cap = align_up(bytes * 2, 4096);
+    if (hipHostMalloc((void **)&s.buf, cap, hipHostMallocDefault) != hipSuccess) {
+      s.buf = nullptr; s.cap = 0;
+      return nullptr;
+    }
+    s.cap = cap;
+  }
+  return s.buf;
+}
+static void staging_release(hipStream_t stream) {
+  if (hipEventRecord(g_stage.ev, stream) == hipSuccess) g_stage.pending = true;
+}
+
+static ctcStatus_t launch(const float *acts, float *grads, const int *flat_labels,
+                          const int *label_lengths, const int *input_lengths, int A, int N,
+                          double *costs_dev, void *workspace, hipStream_t stream, int blank) {
+  Layout lay;
+  std::vector<UttDesc> descs;
+  bool bad = false;
+  if (!make_layout(label_lengths, input_lengths, A, N, &lay, &descs, &bad) || bad)
+    return CTC_STATUS_INVALID_VALUE;
+  if (blank < 0 || blank >= A || !acts || !workspace) return CTC_STATUS_INVALID_VALUE;
+  long long nlab = 0;
+  for (int n = 0; n < N; n++) nlab += label_lengths[n];
+  for (long long i = 0; i < nlab; i++)
+    if (flat_labels[i] < 0 || flat_labels[i] >= A || flat_labels[i] == blank)
+      return CTC_STATUS_INVALID_VALUE;
+  char *ws = static_cast<char *>(workspace);
+  // host staging (pinned, reused once the previous call's copy has landed):
+  // descriptors then labels, one H2D copy
+  char *stage = staging_acquire(lay.costs);
+  if (!stage) return CTC_STATUS_MEMOPS_FAILED;
+  memcpy(stage + lay.desc, descs.data(), sizeof(UttDesc) * N);
+  if (nlab) memcpy(stage + lay.labels, flat_labels, sizeof(int) * nlab);
+  if (hipMemcpyAsync(ws, stage, lay.costs, hipMemcpyHostToDevice, stream) != hipSuccess)
+    return CTC_STATUS_MEMOPS_FAILED;
+  staging_release(stream);
+  UttDesc *d_desc = reinterpret_cast<UttDesc *>(ws + lay.desc);
+  const int *d_lab = reinterpret_cast<const int *>(ws + lay.labels);
+  float *d_logz = reinterpret_cast<float *>(ws + lay.logz);
+  float *d_spill = reinterpret_cast<float *>(ws + lay.spill);
+  double *d_offs = reinterpret_cast<double *>(ws + lay.offs);
+  const long rows = (long)lay.T_max * N;
+  if (rows > 0) {
+    hipLaunchKernelGGL(ctc_logz, dim3(ceil_div(rows, 4)), dim3(256), 0, stream, acts, A, rows,
+                       d_logz);
+  }
+  const int want = grads != nullptr;
+  hipLaunchKernelGGL(ctc_alpha_beta, dim3(want ? 2 * N : N), dim3(kThreads), 0, stream, acts,
+                     d_logz, N, A, blank, d_desc, d_lab, d_spill, d_offs, costs_dev, want);
+  if (want && lay.T_max > 0) {
+    int Lmax = 0;
+    for (int n = 0; n < N; n++) Lmax = label_lengths[n] > Lmax ? label_lengths[n] : Lmax;
+    const int Smax = 2 * Lmax + 1;
+    size_t shm = sizeof(float) * kFR * Smax + sizeof(int) * (Lmax > 0 ? Lmax : 1) +
+                 sizeof(int) * A + 2 * sizeof(float) * kFR;
+    if (shm > 160 * 1024) return CTC_STATUS_INVALID_VALUE;
+    hipLaunchKernelGGL(ctc_grad, dim3(ceil_div(lay.T_max, kFR), N), dim3(kThreads), shm, stream,
+                       acts, d_logz, grads, N, A, lay.T_max, blank, d_desc, d_lab, d_spill,
+                       d_offs, costs_dev);
+  }
+  if (hipGetLastError() != hipSuccess) return CTC_STATUS_EXECUTION_FAILED;
+  return CTC_STATUS_SUCCESS;
+}
+
+}  // namespace ctcimpl
+}  // namespace kctc
+
+using namespace kctc::ctcimpl;
+
+extern "C" {
+
+int get_warpctc_version(void) { return 2; }
+
+const char *ctcGetStatusString(ctcStatus_t status) {
+  switch (status) {
+    case CTC_STATUS_SUCCESS: return "no error";
+    case CTC_STATUS_MEMOPS_FAILED: return "cuda memcpy or memset failed";
+    case CTC_STATUS_INVALID_VALUE: return "invalid value";
+    case CTC_STATUS_EXECUTION_FAILED: return "execution failed";
+    case CTC_STATUS_UNKNOWN_ERROR:
+    default: return "unknown error";
+  }
+}
+
+ctcStatus_t get_workspace_size(const int *const label_lengths, const int *const input_lengths,
+                               int alphabet_size, int minibatch, struct ctcOptions info,
+                               size_t *size_bytes) {
+  if (!size_bytes || info.loc != CTC_GPU) return CTC_STATUS_INVALID_VALUE;
+  Layout lay;
+  bool bad = false;
+  if (!make_layout(label_lengths, input_lengths, alphabet_size, minibatch, &lay, nullptr, &bad) ||
+      bad)
+    return CTC_STATUS_INVALID_VALUE;
+  *size_bytes = lay.total;
+  return CTC_STATUS_SUCCESS;
+}
+
+ctcStatus_t mictc_compute_ctc_loss_async(const float *activations, float *gradients,
+                                         const int *flat_labels, const int *label_lengths,
+                                         const int *input_lengths, int alphabet_size,
+                                         int minibatch, double *costs_dev, void *workspace,
+                                         ctcStream_t stream, int blank_label) {
+  if (!costs_dev) return CTC_STATUS_INVALID_VALUE;
+  try {
+    return launch(activations, gradients, flat_labels, label_lengths, input_lengths,
+                  alphabet_size, minibatch, costs_dev, workspace,
+                  reinterpret_cast<hipStream_t>(stream), blank_label);
+  } catch (...) {
+    return CTC_STATUS_UNKNOWN_ERROR;
+  }
+}
+
+ctcStatus_t compute_ctc_loss(const float *const activations, float *gradients,
+                             const int *const flat_labels, const int *const label_lengths,
+                             const int *const input_lengths, int alphabet_size, int minibatch,
+                             float *costs, void *workspace, struct ctcOptions options) {
+  if (options.loc != CTC_GPU || !costs) return CTC_STATUS_INVALID_VALUE;
+  Layout lay;
+  bool bad = false;
+  if (!make_layout(label_lengths, input_lengths, alphabet_size, minibatch, &lay, nullptr, &bad) ||
+      bad)
+    return CTC_STATUS_INVALID_VALUE;
+  hipStream_t stream = reinterpret_cast<hipStream_t>(options.stream);
+  double *d_costs = reinterpret_cast<double *>(static_cast<char *>(workspace) + lay.costs);
+  ctcStatus_t st = mictc_compute_ctc_loss_async(activations, gradients, flat_labels,
+                                                label_lengths, input_lengths, alphabet_size,
+                                                minibatch, d_costs, workspace, options.stream,
+                                                options.blank_label);
+  if (st != CTC_STATUS_SUCCESS) return st;
+  std::vector<double> hc(minibatch);
+  if (hipMemcpyAsync(hc.data(), d_costs, sizeof(double) * minibatch, hipMemcpyDeviceToHost,
+                     stream) != hipSuccess)
+    return CTC_STATUS_MEMOPS_FAILED;
+  if (hipStreamSynchronize(stream) != hipSuccess) return CTC_STATUS_EXECUTION_FAILED;
+  for (int n = 0; n < minibatch; n++) costs[n] = (float)hc[n];
+  return CTC_STATUS_SUCCESS;
+}
+
+}  // extern "C"

@@ -1,0 +1,22 @@
+// elementwise.h -- small bandwidth-bound kernels of the train step.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+namespace kctc {
+
+// w += lr * clamp(dw, -clip, clip)   (clip <= 0: no clamp)
+void clip_sgd_update(hipStream_t s, float *w, const float *dw, long n, float lr, float clip);
+// ClipGradientComponent norm-based backprop: rows with |row| >= thr scaled to
+// norm thr; *nclipped (device int) += number of such rows.
+void rownorm_clip(hipStream_t s, float *d, long rows, int dim, float thr, int *nclipped);
+// best-path ids: first maximum per row
+void row_argmax(hipStream_t s, const float *m, long rows, int cols, int *ids);
+// out[j] = alpha * sum_rows X[:, j] + beta * out[j]; ws >= sum_rows_ws_floats
+size_t sum_rows_ws_floats(long rows, int cols);
+void sum_rows(hipStream_t s, const float *X, long rows, int cols, float alpha, float beta,
+              float *out, float *ws);
+void fill(hipStream_t s, float *p, long n, float v);
+
+}  // namespace kctc

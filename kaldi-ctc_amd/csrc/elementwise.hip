@@ -1,0 +1,179 @@
+// elementwise.hip -- the small bandwidth-bound kernels of the train step.
+// They replace the CuVector/CuMatrix ops the reference touches on this path
+// (SURVEY.md §2.2): _vec_apply_floor/_ceiling + cublas axpy (dW clip and SGD,
+// nnet-cudnn-component.cc:602-614), the ClipGradientComponent row-norm clip
+// (AddDiagMat2 / ApplyFloor / ApplyPow / MulRowsVec, :921-970) and
+// _find_row_max_id (cu-kernels.cu:2454-2500).  All loads/stores are 16-B
+// vectorised where the row layout allows; no host synchronisation.
+#include "common.h"
+#include "elementwise.h"
+
+namespace kctc {
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void k_clip_sgd(float *__restrict__ w, const float *__restrict__ dw,
+                                                  long n, float lr, float clip) {
+  const long n4 = n / 4;
+  const long stride = (long)gridDim.x * 256;
+  const bool vec = ((uintptr_t)w % 16 == 0) && ((uintptr_t)dw % 16 == 0);
+  long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (vec) {
+    for (; i < n4; i += stride) {
+      floatx4 g = reinterpret_cast<const floatx4 *>(dw)[i];
+      floatx4 v = reinterpret_cast<floatx4 *>(w)[i];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        float x = g[j];
+        if (clip > 0.f) x = fminf(fmaxf(x, -clip), clip);
+        v[j] += lr * x;
+      }
+      reinterpret_cast<floatx4 *>(w)[i] = v;
+    }
+    i = n4 * 4 + (long)blockIdx.x * 256 + threadIdx.x;
+  }
+  for (; i < n; i += stride) {
+    float x = dw[i];
+    if (clip > 0.f) x = fminf(fmaxf(x, -clip), clip);
+    w[i] += lr * x;
+  }
+}
+
+// One wave per row: scale = (|row|^2/thr^2 < 1) ? 1 : rsqrt(|row|^2/thr^2)
+__global__ __launch_bounds__(256) void k_rownorm_clip(float *__restrict__ d, long rows, int dim,
+                                                      float inv_thr2, int *__restrict__ nclipped) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  __shared__ int cnt[4];
+  int clipped = 0;
+  if (row < rows) {
+    float *r = d + row * dim;
+    float ss = 0.f;
+    const bool vec = (dim % 4 == 0) && ((uintptr_t)r % 16 == 0);
+    if (vec) {
+      for (int j = lane; j < dim / 4; j += 64) {
+        floatx4 v = reinterpret_cast<const floatx4 *>(r)[j];
+        ss += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+      }
+    } else {
+      for (int j = lane; j < dim; j += 64) ss += r[j] * r[j];
+    }
+    ss = wave_sum(ss);
+    const float sc = ss * inv_thr2;
+    if (!(sc < 1.f)) {
+      clipped = 1;
+      const float f = rsqrtf(sc);
+      if (vec) {
+        for (int j = lane; j < dim / 4; j += 64) {
+          floatx4 v = reinterpret_cast<const floatx4 *>(r)[j];
+          reinterpret_cast<floatx4 *>(r)[j] = v * f;
+        }
+      } else {
+        for (int j = lane; j < dim; j += 64) r[j] *= f;
+      }
+    }
+  }
+  if (lane == 0) cnt[threadIdx.x >> 6] = clipped;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int c = cnt[0] + cnt[1] + cnt[2] + cnt[3];
+    if (c) atomicAdd(nclipped, c);
+  }
+}
+
+// One wave per row, first maximum wins (CPU FindRowMaxId tie order,
+// cu-matrix.cc:1635-1644).
+__global__ __launch_bounds__(256) void k_row_argmax(const float *__restrict__ m, long rows, int cols,
+                                                    int *__restrict__ ids) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float *r = m + row * cols;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int j = lane; j < cols; j += 64) {
+    float v = r[j];
+    if (v > best || (v == best && j < bi)) { best = v; bi = j; }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    float ob = __shfl_xor(best, o, 64);
+    int oi = __shfl_xor(bi, o, 64);
+    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  }
+  if (lane == 0) ids[row] = bi == 0x7fffffff ? 0 : bi;
+}
+
+// out[j] = alpha * sum_i X[i][j] + beta * out[j]; one workgroup per 64 cols,
+// rows split over 4 wave groups, combined in a fixed order (deterministic).
+__global__ __launch_bounds__(256) void k_sum_rows(const float *__restrict__ X, long rows, int cols,
+                                                  float alpha, float beta, float *__restrict__ out) {
+  __shared__ float part[16][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < cols)
+    for (long r = blockIdx.y * 4 + g; r < rows; r += 4L * gridDim.y) s += X[r * cols + c];
+  part[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0 && c < cols) {
+    float v = ((part[0][threadIdx.x] + part[1][threadIdx.x]) + part[2][threadIdx.x]) + part[3][threadIdx.x];
+    out[(long)blockIdx.y * cols + c] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_sum_partials(const float *__restrict__ part, int nparts,
+                                                      int cols, float alpha, float beta,
+                                                      float *__restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int p = 0; p < nparts; p++) s += part[(long)p * cols + c];
+  out[c] = alpha * s + (beta != 0.f ? beta * out[c] : 0.f);
+}
+
+__global__ void k_fill(float *p, long n, float v) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) p[i] = v;
+}
+
+}  // namespace
+
+static int grid_for(long n, int per = 256) {
+  long b = (n + per - 1) / per;
+  return (int)std::max<long>(1, std::min<long>(b, 4096));
+}
+
+void clip_sgd_update(hipStream_t s, float *w, const float *dw, long n, float lr, float clip) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_clip_sgd, dim3(grid_for((n + 3) / 4)), dim3(256), 0, s, w, dw, n, lr, clip);
+}
+
+void rownorm_clip(hipStream_t s, float *d, long rows, int dim, float thr, int *nclipped) {
+  if (rows <= 0) return;
+  hipLaunchKernelGGL(k_rownorm_clip, dim3(ceil_div(rows, 4)), dim3(256), 0, s, d, rows, dim,
+                     1.f / (thr * thr), nclipped);
+}
+
+void row_argmax(hipStream_t s, const float *m, long rows, int cols, int *ids) {
+  if (rows <= 0) return;
+  hipLaunchKernelGGL(k_row_argmax, dim3(ceil_div(rows, 4)), dim3(256), 0, s, m, rows, cols, ids);
+}
+
+size_t sum_rows_ws_floats(long rows, int cols) { return (size_t)64 * cols; }
+
+void sum_rows(hipStream_t s, const float *X, long rows, int cols, float alpha, float beta,
+              float *out, float *ws) {
+  if (cols <= 0) return;
+  const int parts = (int)std::min<long>(64, std::max<long>(1, rows / 256));
+  hipLaunchKernelGGL(k_sum_rows, dim3(ceil_div(cols, 64), parts), dim3(256), 0, s, X, rows, cols,
+                     alpha, beta, ws);
+  hipLaunchKernelGGL(k_sum_partials, dim3(ceil_div(cols, 256)), dim3(256), 0, s, ws, parts, cols,
+                     alpha, beta, out);
+}
+
+void fill(hipStream_t s, float *p, long n, float v) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(256), 0, s, p, n, v);
+}
+
+}  // namespace kctc

@@ -1,0 +1,38 @@
+// gemm.h -- fp32 MFMA GEMM for gfx950 (v_mfma_f32_16x16x4_f32, exact fp32).
+// Replaces the cublasSgemm calls of the reference's CuMatrix::AddMatMat
+// (src/cudamatrix/cu-matrix.cc:1077-1110) and cuDNN's internal gate GEMMs.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace kctc {
+
+// Row-major: C[b][i][j] = alpha * sum_k opA(b,i,k) opB(b,k,j) + beta * C[b][i][j]
+//                         (+ bias[b][j] + bias2[b][j] when given)
+//   opA(i,k) = transA ? A[k*lda + i] : A[i*lda + k]
+//   opB(k,j) = transB ? B[j*ldb + k] : B[k*ldb + j]
+// Batch strides may be negative.  split_k > 1 needs `ws` of
+// split_k * batch * M * N floats and makes the result deterministic (slab
+// reduce in fixed order).
+struct GemmArgs {
+  bool transA = false, transB = false;
+  int M = 0, N = 0, K = 0;
+  float alpha = 1.f, beta = 0.f;
+  const float *A = nullptr, *B = nullptr;
+  float *C = nullptr;
+  long lda = 0, ldb = 0, ldc = 0;
+  const float *bias = nullptr, *bias2 = nullptr;
+  int batch = 1;
+  long strideA = 0, strideB = 0, strideC = 0, strideBias = 0;
+  int split_k = 1;
+  float *ws = nullptr;
+};
+
+void gemm_f32(hipStream_t stream, const GemmArgs &g);
+// Heuristic split-K so that tiles * split fill the chip; returns 1 if not needed.
+int gemm_pick_split(int M, int N, int K, int batch);
+
+// column sums: out[b][j] (+)= alpha * sum_i X[b][i*ldx + j], i < rows  (accumulate if beta=1)
+void colsum_f32(hipStream_t stream, const float *X, long ldx, int rows, int cols, float alpha,
+                float beta, float *out, int batch = 1, long strideX = 0, long strideOut = 0);
+
+}  // namespace kctc

@@ -1,0 +1,293 @@
+// gemm.hip -- fp32 GEMM on the gfx950 matrix cores (v_mfma_f32_16x16x4_f32).
+//
+// Tile 128x128x32, 256 threads = 4 waves in a 2x2 grid, each wave owns a 64x64
+// sub-tile = 4x4 MFMA tiles (64 accumulator VGPRs).  Both operands are staged
+// through LDS in a "k-contiguous" image ([row][k], padded to 36 floats so the
+// 16 rows a ds_read_b128 lane group touches fall on distinct 16-B slots),
+// register-staged and double-buffered: the next K-tile's global loads are in
+// flight while the current tile is multiplied, one barrier per K-tile.
+//
+// The K index inside each 16-wide group is permuted (lane quad q handles
+// k = 4q..4q+3 over the 4 MFMA k-steps) so that every lane fetches its four
+// k-step operands with ONE ds_read_b128; the sum is over all k either way and
+// v_mfma_f32_16x16x4_f32 is an exact fp32 FMA chain.
+//
+// Block -> tile mapping is XCD-aware (blocks that share an XCD get adjacent
+// tiles along N, so they share A row panels in that XCD's L2).  Split-K writes
+// fp32 slabs that a second kernel reduces in a fixed order (deterministic).
+#include "common.h"
+#include "gemm.h"
+
+namespace kctc {
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 32, LDK = BK + 4, NT = 256;
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+struct KParams {
+  const float *A, *B;
+  float *C;
+  const float *bias, *bias2;
+  long lda, ldb, ldc;
+  long strideA, strideB, strideC, strideBias;
+  int M, N, K, gx, tiles, batch, split, kchunk;
+  float alpha, beta;
+  float *ws;
+  int vecA, vecB;
+};
+
+// Load one operand tile (rows r0.., k0..) into 4 float4 registers.
+//   KC (k-contiguous source): elem(r,k) = P[r*ld + k]
+//   else (r-contiguous source): elem(r,k) = P[k*ld + r]
+template <bool KC>
+__device__ __forceinline__ void load_tile(const float *__restrict__ P, long ld, int rows, int r0,
+                                          int k0, int kend, int vec, floatx4 (&reg)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    int r, k;
+    if (KC) { r = r0 + (t >> 3) + 32 * i; k = k0 + (t & 7) * 4; }
+    else    { k = k0 + (t >> 5) + 8 * i;  r = r0 + (t & 31) * 4; }
+    floatx4 v = {0.f, 0.f, 0.f, 0.f};
+    if (KC) {
+      if (r < rows) {
+        const float *p = P + (long)r * ld + k;
+        if (vec && k + 3 < kend) {
+          v = *reinterpret_cast<const floatx4 *>(p);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; j++) v[j] = (k + j < kend) ? p[j] : 0.f;
+        }
+      }
+    } else {
+      if (k < kend) {
+        const float *p = P + (long)k * ld + r;
+        if (vec && r + 3 < rows) {
+          v = *reinterpret_cast<const floatx4 *>(p);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; j++) v[j] = (r + j < rows) ? p[j] : 0.f;
+        }
+      }
+    }
+    reg[i] = v;
+  }
+}
+
+template <bool KC>
+__device__ __forceinline__ void store_tile(float *__restrict__ S, const floatx4 (&reg)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    if (KC) {
+      int r = (t >> 3) + 32 * i, k = (t & 7) * 4;
+      *reinterpret_cast<floatx4 *>(S + r * LDK + k) = reg[i];
+    } else {
+      int k = (t >> 5) + 8 * i, r = (t & 31) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; j++) S[(r + j) * LDK + k] = reg[i][j];
+    }
+  }
+}
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(NT, 2) void gemm_kernel(KParams p) {
+  __shared__ __attribute__((aligned(16))) float lds[2][(BM + BN) * LDK];
+  // XCD-aware bijective remap of the tile index
+  const int id = blockIdx.x, tiles = p.tiles;
+  const int q = tiles >> 3, rr = tiles & 7, xcd = id & 7, loc = id >> 3;
+  const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  const int tn = wg % p.gx, tm = wg / p.gx;
+  const int bz = blockIdx.z, b = bz % p.batch, ks = bz / p.batch;
+  const float *A = p.A + (long)b * p.strideA;
+  const float *B = p.B + (long)b * p.strideB;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = ks * p.kchunk, kend = min(p.K, kbeg + p.kchunk);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // A operand: rows m; KC iff !TA.  B operand: rows n; KC iff TB.
+  const float *Ab = TA ? A + m0 : A + (long)m0 * p.lda;
+  const float *Bb = TB ? B + (long)n0 * p.ldb : B + n0;
+  const int arows = p.M - m0, brows = p.N - n0;
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  floatx4 ra[4], rb[4];
+  int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk < 0) nk = 0;
+  if (nk > 0) {
+    load_tile<!TA>(Ab, p.lda, arows, 0, kbeg, kend, p.vecA, ra);
+    load_tile<TB>(Bb, p.ldb, brows, 0, kbeg, kend, p.vecB, rb);
+    store_tile<!TA>(lds[0], ra);
+    store_tile<TB>(lds[0] + BM * LDK, rb);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt++) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      const int k0 = kbeg + (kt + 1) * BK;
+      load_tile<!TA>(Ab, p.lda, arows, 0, k0, kend, p.vecA, ra);
+      load_tile<TB>(Bb, p.ldb, brows, 0, k0, kend, p.vecB, rb);
+    }
+    const float *sA = lds[cur], *sB = lds[cur] + BM * LDK;
+#pragma unroll
+    for (int kg = 0; kg < BK / 16; kg++) {
+      floatx4 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        fa[i] = *reinterpret_cast<const floatx4 *>(sA + (wm + i * 16 + fr) * LDK + kg * 16 + fq * 4);
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        fb[j] = *reinterpret_cast<const floatx4 *>(sB + (wn + j * 16 + fr) * LDK + kg * 16 + fq * 4);
+#pragma unroll
+      for (int s = 0; s < 4; s++)
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      store_tile<!TA>(lds[cur ^ 1], ra);
+      store_tile<TB>(lds[cur ^ 1] + BM * LDK, rb);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: acc[i][j][r] -> C[m0+wm+16i+4fq+r][n0+wn+16j+fr]
+  if (p.split > 1) {
+    float *W = p.ws + ((long)ks * p.batch + b) * (long)p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int col = n0 + wn + j * 16 + fr;
+        if (col >= p.N) continue;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int row = m0 + wm + i * 16 + fq * 4 + r;
+          if (row < p.M) W[(long)row * p.N + col] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+  float *C = p.C + (long)b * p.strideC;
+  const float *bias = p.bias ? p.bias + (long)b * p.strideBias : nullptr;
+  const float *bias2 = p.bias2 ? p.bias2 + (long)b * p.strideBias : nullptr;
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int col = n0 + wn + j * 16 + fr;
+      if (col >= p.N) continue;
+      float badd = 0.f;
+      if (bias) badd += bias[col];
+      if (bias2) badd += bias2[col];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = m0 + wm + i * 16 + fq * 4 + r;
+        if (row < p.M) {
+          float *c = C + (long)row * p.ldc + col;
+          float v = p.alpha * acc[i][j][r] + badd;
+          if (p.beta != 0.f) v += p.beta * *c;
+          *c = v;
+        }
+      }
+    }
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce(KParams p) {
+  const long total = (long)p.batch * p.M * p.N;
+  const long MN = (long)p.M * p.N;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int b = (int)(e / MN);
+    const long rem = e - (long)b * MN;
+    const int row = (int)(rem / p.N), col = (int)(rem - (long)row * p.N);
+    float s = 0.f;
+    for (int k = 0; k < p.split; k++) s += p.ws[((long)k * p.batch + b) * MN + rem];
+    float *c = p.C + (long)b * p.strideC + (long)row * p.ldc + col;
+    float v = p.alpha * s;
+    if (p.bias) v += p.bias[(long)b * p.strideBias + col];
+    if (p.bias2) v += p.bias2[(long)b * p.strideBias + col];
+    if (p.beta != 0.f) v += p.beta * *c;
+    *c = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void colsum_kernel(const float *__restrict__ X, long ldx, int rows,
+                                                     int cols, float alpha, float beta,
+                                                     float *__restrict__ out, long strideX,
+                                                     long strideOut) {
+  __shared__ float part[4][64];
+  const int b = blockIdx.y, c = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+  const float *x = X + (long)b * strideX;
+  float s = 0.f;
+  if (c < cols)
+    for (int r = g; r < rows; r += 4) s += x[(long)r * ldx + c];
+  part[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0 && c < cols) {
+    float v = ((part[0][threadIdx.x] + part[1][threadIdx.x]) + part[2][threadIdx.x]) + part[3][threadIdx.x];
+    float *o = out + (long)b * strideOut + c;
+    *o = alpha * v + (beta != 0.f ? beta * *o : 0.f);
+  }
+}
+
+}  // namespace
+
+int gemm_pick_split(int M, int N, int K, int batch) {
+  const long tiles = (long)ceil_div(M, BM) * ceil_div(N, BN) * batch;
+  if (tiles >= 192 || K < 4 * BK) return 1;
+  long want = (256 + tiles - 1) / tiles;
+  long maxs = K / (2 * BK);
+  if (want > maxs) want = maxs;
+  if (want > 64) want = 64;
+  return want < 1 ? 1 : (int)want;
+}
+
+void gemm_f32(hipStream_t stream, const GemmArgs &g) {
+  if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return;
+  KParams p;
+  p.A = g.A; p.B = g.B; p.C = g.C; p.bias = g.bias; p.bias2 = g.bias2;
+  p.lda = g.lda; p.ldb = g.ldb; p.ldc = g.ldc;
+  p.strideA = g.strideA; p.strideB = g.strideB; p.strideC = g.strideC; p.strideBias = g.strideBias;
+  p.M = g.M; p.N = g.N; p.K = g.K; p.alpha = g.alpha; p.beta = g.beta;
+  p.gx = ceil_div(g.N, BN);
+  p.tiles = p.gx * ceil_div(g.M, BM);
+  p.batch = g.batch;
+  p.split = (g.split_k > 1 && g.ws) ? g.split_k : 1;
+  p.kchunk = p.split > 1 ? (int)align_up((size_t)ceil_div(g.K, p.split), BK) : (g.K > 0 ? g.K : 1);
+  if (p.split > 1) p.split = ceil_div(g.K, p.kchunk);
+  p.ws = g.ws;
+  auto aligned = [](const void *ptr, long ld, long stride) {
+    return ((uintptr_t)ptr % 16 == 0) && (ld % 4 == 0) && (stride % 4 == 0);
+  };
+  p.vecA = aligned(g.A, g.lda, g.strideA);
+  p.vecB = aligned(g.B, g.ldb, g.strideB);
+  dim3 grid(p.tiles, 1, p.batch * p.split);
+  if (!g.transA && !g.transB) hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(NT), 0, stream, p);
+  else if (!g.transA && g.transB) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(NT), 0, stream, p);
+  else if (g.transA && !g.transB) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, dim3(NT), 0, stream, p);
+  else hipLaunchKernelGGL((gemm_kernel<true, true>), grid, dim3(NT), 0, stream, p);
+  if (p.split > 1) {
+    long total = (long)p.batch * p.M * p.N;
+    int blocks = (int)std::min<long>(2048, (total + 255) / 256);
+    hipLaunchKernelGGL(splitk_reduce, dim3(blocks), dim3(256), 0, stream, p);
+  }
+}
+
+void colsum_f32(hipStream_t stream, const float *X, long ldx, int rows, int cols, float alpha,
+                float beta, float *out, int batch, long strideX, long strideOut) {
+  if (cols <= 0 || batch <= 0) return;
+  hipLaunchKernelGGL(colsum_kernel, dim3(ceil_div(cols, 64), batch), dim3(256), 0, stream, X, ldx,
+                     rows, cols, alpha, beta, out, strideX, strideOut);
+}
+
+}  // namespace kctc

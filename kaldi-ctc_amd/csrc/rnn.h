@@ -1,0 +1,53 @@
+// rnn.h -- cuDNN-v5-compatible recurrent layer on gfx950 (internal C++ API).
+// Replaces cudnnRNNForwardTraining / BackwardData / BackwardWeights as wrapped
+// by src/cudamatrix/cudnn-recurrent.cc:13-102 of the reference.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+namespace kctc {
+
+enum RnnMode { kRelu = 0, kTanh = 1, kLstm = 2, kGru = 3 };
+
+inline int rnn_nw(int mode) { return mode == kLstm ? 4 : mode == kGru ? 3 : 1; }
+
+struct RnnDesc {
+  int mode = kLstm, D = 0, H = 0, layers = 1, dirs = 2;
+  int nw() const { return rnn_nw(mode); }
+  int din(int layer) const { return layer == 0 ? D : dirs * H; }
+  // floats of one pseudo-layer block [W | R | bW | bR] of stacked layer `layer`
+  long pl_size(int layer) const {
+    long n = nw();
+    return n * H * (long)din(layer) + n * H * (long)H + 2 * n * H;
+  }
+  long params_size() const;
+  // float offset of lin layer `lin` (matrix or bias) of pseudo-layer p = layer*dirs + dir
+  long lin_offset(int p, int lin, bool bias) const;
+};
+
+// Per-layer regions of the training reserve (floats), kept from forward to
+// backward exactly like cuDNN's reserveSpace.
+struct RnnReserveLayout {
+  long G, aux, E, DX, bias, out, dout, per_layer, total;
+};
+RnnReserveLayout rnn_reserve_layout(const RnnDesc &d, int T, int N);
+size_t rnn_workspace_bytes(const RnnDesc &d, int T, int N);
+
+// Status codes of the RNN ABI (include/kaldi_rnn.h)
+enum { KRNN_OK = 0, KRNN_BAD_PARAM = 1, KRNN_NOT_SUPPORTED = 2, KRNN_EXEC_FAILED = 3,
+       KRNN_TIMEOUT = 4 };
+
+// All calls are stream-ordered; `err` is a device word (0 = ok) that the
+// persistent kernels set on a bounded-spin timeout.
+int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
+                         const float *w, float *y, void *workspace, size_t ws_bytes,
+                         void *reserve, size_t res_bytes, unsigned *err);
+int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float *y,
+                      const float *dy, const float *w, float *dx, void *workspace,
+                      size_t ws_bytes, void *reserve, size_t res_bytes, unsigned *err);
+int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
+                         const float *y, void *workspace, size_t ws_bytes, float *dw,
+                         void *reserve, size_t res_bytes);
+
+}  // namespace kctc

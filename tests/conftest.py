@@ -37,3 +37,32 @@ def oracle():
     import oracle_lib
     oracle_lib.lib()
     return oracle_lib
+
+
+def load_kctc():
+    """Import kaldi-ctc_amd/ (hyphenated dir) as the package `kaldi_ctc_amd`."""
+    import importlib.util
+    if "kaldi_ctc_amd" in sys.modules:
+        return sys.modules["kaldi_ctc_amd"]
+    pkg = os.path.join(ROOT, "kaldi-ctc_amd")
+    spec = importlib.util.spec_from_file_location("kaldi_ctc_amd", os.path.join(pkg, "__init__.py"),
+                                                  submodule_search_locations=[pkg])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["kaldi_ctc_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+@pytest.fixture(scope="session")
+def kctc():
+    return load_kctc()
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("gpu-marked test run without a visible GPU")
+    m = load_kctc()
+    m.lib()  # fail loudly if the HIP library is missing
+    return torch.device("cuda:0")

@@ -1,0 +1,163 @@
+"""RNN HIP kernels (cuDNN-shaped ABI, include/kaldi_rnn.h) and the fp32 MFMA
+GEMM (include/kaldi_cumatrix.h) vs the fp64 oracle.
+
+Tolerances (north_star: RNN gradients within 1e-4 relative fp32): norm-wise
+relative error <= 1e-5 on y, <= 1e-4 on dx and dw."""
+import numpy as np
+import pytest
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _mk(kctc, gpu, mode, T, N, D, H, layers, bidir, seed, wscale=0.15):
+    import torch
+    rng = np.random.default_rng(seed)
+    r = kctc.Rnn(mode, D, H, layers, bidir)
+    P = r.num_params
+    w = (rng.standard_normal(P) * wscale).astype(np.float32)
+    x = rng.standard_normal((T, N, D)).astype(np.float32)
+    dy = rng.standard_normal((T, N, r.dirs * H)).astype(np.float32)
+    ws_b, res_b = r.sizes(T, N)
+    t = lambda a: torch.from_numpy(a).to(gpu)
+    bufs = dict(w=t(w), x=t(x), dy=t(dy), y=torch.empty((T, N, r.dirs * H), device=gpu),
+                dx=torch.empty((T, N, D), device=gpu), dw=torch.zeros(P, device=gpu),
+                ws=torch.empty(ws_b, dtype=torch.uint8, device=gpu),
+                res=torch.empty(res_b, dtype=torch.uint8, device=gpu))
+    return r, (w, x, dy), bufs
+
+
+def _run_gpu(r, b):
+    import torch
+    r.forward_training(b["x"], b["w"], b["y"], b["ws"], b["res"])
+    r.backward_data(b["y"], b["dy"], b["w"], b["dx"], b["ws"], b["res"])
+    r.backward_weights(b["x"], b["y"], b["dw"], b["ws"], b["res"])
+    torch.cuda.synchronize()
+    assert r.device_status() == 0
+    return b["y"].cpu().numpy(), b["dx"].cpu().numpy(), b["dw"].cpu().numpy()
+
+
+CASES = [
+    # (mode, T, N, D, H, layers, bidir)
+    (2, 23, 5, 24, 64, 1, True),     # LSTM, the recipe's component shape in miniature
+    (2, 17, 3, 40, 64, 1, False),
+    (2, 11, 4, 16, 32, 2, True),     # stacked (num-layers 2)
+    (3, 19, 6, 20, 64, 1, True),     # GRU
+    (3, 9, 2, 8, 48, 2, False),
+    (0, 15, 4, 12, 32, 1, True),     # RELU
+    (1, 15, 4, 12, 32, 1, True),     # TANH
+    (2, 9, 40, 32, 64, 1, True),     # N > 16: several MFMA row tiles
+    (2, 40, 16, 256, 512, 1, True),  # BLSTM-512 width (U=8 / U=16 partitions)
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"m{c[0]}_T{c[1]}_N{c[2]}_D{c[3]}_H{c[4]}_L{c[5]}_{'bi' if c[6] else 'uni'}"
+                                             for c in CASES])
+def test_rnn_matches_oracle(kctc, gpu, oracle, case):
+    mode, T, N, D, H, layers, bidir = case
+    r, (w, x, dy), b = _mk(kctc, gpu, mode, T, N, D, H, layers, bidir, seed=sum(case))
+    assert r.num_params == oracle.params_size(mode, D, H, layers, r.dirs)
+    y, dx, dw = _run_gpu(r, b)
+    ry, res = oracle.rnn_forward(mode, x.astype(np.float64), w.astype(np.float64), H, layers, r.dirs)
+    rdx, rdw = oracle.rnn_backward(mode, x.astype(np.float64), w.astype(np.float64), ry,
+                                   dy.astype(np.float64), res, H, layers, r.dirs)
+    assert rel_err(y, ry) < 1e-5
+    assert rel_err(dx, rdx) < 1e-4
+    assert rel_err(dw, rdw) < 1e-4
+    # per-region check of dW (W, R, biases of every pseudo-layer)
+    nlin = 2 * (4 if mode == 2 else 3 if mode == 3 else 1)
+    for pl in range(layers * r.dirs):
+        for lin in range(nlin):
+            for isb in (0, 1):
+                off, (h, c) = r.lin_offset(pl, lin, isb)
+                sl = slice(off, off + h * c)
+                assert rel_err(dw[sl], rdw[sl]) < 2e-4, (pl, lin, isb)
+
+
+def test_rnn_golden_layout(kctc, gpu):
+    """The torch-fp64 golden fixture through the HIP path (cuDNN layout)."""
+    import torch
+    from conftest import golden
+    g = golden("rnn_lstm_bi_h32")
+    mode, H, layers, dirs = int(g["mode"]), int(g["H"]), int(g["layers"]), int(g["dirs"])
+    T, N, D = g["x"].shape
+    r = kctc.Rnn(mode, D, H, layers, dirs == 2)
+    ws_b, res_b = r.sizes(T, N)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+    b = dict(w=t(g["w"]), x=t(g["x"]), dy=t(g["dy"]), y=torch.empty((T, N, dirs * H), device=gpu),
+             dx=torch.empty((T, N, D), device=gpu), dw=torch.zeros(g["w"].size, device=gpu),
+             ws=torch.empty(ws_b, dtype=torch.uint8, device=gpu),
+             res=torch.empty(res_b, dtype=torch.uint8, device=gpu))
+    y, dx, dw = _run_gpu(r, b)
+    assert rel_err(y, g["y"]) < 1e-5
+    assert rel_err(dx, g["dx"]) < 1e-4
+    assert rel_err(dw, g["dw"]) < 1e-4
+
+
+def test_rnn_weights_accumulate_and_inference(kctc, gpu, oracle):
+    import torch
+    r, (w, x, dy), b = _mk(kctc, gpu, 2, 13, 4, 16, 32, 1, True, seed=3)
+    _, _, dw1 = _run_gpu(r, b)
+    # second BackwardWeights accumulates (cudnnRNNBackwardWeights semantics)
+    r.backward_weights(b["x"], b["y"], b["dw"], b["ws"], b["res"])
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(b["dw"].cpu().numpy(), 2 * dw1, rtol=1e-5, atol=1e-6)
+    y_inf = torch.empty_like(b["y"])
+    ws = torch.empty(r.sizes(13, 4)[0], dtype=torch.uint8, device=gpu)
+    r.forward_inference(b["x"], b["w"], y_inf, ws)
+    torch.cuda.synchronize()
+    assert torch.equal(y_inf, b["y"])
+
+
+def test_rnn_full_size_properties(kctc, gpu):
+    """configs[1] layer 2-5 shape (T=2000, N=16, D=1024, H=512, bidir): too big
+    for the fp64 oracle in test time, so check size-independent properties:
+    bitwise determinism, finite outputs, no sentinel left in the exchange."""
+    import torch
+    T, N, D, H = 2000, 16, 1024, 512
+    r = kctc.Rnn(2, D, H, 1, True)
+    g = torch.Generator(device=gpu).manual_seed(0)
+    w = torch.randn(r.num_params, device=gpu, generator=g) * 0.02
+    x = torch.randn((T, N, D), device=gpu, generator=g)
+    dy = torch.randn((T, N, 2 * H), device=gpu, generator=g)
+    ws_b, res_b = r.sizes(T, N)
+    ws = torch.empty(ws_b, dtype=torch.uint8, device=gpu)
+    res = torch.empty(res_b, dtype=torch.uint8, device=gpu)
+    outs = []
+    for _ in range(2):
+        y = torch.empty((T, N, 2 * H), device=gpu)
+        dx = torch.empty((T, N, D), device=gpu)
+        dw = torch.zeros(r.num_params, device=gpu)
+        r.forward_training(x, w, y, ws, res)
+        r.backward_data(y, dy, w, dx, ws, res)
+        r.backward_weights(x, y, dw, ws, res)
+        torch.cuda.synchronize()
+        assert r.device_status() == 0
+        outs.append((y, dx, dw))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+        assert torch.isfinite(a).all()
+    # forward direction at t=0 depends only on x[0]: compare with a T=1 run
+    y1 = torch.empty((1, N, 2 * H), device=gpu)
+    ws1 = torch.empty(r.sizes(1, N)[0], dtype=torch.uint8, device=gpu)
+    res1 = torch.empty(r.sizes(1, N)[1], dtype=torch.uint8, device=gpu)
+    r.forward_training(x[:1].contiguous(), w, y1, ws1, res1)
+    torch.cuda.synchronize()
+    assert torch.allclose(y1[0, :, :H], outs[0][0][0, :, :H], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("ta,tb,M,N,K", [(0, 0, 77, 41, 40), (0, 1, 300, 130, 257), (1, 0, 64, 96, 1000),
+                                         (1, 1, 33, 17, 9), (0, 1, 1024, 1024, 1024)])
+def test_gemm_matches_numpy(kctc, gpu, ta, tb, M, N, K):
+    import torch
+    rng = np.random.default_rng(M + N + K)
+    A = rng.standard_normal((K, M) if ta else (M, K)).astype(np.float32)
+    B = rng.standard_normal((N, K) if tb else (K, N)).astype(np.float32)
+    C0 = rng.standard_normal((M, N)).astype(np.float32)
+    C = torch.from_numpy(C0).to(gpu)
+    kctc.add_mat_mat(C, torch.from_numpy(A).to(gpu), torch.from_numpy(B).to(gpu), bool(ta), bool(tb),
+                     alpha=0.5, beta=-1.5)
+    torch.cuda.synchronize()
+    ref = 0.5 * ((A.T if ta else A).astype(np.float64) @ (B.T if tb else B).astype(np.float64)) - 1.5 * C0
+    assert rel_err(C.cpu().numpy(), ref) < 1e-6
