@@ -234,3 +234,162 @@ def add_mat_mat(C, A, B, transA=False, transB=False, alpha=1.0, beta=0.0, stream
                                _ptr(A), A.stride(0), _ptr(B), B.stride(0), beta, _ptr(C), C.stride(0))
     if st != 0:
         raise KctcError(f"kcm_add_mat_mat failed ({st})")
+
+
+# ---------------------------------------------------------------------------
+# nnet2 trainer (include/kaldi_ctc_train.h)
+# ---------------------------------------------------------------------------
+def _tcheck(st, where):
+    if st != 0:
+        raise KctcError(f"{where}: {lib().kctc_last_error().decode()}")
+
+
+def recipe_config(num_rnn=5, input_dim=40, hidden=512, num_targets=41, rnn_mode=2, bidirectional=True,
+                  learning_rate=5e-4, max_seq_length=2000, clipping_threshold=30.0, param_stddev=0.02,
+                  bias_stddev=0.2, num_layers=1, norm_based_clipping=True):
+    """Component config lines of the CTC recipe, as written by
+    egs/wsj/s5/steps/ctc/nnet2/components.py:73-102 (AddRnnLayer ->
+    CuDNNRecurrentComponent + ClipGradientComponent) and an output
+    AffineComponent; Splice with context 0 first (make_configs.py)."""
+    lines = [f"SpliceComponent input-dim={input_dim} context=0"]
+    dim = input_dim
+    out = hidden * (2 if bidirectional else 1)
+    for _ in range(num_rnn):
+        lines.append(f"CuDNNRecurrentComponent input-dim={dim} output-dim={hidden} "
+                     f"bidirectional={'true' if bidirectional else 'false'} max-seq-length={max_seq_length} "
+                     f"learning-rate={learning_rate} rnn-mode={rnn_mode} num-layers={num_layers} "
+                     f"param-stddev={param_stddev} bias-stddev={bias_stddev}")
+        lines.append(f"ClipGradientComponent dim={out} clipping-threshold={clipping_threshold} "
+                     f"norm-based-clipping={'true' if norm_based_clipping else 'false'}")
+        dim = out
+    lines.append(f"AffineComponent input-dim={dim} output-dim={num_targets} learning-rate={learning_rate}")
+    return "\n".join(lines) + "\n"
+
+
+class Nnet:
+    """nnet2 CTC model on one GPU (the C++ mirror of Nnet + NnetCtcUpdater)."""
+
+    def __init__(self, config=None, seed=0, device=0, _handle=None):
+        if _handle is not None:
+            self.h = _handle
+            return
+        h = ctypes.c_void_p()
+        _tcheck(lib().kctc_nnet_create(ctypes.byref(h), config.encode(), seed, device), "kctc_nnet_create")
+        self.h = h
+
+    @classmethod
+    def read(cls, path, device=0):
+        h = ctypes.c_void_p()
+        _tcheck(lib().kctc_nnet_read(ctypes.byref(h), str(path).encode(), device), "kctc_nnet_read")
+        return cls(_handle=h)
+
+    def write(self, path):
+        _tcheck(lib().kctc_nnet_write(self.h, str(path).encode()), "kctc_nnet_write")
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().kctc_nnet_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def num_components(self):
+        return lib().kctc_nnet_num_components(self.h)
+
+    def info(self, c):
+        buf = ctypes.create_string_buffer(1024)
+        _tcheck(lib().kctc_nnet_component_info(self.h, c, buf, 1024), "component_info")
+        return buf.value.decode()
+
+    def num_params(self, c):
+        return lib().kctc_nnet_num_params(self.h, c)
+
+    def get_params(self, c):
+        out = np.zeros(self.num_params(c), np.float32)
+        _tcheck(lib().kctc_nnet_get_params(self.h, c, out.ctypes.data, out.size), "get_params")
+        return out
+
+    def set_params(self, c, arr):
+        a = np.ascontiguousarray(arr, dtype=np.float32)
+        _tcheck(lib().kctc_nnet_set_params(self.h, c, a.ctypes.data, a.size), "set_params")
+
+    def set_learning_rate(self, lr):
+        _tcheck(lib().kctc_nnet_set_learning_rate(self.h, lr), "set_learning_rate")
+
+    def clip_stats(self, c):
+        a, b = ctypes.c_double(), ctypes.c_double()
+        _tcheck(lib().kctc_nnet_clip_stats(self.h, c, ctypes.byref(a), ctypes.byref(b)), "clip_stats")
+        return a.value, b.value
+
+    def set_repair_seed(self, seed):
+        _tcheck(lib().kctc_nnet_set_repair_seed(self.h, seed), "set_repair_seed")
+
+    def _step(self, fn, feats, T, N, num_frames, flat_labels, label_lengths):
+        nf = np.ascontiguousarray(num_frames, dtype=np.int32)
+        fl = np.ascontiguousarray(flat_labels, dtype=np.int32)
+        if fl.size == 0:
+            fl = np.zeros(1, np.int32)
+        ll = np.ascontiguousarray(label_lengths, dtype=np.int32)
+        o, a, w = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        _tcheck(fn(self.h, _ptr(feats), T, N, nf.ctypes.data, fl.ctypes.data, ll.ctypes.data,
+                   ctypes.byref(o), ctypes.byref(a), ctypes.byref(w)), fn.__name__)
+        return o.value, a.value, w.value
+
+    def train_step(self, feats, T, N, num_frames, flat_labels, label_lengths):
+        """DoBackprop on one minibatch; feats: device [T*N, D]. -> (objf, accuracy, weight)"""
+        return self._step(lib().kctc_nnet_train_step, feats, T, N, num_frames, flat_labels, label_lengths)
+
+    def compute_objf(self, feats, T, N, num_frames, flat_labels, label_lengths):
+        return self._step(lib().kctc_nnet_compute_objf, feats, T, N, num_frames, flat_labels, label_lengths)
+
+    @property
+    def stream(self):
+        return lib().kctc_nnet_stream(self.h)
+
+    def set_profiling(self, on):
+        _tcheck(lib().kctc_nnet_set_profiling(self.h, int(on)), "set_profiling")
+
+    def profile(self, family):
+        ms, n = ctypes.c_double(), ctypes.c_int()
+        _tcheck(lib().kctc_nnet_profile(self.h, family.encode(), ctypes.byref(ms), ctypes.byref(n)), "profile")
+        return ms.value, n.value
+
+    def enable_dp(self, uid, rank, world):
+        buf = ctypes.create_string_buffer(bytes(uid), 128)
+        _tcheck(lib().kctc_nnet_enable_dp(self.h, buf, rank, world), "enable_dp")
+
+
+def dp_unique_id():
+    buf = ctypes.create_string_buffer(128)
+    _tcheck(lib().kctc_dp_unique_id(buf), "kctc_dp_unique_id")
+    return buf.raw
+
+
+def synth_minibatch(seed, T_max, N, dim, A, label_ratio=0.125, want_feats=True):
+    """BASELINE.md §2 synthetic minibatch, already in FormatNnetInput layout."""
+    feats = np.empty((T_max * N, dim), np.float32) if want_feats else None
+    nf = np.zeros(N, np.int32)
+    ll = np.zeros(N, np.int32)
+    fl = np.zeros(N * 639 + 1, np.int32)
+    n = lib().kctc_synth_minibatch(seed, T_max, N, dim, A, label_ratio,
+                                   feats.ctypes.data if feats is not None else None,
+                                   nf.ctypes.data, fl.ctypes.data, ll.ctypes.data)
+    return feats, nf, fl[:n].copy(), ll
+
+
+def format_input(utt_feats, T_max=None):
+    """FormatNnetInput on a list of [T_n, dim] arrays -> [T_max*N, dim]."""
+    N = len(utt_feats)
+    dim = utt_feats[0].shape[1]
+    nf = np.array([u.shape[0] for u in utt_feats], np.int32)
+    T_max = int(T_max or nf.max())
+    cat = np.ascontiguousarray(np.concatenate(utt_feats, 0), dtype=np.float32)
+    out = np.empty((T_max * N, dim), np.float32)
+    _tcheck(lib().kctc_format_input(cat.ctypes.data, nf.ctypes.data, N, dim, T_max, out.ctypes.data),
+            "kctc_format_input")
+    return out

@@ -28,6 +28,31 @@ SIGS = {
     "kcm_clip_gradient_rows": (ci, [vp, vp, cl, ci, cf, vp]),
     "kcm_add_vec_clipped": (ci, [vp, vp, vp, cl, cf, cf]),
     "kcm_add_row_sum_mat": (ci, [vp, vp, cl, ci, cf, cf, vp, vp]),
+    # include/kaldi_ctc_train.h
+    "kctc_last_error": (ctypes.c_char_p, []),
+    "kctc_nnet_create": (ci, [ctypes.POINTER(vp), ctypes.c_char_p, ctypes.c_ulonglong, ci]),
+    "kctc_nnet_destroy": (ci, [vp]),
+    "kctc_nnet_num_components": (ci, [vp]),
+    "kctc_nnet_component_info": (ci, [vp, ci, ctypes.c_char_p, sz]),
+    "kctc_nnet_num_params": (cl, [vp, ci]),
+    "kctc_nnet_get_params": (ci, [vp, ci, vp, cl]),
+    "kctc_nnet_set_params": (ci, [vp, ci, vp, cl]),
+    "kctc_nnet_set_learning_rate": (ci, [vp, cf]),
+    "kctc_nnet_clip_stats": (ci, [vp, ci, ctypes.POINTER(cd), ctypes.POINTER(cd)]),
+    "kctc_nnet_set_repair_seed": (ci, [vp, ctypes.c_ulonglong]),
+    "kctc_nnet_train_step": (ci, [vp, vp, ci, ci, vp, vp, vp, ctypes.POINTER(cd), ctypes.POINTER(cd),
+                                  ctypes.POINTER(cd)]),
+    "kctc_nnet_compute_objf": (ci, [vp, vp, ci, ci, vp, vp, vp, ctypes.POINTER(cd), ctypes.POINTER(cd),
+                                    ctypes.POINTER(cd)]),
+    "kctc_nnet_stream": (vp, [vp]),
+    "kctc_nnet_set_profiling": (ci, [vp, ci]),
+    "kctc_nnet_profile": (ci, [vp, ctypes.c_char_p, ctypes.POINTER(cd), ctypes.POINTER(ci)]),
+    "kctc_nnet_write": (ci, [vp, ctypes.c_char_p]),
+    "kctc_nnet_read": (ci, [ctypes.POINTER(vp), ctypes.c_char_p, ci]),
+    "kctc_dp_unique_id": (ci, [vp]),
+    "kctc_nnet_enable_dp": (ci, [vp, vp, ci, ci]),
+    "kctc_format_input": (ci, [vp, vp, ci, ci, ci, vp]),
+    "kctc_synth_minibatch": (cl, [ctypes.c_ulonglong, ci, ci, ci, ci, cd, vp, vp, vp, vp]),
 }
 
 

@@ -26,6 +26,7 @@
 
 #include "common.h"
 #include "ctc.h"
+#include "prof.h"
 
 namespace kctc {
 namespace ctcimpl {
@@ -417,12 +418,16 @@ static ctcStatus_t launch(const float *acts, float *grads, const int *flat_label
   double *d_offs = reinterpret_cast<double *>(ws + lay.offs);
   const long rows = (long)lay.T_max * N;
   if (rows > 0) {
+    ProfSpan ps(stream, "ctc_logz");
     hipLaunchKernelGGL(ctc_logz, dim3(ceil_div(rows, 4)), dim3(256), 0, stream, acts, A, rows,
                        d_logz);
   }
   const int want = grads != nullptr;
+  {
+  ProfSpan ps(stream, "ctc_alpha_beta");
   hipLaunchKernelGGL(ctc_alpha_beta, dim3(want ? 2 * N : N), dim3(kThreads), 0, stream, acts,
                      d_logz, N, A, blank, d_desc, d_lab, d_spill, d_offs, costs_dev, want);
+  }
   if (want && lay.T_max > 0) {
     int Lmax = 0;
     for (int n = 0; n < N; n++) Lmax = label_lengths[n] > Lmax ? label_lengths[n] : Lmax;
@@ -430,6 +435,7 @@ static ctcStatus_t launch(const float *acts, float *grads, const int *flat_label
     size_t shm = sizeof(float) * kFR * Smax + sizeof(int) * (Lmax > 0 ? Lmax : 1) +
                  sizeof(int) * A + 2 * sizeof(float) * kFR;
     if (shm > 160 * 1024) return CTC_STATUS_INVALID_VALUE;
+    ProfSpan ps(stream, "ctc_grad");
     hipLaunchKernelGGL(ctc_grad, dim3(ceil_div(lay.T_max, kFR), N), dim3(kThreads), shm, stream,
                        acts, d_logz, grads, N, A, lay.T_max, blank, d_desc, d_lab, d_spill,
                        d_offs, costs_dev);

@@ -18,5 +18,6 @@ size_t sum_rows_ws_floats(long rows, int cols);
 void sum_rows(hipStream_t s, const float *X, long rows, int cols, float alpha, float beta,
               float *out, float *ws);
 void fill(hipStream_t s, float *p, long n, float v);
+void scale_inplace(hipStream_t s, float *p, long n, float alpha);
 
 }  // namespace kctc

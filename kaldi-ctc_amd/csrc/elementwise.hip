@@ -132,6 +132,10 @@ __global__ __launch_bounds__(256) void k_sum_partials(const float *__restrict__ 
   out[c] = alpha * s + (beta != 0.f ? beta * out[c] : 0.f);
 }
 
+__global__ void k_scale(float *p, long n, float a) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) p[i] *= a;
+}
+
 __global__ void k_fill(float *p, long n, float v) {
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) p[i] = v;
 }
@@ -174,6 +178,11 @@ void sum_rows(hipStream_t s, const float *X, long rows, int cols, float alpha, f
 void fill(hipStream_t s, float *p, long n, float v) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(256), 0, s, p, n, v);
+}
+
+void scale_inplace(hipStream_t s, float *p, long n, float alpha) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_scale, dim3(grid_for(n)), dim3(256), 0, s, p, n, alpha);
 }
 
 }  // namespace kctc

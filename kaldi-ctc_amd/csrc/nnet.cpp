@@ -1,0 +1,992 @@
+// nnet.cpp -- nnet2 CTC training path on MI355X (see nnet.h for the mapping to
+// the reference's classes).
+#include "nnet.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <iomanip>
+#include <iostream>
+#include <sstream>
+
+#include "common.h"
+#include "ctc.h"
+#include "elementwise.h"
+#include "gemm.h"
+#include "prof.h"
+
+namespace kctc {
+namespace nnet2 {
+
+// ---------------------------------------------------------------------------
+// plumbing
+// ---------------------------------------------------------------------------
+DevBuf::~DevBuf() {
+  if (p) (void)hipFree(p);
+}
+
+void DevBuf::ensure(size_t b) {
+  if (b <= bytes && p) return;
+  if (p) {
+    KCTC_HIP_CHECK(hipStreamSynchronize(CuDevice::Instantiate().stream));
+    KCTC_HIP_CHECK(hipFree(p));
+    p = nullptr;
+  }
+  size_t nb = align_up(std::max<size_t>(b, 256), 4096);
+  KCTC_HIP_CHECK(hipMalloc(&p, nb));
+  bytes = nb;
+}
+
+void CuMatrix::Resize(long rows, int cols) {
+  buf_.ensure(sizeof(float) * (size_t)std::max<long>(1, rows * (long)cols));
+  data_ = buf_.f();
+  rows_ = rows;
+  cols_ = cols;
+}
+
+CuDevice &CuDevice::Instantiate() {
+  static thread_local CuDevice dev;
+  return dev;
+}
+
+void CuDevice::Begin(const char *family) {
+  if (!profiling) return;
+  if (pool.size() < 2) {
+    for (int i = 0; i < 64; i++) {
+      hipEvent_t e;
+      KCTC_HIP_CHECK(hipEventCreate(&e));
+      pool.push_back(e);
+    }
+  }
+  Span sp;
+  sp.family = family;
+  sp.a = pool.back(); pool.pop_back();
+  sp.b = pool.back(); pool.pop_back();
+  KCTC_HIP_CHECK(hipEventRecord(sp.a, stream));
+  open.push_back(spans.size());
+  spans.push_back(sp);
+}
+
+void CuDevice::End() {
+  if (!profiling || open.empty()) return;
+  KCTC_HIP_CHECK(hipEventRecord(spans[open.back()].b, stream));
+  open.pop_back();
+}
+
+void CuDevice::Collect() {
+  for (auto &sp : spans) {
+    float ms = 0.f;
+    KCTC_HIP_CHECK(hipEventElapsedTime(&ms, sp.a, sp.b));
+    auto &e = prof[sp.family];
+    e.first += ms;
+    e.second += 1;
+    pool.push_back(sp.a);
+    pool.push_back(sp.b);
+  }
+  spans.clear();
+}
+
+}  // namespace nnet2
+
+void prof_begin(hipStream_t s, const char *family) {
+  auto &d = nnet2::CuDevice::Instantiate();
+  if (d.profiling && s == d.stream) d.Begin(family);
+}
+void prof_end(hipStream_t s) {
+  auto &d = nnet2::CuDevice::Instantiate();
+  if (d.profiling && s == d.stream) d.End();
+}
+
+namespace nnet2 {
+
+struct ProfScope {
+  explicit ProfScope(const char *f) { CuDevice::Instantiate().Begin(f); }
+  ~ProfScope() { CuDevice::Instantiate().End(); }
+};
+
+uint64_t Rng::next() {
+  uint64_t z = (s += 0x9E3779B97F4A7C15ULL);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+double Rng::uniform() { return ((double)(next() >> 11) + 0.5) * (1.0 / 9007199254740992.0); }
+double Rng::gauss() {
+  const double u1 = uniform(), u2 = uniform();
+  return std::sqrt(-2.0 * std::log(u1)) * std::cos(6.283185307179586 * u2);
+}
+
+static hipStream_t S() { return CuDevice::Instantiate().stream; }
+
+// ---- config parsing: ParseFromString (src/nnet2/nnet-component.cc:160-260) ----
+static std::vector<std::string> split_ws(const std::string &s) {
+  std::vector<std::string> out;
+  std::istringstream is(s);
+  std::string t;
+  while (is >> t) out.push_back(t);
+  return out;
+}
+
+static bool take(const std::string &name, std::string *args, std::string *val) {
+  auto parts = split_ws(*args);
+  const std::string ne = name + "=";
+  for (size_t i = 0; i < parts.size(); i++) {
+    if (parts[i].compare(0, ne.size(), ne) == 0) {
+      *val = parts[i].substr(ne.size());
+      std::string rest;
+      for (size_t j = 0; j < parts.size(); j++)
+        if (j != i) rest += (rest.empty() ? "" : " ") + parts[j];
+      *args = rest;
+      return true;
+    }
+  }
+  return false;
+}
+static bool ParseFromString(const std::string &name, std::string *args, int *v) {
+  std::string s;
+  if (!take(name, args, &s)) return false;
+  char *end = nullptr;
+  long x = strtol(s.c_str(), &end, 10);
+  if (s.empty() || *end) throw std::invalid_argument("Bad option " + name + "=" + s);
+  *v = (int)x;
+  return true;
+}
+static bool ParseFromString(const std::string &name, std::string *args, float *v) {
+  std::string s;
+  if (!take(name, args, &s)) return false;
+  char *end = nullptr;
+  double x = strtod(s.c_str(), &end);
+  if (s.empty() || *end) throw std::invalid_argument("Bad option " + name + "=" + s);
+  *v = (float)x;
+  return true;
+}
+static bool ParseFromString(const std::string &name, std::string *args, bool *v) {
+  std::string s;
+  if (!take(name, args, &s)) return false;
+  if (s.empty()) throw std::invalid_argument("Bad option " + name);
+  if (s[0] == 'f' || s[0] == 'F') *v = false;
+  else if (s[0] == 't' || s[0] == 'T') *v = true;
+  else throw std::invalid_argument("Bad option " + name + "=" + s);
+  return true;
+}
+static bool ParseFromString(const std::string &name, std::string *args, std::vector<int> *v) {
+  std::string s;
+  if (!take(name, args, &s)) return false;
+  v->clear();
+  std::stringstream ss(s);
+  std::string tok;
+  while (std::getline(ss, tok, ':')) v->push_back(std::stoi(tok));
+  return true;
+}
+
+// ---- text I/O helpers (Kaldi text-mode token stream) ----
+static void WriteToken(std::ostream &os, const char *t) { os << t << ' '; }
+static void ExpectToken(std::istream &is, const char *t) {
+  std::string s;
+  is >> s;
+  if (s != t) throw std::runtime_error(std::string("Expected token ") + t + ", got " + s);
+}
+static void WriteVec(std::ostream &os, const std::vector<float> &v) {
+  os << " [ ";
+  for (float x : v) os << std::setprecision(9) << x << ' ';
+  os << "]\n";
+}
+static std::vector<float> ReadVec(std::istream &is) {
+  std::string s;
+  is >> s;
+  if (s != "[") throw std::runtime_error("Expected [ , got " + s);
+  std::vector<float> v;
+  while (is >> s && s != "]") v.push_back(std::stof(s));
+  return v;
+}
+static std::vector<float> d2h(const float *d, long n) {
+  std::vector<float> h((size_t)n);
+  if (n) {
+    KCTC_HIP_CHECK(hipMemcpyAsync(h.data(), d, sizeof(float) * n, hipMemcpyDeviceToHost, S()));
+    KCTC_HIP_CHECK(hipStreamSynchronize(S()));
+  }
+  return h;
+}
+static void h2d(float *d, const float *h, long n) {
+  if (!n) return;
+  KCTC_HIP_CHECK(hipMemcpyAsync(d, h, sizeof(float) * n, hipMemcpyHostToDevice, S()));
+  KCTC_HIP_CHECK(hipStreamSynchronize(S()));
+}
+
+std::string Component::Info() const {
+  std::ostringstream os;
+  os << Type() << ", input-dim=" << InputDim() << ", output-dim=" << OutputDim();
+  return os.str();
+}
+
+Component *Component::NewComponentOfType(const std::string &type) {
+  if (type == "SpliceComponent") return new SpliceComponent;
+  if (type == "CuDNNRecurrentComponent") return new CuDNNRecurrentComponent;
+  if (type == "ClipGradientComponent") return new ClipGradientComponent;
+  if (type == "AffineComponent") return new AffineComponent;
+  return nullptr;
+}
+
+// ---------------------------------------------------------------------------
+// SpliceComponent (nnet-component.cc:2517-2760), context {0} on this path
+// ---------------------------------------------------------------------------
+void SpliceComponent::InitFromString(std::string args, Rng &) {
+  const std::string orig = args;
+  int left = 0, right = 0, cdim = 0;
+  bool in_ok = ParseFromString("input-dim", &args, &input_dim_);
+  bool ctx_ok = ParseFromString("context", &args, &context_);
+  bool lr_ok = ParseFromString("left-context", &args, &left) &&
+               ParseFromString("right-context", &args, &right);
+  ParseFromString("const-component-dim", &args, &cdim);
+  if (!(in_ok && (ctx_ok || lr_ok)) || !args.empty() || input_dim_ <= 0)
+    throw std::invalid_argument("Invalid initializer for layer of type SpliceComponent: \"" + orig + "\"");
+  if (lr_ok) {
+    context_.clear();
+    for (int i = -left; i <= right; i++) context_.push_back(i);
+  }
+  if (context_ != std::vector<int>{0} || cdim != 0)
+    throw std::invalid_argument("SpliceComponent: only context=0 (the CTC recipe's splice) is "
+                                "supported on this path");
+}
+void SpliceComponent::Propagate(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &in,
+                                CuMatrixBase *out) const {
+  if (out->Data() != in.Data())
+    KCTC_HIP_CHECK(hipMemcpyAsync(out->Data(), in.Data(), sizeof(float) * in.NumRows() * in.NumCols(),
+                                  hipMemcpyDeviceToDevice, S()));
+}
+void SpliceComponent::Backprop(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &,
+                               const CuMatrixBase &, const CuMatrixBase &out_deriv, Component *,
+                               CuMatrixBase *in_deriv) const {
+  if (in_deriv && in_deriv->Data() != out_deriv.Data())
+    KCTC_HIP_CHECK(hipMemcpyAsync(in_deriv->Data(), out_deriv.Data(),
+                                  sizeof(float) * out_deriv.NumRows() * out_deriv.NumCols(),
+                                  hipMemcpyDeviceToDevice, S()));
+}
+void SpliceComponent::Write(std::ostream &os) const {
+  WriteToken(os, "<SpliceComponent>");
+  WriteToken(os, "<InputDim>");
+  os << input_dim_ << ' ';
+  WriteToken(os, "<Context>");
+  os << "[ ";
+  for (int c : context_) os << c << ' ';
+  os << "] ";
+  WriteToken(os, "<ConstComponentDim>");
+  os << 0 << ' ';
+  WriteToken(os, "</SpliceComponent>");
+}
+void SpliceComponent::Read(std::istream &is) {
+  ExpectToken(is, "<InputDim>");
+  is >> input_dim_;
+  ExpectToken(is, "<Context>");
+  std::string s;
+  is >> s;
+  context_.clear();
+  while (is >> s && s != "]") context_.push_back(std::stoi(s));
+  ExpectToken(is, "<ConstComponentDim>");
+  int c;
+  is >> c;
+  ExpectToken(is, "</SpliceComponent>");
+}
+
+// ---------------------------------------------------------------------------
+// CuDNNRecurrentComponent (nnet-cudnn-component.cc:56-772)
+// ---------------------------------------------------------------------------
+CuDNNRecurrentComponent::CuDNNRecurrentComponent() {
+  desc_.mode = kLstm;
+  desc_.dirs = 2;
+  KCTC_HIP_CHECK(hipMalloc(&err_, 256));
+  KCTC_HIP_CHECK(hipMemset(err_, 0, 256));
+}
+CuDNNRecurrentComponent::~CuDNNRecurrentComponent() {
+  if (err_) (void)hipFree(err_);
+}
+
+void CuDNNRecurrentComponent::InitFromString(std::string args, Rng &rng) {
+  const std::string orig = args;
+  bool ok = true, bidir = true;
+  int layers = 0, D = 0, H = 0, mode = 2, mb = 0;
+  ok = ok && ParseFromString("learning-rate", &args, &learning_rate_);
+  ok = ok && ParseFromString("num-layers", &args, &layers);
+  ok = ok && ParseFromString("input-dim", &args, &D);
+  ok = ok && ParseFromString("output-dim", &args, &H);
+  ok = ok && ParseFromString("rnn-mode", &args, &mode);
+  ok = ok && ParseFromString("bidirectional", &args, &bidir);
+  ok = ok && ParseFromString("max-seq-length", &args, &max_seq_length_);
+  ParseFromString("param-stddev", &args, &param_stddev_);
+  ParseFromString("bias-stddev", &args, &bias_stddev_);
+  ParseFromString("clip-gradient", &args, &clip_gradient_);
+  ParseFromString("mini-batch", &args, &mb);
+  if (!ok) throw std::invalid_argument("Bad initializer " + orig);
+  if (mode < 0 || mode > 3)
+    throw std::invalid_argument("rnn_mode_ = " + std::to_string(mode) + ", should in [0, 1, 2, 3].");
+  desc_.mode = mode;
+  desc_.D = D;
+  desc_.H = H;
+  desc_.layers = layers;
+  desc_.dirs = bidir ? 2 : 1;
+  Init(rng);
+}
+
+// weights: every lin-layer matrix ~ N(0, param_stddev^2), every bias vector =
+// bias_stddev (SetRandn then Set, nnet-cudnn-component.cc:336-407)
+void CuDNNRecurrentComponent::Init(Rng &rng) {
+  const long P = desc_.params_size();
+  std::vector<float> h((size_t)P, 0.f);
+  const int nlin = 2 * desc_.nw();
+  for (int pl = 0; pl < desc_.layers * desc_.dirs; pl++) {
+    for (int lin = 0; lin < nlin; lin++) {
+      const long off = desc_.lin_offset(pl, lin, false);
+      const long n = (long)desc_.H * (lin < desc_.nw() ? desc_.din(pl / desc_.dirs) : desc_.H);
+      for (long i = 0; i < n; i++) h[off + i] = (float)(rng.gauss() * param_stddev_);
+      const long bo = desc_.lin_offset(pl, lin, true);
+      for (long i = 0; i < desc_.H; i++) h[bo + i] = bias_stddev_;
+    }
+  }
+  params_.ensure(sizeof(float) * P);
+  grad_.ensure(sizeof(float) * P);
+  h2d(params_.f(), h.data(), P);
+}
+
+std::string CuDNNRecurrentComponent::Info() const {
+  std::ostringstream os;
+  os << Type() << ", input-dim=" << desc_.D << ", output-dim=" << OutputDim()
+     << ", learning-rate=" << learning_rate_ << ", hidden-dim=" << desc_.H
+     << ", num-layers=" << desc_.layers << ", max-seq-length=" << max_seq_length_
+     << ", rnn-mode=" << desc_.mode << (desc_.dirs == 2 ? ", BIDIRECTIONAL" : ", UNIDIRECTIONAL");
+  return os.str();
+}
+
+void CuDNNRecurrentComponent::Propagate(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &in,
+                                        CuMatrixBase *out) const {
+  // seq_length = rows / mini_batch, no masking (nnet-cudnn-component.cc:521-555)
+  const int N = mini_batch_ > 0 ? mini_batch_ : 1;
+  const int T = (int)(in.NumRows() / N);
+  if (in.NumCols() != desc_.D || in.NumRows() % N)
+    throw std::invalid_argument("CuDNNRecurrentComponent::Propagate: bad input shape");
+  seq_length_ = T;
+  reserve_.ensure(sizeof(float) * rnn_reserve_layout(desc_, T, N).total);
+  workspace_.ensure(rnn_workspace_bytes(desc_, T, N));
+  ProfScope ps("layer_rnn_forward");
+  int st = rnn_forward_training(desc_, S(), T, N, in.Data(), params_.f(), out->Data(), workspace_.p,
+                                workspace_.bytes, reserve_.p, reserve_.bytes, err_);
+  if (st) throw std::runtime_error("rnn_forward_training failed: " + std::to_string(st));
+}
+
+void CuDNNRecurrentComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
+                                       const CuMatrixBase &in_value, const CuMatrixBase &out_value,
+                                       const CuMatrixBase &out_deriv, Component *to_update_in,
+                                       CuMatrixBase *in_deriv) const {
+  const int N = mini_batch_, T = seq_length_;
+  {
+    ProfScope ps("layer_rnn_backward_data");
+    int st = rnn_backward_data(desc_, S(), T, N, out_value.Data(), out_deriv.Data(), params_.f(),
+                               in_deriv ? in_deriv->Data() : nullptr, workspace_.p, workspace_.bytes,
+                               reserve_.p, reserve_.bytes, err_);
+    if (st) throw std::runtime_error("rnn_backward_data failed: " + std::to_string(st));
+  }
+  if (to_update_in) {
+    auto *to_update = dynamic_cast<CuDNNRecurrentComponent *>(to_update_in);
+    if (!to_update) throw std::invalid_argument("CuDNNRecurrentComponent: bad to_update");
+    // filter_params_grad_ is zeroed, then cudnnRNNBackwardWeights accumulates
+    KCTC_HIP_CHECK(hipMemsetAsync(to_update->grad_.p, 0, sizeof(float) * NumParameters(), S()));
+    ProfScope ps("layer_rnn_backward_weights");
+    int st = rnn_backward_weights(desc_, S(), T, N, in_value.Data(), out_value.Data(), workspace_.p,
+                                  workspace_.bytes, to_update->grad_.f(), reserve_.p, reserve_.bytes);
+    if (st) throw std::runtime_error("rnn_backward_weights failed: " + std::to_string(st));
+  }
+}
+
+void CuDNNRecurrentComponent::ApplyUpdate() {
+  // ApplyFloor(-clip) / ApplyCeiling(clip) then filter_params_ += lr * grad
+  clip_sgd_update(S(), params_.f(), grad_.f(), NumParameters(), learning_rate_, clip_gradient_);
+}
+
+void CuDNNRecurrentComponent::Vectorize(float *host) const {
+  auto v = d2h(params_.f(), NumParameters());
+  std::copy(v.begin(), v.end(), host);
+}
+void CuDNNRecurrentComponent::UnVectorize(const float *host) { h2d(params_.f(), host, NumParameters()); }
+
+void CuDNNRecurrentComponent::Write(std::ostream &os) const {
+  WriteToken(os, "<CuDNNRecurrentComponent>");
+  WriteToken(os, "<LearningRate>"); os << learning_rate_ << ' ';
+  WriteToken(os, "<IsGradient>"); os << (is_gradient_ ? "T" : "F") << ' ';
+  WriteToken(os, "<ClipGradient>"); os << clip_gradient_ << ' ';
+  WriteToken(os, "<InputDim>"); os << desc_.D << ' ';
+  WriteToken(os, "<HiddenDim>"); os << desc_.H << ' ';
+  WriteToken(os, "<NumLayers>"); os << desc_.layers << ' ';
+  WriteToken(os, "<Bidirectional>"); os << (desc_.dirs == 2 ? "T" : "F") << ' ';
+  WriteToken(os, "<RNNMode>"); os << desc_.mode << ' ';
+  WriteToken(os, "<MaxSeqLength>"); os << max_seq_length_ << ' ';
+  WriteToken(os, "<FilterParams>");
+  WriteVec(os, d2h(params_.f(), NumParameters()));
+  WriteToken(os, "</CuDNNRecurrentComponent>");
+}
+void CuDNNRecurrentComponent::Read(std::istream &is) {
+  std::string b;
+  ExpectToken(is, "<LearningRate>"); is >> learning_rate_;
+  ExpectToken(is, "<IsGradient>"); is >> b; is_gradient_ = (b == "T" || b == "1");
+  ExpectToken(is, "<ClipGradient>"); is >> clip_gradient_;
+  ExpectToken(is, "<InputDim>"); is >> desc_.D;
+  ExpectToken(is, "<HiddenDim>"); is >> desc_.H;
+  ExpectToken(is, "<NumLayers>"); is >> desc_.layers;
+  ExpectToken(is, "<Bidirectional>"); is >> b; desc_.dirs = (b == "T" || b == "1") ? 2 : 1;
+  ExpectToken(is, "<RNNMode>"); is >> desc_.mode;
+  ExpectToken(is, "<MaxSeqLength>"); is >> max_seq_length_;
+  ExpectToken(is, "<FilterParams>");
+  auto v = ReadVec(is);
+  if ((long)v.size() != desc_.params_size())
+    throw std::runtime_error("CuDNNRecurrentComponent: FilterParams size mismatch");
+  params_.ensure(sizeof(float) * v.size());
+  grad_.ensure(sizeof(float) * v.size());
+  h2d(params_.f(), v.data(), (long)v.size());
+  ExpectToken(is, "</CuDNNRecurrentComponent>");
+}
+
+// ---------------------------------------------------------------------------
+// ClipGradientComponent (nnet-cudnn-component.cc:775-1075)
+// ---------------------------------------------------------------------------
+ClipGradientComponent::ClipGradientComponent() {
+  KCTC_HIP_CHECK(hipMalloc(&dev_, sizeof(ClipState)));
+  KCTC_HIP_CHECK(hipMemset(dev_, 0, sizeof(ClipState)));
+}
+ClipGradientComponent::~ClipGradientComponent() {
+  if (dev_) (void)hipFree(dev_);
+}
+
+void ClipGradientComponent::InitFromString(std::string args, Rng &) {
+  const std::string orig = args;
+  bool ok = ParseFromString("dim", &args, &dim_);
+  clipping_threshold_ = 15.0f;
+  norm_based_clipping_ = false;
+  self_repair_clipped_proportion_threshold_ = 0.01f;
+  self_repair_target_ = 0.0f;
+  self_repair_scale_ = 1.0f;
+  ParseFromString("clipping-threshold", &args, &clipping_threshold_);
+  ParseFromString("norm-based-clipping", &args, &norm_based_clipping_);
+  ParseFromString("self-repair-clipped-proportion-threshold", &args,
+                  &self_repair_clipped_proportion_threshold_);
+  ParseFromString("self-repair-target", &args, &self_repair_target_);
+  ParseFromString("self-repair-scale", &args, &self_repair_scale_);
+  if (!ok || !args.empty() || clipping_threshold_ < 0 || dim_ <= 0 ||
+      self_repair_clipped_proportion_threshold_ < 0 || self_repair_target_ < 0 ||
+      self_repair_scale_ < 0)
+    throw std::invalid_argument("Invalid initializer for layer of type ClipGradientComponent: \"" +
+                                orig + "\"");
+  ZeroStats();
+}
+
+std::string ClipGradientComponent::Info() const {
+  SyncStats();
+  std::ostringstream os;
+  os << Type() << ", dim=" << dim_ << ", norm-based-clipping=" << (norm_based_clipping_ ? "true" : "false")
+     << ", clipping-threshold=" << clipping_threshold_
+     << ", clipped-proportion=" << (count_ > 0 ? num_clipped_ / count_ : 0.0);
+  if (self_repair_scale_ != 0.0f)
+    os << ", self-repair-clipped-proportion-threshold=" << self_repair_clipped_proportion_threshold_
+       << ", self-repair-target=" << self_repair_target_ << ", self-repair-scale=" << self_repair_scale_;
+  return os.str();
+}
+
+void ClipGradientComponent::Propagate(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &in,
+                                      CuMatrixBase *out) const {
+  if (out->Data() != in.Data())
+    KCTC_HIP_CHECK(hipMemcpyAsync(out->Data(), in.Data(), sizeof(float) * in.NumRows() * in.NumCols(),
+                                  hipMemcpyDeviceToDevice, S()));
+}
+
+void ClipGradientComponent::Backprop(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &in_value,
+                                     const CuMatrixBase &, const CuMatrixBase &out_deriv,
+                                     Component *to_update_in, CuMatrixBase *in_deriv) const {
+  if (!in_deriv) return;
+  if (in_deriv->Data() != out_deriv.Data())
+    KCTC_HIP_CHECK(hipMemcpyAsync(in_deriv->Data(), out_deriv.Data(),
+                                  sizeof(float) * out_deriv.NumRows() * out_deriv.NumCols(),
+                                  hipMemcpyDeviceToDevice, S()));
+  auto *to_update = dynamic_cast<ClipGradientComponent *>(to_update_in);
+  if (!(clipping_threshold_ > 0)) return;
+  const long rows = in_deriv->NumRows();
+  // RepairGradients' host-side gate, in the reference's short-circuit order
+  // (:988-991): the RandUniform() draw is consumed only when the preceding
+  // conditions pass.  count_ includes this minibatch when norm-based.
+  bool try_repair = false;
+  if (to_update) {
+    to_update->num_backpropped_ += 1;
+    const double count_after = count_ + (norm_based_clipping_ ? rows : 0);
+    if (!(self_repair_clipped_proportion_threshold_ >= 1.0f || self_repair_scale_ == 0.0f ||
+          count_after == 0))
+      try_repair = !(next_draw_ > 0.5f);
+    if (norm_based_clipping_) to_update->count_ += rows;
+  }
+  ProfScope ps("clip_gradient");
+  scratch_.ensure(clipgrad_scratch_bytes(rows));
+  clipgrad_backprop(S(), in_deriv->Data(), in_value.Data(), rows, dim_, clipping_threshold_,
+                    norm_based_clipping_, try_repair, self_repair_clipped_proportion_threshold_,
+                    self_repair_target_, self_repair_scale_, (to_update ? to_update : this)->dev_,
+                    scratch_.p);
+}
+
+void ClipGradientComponent::SyncStats() const {
+  ClipState h;
+  KCTC_HIP_CHECK(hipMemcpyAsync(&h, dev_, sizeof(h), hipMemcpyDeviceToHost, S()));
+  KCTC_HIP_CHECK(hipStreamSynchronize(S()));
+  num_clipped_ = h.num_clipped;
+  count_ = h.count;
+  num_self_repaired_ = h.num_self_repaired;
+}
+
+void ClipGradientComponent::ZeroStats() {
+  KCTC_HIP_CHECK(hipMemsetAsync(dev_, 0, sizeof(ClipState), S()));
+  num_clipped_ = count_ = num_self_repaired_ = num_backpropped_ = 0;
+}
+
+void ClipGradientComponent::Write(std::ostream &os) const {
+  SyncStats();
+  WriteToken(os, "<ClipGradientComponent>");
+  WriteToken(os, "<Dim>"); os << dim_ << ' ';
+  WriteToken(os, "<ClippingThreshold>"); os << clipping_threshold_ << ' ';
+  WriteToken(os, "<NormBasedClipping>"); os << (norm_based_clipping_ ? "T" : "F") << ' ';
+  WriteToken(os, "<SelfRepairClippedProportionThreshold>");
+  os << self_repair_clipped_proportion_threshold_ << ' ';
+  WriteToken(os, "<SelfRepairTarget>"); os << self_repair_target_ << ' ';
+  WriteToken(os, "<SelfRepairScale>"); os << self_repair_scale_ << ' ';
+  WriteToken(os, "<NumElementsClipped>"); os << num_clipped_ << ' ';
+  WriteToken(os, "<NumElementsProcessed>"); os << count_ << ' ';
+  WriteToken(os, "<NumSelfRepaired>"); os << num_self_repaired_ << ' ';
+  WriteToken(os, "<NumBackpropped>"); os << num_backpropped_ << ' ';
+  WriteToken(os, "</ClipGradientComponent>");
+}
+void ClipGradientComponent::Read(std::istream &is) {
+  std::string b;
+  ExpectToken(is, "<Dim>"); is >> dim_;
+  ExpectToken(is, "<ClippingThreshold>"); is >> clipping_threshold_;
+  ExpectToken(is, "<NormBasedClipping>"); is >> b; norm_based_clipping_ = (b == "T" || b == "1");
+  is >> b;
+  if (b == "<SelfRepairClippedProportionThreshold>") {
+    is >> self_repair_clipped_proportion_threshold_;
+    ExpectToken(is, "<SelfRepairTarget>"); is >> self_repair_target_;
+    ExpectToken(is, "<SelfRepairScale>"); is >> self_repair_scale_;
+    ExpectToken(is, "<NumElementsClipped>");
+  } else {
+    self_repair_clipped_proportion_threshold_ = 1.0f;
+    self_repair_target_ = 0.0f;
+    self_repair_scale_ = 0.0f;
+    if (b != "<NumElementsClipped>") throw std::runtime_error("ClipGradientComponent: bad token " + b);
+  }
+  is >> num_clipped_;
+  ExpectToken(is, "<NumElementsProcessed>"); is >> count_;
+  is >> b;
+  if (b == "<NumSelfRepaired>") {
+    is >> num_self_repaired_;
+    ExpectToken(is, "<NumBackpropped>"); is >> num_backpropped_;
+    ExpectToken(is, "</ClipGradientComponent>");
+  } else {
+    num_self_repaired_ = num_backpropped_ = 0;
+  }
+  ClipState h{};
+  h.num_clipped = num_clipped_;
+  h.count = count_;
+  h.num_self_repaired = num_self_repaired_;
+  KCTC_HIP_CHECK(hipMemcpy(dev_, &h, sizeof(h), hipMemcpyHostToDevice));
+}
+
+// ---------------------------------------------------------------------------
+// AffineComponent (nnet-component.cc:1125-1274)
+// ---------------------------------------------------------------------------
+void AffineComponent::InitFromString(std::string args, Rng &rng) {
+  const std::string orig = args;
+  bool ok = true;
+  ParseFromString("learning-rate", &args, &learning_rate_);
+  ok = ok && ParseFromString("input-dim", &args, &in_dim_);
+  ok = ok && ParseFromString("output-dim", &args, &out_dim_);
+  if (!ok || in_dim_ <= 0 || out_dim_ <= 0) throw std::invalid_argument("Bad initializer " + orig);
+  float param_stddev = 1.0f / std::sqrt((float)in_dim_), bias_stddev = 1.0f;
+  ParseFromString("param-stddev", &args, &param_stddev);
+  ParseFromString("bias-stddev", &args, &bias_stddev);
+  if (!args.empty()) throw std::invalid_argument("Could not process these elements in initializer: " + args);
+  std::vector<float> h((size_t)NumParameters());
+  for (long i = 0; i < (long)in_dim_ * out_dim_; i++) h[i] = (float)(rng.gauss() * param_stddev);
+  for (int i = 0; i < out_dim_; i++) h[(long)in_dim_ * out_dim_ + i] = (float)(rng.gauss() * bias_stddev);
+  params_.ensure(sizeof(float) * h.size());
+  grad_.ensure(sizeof(float) * h.size());
+  h2d(params_.f(), h.data(), (long)h.size());
+}
+
+std::string AffineComponent::Info() const {
+  std::ostringstream os;
+  os << Type() << ", input-dim=" << in_dim_ << ", output-dim=" << out_dim_
+     << ", learning-rate=" << learning_rate_;
+  return os.str();
+}
+
+void AffineComponent::Propagate(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &in,
+                                CuMatrixBase *out) const {
+  // out = 1 b^T + in W^T (CopyRowsFromVec + AddMatMat, :1184-1196), fused bias
+  ProfScope ps("affine");
+  GemmArgs g;
+  g.transA = false; g.transB = true;
+  g.M = (int)in.NumRows(); g.N = out_dim_; g.K = in_dim_;
+  g.A = in.Data(); g.lda = in_dim_;
+  g.B = params_.f(); g.ldb = in_dim_;
+  g.C = out->Data(); g.ldc = out_dim_;
+  g.bias = params_.f() + (long)in_dim_ * out_dim_;
+  gemm_f32(S(), g);
+}
+
+void AffineComponent::Backprop(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &in_value,
+                               const CuMatrixBase &, const CuMatrixBase &out_deriv,
+                               Component *to_update_in, CuMatrixBase *in_deriv) const {
+  ProfScope ps("affine");
+  const long rows = out_deriv.NumRows();
+  if (in_deriv) {  // in_deriv = out_deriv W
+    GemmArgs g;
+    g.M = (int)rows; g.N = in_dim_; g.K = out_dim_;
+    g.A = out_deriv.Data(); g.lda = out_dim_;
+    g.B = params_.f(); g.ldb = in_dim_;
+    g.C = in_deriv->Data(); g.ldc = in_dim_;
+    gemm_f32(S(), g);
+  }
+  if (to_update_in) {
+    auto *to_update = dynamic_cast<AffineComponent *>(to_update_in);
+    if (!to_update) throw std::invalid_argument("AffineComponent: bad to_update");
+    // UpdateSimple (:1190-1195): grad_W = out_deriv^T in_value, grad_b = row sum
+    GemmArgs g;
+    g.transA = true;
+    g.M = out_dim_; g.N = in_dim_; g.K = (int)rows;
+    g.A = out_deriv.Data(); g.lda = out_dim_;
+    g.B = in_value.Data(); g.ldb = in_dim_;
+    g.C = to_update->grad_.f(); g.ldc = in_dim_;
+    g.split_k = gemm_pick_split(g.M, g.N, g.K, 1);
+    const size_t wsf = (size_t)g.split_k * g.M * g.N + sum_rows_ws_floats(rows, out_dim_);
+    ws_.ensure(sizeof(float) * wsf);
+    g.ws = ws_.f();
+    gemm_f32(S(), g);
+    sum_rows(S(), out_deriv.Data(), rows, out_dim_, 1.f, 0.f,
+             to_update->grad_.f() + (long)in_dim_ * out_dim_, ws_.f() + (size_t)g.split_k * g.M * g.N);
+  }
+}
+
+void AffineComponent::ApplyUpdate() {
+  clip_sgd_update(S(), params_.f(), grad_.f(), NumParameters(), learning_rate_, 0.f);
+}
+void AffineComponent::Vectorize(float *host) const {
+  auto v = d2h(params_.f(), NumParameters());
+  std::copy(v.begin(), v.end(), host);
+}
+void AffineComponent::UnVectorize(const float *host) { h2d(params_.f(), host, NumParameters()); }
+
+void AffineComponent::Write(std::ostream &os) const {
+  auto v = d2h(params_.f(), NumParameters());
+  WriteToken(os, "<AffineComponent>");
+  WriteToken(os, "<LearningRate>"); os << learning_rate_ << ' ';
+  WriteToken(os, "<LinearParams>");
+  os << " [\n";
+  for (int r = 0; r < out_dim_; r++) {
+    os << "  ";
+    for (int c = 0; c < in_dim_; c++) os << std::setprecision(9) << v[(size_t)r * in_dim_ + c] << ' ';
+    os << (r + 1 == out_dim_ ? "]\n" : "\n");
+  }
+  WriteToken(os, "<BiasParams>");
+  WriteVec(os, std::vector<float>(v.begin() + (long)in_dim_ * out_dim_, v.end()));
+  WriteToken(os, "<IsGradient>"); os << "F ";
+  WriteToken(os, "</AffineComponent>");
+}
+void AffineComponent::Read(std::istream &is) {
+  ExpectToken(is, "<LearningRate>"); is >> learning_rate_;
+  ExpectToken(is, "<LinearParams>");
+  std::string s;
+  is >> s;
+  if (s != "[") throw std::runtime_error("AffineComponent: expected [");
+  std::vector<float> lin;
+  std::vector<int> row_len;
+  // rows are newline separated; count columns from the first line
+  std::string line;
+  std::getline(is, line);
+  while (std::getline(is, line)) {
+    std::istringstream ls(line);
+    int n = 0;
+    bool end = false;
+    while (ls >> s) {
+      if (s == "]") { end = true; break; }
+      lin.push_back(std::stof(s));
+      n++;
+    }
+    if (n) row_len.push_back(n);
+    if (end) break;
+  }
+  if (row_len.empty()) throw std::runtime_error("AffineComponent: empty LinearParams");
+  out_dim_ = (int)row_len.size();
+  in_dim_ = row_len[0];
+  ExpectToken(is, "<BiasParams>");
+  auto b = ReadVec(is);
+  if ((int)b.size() != out_dim_) throw std::runtime_error("AffineComponent: bias size mismatch");
+  is >> s;
+  if (s == "<IsGradient>") { is >> s; ExpectToken(is, "</AffineComponent>"); }
+  lin.insert(lin.end(), b.begin(), b.end());
+  params_.ensure(sizeof(float) * lin.size());
+  grad_.ensure(sizeof(float) * lin.size());
+  h2d(params_.f(), lin.data(), (long)lin.size());
+}
+
+// ---------------------------------------------------------------------------
+// Nnet
+// ---------------------------------------------------------------------------
+Nnet::~Nnet() {
+  for (auto *c : components_) delete c;
+}
+
+void Nnet::Init(const std::string &config, Rng &rng) {
+  std::istringstream is(config);
+  std::string line;
+  while (std::getline(is, line)) {
+    auto hash = line.find('#');
+    if (hash != std::string::npos) line = line.substr(0, hash);
+    auto parts = split_ws(line);
+    if (parts.empty()) continue;
+    Component *c = Component::NewComponentOfType(parts[0]);
+    if (!c) throw std::invalid_argument("Unknown component type " + parts[0] + " (not on the CTC path)");
+    std::string args;
+    for (size_t i = 1; i < parts.size(); i++) args += (i > 1 ? " " : "") + parts[i];
+    c->InitFromString(args, rng);
+    if (!components_.empty() && components_.back()->OutputDim() != c->InputDim()) {
+      delete c;
+      throw std::invalid_argument("dimension mismatch at component " + parts[0]);
+    }
+    components_.push_back(c);
+  }
+  if (components_.empty()) throw std::invalid_argument("empty nnet config");
+}
+
+int Nnet::FirstUpdatableComponent() const {  // nnet-nnet.cc:838-845
+  for (int i = 0; i < NumComponents(); i++)
+    if (components_[i]->IsUpdatable()) return i;
+  return NumComponents();
+}
+
+void Nnet::ZeroStats() {
+  for (auto *c : components_) c->ZeroStats();
+}
+
+void Nnet::SetLearningRate(float lr) {
+  for (auto *c : components_)
+    if (c->IsUpdatable()) static_cast<UpdatableComponent *>(c)->SetLearningRate(lr);
+}
+
+void Nnet::Write(std::ostream &os) const {
+  os << "<Nnet> <NumComponents> " << components_.size() << "\n<Components> ";
+  for (auto *c : components_) {
+    c->Write(os);
+    os << "\n";
+  }
+  os << "</Components> </Nnet>\n";
+}
+
+void Nnet::Read(std::istream &is) {
+  ExpectToken(is, "<Nnet>");
+  ExpectToken(is, "<NumComponents>");
+  int n;
+  is >> n;
+  ExpectToken(is, "<Components>");
+  for (int i = 0; i < n; i++) {
+    std::string t;
+    is >> t;
+    if (t.size() < 3) throw std::runtime_error("bad component token " + t);
+    Component *c = Component::NewComponentOfType(t.substr(1, t.size() - 2));
+    if (!c) throw std::runtime_error("Unknown component " + t);
+    c->Read(is);
+    components_.push_back(c);
+  }
+  ExpectToken(is, "</Components>");
+  ExpectToken(is, "</Nnet>");
+}
+
+// ---------------------------------------------------------------------------
+// NnetCtcUpdater (src/ctc/ctc-nnet-update.cc:76-348)
+// ---------------------------------------------------------------------------
+NnetCtcUpdater::NnetCtcUpdater(Nnet *nnet, bool update) : nnet_(nnet), update_(update) {}
+
+static void set_minibatch(Nnet *nnet, int N) {  // Nnet::SetMiniBatch (nnet-nnet.cc:42-50)
+  for (int c = 0; c < nnet->NumComponents(); c++) {
+    auto *r = dynamic_cast<CuDNNRecurrentComponent *>(&nnet->GetComponent(c));
+    if (r) r->SetMiniBatch(N);
+  }
+}
+
+MinibatchStats NnetCtcUpdater::ComputeForMinibatch(const float *feats, int T_max, int N,
+                                                   const int *num_frames, const int *flat_labels,
+                                                   const int *label_lengths) {
+  const int C = nnet_->NumComponents();
+  if (N <= 0 || T_max <= 0) throw std::invalid_argument("empty minibatch");
+  const long rows = (long)T_max * N;
+  set_minibatch(nnet_, N);
+  forward_data_.resize(C + 1);
+  chunk_info_.resize(C + 1);
+  for (int c = 0; c <= C; c++) {
+    chunk_info_[c].num_chunks = N;
+    chunk_info_[c].chunk_size = T_max;
+    chunk_info_[c].feat_dim = c == 0 ? nnet_->InputDim() : nnet_->GetComponent(c - 1).OutputDim();
+  }
+  forward_data_[0].SetView(const_cast<float *>(feats), rows, nnet_->InputDim());
+  Propagate(T_max, N);
+
+  // ---- ComputeObjfAndDeriv (:171-259) with the warp-ctc ABI ----
+  const CuMatrixBase &out = forward_data_[C];
+  const int A = nnet_->OutputDim();
+  for (int n = 0; n < N; n++)
+    if (label_lengths[n] < 0) throw std::invalid_argument("negative label length");
+  // input_lengths = NumFrames - ignore_frames (left_context + RightContext = 0 here)
+  size_t ws = 0;
+  {
+    ctcOptions o;
+    o.loc = CTC_GPU;
+    o.stream = reinterpret_cast<ctcStream_t>(S());
+    o.blank_label = 0;
+    ctcStatus_t st = get_workspace_size(label_lengths, num_frames, A, N, o, &ws);
+    if (st != CTC_STATUS_SUCCESS)
+      throw std::runtime_error(std::string("get_workspace_size: ") + ctcGetStatusString(st));
+  }
+  ctc_ws_.ensure(ws);
+  costs_dev_.ensure(sizeof(double) * N);
+  ids_dev_.ensure(sizeof(int) * rows);
+  CuMatrix &deriv = deriv_a_;
+  deriv.Resize(rows, A);
+  {
+    ProfScope ps("layer_ctc");
+    ctcStatus_t st = mictc_compute_ctc_loss_async(out.Data(), update_ ? deriv.Data() : nullptr,
+                                                  flat_labels, label_lengths, num_frames, A, N,
+                                                  static_cast<double *>(costs_dev_.p), ctc_ws_.p,
+                                                  reinterpret_cast<ctcStream_t>(S()), 0);
+    if (st != CTC_STATUS_SUCCESS)
+      throw std::runtime_error(std::string("compute_ctc_loss: ") + ctcGetStatusString(st));
+  }
+  {
+    ProfScope ps("argmax");
+    row_argmax(S(), out.Data(), rows, A, static_cast<int *>(ids_dev_.p));  // FindRowMaxId
+  }
+  if (update_) Backprop(T_max, N);
+
+  // ---- the single end-of-step device->host copy: costs, best-path ids ----
+  const size_t need = sizeof(double) * N + sizeof(int) * rows;
+  if (need > pinned_bytes_) {
+    if (pinned_) (void)hipHostFree(pinned_);
+    KCTC_HIP_CHECK(hipHostMalloc((void **)&pinned_, need, hipHostMallocDefault));
+    pinned_bytes_ = need;
+  }
+  double *hcost = reinterpret_cast<double *>(pinned_);
+  int *hids = reinterpret_cast<int *>(reinterpret_cast<char *>(pinned_) + sizeof(double) * N);
+  KCTC_HIP_CHECK(hipMemcpyAsync(hcost, costs_dev_.p, sizeof(double) * N, hipMemcpyDeviceToHost, S()));
+  KCTC_HIP_CHECK(hipMemcpyAsync(hids, ids_dev_.p, sizeof(int) * rows, hipMemcpyDeviceToHost, S()));
+  KCTC_HIP_CHECK(hipStreamSynchronize(S()));
+  CuDevice::Instantiate().Collect();
+  for (int c = 0; c < C; c++) {
+    auto *r = dynamic_cast<CuDNNRecurrentComponent *>(&nnet_->GetComponent(c));
+    if (r) {
+      unsigned e = 0;
+      KCTC_HIP_CHECK(hipMemcpy(&e, r->DeviceError(), sizeof(e), hipMemcpyDeviceToHost));
+      if (e) throw std::runtime_error("recurrence hand-off timed out (device error word set)");
+    }
+  }
+  MinibatchStats st;
+  for (int n = 0; n < N; n++) st.tot_objf += hcost[n];
+  if (!(st.tot_objf == st.tot_objf)) throw std::runtime_error("costs sum is nan");  // :254
+  // ---- ComputeTotAccuracy (:261-317) on the host ----
+  const int blank = 0;
+  long off = 0;
+  double err = 0;
+  std::vector<int> hyp;
+  for (int n = 0; n < N; n++) {
+    const int F = num_frames[n], L = label_lengths[n];
+    hyp.assign((size_t)std::max(F, 0), 0);
+    for (int i = 0; i < F; i++) hyp[i] = hids[(long)i * N + n];
+    int i = 1, j = 1;
+    while (j < F) {
+      if (hyp[j] != hyp[j - 1] && hyp[j] != blank) hyp[i++] = hyp[j];
+      j++;
+    }
+    hyp.resize(F > 0 ? i : 0);
+    // LevenshteinEditDistance, unit costs
+    std::vector<int> prev(hyp.size() + 1), cur(hyp.size() + 1);
+    for (size_t q = 0; q <= hyp.size(); q++) prev[q] = (int)q;
+    for (int a = 1; a <= L; a++) {
+      cur[0] = a;
+      for (size_t b = 1; b <= hyp.size(); b++)
+        cur[b] = std::min({prev[b - 1] + (flat_labels[off + a - 1] != hyp[b - 1]), prev[b] + 1,
+                           cur[b - 1] + 1});
+      std::swap(prev, cur);
+    }
+    err += prev[hyp.size()];
+    st.tot_weight += L;
+    off += L;
+  }
+  st.tot_accuracy = st.tot_weight - err;
+  return st;
+}
+
+void NnetCtcUpdater::Propagate(int T, int N) {  // :136-169
+  const int C = nnet_->NumComponents();
+  for (int c = 0; c < C; c++) {
+    const Component &comp = nnet_->GetComponent(c);
+    const CuMatrixBase &in = forward_data_[c];
+    CuMatrix &out = forward_data_[c + 1];
+    if (comp.IsIdentityForward()) {
+      out.SetView(in.Data(), in.NumRows(), comp.OutputDim());  // alias, no copy
+      continue;
+    }
+    out.Resize((long)T * N, comp.OutputDim());
+    comp.Propagate(chunk_info_[c], chunk_info_[c + 1], in, &out);
+  }
+}
+
+void NnetCtcUpdater::Backprop(int T, int N) {  // :320-348
+  const int C = nnet_->NumComponents();
+  const long rows = (long)T * N;
+  const int A = nnet_->OutputDim();
+  // deriv->Scale(-1) (:323)
+  {
+    ProfScope ps("scale");
+    scale_inplace(S(), deriv_a_.Data(), rows * (long)A, -1.f);
+  }
+  CuMatrix *cur = &deriv_a_, *other = &deriv_b_;
+  const int first = nnet_->FirstUpdatableComponent();
+  int max_dim = A;
+  for (int c = 0; c <= C; c++) max_dim = std::max(max_dim, chunk_info_[c].feat_dim);
+  std::vector<int> updated;
+  for (int c = C - 1; c >= first; c--) {
+    Component &comp = nnet_->GetComponent(c);
+    const CuMatrixBase &in = forward_data_[c], &outv = forward_data_[c + 1];
+    Component *to_update = &comp;
+    const bool need_in_deriv = c > first;
+    CuMatrixBase *in_deriv = nullptr;
+    CuMatrixBase view;
+    if (need_in_deriv) {
+      if (comp.IsIdentityForward()) {
+        view = CuMatrixBase(cur->Data(), rows, comp.InputDim());  // in place
+        in_deriv = &view;
+      } else {
+        other->Resize(rows, std::max(comp.InputDim(), max_dim));
+        view = CuMatrixBase(other->Data(), rows, comp.InputDim());
+        in_deriv = &view;
+      }
+    }
+    if (auto *cg = dynamic_cast<ClipGradientComponent *>(&comp)) {
+      // RandUniform() for RepairGradients, one stream per updater
+      cg->next_draw_ = (float)repair_rng_.uniform();
+    }
+    const CuMatrixBase od(cur->Data(), rows, comp.OutputDim());
+    comp.Backprop(chunk_info_[c], chunk_info_[c + 1], in, outv, od, to_update, in_deriv);
+    if (comp.IsUpdatable()) {
+      auto *u = static_cast<UpdatableComponent *>(&comp);
+      if (exchange_) exchange_->GradReady(c, u->GradData(), u->NumParameters());
+      updated.push_back(c);
+    }
+    if (need_in_deriv && !comp.IsIdentityForward()) std::swap(cur, other);
+  }
+  if (exchange_) exchange_->Finish();
+  for (int c : updated) {
+    ProfScope ps("update");
+    static_cast<UpdatableComponent *>(&nnet_->GetComponent(c))->ApplyUpdate();
+  }
+}
+
+}  // namespace nnet2
+}  // namespace kctc

@@ -1,0 +1,341 @@
+// nnet.h -- MI355X-native mirror of the reference's nnet2 CTC training path.
+//
+// Same class names and method meanings as the reference's nnet2 API
+// (src/nnet2/nnet-component.h:157-348, nnet-cudnn-component.h, nnet-nnet.h,
+// src/ctc/ctc-nnet-update.h), on device buffers and one HIP stream:
+//   Component / UpdatableComponent      Propagate / Backprop / InitFromString /
+//                                       Info / Read / Write / Vectorize ...
+//   SpliceComponent                     context 0 only (the CTC recipe)
+//   CuDNNRecurrentComponent             -> rnn.hip (cuDNN-shaped gfx950 kernels)
+//   ClipGradientComponent               -> elementwise.hip / clipgrad.hip
+//   AffineComponent                     -> gemm.hip
+//   Nnet                                component list, FirstUpdatableComponent
+//   NnetCtcUpdater                      ComputeForMinibatch: forward, warp-ctc ABI
+//                                       (ctc.hip), accuracy, backprop, SGD.
+// Differences from the reference, all semantics-preserving:
+//   * identity components (Splice context 0, ClipGradient forward) alias their
+//     input instead of copying it;
+//   * updates are applied after the whole backprop instead of inside each
+//     component's Backprop; each component's input derivative is computed
+//     before its update in the reference too, so the result is identical
+//      and it leaves room for the RCCL gradient all-reduce;
+//   * the first updatable component's input derivative (discarded by the
+//     reference, FirstUpdatableComponent = 1) is not computed;
+//   * the ~25 host synchronisations per minibatch of the reference (NaN-check
+//     Sum()s, ApplyFloor counts, cost/id copies) become ONE end-of-step copy.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <iosfwd>
+#include <map>
+#include <memory>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "clipgrad.h"
+#include "rnn.h"
+
+namespace kctc {
+namespace nnet2 {
+
+// ---- minimal CuMatrix / ChunkInfo ------------------------------------------
+struct DevBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf &) = delete;
+  DevBuf &operator=(const DevBuf &) = delete;
+  DevBuf(DevBuf &&o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+  DevBuf &operator=(DevBuf &&o) noexcept {
+    std::swap(p, o.p);
+    std::swap(bytes, o.bytes);
+    return *this;
+  }
+  ~DevBuf();
+  void ensure(size_t b);  // grows (no copy), never shrinks
+  float *f() const { return static_cast<float *>(p); }
+};
+
+class CuMatrixBase {
+ public:
+  CuMatrixBase() = default;
+  CuMatrixBase(float *d, long r, int c) : data_(d), rows_(r), cols_(c) {}
+  long NumRows() const { return rows_; }
+  int NumCols() const { return cols_; }
+  int Stride() const { return cols_; }
+  float *Data() const { return data_; }
+
+ protected:
+  float *data_ = nullptr;
+  long rows_ = 0;
+  int cols_ = 0;
+};
+
+class CuMatrix : public CuMatrixBase {
+ public:
+  void Resize(long rows, int cols);  // kSetZero-free: contents undefined
+  void SetView(float *d, long rows, int cols) { data_ = d; rows_ = rows; cols_ = cols; }
+
+ private:
+  DevBuf buf_;
+};
+
+struct ChunkInfo {  // src/nnet2/nnet-component.h:72-146 (contiguous case)
+  int feat_dim = 0, num_chunks = 0, chunk_size = 0;
+  long NumRows() const { return (long)num_chunks * chunk_size; }
+  int NumCols() const { return feat_dim; }
+  int NumChunks() const { return num_chunks; }
+};
+
+// Device/stream context (the role of CuDevice::Instantiate()).
+struct CuDevice {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  // optional per-kernel-family timing (hipEvents on `stream`)
+  bool profiling = false;
+  struct Span { std::string family; hipEvent_t a, b; };
+  std::vector<Span> spans;
+  std::vector<size_t> open;  // indices of spans begun but not ended (LIFO)
+  std::vector<hipEvent_t> pool;
+  std::map<std::string, std::pair<double, int>> prof;  // family -> (ms, launches)
+  void Begin(const char *family);
+  void End();
+  void Collect();  // after a stream sync
+  static CuDevice &Instantiate();
+};
+
+struct Rng {  // splitmix64 + Box-Muller (replaces Kaldi's rand()-based RandGauss)
+  uint64_t s;
+  explicit Rng(uint64_t seed) : s(seed) {}
+  uint64_t next();
+  double uniform();  // (0, 1)
+  double gauss();
+};
+
+// ---- components -------------------------------------------------------------
+class Component {
+ public:
+  virtual ~Component() = default;
+  virtual std::string Type() const = 0;
+  virtual int InputDim() const = 0;
+  virtual int OutputDim() const = 0;
+  virtual void InitFromString(std::string args, Rng &rng) = 0;
+  virtual std::string Info() const;
+  virtual bool IsUpdatable() const { return false; }
+  virtual bool IsIdentityForward() const { return false; }
+  virtual bool BackpropNeedsInput() const { return true; }
+  virtual bool BackpropNeedsOutput() const { return true; }
+  virtual void Propagate(const ChunkInfo &in_info, const ChunkInfo &out_info,
+                         const CuMatrixBase &in, CuMatrixBase *out) const = 0;
+  // in_deriv may alias out_deriv (in-place) or be nullptr (not needed).
+  virtual void Backprop(const ChunkInfo &in_info, const ChunkInfo &out_info,
+                        const CuMatrixBase &in_value, const CuMatrixBase &out_value,
+                        const CuMatrixBase &out_deriv, Component *to_update,
+                        CuMatrixBase *in_deriv) const = 0;
+  virtual void Write(std::ostream &os) const = 0;
+  virtual void Read(std::istream &is) = 0;
+  virtual void ZeroStats() {}
+  static Component *NewComponentOfType(const std::string &type);
+};
+
+class UpdatableComponent : public Component {
+ public:
+  bool IsUpdatable() const override { return true; }
+  float LearningRate() const { return learning_rate_; }
+  void SetLearningRate(float lr) { learning_rate_ = lr; }
+  virtual long NumParameters() const = 0;
+  virtual void Vectorize(float *host) const = 0;      // host copy of all params
+  virtual void UnVectorize(const float *host) = 0;
+  // gradient produced by the last Backprop (device), in Vectorize order
+  virtual float *GradData() = 0;
+  virtual void ApplyUpdate() = 0;  // params += lr * (clipped) grad
+
+ protected:
+  float learning_rate_ = 0.001f;
+};
+
+class SpliceComponent : public Component {
+ public:
+  std::string Type() const override { return "SpliceComponent"; }
+  int InputDim() const override { return input_dim_; }
+  int OutputDim() const override { return input_dim_ * (int)context_.size(); }
+  void InitFromString(std::string args, Rng &rng) override;
+  bool IsIdentityForward() const override { return true; }
+  bool BackpropNeedsInput() const override { return false; }
+  bool BackpropNeedsOutput() const override { return false; }
+  void Propagate(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &in,
+                 CuMatrixBase *out) const override;
+  void Backprop(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &, const CuMatrixBase &,
+                const CuMatrixBase &, Component *, CuMatrixBase *) const override;
+  void Write(std::ostream &os) const override;
+  void Read(std::istream &is) override;
+
+ private:
+  int input_dim_ = 0;
+  std::vector<int> context_{0};
+};
+
+class CuDNNRecurrentComponent : public UpdatableComponent {
+ public:
+  CuDNNRecurrentComponent();
+  ~CuDNNRecurrentComponent() override;
+  std::string Type() const override { return "CuDNNRecurrentComponent"; }
+  int InputDim() const override { return desc_.D; }
+  int OutputDim() const override { return desc_.H * desc_.dirs; }
+  void InitFromString(std::string args, Rng &rng) override;
+  std::string Info() const override;
+  void Propagate(const ChunkInfo &in_info, const ChunkInfo &out_info, const CuMatrixBase &in,
+                 CuMatrixBase *out) const override;
+  void Backprop(const ChunkInfo &in_info, const ChunkInfo &out_info,
+                const CuMatrixBase &in_value, const CuMatrixBase &out_value,
+                const CuMatrixBase &out_deriv, Component *to_update,
+                CuMatrixBase *in_deriv) const override;
+  void Write(std::ostream &os) const override;
+  void Read(std::istream &is) override;
+  long NumParameters() const override { return desc_.params_size(); }
+  void Vectorize(float *host) const override;
+  void UnVectorize(const float *host) override;
+  float *GradData() override { return grad_.f(); }
+  void ApplyUpdate() override;
+  unsigned *DeviceError() const { return err_; }
+  const RnnDesc &Desc() const { return desc_; }
+  void SetMiniBatch(int n) const { mini_batch_ = n; }  // Init(mini_batch) on change
+
+ private:
+  void Init(Rng &rng);
+  RnnDesc desc_;
+  int max_seq_length_ = 2000;
+  float param_stddev_ = 0.02f, bias_stddev_ = 0.2f, clip_gradient_ = 5.0f;
+  bool is_gradient_ = false;
+  DevBuf params_, grad_;
+  mutable DevBuf reserve_, workspace_;
+  mutable int mini_batch_ = 0, seq_length_ = 0;
+  unsigned *err_ = nullptr;
+};
+
+class ClipGradientComponent : public Component {
+ public:
+  ClipGradientComponent();
+  ~ClipGradientComponent() override;
+  std::string Type() const override { return "ClipGradientComponent"; }
+  int InputDim() const override { return dim_; }
+  int OutputDim() const override { return dim_; }
+  void InitFromString(std::string args, Rng &rng) override;
+  std::string Info() const override;
+  bool IsIdentityForward() const override { return true; }
+  bool BackpropNeedsOutput() const override { return false; }
+  void Propagate(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &in,
+                 CuMatrixBase *out) const override;
+  void Backprop(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &in_value,
+                const CuMatrixBase &, const CuMatrixBase &out_deriv, Component *to_update,
+                CuMatrixBase *in_deriv) const override;
+  void Write(std::ostream &os) const override;
+  void Read(std::istream &is) override;
+  void ZeroStats() override;
+  // host view of the device counters (valid after a stream sync)
+  void SyncStats() const;
+  double NumClipped() const { return num_clipped_; }
+  double Count() const { return count_; }
+  // one RandUniform() per Backprop, drawn by the updater (glibc rand() in the reference)
+  mutable float next_draw_ = 1.0f;
+
+
+ private:
+  int dim_ = 0;
+  float clipping_threshold_ = 15.0f;
+  bool norm_based_clipping_ = false;
+  float self_repair_clipped_proportion_threshold_ = 0.01f, self_repair_target_ = 0.0f,
+        self_repair_scale_ = 1.0f;
+  mutable double num_clipped_ = 0, count_ = 0, num_self_repaired_ = 0, num_backpropped_ = 0;
+  ClipState *dev_ = nullptr;
+  mutable DevBuf scratch_;
+};
+
+class AffineComponent : public UpdatableComponent {
+ public:
+  std::string Type() const override { return "AffineComponent"; }
+  int InputDim() const override { return in_dim_; }
+  int OutputDim() const override { return out_dim_; }
+  void InitFromString(std::string args, Rng &rng) override;
+  std::string Info() const override;
+  bool BackpropNeedsOutput() const override { return false; }
+  void Propagate(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &in,
+                 CuMatrixBase *out) const override;
+  void Backprop(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &in_value,
+                const CuMatrixBase &, const CuMatrixBase &out_deriv, Component *to_update,
+                CuMatrixBase *in_deriv) const override;
+  void Write(std::ostream &os) const override;
+  void Read(std::istream &is) override;
+  long NumParameters() const override { return (long)(in_dim_ + 1) * out_dim_; }
+  void Vectorize(float *host) const override;  // linear (row-major) then bias
+  void UnVectorize(const float *host) override;
+  float *GradData() override { return grad_.f(); }
+  void ApplyUpdate() override;
+
+ private:
+  int in_dim_ = 0, out_dim_ = 0;
+  DevBuf params_, grad_;  // [out][in] followed by [out]
+  mutable DevBuf ws_;
+};
+
+// ---- Nnet / updater ---------------------------------------------------------
+class Nnet {
+ public:
+  ~Nnet();
+  void Init(const std::string &config, Rng &rng);
+  int NumComponents() const { return (int)components_.size(); }
+  Component &GetComponent(int c) { return *components_[c]; }
+  const Component &GetComponent(int c) const { return *components_[c]; }
+  int FirstUpdatableComponent() const;
+  int InputDim() const { return components_.front()->InputDim(); }
+  int OutputDim() const { return components_.back()->OutputDim(); }
+  void ZeroStats();
+  void SetLearningRate(float lr);
+  void Write(std::ostream &os) const;
+  void Read(std::istream &is);
+
+ private:
+  std::vector<Component *> components_;
+};
+
+// Data-parallel gradient exchange (RCCL over xGMI); implemented in dp.cpp.
+class GradExchange {
+ public:
+  virtual ~GradExchange() = default;
+  virtual void GradReady(int component, float *grad, long n) = 0;  // on the compute stream
+  virtual void Finish() = 0;  // compute stream waits for every launched all-reduce
+  virtual int WorldSize() const = 0;
+};
+
+struct MinibatchStats {
+  double tot_objf = 0, tot_accuracy = 0, tot_weight = 0;
+};
+
+class NnetCtcUpdater {
+ public:
+  NnetCtcUpdater(Nnet *nnet, bool update);
+  // feats: device [T_max*N][input_dim] (FormatNnetInput layout)
+  MinibatchStats ComputeForMinibatch(const float *feats, int T_max, int N, const int *num_frames,
+                                     const int *flat_labels, const int *label_lengths);
+  void SetExchange(GradExchange *ex) { exchange_ = ex; }
+  void SetRepairRng(uint64_t seed) { repair_rng_ = Rng(seed); }
+
+ private:
+  void Propagate(int T, int N);
+  void Backprop(int T, int N);
+  Nnet *nnet_;
+  bool update_;
+  GradExchange *exchange_ = nullptr;
+  Rng repair_rng_{12345};
+  std::vector<CuMatrix> forward_data_;
+  std::vector<ChunkInfo> chunk_info_;
+  CuMatrix deriv_a_, deriv_b_;
+  DevBuf ctc_ws_, costs_dev_, ids_dev_;
+  float *pinned_ = nullptr;
+  size_t pinned_bytes_ = 0;
+};
+
+}  // namespace nnet2
+}  // namespace kctc

@@ -37,6 +37,7 @@
 #include "common.h"
 #include "elementwise.h"
 #include "gemm.h"
+#include "prof.h"
 #include "rnn.h"
 
 namespace kctc {
@@ -589,7 +590,10 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     g.bias = wl + bW;
     g.bias2 = (d.mode == kGru) ? nullptr : wl + bR;
     g.batch = dirs; g.strideA = 0; g.strideB = pls; g.strideC = (long)NW * H; g.strideBias = pls;
-    gemm_f32(s, g);
+    {
+      ProfSpan ps(s, "gemm_fwd_proj");
+      gemm_f32(s, g);
+    }
     RecParams p{};
     p.T = T; p.N = N; p.H = H; p.dirs = dirs; p.U = U; p.nwg = H / U;
     p.ncol = (NW * U + 15) / 16 * 16; p.Npad = (N + 15) / 16 * 16;
@@ -597,6 +601,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.G = R0 + lay.G; p.y = out; p.aux = R0 + lay.aux; p.err = err;
     const size_t lds = sizeof(float) * ((size_t)p.ncol * (H + 4) + 4 * (size_t)p.Npad * p.ncol);
     const dim3 grid(dirs * p.nwg);
+    ProfSpan ps(s, "rnn_fwd_rec");
     switch (d.mode) {
       case kLstm: set_lds(rnn_fwd_rec<kLstm>, lds);
         hipLaunchKernelGGL(rnn_fwd_rec<kLstm>, grid, dim3(NT), lds, s, p); break;
@@ -648,6 +653,8 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     const size_t lds = sizeof(float) * ((size_t)U * (NW * H + 4) +
                                         std::max(4 * (size_t)p.Npad * 16, (size_t)2 * N * U * NW));
     const dim3 grid(dirs * p.nwg);
+    {
+    ProfSpan ps(s, "rnn_bwd_rec");
     switch (d.mode) {
       case kLstm: set_lds(rnn_bwd_rec<kLstm>, lds);
         hipLaunchKernelGGL(rnn_bwd_rec<kLstm>, grid, dim3(NT), lds, s, p); break;
@@ -657,6 +664,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
         hipLaunchKernelGGL(rnn_bwd_rec<kRelu>, grid, dim3(NT), lds, s, p); break;
       default: set_lds(rnn_bwd_rec<kTanh>, lds);
         hipLaunchKernelGGL(rnn_bwd_rec<kTanh>, grid, dim3(NT), lds, s, p); break;
+    }
     }
     KCTC_HIP_CHECK(hipGetLastError());
     // dx_l = sum_dir DX_dir W_dir   (lower layer's dy, or the caller's dx)
@@ -670,6 +678,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
         g.B = wl + dir * pls; g.ldb = Din;
         g.C = dxl; g.ldc = Din;
         g.beta = dir == 0 ? 0.f : 1.f;
+        ProfSpan ps(s, "gemm_bwd_data");
         gemm_f32(s, g);
       }
     }
@@ -711,7 +720,10 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     g.batch = dirs; g.strideA = G4; g.strideB = 0; g.strideC = pls;
     g.split_k = gemm_pick_split(g.M, g.N, g.K, dirs);
     g.ws = ws;
-    gemm_f32(s, g);
+    {
+      ProfSpan ps(s, "gemm_bwd_w");
+      gemm_f32(s, g);
+    }
     // dR_dir += E_dir(shifted)^T h_prev:  fwd pairs rows t>=1 with y rows t-1,
     // bwd pairs rows t<=T-2 with y rows t+1 (column half H..2H-1)
     if (T > 1) {
@@ -727,6 +739,7 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       r.strideC = pls;
       r.split_k = gemm_pick_split(r.M, r.N, r.K, dirs);
       r.ws = ws;
+      ProfSpan ps(s, "gemm_bwd_r");
       gemm_f32(s, r);
     }
     // biases: dbW += sum dGx, dbR += sum dGh (partials from the recurrence)

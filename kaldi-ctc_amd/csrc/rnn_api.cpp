@@ -12,6 +12,13 @@
 struct krnnContext {
   kctc::RnnDesc desc;
   unsigned *err = nullptr;  // device error word of the persistent kernels
+  unsigned *dev_err() {
+    if (!err) {
+      KCTC_HIP_CHECK(hipMalloc(&err, 256));
+      KCTC_HIP_CHECK(hipMemset(err, 0, 256));
+    }
+    return err;
+  }
 };
 
 
@@ -28,17 +35,13 @@ int krnnCreate(krnnDescriptor_t *desc, int mode, int input_dim, int hidden_dim, 
   c->desc.H = hidden_dim;
   c->desc.layers = num_layers;
   c->desc.dirs = bidirectional ? 2 : 1;
-  if (hipMalloc(&c->err, 256) != hipSuccess || hipMemset(c->err, 0, 256) != hipSuccess) {
-    delete c;
-    return KRNN_STATUS_EXECUTION_FAILED;
-  }
-  *desc = c;
+  *desc = c;  // the device error word is allocated on first use (no GPU needed here)
   return KRNN_STATUS_SUCCESS;
 }
 
 int krnnDestroy(krnnDescriptor_t desc) {
   if (!desc) return KRNN_STATUS_BAD_PARAM;
-  (void)hipFree(desc->err);
+  if (desc->err) (void)hipFree(desc->err);
   delete desc;
   return KRNN_STATUS_SUCCESS;
 }
@@ -92,7 +95,7 @@ int krnnForwardTraining(krnnDescriptor_t desc, struct ihipStream_t *stream, int 
   if (!desc || !x || !w || !y || !reserve) return KRNN_STATUS_BAD_PARAM;
   try {
     return kctc::rnn_forward_training(desc->desc, stream, seq_length, minibatch, x, w, y, workspace,
-                                      workspace_bytes, reserve, reserve_bytes, desc->err);
+                                      workspace_bytes, reserve, reserve_bytes, desc->dev_err());
   } catch (...) {
     return KRNN_STATUS_EXECUTION_FAILED;
   }
@@ -109,7 +112,7 @@ int krnnForwardInference(krnnDescriptor_t desc, struct ihipStream_t *stream, int
   try {
     return kctc::rnn_forward_training(desc->desc, stream, seq_length, minibatch, x, w, y, ws,
                                       scratch, ws + kctc::align_up(scratch, 256),
-                                      workspace_bytes - kctc::align_up(scratch, 256), desc->err);
+                                      workspace_bytes - kctc::align_up(scratch, 256), desc->dev_err());
   } catch (...) {
     return KRNN_STATUS_EXECUTION_FAILED;
   }
@@ -122,7 +125,7 @@ int krnnBackwardData(krnnDescriptor_t desc, struct ihipStream_t *stream, int seq
   if (!desc || !y || !dy || !w || !reserve) return KRNN_STATUS_BAD_PARAM;
   try {
     return kctc::rnn_backward_data(desc->desc, stream, seq_length, minibatch, y, dy, w, dx,
-                                   workspace, workspace_bytes, reserve, reserve_bytes, desc->err);
+                                   workspace, workspace_bytes, reserve, reserve_bytes, desc->dev_err());
   } catch (...) {
     return KRNN_STATUS_EXECUTION_FAILED;
   }
@@ -143,6 +146,7 @@ int krnnBackwardWeights(krnnDescriptor_t desc, struct ihipStream_t *stream, int 
 int krnnGetDeviceStatus(krnnDescriptor_t desc, struct ihipStream_t *stream) {
   if (!desc) return KRNN_STATUS_BAD_PARAM;
   unsigned e = 0;
+  if (!desc->err) return KRNN_STATUS_SUCCESS;
   if (hipMemcpyAsync(&e, desc->err, sizeof(e), hipMemcpyDeviceToHost, stream) != hipSuccess ||
       hipStreamSynchronize(stream) != hipSuccess)
     return KRNN_STATUS_EXECUTION_FAILED;

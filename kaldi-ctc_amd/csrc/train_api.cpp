@@ -1,0 +1,348 @@
+// train_api.cpp -- C ABI of include/kaldi_ctc_train.h: the nnet2 trainer,
+// RCCL data parallelism, FormatNnetInput and the synthetic minibatch generator.
+#include "kaldi_ctc_train.h"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+
+#include "common.h"
+#include "nnet.h"
+
+using kctc::nnet2::CuDevice;
+
+namespace {
+
+thread_local std::string g_err;
+
+// Gradient all-reduce over RCCL on a dedicated stream: each component's
+// gradient bucket is reduced as soon as its Backprop has produced it, while
+// the compute stream goes on with the layers below (overlap); the SGD updates
+// wait for the last bucket.  Sum semantics: the summed gradient of the G
+// per-rank minibatches equals the gradient of their concatenation, then the
+// reference's per-component clip (+-clip-gradient) and SGD run identically
+// on every rank, so replicas stay bit-identical.
+class RcclExchange : public kctc::nnet2::GradExchange {
+ public:
+  RcclExchange(const void *uid, int rank, int world, hipStream_t compute)
+      : world_(world), compute_(compute) {
+    ncclUniqueId id;
+    memcpy(&id, uid, sizeof(id));
+    if (ncclCommInitRank(&comm_, world, id, rank) != ncclSuccess)
+      throw std::runtime_error("ncclCommInitRank failed");
+    KCTC_HIP_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
+    KCTC_HIP_CHECK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
+    KCTC_HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+  }
+  ~RcclExchange() override {
+    (void)hipStreamSynchronize(comm_stream_);
+    ncclCommDestroy(comm_);
+    (void)hipStreamDestroy(comm_stream_);
+    (void)hipEventDestroy(ready_);
+    (void)hipEventDestroy(done_);
+  }
+  void GradReady(int, float *grad, long n) override {
+    KCTC_HIP_CHECK(hipEventRecord(ready_, compute_));
+    KCTC_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ready_, 0));
+    if (ncclAllReduce(grad, grad, (size_t)n, ncclFloat, ncclSum, comm_, comm_stream_) != ncclSuccess)
+      throw std::runtime_error("ncclAllReduce failed");
+  }
+  void Finish() override {
+    KCTC_HIP_CHECK(hipEventRecord(done_, comm_stream_));
+    KCTC_HIP_CHECK(hipStreamWaitEvent(compute_, done_, 0));
+  }
+  int WorldSize() const override { return world_; }
+
+ private:
+  int world_;
+  hipStream_t compute_, comm_stream_ = nullptr;
+  ncclComm_t comm_ = nullptr;
+  hipEvent_t ready_ = nullptr, done_ = nullptr;
+};
+
+}  // namespace
+
+struct kctcNnetImpl {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  kctc::nnet2::Nnet nnet;
+  kctc::nnet2::NnetCtcUpdater trainer{&nnet, true};
+  kctc::nnet2::NnetCtcUpdater evaluator{&nnet, false};
+  RcclExchange *dp = nullptr;
+  ~kctcNnetImpl() {
+    delete dp;
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+  void activate() {
+    KCTC_HIP_CHECK(hipSetDevice(device));
+    CuDevice::Instantiate().device = device;
+    CuDevice::Instantiate().stream = stream;
+  }
+};
+
+template <typename F>
+static int guarded(F f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception &e) {
+    g_err = e.what();
+    return 1;
+  } catch (...) {
+    g_err = "unknown error";
+    return 1;
+  }
+}
+
+static kctc::nnet2::Component &comp(kctcNnet_t n, int c) {
+  if (c < 0 || c >= n->nnet.NumComponents()) throw std::out_of_range("component index");
+  return n->nnet.GetComponent(c);
+}
+static kctc::nnet2::UpdatableComponent &ucomp(kctcNnet_t n, int c) {
+  auto &x = comp(n, c);
+  if (!x.IsUpdatable()) throw std::invalid_argument("component is not updatable");
+  return static_cast<kctc::nnet2::UpdatableComponent &>(x);
+}
+
+extern "C" {
+
+const char *kctc_last_error(void) { return g_err.c_str(); }
+
+int kctc_nnet_create(kctcNnet_t *out, const char *config, unsigned long long seed, int device) {
+  return guarded([&] {
+    auto *n = new kctcNnetImpl;
+    try {
+      n->device = device;
+      KCTC_HIP_CHECK(hipSetDevice(device));
+      KCTC_HIP_CHECK(hipStreamCreateWithFlags(&n->stream, hipStreamNonBlocking));
+      n->activate();
+      kctc::nnet2::Rng rng(seed);
+      n->nnet.Init(config ? config : "", rng);
+      n->trainer.SetRepairRng(seed ^ 0x5DEECE66DULL);
+    } catch (...) {
+      delete n;
+      throw;
+    }
+    *out = n;
+  });
+}
+
+int kctc_nnet_destroy(kctcNnet_t n) {
+  return guarded([&] {
+    if (n) {
+      n->activate();
+      KCTC_HIP_CHECK(hipStreamSynchronize(n->stream));
+    }
+    delete n;
+  });
+}
+
+int kctc_nnet_num_components(kctcNnet_t n) { return n ? n->nnet.NumComponents() : -1; }
+
+int kctc_nnet_component_info(kctcNnet_t n, int c, char *buf, size_t len) {
+  return guarded([&] {
+    n->activate();
+    std::string s = comp(n, c).Info();
+    if (len) {
+      strncpy(buf, s.c_str(), len - 1);
+      buf[len - 1] = 0;
+    }
+  });
+}
+
+long kctc_nnet_num_params(kctcNnet_t n, int c) {
+  if (!n || c < 0 || c >= n->nnet.NumComponents() || !n->nnet.GetComponent(c).IsUpdatable()) return 0;
+  return static_cast<kctc::nnet2::UpdatableComponent &>(n->nnet.GetComponent(c)).NumParameters();
+}
+
+int kctc_nnet_get_params(kctcNnet_t n, int c, float *host, long len) {
+  return guarded([&] {
+    n->activate();
+    auto &u = ucomp(n, c);
+    if (len != u.NumParameters()) throw std::invalid_argument("size mismatch");
+    u.Vectorize(host);
+  });
+}
+
+int kctc_nnet_set_params(kctcNnet_t n, int c, const float *host, long len) {
+  return guarded([&] {
+    n->activate();
+    auto &u = ucomp(n, c);
+    if (len != u.NumParameters()) throw std::invalid_argument("size mismatch");
+    u.UnVectorize(host);
+  });
+}
+
+int kctc_nnet_set_learning_rate(kctcNnet_t n, float lr) {
+  return guarded([&] { n->nnet.SetLearningRate(lr); });
+}
+
+int kctc_nnet_clip_stats(kctcNnet_t n, int c, double *num_clipped, double *count) {
+  return guarded([&] {
+    n->activate();
+    auto *cg = dynamic_cast<kctc::nnet2::ClipGradientComponent *>(&comp(n, c));
+    if (!cg) throw std::invalid_argument("not a ClipGradientComponent");
+    cg->SyncStats();
+    *num_clipped = cg->NumClipped();
+    *count = cg->Count();
+  });
+}
+
+int kctc_nnet_set_repair_seed(kctcNnet_t n, unsigned long long seed) {
+  return guarded([&] { n->trainer.SetRepairRng(seed); });
+}
+
+int kctc_nnet_train_step(kctcNnet_t n, const float *feats_dev, int T_max, int N,
+                         const int *num_frames, const int *flat_labels, const int *label_lengths,
+                         double *tot_objf, double *tot_accuracy, double *tot_weight) {
+  return guarded([&] {
+    n->activate();
+    auto st = n->trainer.ComputeForMinibatch(feats_dev, T_max, N, num_frames, flat_labels,
+                                             label_lengths);
+    if (tot_objf) *tot_objf = st.tot_objf;
+    if (tot_accuracy) *tot_accuracy = st.tot_accuracy;
+    if (tot_weight) *tot_weight = st.tot_weight;
+  });
+}
+
+int kctc_nnet_compute_objf(kctcNnet_t n, const float *feats_dev, int T_max, int N,
+                           const int *num_frames, const int *flat_labels, const int *label_lengths,
+                           double *tot_objf, double *tot_accuracy, double *tot_weight) {
+  return guarded([&] {
+    n->activate();
+    auto st = n->evaluator.ComputeForMinibatch(feats_dev, T_max, N, num_frames, flat_labels,
+                                               label_lengths);
+    if (tot_objf) *tot_objf = st.tot_objf;
+    if (tot_accuracy) *tot_accuracy = st.tot_accuracy;
+    if (tot_weight) *tot_weight = st.tot_weight;
+  });
+}
+
+struct ihipStream_t *kctc_nnet_stream(kctcNnet_t n) { return n ? n->stream : nullptr; }
+
+int kctc_nnet_set_profiling(kctcNnet_t n, int on) {
+  return guarded([&] {
+    n->activate();
+    auto &d = CuDevice::Instantiate();
+    d.profiling = on != 0;
+    d.prof.clear();
+  });
+}
+
+int kctc_nnet_profile(kctcNnet_t n, const char *family, double *ms_total, int *launches) {
+  return guarded([&] {
+    auto &d = CuDevice::Instantiate();
+    auto it = d.prof.find(family ? family : "");
+    *ms_total = it == d.prof.end() ? 0.0 : it->second.first;
+    *launches = it == d.prof.end() ? 0 : it->second.second;
+  });
+}
+
+int kctc_nnet_write(kctcNnet_t n, const char *path) {
+  return guarded([&] {
+    n->activate();
+    std::ofstream os(path);
+    if (!os) throw std::runtime_error(std::string("cannot open ") + path);
+    n->nnet.Write(os);
+  });
+}
+
+int kctc_nnet_read(kctcNnet_t *out, const char *path, int device) {
+  return guarded([&] {
+    auto *n = new kctcNnetImpl;
+    try {
+      n->device = device;
+      KCTC_HIP_CHECK(hipSetDevice(device));
+      KCTC_HIP_CHECK(hipStreamCreateWithFlags(&n->stream, hipStreamNonBlocking));
+      n->activate();
+      std::ifstream is(path);
+      if (!is) throw std::runtime_error(std::string("cannot open ") + path);
+      n->nnet.Read(is);
+    } catch (...) {
+      delete n;
+      throw;
+    }
+    *out = n;
+  });
+}
+
+int kctc_dp_unique_id(void *uid128) {
+  return guarded([&] {
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) throw std::runtime_error("ncclGetUniqueId failed");
+    static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
+    memcpy(uid128, &id, sizeof(id));
+  });
+}
+
+int kctc_nnet_enable_dp(kctcNnet_t n, const void *uid128, int rank, int world_size) {
+  return guarded([&] {
+    n->activate();
+    delete n->dp;
+    n->dp = nullptr;
+    n->trainer.SetExchange(nullptr);
+    if (world_size > 1) {
+      n->dp = new RcclExchange(uid128, rank, world_size, n->stream);
+      n->trainer.SetExchange(n->dp);
+    }
+  });
+}
+
+int kctc_format_input(const float *feats, const int *num_frames, int N, int dim, int T_max,
+                      float *out) {
+  return guarded([&] {
+    // FormatNnetInput (ctc-nnet-update.cc:351-424): row t*N+n, zero padded
+    memset(out, 0, sizeof(float) * (size_t)T_max * N * dim);
+    long off = 0;
+    for (int n = 0; n < N; n++) {
+      if (num_frames[n] > T_max) throw std::invalid_argument("num_frames > T_max");
+      for (int t = 0; t < num_frames[n]; t++)
+        memcpy(out + ((size_t)t * N + n) * dim, feats + (off + t) * (size_t)dim, sizeof(float) * dim);
+      off += num_frames[n];
+    }
+  });
+}
+
+long kctc_synth_minibatch(unsigned long long seed, int T_max, int N, int dim, int A,
+                          double label_ratio, float *feats, int *num_frames, int *flat_labels,
+                          int *label_lengths) {
+  kctc::nnet2::Rng rng(seed);
+  long nl = 0;
+  for (int n = 0; n < N; n++) {
+    int T = n == 0 ? T_max : T_max - (int)std::floor(rng.uniform() * 0.1 * T_max);
+    if (T < 1) T = 1;
+    num_frames[n] = T;
+    long L = (long)std::floor(T * label_ratio);
+    L = std::min<long>(L, 639);
+    L = std::min<long>(L, (T - 1) / 2);
+    L = std::max<long>(L, 0);
+    label_lengths[n] = (int)L;
+    int prev = -1;
+    for (long i = 0; i < L; i++) {
+      int v;
+      do {
+        v = 1 + (int)(rng.next() % (unsigned long long)(A - 1));
+      } while (v == prev && A > 2);
+      flat_labels[nl++] = v;
+      prev = v;
+    }
+  }
+  if (feats) {
+    for (int t = 0; t < T_max; t++)
+      for (int n = 0; n < N; n++) {
+        float *row = feats + ((size_t)t * N + n) * dim;
+        if (t < num_frames[n])
+          for (int j = 0; j < dim; j++) row[j] = (float)rng.gauss();
+        else
+          memset(row, 0, sizeof(float) * dim);
+      }
+  }
+  return nl;
+}
+
+}  // extern "C"

@@ -30,40 +30,40 @@ void FN(oracle_gemm)(int transA, int transB, int M, int N, int K, REAL alpha,
       for (int j = 0; j < N; j++) Bt[(size_t)k * N + j] = B[(size_t)j * ldb + k];
     Br = Bt; ldb2 = N;
   }
-  const int IB = 32, KB = 128, JB = 512;
-  int nib = (M + IB - 1) / IB;
+  /* tasks = (row block, column block) pairs so that the skinny per-step
+   * recurrent GEMMs (M = minibatch) also spread over the threads */
+  const int IB = 32, KB = 128, JB = M < 64 ? 64 : 512;
+  const int nib = (M + IB - 1) / IB, njb = (N + JB - 1) / JB;
 #pragma omp parallel for schedule(dynamic)
-  for (int ib = 0; ib < nib; ib++) {
-    int i0 = ib * IB, i1 = i0 + IB < M ? i0 + IB : M;
-    REAL *acc = (REAL *)malloc(sizeof(REAL) * IB * JB);
-    for (int j0 = 0; j0 < N; j0 += JB) {
-      int j1 = j0 + JB < N ? j0 + JB : N, nj = j1 - j0;
-      for (int i = i0; i < i1; i++)
-        for (int j = 0; j < nj; j++) acc[(i - i0) * JB + j] = 0;
-      for (int k0 = 0; k0 < K; k0 += KB) {
-        int k1 = k0 + KB < K ? k0 + KB : K;
-        for (int i = i0; i < i1; i++) {
-          REAL *ci = acc + (i - i0) * JB;
-          const REAL *ai = Ar + (size_t)i * lda2;
-          for (int k = k0; k < k1; k++) {
-            REAL a = ai[k];
-            const REAL *bk = Br + (size_t)k * ldb2 + j0;
-#pragma omp simd
-            for (int j = 0; j < nj; j++) ci[j] += a * bk[j];
-          }
-        }
-      }
+  for (int task = 0; task < nib * njb; task++) {
+    const int ib = task / njb, jb = task - ib * njb;
+    const int i0 = ib * IB, i1 = i0 + IB < M ? i0 + IB : M;
+    const int j0 = jb * JB, j1 = j0 + JB < N ? j0 + JB : N, nj = j1 - j0;
+    REAL acc[32 * 512];
+    for (int i = i0; i < i1; i++)
+      for (int j = 0; j < nj; j++) acc[(i - i0) * JB + j] = 0;
+    for (int k0 = 0; k0 < K; k0 += KB) {
+      int k1 = k0 + KB < K ? k0 + KB : K;
       for (int i = i0; i < i1; i++) {
-        REAL *ci = C + (size_t)i * ldc + j0;
-        const REAL *ac = acc + (i - i0) * JB;
-        if (beta == 0) {
-          for (int j = 0; j < nj; j++) ci[j] = alpha * ac[j];
-        } else {
-          for (int j = 0; j < nj; j++) ci[j] = alpha * ac[j] + beta * ci[j];
+        REAL *ci = acc + (i - i0) * JB;
+        const REAL *ai = Ar + (size_t)i * lda2;
+        for (int k = k0; k < k1; k++) {
+          REAL a = ai[k];
+          const REAL *bk = Br + (size_t)k * ldb2 + j0;
+#pragma omp simd
+          for (int j = 0; j < nj; j++) ci[j] += a * bk[j];
         }
       }
     }
-    free(acc);
+    for (int i = i0; i < i1; i++) {
+      REAL *ci = C + (size_t)i * ldc + j0;
+      const REAL *ac = acc + (i - i0) * JB;
+      if (beta == 0) {
+        for (int j = 0; j < nj; j++) ci[j] = alpha * ac[j];
+      } else {
+        for (int j = 0; j < nj; j++) ci[j] = alpha * ac[j] + beta * ci[j];
+      }
+    }
   }
   free(At);
   free(Bt);
@@ -182,10 +182,13 @@ static void FN(rnn_layer_fwd)(int mode, int T, int N, int Din, int H, int dirs,
   REAL *G = (REAL *)malloc(sizeof(REAL) * TN * G4);
   REAL *Rh = (REAL *)malloc(sizeof(REAL) * (size_t)N * G4);
   REAL *c = (REAL *)malloc(sizeof(REAL) * (size_t)N * H);
+  REAL *Rt = (REAL *)malloc(sizeof(REAL) * (size_t)H * G4);
   for (int d = 0; d < dirs; d++) {
     int p = layer * dirs + d;
     const REAL *W = params + oracle_rnn_lin_offset(mode, D0, H, layers, dirs, p, 0, 0);
     const REAL *R = params + oracle_rnn_lin_offset(mode, D0, H, layers, dirs, p, nW, 0);
+    for (int j = 0; j < G4; j++)  /* R^T once per direction: the per-step GEMM is then NN */
+      for (int k = 0; k < H; k++) Rt[(size_t)k * G4 + j] = R[(size_t)j * H + k];
     const REAL *bW = params + oracle_rnn_lin_offset(mode, D0, H, layers, dirs, p, 0, 1);
     const REAL *bR = params + oracle_rnn_lin_offset(mode, D0, H, layers, dirs, p, nW, 1);
     FN(oracle_gemm)(0, 1, (int)TN, G4, Din, 1, x, Din, W, Din, 0, G, G4);
@@ -201,7 +204,7 @@ static void FN(rnn_layer_fwd)(int mode, int T, int N, int Din, int H, int dirs,
       } else {
         for (int n = 0; n < N; n++)
           for (int j = 0; j < G4; j++) Rh[n * G4 + j] = bR[j];
-        FN(oracle_gemm)(0, 1, N, G4, H, 1, y + (size_t)tp * N * ldy + d * H, ldy, R, H, 1, Rh, G4);
+        FN(oracle_gemm)(0, 0, N, G4, H, 1, y + (size_t)tp * N * ldy + d * H, ldy, Rt, G4, 1, Rh, G4);
       }
       for (int n = 0; n < N; n++) {
         const REAL *g = G + ((size_t)t * N + n) * G4;
@@ -235,7 +238,7 @@ static void FN(rnn_layer_fwd)(int mode, int T, int N, int Din, int H, int dirs,
       }
     }
   }
-  free(G); free(Rh); free(c);
+  free(G); free(Rh); free(c); free(Rt);
 }
 
 static void FN(rnn_layer_bwd)(int mode, int T, int N, int Din, int H, int dirs,

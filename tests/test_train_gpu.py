@@ -1,0 +1,131 @@
+"""The nnet2 CTC train step (include/kaldi_ctc_train.h) end to end on the GPU
+vs the fp64 oracle (oracle_train_step: NnetCtcUpdater::ComputeForMinibatch
+with the in-place SGD of the reference) and the torch-fp64 cfg0 golden.
+
+Tolerances: objective 1e-5 relative; parameter updates (lr * clipped grad)
+1e-4 relative norm-wise per component (north_star: grads within 1e-4)."""
+import numpy as np
+import pytest
+
+from conftest import golden, rel_err
+
+pytestmark = pytest.mark.gpu
+
+M64 = (1 << 64) - 1
+
+
+def splitmix_uniforms(seed, n):
+    """The trainer's RandUniform() stream (nnet.cpp Rng): splitmix64."""
+    s, out = seed & M64, []
+    for _ in range(n):
+        s = (s + 0x9E3779B97F4A7C15) & M64
+        z = s
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+        z ^= z >> 31
+        out.append(((z >> 11) + 0.5) / 9007199254740992.0)
+    return out
+
+
+def test_train_step_cfg0_golden(kctc, gpu):
+    """configs[0]: 1 x uni-LSTM-256, N=2, T_max=200, D=40, A=41 vs torch fp64."""
+    import torch
+    g = golden("step_cfg0")
+    cfg = kctc.recipe_config(num_rnn=1, input_dim=40, hidden=256, num_targets=41, bidirectional=False,
+                             learning_rate=float(g["lr"]))
+    net = kctc.Nnet(cfg, seed=1)
+    assert net.num_components == 4
+    net.set_params(1, g["w0"])
+    net.set_params(3, np.concatenate([g["Wa0"].ravel(), g["ba0"]]))
+    T, N = int(g["T"]), int(g["N"])
+    feats = torch.from_numpy(g["feats"].reshape(T * N, -1)).to(gpu)
+    objf, acc, wt = net.train_step(feats, T, N, g["num_frames"], g["flat_labels"], g["label_lengths"])
+    np.testing.assert_allclose(objf, g["costs"].sum(), rtol=1e-5)
+    assert wt == g["label_lengths"].sum()
+    assert rel_err(net.get_params(1) - g["w0"], g["w_delta"]) < 1e-4
+    aff = net.get_params(3)
+    assert rel_err(aff[:-41] - g["Wa0"].ravel(), g["Wa_delta"].ravel()) < 1e-4
+    assert rel_err(aff[-41:] - g["ba0"], g["ba_delta"]) < 1e-4
+
+
+def _oracle_spec(oracle, R, mode, H, dirs, D, A, thr, lr, repair_scale=1.0):
+    s = oracle.NnetSpec()
+    s.num_rnn, s.mode, s.hidden, s.dirs, s.layers_per_rnn = R, mode, H, dirs, 1
+    s.input_dim, s.num_targets = D, A
+    s.clip_threshold, s.repair_threshold, s.repair_scale, s.repair_target = thr, 0.01, repair_scale, 0.0
+    s.rnn_clip_gradient, s.lr_rnn, s.lr_affine = 5.0, lr, lr
+    return s
+
+
+@pytest.mark.parametrize("mode,H,thr,steps", [
+    (2, 64, 30.0, 2),     # BLSTM, recipe clip threshold (rarely clips)
+    (2, 64, 0.02, 3),     # every row clipped -> self-repair active on draws <= 0.5
+    (3, 48, 30.0, 2),     # BGRU
+])
+def test_train_steps_match_oracle(kctc, gpu, oracle, mode, H, thr, steps):
+    import torch
+    R, D, A, T, N, lr = 2, 24, 11, 30, 4, 0.02
+    cfg = kctc.recipe_config(num_rnn=R, input_dim=D, hidden=H, num_targets=A, rnn_mode=mode,
+                             learning_rate=lr, clipping_threshold=thr, param_stddev=0.2)
+    net = kctc.Nnet(cfg, seed=5)
+    net.set_repair_seed(99)
+    draws = splitmix_uniforms(99, steps * R)
+    upd = [c for c in range(net.num_components) if net.num_params(c) > 0]
+    params = [net.get_params(c).astype(np.float64) for c in upd]
+    spec = _oracle_spec(oracle, R, mode, H, 2, D, A, thr, lr)
+    cnc, cc = np.zeros(R), np.zeros(R)
+    for step in range(steps):
+        feats, nf, fl, ll = kctc.synth_minibatch(1000 + step, T, N, D, A, 0.2)
+        objf, acc, wt = net.train_step(torch.from_numpy(feats).to(gpu), T, N, nf, fl, ll)
+        # the trainer draws top clip component first
+        d = draws[step * R:(step + 1) * R][::-1]
+        rnn_p = [p for p in params[:-1]]
+        aff = params[-1]
+        Wa = aff[:-A].reshape(A, -1).copy()
+        ba = aff[-A:].copy()
+        robjf, racc, rwt = oracle.train_step(spec, rnn_p, Wa, ba, feats.reshape(T, N, D).astype(np.float64),
+                                             nf, fl, ll, repair_draws=np.array(d, np.float32),
+                                             clip_num_clipped=cnc, clip_count=cc)
+        params[-1] = np.concatenate([Wa.ravel(), ba])
+        np.testing.assert_allclose(objf, robjf, rtol=1e-5)
+        assert wt == rwt
+        assert abs(acc - racc) <= 1  # argmax ties on nearly-equal logits may differ by one edit
+    for c, p in zip(upd, params):
+        got = net.get_params(c).astype(np.float64)
+        init = None
+        assert rel_err(got, p) < 1e-5, c
+    for i, c in enumerate([c for c in range(net.num_components) if "ClipGradient" in net.info(c)]):
+        ncl, cnt = net.clip_stats(c)
+        assert cnt == cc[i] and ncl == cnc[i]
+
+
+def test_train_loss_decreases_and_objf_only(kctc, gpu):
+    import torch
+    D, A, T, N = 40, 41, 120, 8
+    cfg = kctc.recipe_config(num_rnn=2, input_dim=D, hidden=128, num_targets=A, learning_rate=2e-3)
+    net = kctc.Nnet(cfg, seed=3)
+    feats, nf, fl, ll = kctc.synth_minibatch(7, T, N, D, A, 0.125)
+    f = torch.from_numpy(feats).to(gpu)
+    o0, _, w = net.compute_objf(f, T, N, nf, fl, ll)
+    o0b, _, _ = net.compute_objf(f, T, N, nf, fl, ll)
+    assert o0 == o0b  # no update, deterministic
+    for _ in range(12):
+        net.train_step(f, T, N, nf, fl, ll)
+    o1, _, _ = net.compute_objf(f, T, N, nf, fl, ll)
+    assert o1 < 0.9 * o0, (o0, o1)
+
+
+def test_model_write_read_roundtrip(kctc, gpu, tmp_path):
+    import torch
+    D, A, T, N = 16, 9, 20, 3
+    net = kctc.Nnet(kctc.recipe_config(num_rnn=2, input_dim=D, hidden=32, num_targets=A), seed=2)
+    p = tmp_path / "m.txt"
+    net.write(p)
+    net2 = kctc.Nnet.read(p)
+    assert net2.num_components == net.num_components
+    for c in range(net.num_components):
+        if net.num_params(c):
+            np.testing.assert_array_equal(net.get_params(c), net2.get_params(c))
+    feats, nf, fl, ll = kctc.synth_minibatch(3, T, N, D, A, 0.2)
+    f = torch.from_numpy(feats).to(gpu)
+    assert net.compute_objf(f, T, N, nf, fl, ll) == net2.compute_objf(f, T, N, nf, fl, ll)
