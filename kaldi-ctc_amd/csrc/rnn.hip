@@ -91,9 +91,11 @@ static long drec_split_floats(const RnnDesc &d, int T, int N) {
   return need;
 }
 
-size_t rnn_workspace_bytes(const RnnDesc &d, int T, int N) {
-  return sizeof(float) * (size_t)al64(drec_split_floats(d, T, N)) + 256;
+// split-K slabs of the weight-gradient GEMMs, then the recurrence flag words
+static size_t flags_offset(const RnnDesc &d, int T, int N) {
+  return sizeof(float) * (size_t)al64(drec_split_floats(d, T, N));
 }
+size_t rnn_workspace_bytes(const RnnDesc &d, int T, int N) { return flags_offset(d, T, N) + 4096; }
 
 namespace {
 
@@ -158,26 +160,103 @@ struct RecParams {
   float *E;         // backward: dGates (recurrent part) exchange [T*N][dirs*nW*H]
   float *DX;        // backward GRU: dGates (input part); == E otherwise
   float *bias;      // backward: bias partial sums [dirs][2][nW*H]
+  unsigned *flags;  // flag protocol: [dirs][nwg] step epochs, zeroed before launch
   unsigned *err;
+  int sync;         // kSyncData / kSyncFlag
 };
+
+// Hand-off protocols (selected per launch; both placement-independent):
+//  kSyncData: the payload is the flag (sentinel-filled buffer, sc1 4-B stores,
+//             sc1 16-B loads re-polled until no sentinel is left).
+//  kSyncFlag: payload sc1 stores -> every storing wave s_waitcnt vmcnt(0) ->
+//             workgroup barrier -> ONE lane stores the step epoch (sc1) into
+//             the workgroup's flag word; consumers: wave 0 polls the nwg flag
+//             words of its direction with one sc1 load per lane, barrier, then
+//             every wave loads the payload with sc1 loads (MI355X_MICROARCH.md
+//             "Valid forms", row 1).  Polling traffic: 4 B per producer, not
+//             the whole payload.
+enum { kSyncData = 0, kSyncFlag = 1 };
+
+__device__ __forceinline__ void wait_flags(const unsigned *flags, int nwg, unsigned epoch,
+                                           unsigned *err, int &bad, int *bad_lds) {
+  if (threadIdx.x < 64) {
+    int spins = 0;
+    while (true) {
+      bool ok = true;
+      for (int i = threadIdx.x; i < nwg; i += 64)
+        ok &= __hip_atomic_load(flags + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= epoch;
+      if (__all(ok)) break;
+      if (++spins > kSpinLimit ||
+          ((spins & 255) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        bad = 1;
+        if (threadIdx.x == 0) *bad_lds = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  if (*bad_lds) bad = 1;
+}
+
+__device__ __forceinline__ void signal_flag(unsigned *flag, unsigned epoch) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A-operand fragments of one step: rows n (RT 16-row tiles) x this wave's
+// k-groups {w, w+4, ...}, CH k-groups per pass, straight from the exchange
+// buffer into registers with sc1 16-B loads.  Returns false on timeout.
+template <int RT, int CH>
+__device__ __forceinline__ void load_frags(u32x4 (&af)[RT][CH], __amdgpu_buffer_rsrc_t rs, long ld,
+                                           long col0, int c0, int KG, int N, int sync, unsigned *err,
+                                           int &bad) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < CH; i++) {
+    const int kg = w + 4 * (c0 + i);
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++) {
+      const int n = rt * 16 + fr;
+      af[rt][i] = u32x4{0u, 0u, 0u, 0u};
+      if (kg < KG && n < N) af[rt][i] = ld_sc1(rs, (unsigned)(((long)n * ld + col0 + kg * 16 + fq * 4) * 4));
+    }
+  }
+  if (sync == kSyncData) {
+#pragma unroll
+    for (int i = 0; i < CH; i++) {
+      const int kg = w + 4 * (c0 + i);
+#pragma unroll
+      for (int rt = 0; rt < RT; rt++) {
+        const int n = rt * 16 + fr;
+        if (kg < KG && n < N)
+          af[rt][i] = settle(rs, (unsigned)(((long)n * ld + col0 + kg * 16 + fq * 4) * 4), af[rt][i], err, bad);
+      }
+    }
+  }
+}
 
 // ---------------------------------------------------------------------------
 // forward recurrence
 // ---------------------------------------------------------------------------
-template <int MODE>
+template <int MODE, int RT>
 __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec(RecParams p) {
   constexpr int NW = MODE == kLstm ? 4 : MODE == kGru ? 3 : 1;
+  constexpr int CH = 32 / RT;  // k-groups per wave per pass (<= 32 A-fragment registers x4)
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ int bad_lds;
   const int H = p.H, U = p.U, N = p.N, T = p.T, ncol = p.ncol;
   const int LDR = H + 4;
-  const int d = blockIdx.x / p.nwg, u0 = (blockIdx.x % p.nwg) * U;
+  const int d = blockIdx.x / p.nwg, g = blockIdx.x % p.nwg, u0 = g * U;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
-  const int RT = p.Npad / 16, CT = ncol / 16;
+  const int CT = ncol / 16;
   const long ldy = (long)p.dirs * H, ldg = (long)p.dirs * NW * H;
   float *Rs = smem;                      // [ncol][LDR]
   float *red = Rs + (long)ncol * LDR;    // [4][Npad][ncol]
   const float *Wd = p.w + d * p.pl_stride;
   const float *R = Wd + p.r_off;
+  if (tid == 0) bad_lds = 0;
   for (int idx = tid; idx < ncol * H; idx += NT) {
     const int c = idx / H, k = idx - c * H;
     float v = 0.f;
@@ -196,13 +275,12 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec(RecParams p) {
     hpv[j] = 0.f;
     const int it = tid + j * NT, u = it % U;
 #pragma unroll
-    for (int g = 0; g < NW; g++) {
-      bR[j][g] = (MODE == kGru && it < items) ? Wd[p.bR_off + g * H + u0 + u] : 0.f;
-      gin[j][g] = 0.f;
+    for (int q = 0; q < NW; q++) {
+      bR[j][q] = (MODE == kGru && it < items) ? Wd[p.bR_off + q * H + u0 + u] : 0.f;
+      gin[j][q] = 0.f;
     }
   }
-  // prefetch the input projection of the first step
-  {
+  {  // prefetch the input projection of the first step
     const int t = d == 0 ? 0 : T - 1;
 #pragma unroll
     for (int j = 0; j < kMaxIPT; j++) {
@@ -210,51 +288,33 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec(RecParams p) {
       if (it < items) {
         const int n = it / U, u = it - n * U;
 #pragma unroll
-        for (int g = 0; g < NW; g++)
-          gin[j][g] = p.G[((long)t * N + n) * ldg + (long)d * NW * H + g * H + u0 + u];
+        for (int q = 0; q < NW; q++)
+          gin[j][q] = p.G[((long)t * N + n) * ldg + (long)d * NW * H + q * H + u0 + u];
       }
     }
   }
   __syncthreads();
   int bad = 0;
-  const int KG = H / 16;  // k-groups, dealt round-robin to the 4 waves
+  const int KG = H / 16;
+  const int KGW = (KG + 3) / 4;  // k-groups per wave
   const unsigned step_bytes = (unsigned)((long)N * ldy * sizeof(float));
+  unsigned *myflag = p.flags + d * p.nwg + g;
   for (int k = 0; k < T; k++) {
     const int t = d == 0 ? k : T - 1 - k, tp = d == 0 ? t - 1 : t + 1;
-    floatx4 acc[kMaxRT][kMaxCT];
+    floatx4 acc[RT][kMaxCT];
 #pragma unroll
-    for (int a = 0; a < kMaxRT; a++)
+    for (int a = 0; a < RT; a++)
 #pragma unroll
       for (int b = 0; b < kMaxCT; b++) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
     if (k > 0) {
+      if (p.sync == kSyncFlag) wait_flags(p.flags + d * p.nwg, p.nwg, (unsigned)k, p.err, bad, &bad_lds);
       const auto rs = rsrc(p.y + (long)tp * N * ldy, step_bytes);
-      for (int c0 = w; c0 < KG; c0 += 4 * kCH) {
-        u32x4 af[kMaxRT][kCH];
+      for (int c0 = 0; c0 < KGW; c0 += CH) {
+        u32x4 af[RT][CH];
+        load_frags<RT, CH>(af, rs, ldy, (long)d * H, c0, KG, N, p.sync, p.err, bad);
 #pragma unroll
-        for (int i = 0; i < kCH; i++) {
-          const int kg = c0 + 4 * i;
-#pragma unroll
-          for (int rt = 0; rt < kMaxRT; rt++) {
-            const int n = rt * 16 + fr;
-            af[rt][i] = u32x4{0u, 0u, 0u, 0u};
-            if (rt < RT && kg < KG && n < N)
-              af[rt][i] = ld_sc1(rs, (unsigned)(((long)n * ldy + (long)d * H + kg * 16 + fq * 4) * 4));
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < kCH; i++) {
-          const int kg = c0 + 4 * i;
-#pragma unroll
-          for (int rt = 0; rt < kMaxRT; rt++) {
-            const int n = rt * 16 + fr;
-            if (rt < RT && kg < KG && n < N)
-              af[rt][i] = settle(rs, (unsigned)(((long)n * ldy + (long)d * H + kg * 16 + fq * 4) * 4),
-                                 af[rt][i], p.err, bad);
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < kCH; i++) {
-          const int kg = c0 + 4 * i;
+        for (int i = 0; i < CH; i++) {
+          const int kg = w + 4 * (c0 + i);
           if (kg < KG) {
 #pragma unroll
             for (int ct = 0; ct < kMaxCT; ct++) {
@@ -263,10 +323,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec(RecParams p) {
 #pragma unroll
                 for (int s = 0; s < 4; s++)
 #pragma unroll
-                  for (int rt = 0; rt < kMaxRT; rt++)
-                    if (rt < RT)
-                      acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                          __uint_as_float(af[rt][i][s]), b[s], acc[rt][ct], 0, 0, 0);
+                  for (int rt = 0; rt < RT; rt++)
+                    acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[rt][i][s]), b[s],
+                                                                       acc[rt][ct], 0, 0, 0);
               }
             }
           }
@@ -275,15 +334,16 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec(RecParams p) {
     }
     // cross-wave K reduction through LDS
 #pragma unroll
-    for (int rt = 0; rt < kMaxRT; rt++)
+    for (int rt = 0; rt < RT; rt++)
 #pragma unroll
       for (int ct = 0; ct < kMaxCT; ct++)
-        if (rt < RT && ct < CT)
+        if (ct < CT)
 #pragma unroll
           for (int r = 0; r < 4; r++)
             red[((long)w * p.Npad + rt * 16 + fq * 4 + r) * ncol + ct * 16 + fr] = acc[rt][ct][r];
     __syncthreads();
-    // pointwise cell update for owned (n, u)
+    // pointwise cell update for owned (n, u); publish h_t first, then the rest
+    float act[kMaxIPT][NW], cnew[kMaxIPT];
 #pragma unroll
     for (int j = 0; j < kMaxIPT; j++) {
       const int it = tid + j * NT;
@@ -291,44 +351,54 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec(RecParams p) {
         const int n = it / U, u = it - n * U;
         float rh[NW];
 #pragma unroll
-        for (int g = 0; g < NW; g++) {
-          const int c = g * U + u;
-          rh[g] = ((red[((long)0 * p.Npad + n) * ncol + c] + red[((long)1 * p.Npad + n) * ncol + c]) +
+        for (int q = 0; q < NW; q++) {
+          const int c = q * U + u;
+          rh[q] = ((red[((long)0 * p.Npad + n) * ncol + c] + red[((long)1 * p.Npad + n) * ncol + c]) +
                    red[((long)2 * p.Npad + n) * ncol + c]) + red[((long)3 * p.Npad + n) * ncol + c];
         }
-        const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
         const long yrow = ((long)t * N + n) * ldy + (long)d * H + u0 + u;
         float h;
         if (MODE == kLstm) {
-          const float ig = sigm(gin[j][0] + rh[0]);
-          const float fg = sigm(gin[j][1] + rh[1]);
-          const float gg = tanhf(gin[j][2] + rh[2]);
-          const float og = sigm(gin[j][3] + rh[3]);
-          const float cc = fg * cst[j] + ig * gg;
+          act[j][0] = sigm(gin[j][0] + rh[0]);
+          act[j][1] = sigm(gin[j][1] + rh[1]);
+          act[j][2] = tanhf(gin[j][2] + rh[2]);
+          act[j][3] = sigm(gin[j][3] + rh[3]);
+          const float cc = act[j][1] * cst[j] + act[j][0] * act[j][2];
           cst[j] = cc;
-          h = og * tanhf(cc);
-          p.G[grow] = ig; p.G[grow + H] = fg; p.G[grow + 2 * H] = gg; p.G[grow + 3 * H] = og;
-          p.aux[yrow] = cc;
+          cnew[j] = cc;
+          h = act[j][3] * tanhf(cc);
         } else if (MODE == kGru) {
-          const float r = sigm(gin[j][0] + rh[0] + bR[j][0]);
-          const float z = sigm(gin[j][1] + rh[1] + bR[j][1]);
-          const float rhn = rh[2] + bR[j][2];
-          const float nn = tanhf(gin[j][2] + r * rhn);
-          h = (1.f - z) * nn + z * hpv[j];
+          act[j][0] = sigm(gin[j][0] + rh[0] + bR[j][0]);
+          act[j][1] = sigm(gin[j][1] + rh[1] + bR[j][1]);
+          cnew[j] = rh[2] + bR[j][2];
+          act[j][2] = tanhf(gin[j][2] + act[j][0] * cnew[j]);
+          h = (1.f - act[j][1]) * act[j][2] + act[j][1] * hpv[j];
           hpv[j] = h;
-          p.G[grow] = r; p.G[grow + H] = z; p.G[grow + 2 * H] = nn;
-          p.aux[yrow] = rhn;
         } else {
           const float pre = gin[j][0] + rh[0];
           h = MODE == kRelu ? fmaxf(pre, 0.f) : tanhf(pre);
         }
         publish(p.y + yrow, h);
-        // prefetch the next step's input projection
-        if (k + 1 < T) {
+      }
+    }
+    if (p.sync == kSyncFlag) signal_flag(myflag, (unsigned)(k + 1));
+#pragma unroll
+    for (int j = 0; j < kMaxIPT; j++) {
+      const int it = tid + j * NT;
+      if (it < items) {
+        const int n = it / U, u = it - n * U;
+        const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
+        const long yrow = ((long)t * N + n) * ldy + (long)d * H + u0 + u;
+        if (MODE != kRelu && MODE != kTanh) {
+#pragma unroll
+          for (int q = 0; q < NW; q++) p.G[grow + q * H] = act[j][q];
+          p.aux[yrow] = cnew[j];
+        }
+        if (k + 1 < T) {  // prefetch the next step's input projection
           const int tn = d == 0 ? t + 1 : t - 1;
 #pragma unroll
-          for (int g = 0; g < NW; g++)
-            gin[j][g] = p.G[((long)tn * N + n) * ldg + (long)d * NW * H + g * H + u0 + u];
+          for (int q = 0; q < NW; q++)
+            gin[j][q] = p.G[((long)tn * N + n) * ldg + (long)d * NW * H + q * H + u0 + u];
         }
       }
     }
@@ -340,20 +410,22 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec(RecParams p) {
 // ---------------------------------------------------------------------------
 // backward-data recurrence
 // ---------------------------------------------------------------------------
-template <int MODE>
+template <int MODE, int RT>
 __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec(RecParams p) {
   constexpr int NW = MODE == kLstm ? 4 : MODE == kGru ? 3 : 1;
+  constexpr int CH = 32 / RT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ int bad_lds;
   const int H = p.H, U = p.U, N = p.N, T = p.T;
   const int K = NW * H, LDK = K + 4;
-  const int d = blockIdx.x / p.nwg, u0 = (blockIdx.x % p.nwg) * U;
+  const int d = blockIdx.x / p.nwg, g = blockIdx.x % p.nwg, u0 = g * U;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
-  const int RT = p.Npad / 16;
   const long ldy = (long)p.dirs * H, ldg = (long)p.dirs * NW * H;
   float *RT_s = smem;                       // [U][LDK]: RT_s[u][kk] = R[kk][u0+u]
   float *red = RT_s + (long)U * LDK;        // [4][Npad][16]
   const float *Wd = p.w + d * p.pl_stride;
   const float *R = Wd + p.r_off;
+  if (tid == 0) bad_lds = 0;
   for (int idx = tid; idx < U * K; idx += NT) {
     const int kk = idx / U, u = idx - kk * U;
     RT_s[u * LDK + kk] = R[(long)kk * H + u0 + u];
@@ -361,72 +433,78 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec(RecParams p) {
   const int items = N * U;
   float carry[kMaxIPT];   // LSTM: dc carried to the previous step; GRU: dh*z direct term
   float bsx[kMaxIPT][NW], bsh[kMaxIPT][NW];
+  // prefetched pointwise operands of the step about to be processed
+  float pdy[kMaxIPT], pg[kMaxIPT][NW], pa[kMaxIPT], pap[kMaxIPT];
 #pragma unroll
   for (int j = 0; j < kMaxIPT; j++) {
     carry[j] = 0.f;
 #pragma unroll
-    for (int g = 0; g < NW; g++) bsx[j][g] = bsh[j][g] = 0.f;
+    for (int q = 0; q < NW; q++) bsx[j][q] = bsh[j][q] = pg[j][q] = 0.f;
+    pdy[j] = pa[j] = pap[j] = 0.f;
   }
+  auto prefetch = [&](int k) {
+    const int t = d == 0 ? k : T - 1 - k, tp = d == 0 ? t - 1 : t + 1;
+#pragma unroll
+    for (int j = 0; j < kMaxIPT; j++) {
+      const int it = tid + j * NT;
+      if (it < items) {
+        const int n = it / U, u = it - n * U;
+        const long yrow = ((long)t * N + n) * ldy + (long)d * H + u0 + u;
+        const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
+        const long prow = ((long)tp * N + n) * ldy + (long)d * H + u0 + u;
+        pdy[j] = p.dy[yrow];
+        if (MODE == kLstm || MODE == kGru) {
+#pragma unroll
+          for (int q = 0; q < NW; q++) pg[j][q] = p.G[grow + q * H];
+          pa[j] = p.aux[yrow];
+        }
+        if (MODE == kLstm) pap[j] = k > 0 ? p.aux[prow] : 0.f;
+        else if (MODE == kGru) pap[j] = k > 0 ? p.y[prow] : 0.f;
+        else pap[j] = p.y[yrow];
+      }
+    }
+  };
+  prefetch(T - 1);
   __syncthreads();
   int bad = 0;
   const int KG = K / 16;
+  const int KGW = (KG + 3) / 4;
   const unsigned step_bytes = (unsigned)((long)N * ldg * sizeof(float));
+  unsigned *myflag = p.flags + d * p.nwg + g;
   for (int k = T - 1; k >= 0; k--) {
     const int t = d == 0 ? k : T - 1 - k;       // forward-order index k
     const int tn = d == 0 ? t + 1 : t - 1;      // processed just before (k+1)
-    const int tp = d == 0 ? t - 1 : t + 1;      // forward predecessor (k-1)
-    floatx4 acc[kMaxRT];
+    const unsigned epoch = (unsigned)(T - k);   // number of steps published so far
+    floatx4 acc[RT];
 #pragma unroll
-    for (int a = 0; a < kMaxRT; a++) acc[a] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int a = 0; a < RT; a++) acc[a] = floatx4{0.f, 0.f, 0.f, 0.f};
     if (k < T - 1) {
+      if (p.sync == kSyncFlag) wait_flags(p.flags + d * p.nwg, p.nwg, epoch - 1, p.err, bad, &bad_lds);
       const auto rs = rsrc(p.E + (long)tn * N * ldg, step_bytes);
-      for (int c0 = w; c0 < KG; c0 += 4 * kCH) {
-        u32x4 af[kMaxRT][kCH];
+      for (int c0 = 0; c0 < KGW; c0 += CH) {
+        u32x4 af[RT][CH];
+        load_frags<RT, CH>(af, rs, ldg, (long)d * K, c0, KG, N, p.sync, p.err, bad);
 #pragma unroll
-        for (int i = 0; i < kCH; i++) {
-          const int kg = c0 + 4 * i;
-#pragma unroll
-          for (int rt = 0; rt < kMaxRT; rt++) {
-            const int n = rt * 16 + fr;
-            af[rt][i] = u32x4{0u, 0u, 0u, 0u};
-            if (rt < RT && kg < KG && n < N)
-              af[rt][i] = ld_sc1(rs, (unsigned)(((long)n * ldg + (long)d * K + kg * 16 + fq * 4) * 4));
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < kCH; i++) {
-          const int kg = c0 + 4 * i;
-#pragma unroll
-          for (int rt = 0; rt < kMaxRT; rt++) {
-            const int n = rt * 16 + fr;
-            if (rt < RT && kg < KG && n < N)
-              af[rt][i] = settle(rs, (unsigned)(((long)n * ldg + (long)d * K + kg * 16 + fq * 4) * 4),
-                                 af[rt][i], p.err, bad);
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < kCH; i++) {
-          const int kg = c0 + 4 * i;
+        for (int i = 0; i < CH; i++) {
+          const int kg = w + 4 * (c0 + i);
           if (kg < KG) {
             floatx4 b = floatx4{0.f, 0.f, 0.f, 0.f};
             if (fr < U) b = *reinterpret_cast<const floatx4 *>(RT_s + fr * LDK + kg * 16 + fq * 4);
 #pragma unroll
             for (int s = 0; s < 4; s++)
 #pragma unroll
-              for (int rt = 0; rt < kMaxRT; rt++)
-                if (rt < RT)
-                  acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[rt][i][s]), b[s],
-                                                                 acc[rt], 0, 0, 0);
+              for (int rt = 0; rt < RT; rt++)
+                acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[rt][i][s]), b[s], acc[rt], 0, 0, 0);
           }
         }
       }
     }
 #pragma unroll
-    for (int rt = 0; rt < kMaxRT; rt++)
-      if (rt < RT)
+    for (int rt = 0; rt < RT; rt++)
 #pragma unroll
-        for (int r = 0; r < 4; r++) red[((long)w * p.Npad + rt * 16 + fq * 4 + r) * 16 + fr] = acc[rt][r];
+      for (int r = 0; r < 4; r++) red[((long)w * p.Npad + rt * 16 + fq * 4 + r) * 16 + fr] = acc[rt][r];
     __syncthreads();
+    float dx_keep[kMaxIPT][NW];
 #pragma unroll
     for (int j = 0; j < kMaxIPT; j++) {
       const int it = tid + j * NT;
@@ -434,13 +512,11 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec(RecParams p) {
         const int n = it / U, u = it - n * U;
         const float dhr = ((red[((long)0 * p.Npad + n) * 16 + u] + red[((long)1 * p.Npad + n) * 16 + u]) +
                            red[((long)2 * p.Npad + n) * 16 + u]) + red[((long)3 * p.Npad + n) * 16 + u];
-        const long yrow = ((long)t * N + n) * ldy + (long)d * H + u0 + u;
         const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
-        float dh = p.dy[yrow] + dhr;
+        float dh = pdy[j] + dhr;
         if (MODE == kLstm) {
-          const float ig = p.G[grow], fg = p.G[grow + H], gg = p.G[grow + 2 * H], og = p.G[grow + 3 * H];
-          const float cc = p.aux[yrow];
-          const float cp = k > 0 ? p.aux[((long)tp * N + n) * ldy + (long)d * H + u0 + u] : 0.f;
+          const float ig = pg[j][0], fg = pg[j][1], gg = pg[j][2], og = pg[j][3];
+          const float cc = pa[j], cp = pap[j];
           const float tc = tanhf(cc);
           const float dO = dh * tc;
           const float dc = dh * og * (1.f - tc * tc) + carry[j];
@@ -456,22 +532,21 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec(RecParams p) {
           bsx[j][0] += dpi; bsx[j][1] += dpf; bsx[j][2] += dpg; bsx[j][3] += dpo;
         } else if (MODE == kGru) {
           dh += carry[j];
-          const float r = p.G[grow], z = p.G[grow + H], nn = p.G[grow + 2 * H];
-          const float rhn = p.aux[yrow];
-          const float hp = k > 0 ? p.y[((long)tp * N + n) * ldy + (long)d * H + u0 + u] : 0.f;
+          const float r = pg[j][0], z = pg[j][1], nn = pg[j][2];
+          const float rhn = pa[j], hp = pap[j];
           const float dn = dh * (1.f - z), dz = dh * (hp - nn);
           const float dpn = dn * (1.f - nn * nn);
           const float dpr = dpn * rhn * r * (1.f - r);
           const float dpz = dz * z * (1.f - z);
           carry[j] = dh * z;
-          p.DX[grow] = dpr; p.DX[grow + H] = dpz; p.DX[grow + 2 * H] = dpn;
+          dx_keep[j][0] = dpr; dx_keep[j][1] = dpz; dx_keep[j][2] = dpn;
           publish(p.E + grow, dpr);
           publish(p.E + grow + H, dpz);
           publish(p.E + grow + 2 * H, dpn * r);
           bsx[j][0] += dpr; bsx[j][1] += dpz; bsx[j][2] += dpn;
           bsh[j][0] += dpr; bsh[j][1] += dpz; bsh[j][2] += dpn * r;
         } else {
-          const float h = p.y[yrow];
+          const float h = pap[j];
           const float der = MODE == kRelu ? (h > 0.f ? 1.f : 0.f) : (1.f - h * h);
           const float dp = dh * der;
           publish(p.E + grow, dp);
@@ -479,6 +554,19 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec(RecParams p) {
         }
       }
     }
+    if (p.sync == kSyncFlag) signal_flag(myflag, epoch);
+    if (MODE == kGru) {
+#pragma unroll
+      for (int j = 0; j < kMaxIPT; j++) {
+        const int it = tid + j * NT;
+        if (it < items) {
+          const int n = it / U, u = it - n * U;
+          const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
+          p.DX[grow] = dx_keep[j][0]; p.DX[grow + H] = dx_keep[j][1]; p.DX[grow + 2 * H] = dx_keep[j][2];
+        }
+      }
+    }
+    if (k > 0) prefetch(k - 1);
     __syncthreads();
   }
   // bias partial sums: reduce over n in a fixed order through LDS
@@ -488,17 +576,17 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec(RecParams p) {
     const int it = tid + j * NT;
     if (it < items)
 #pragma unroll
-      for (int g = 0; g < NW; g++) {
-        bs[(long)it * NW + g] = bsx[j][g];
-        bs[(long)items * NW + (long)it * NW + g] = (MODE == kGru) ? bsh[j][g] : bsx[j][g];
+      for (int q = 0; q < NW; q++) {
+        bs[(long)it * NW + q] = bsx[j][q];
+        bs[(long)items * NW + (long)it * NW + q] = (MODE == kGru) ? bsh[j][q] : bsx[j][q];
       }
   }
   __syncthreads();
   for (int q = tid; q < 2 * NW * U; q += NT) {
-    const int part = q / (NW * U), rem = q - part * NW * U, g = rem / U, u = rem - g * U;
+    const int part = q / (NW * U), rem = q - part * NW * U, gt = rem / U, u = rem - gt * U;
     float s = 0.f;
-    for (int n = 0; n < N; n++) s += bs[(long)part * items * NW + ((long)n * U + u) * NW + g];
-    p.bias[((long)d * 2 + part) * NW * H + g * H + u0 + u] = s;
+    for (int n = 0; n < N; n++) s += bs[(long)part * items * NW + ((long)n * U + u) * NW + gt];
+    p.bias[((long)d * 2 + part) * NW * H + gt * H + u0 + u] = s;
   }
   if (bad && tid == 0) atomicOr(p.err, 1u);
 }
@@ -509,6 +597,34 @@ static void set_lds(F f, size_t bytes) {
   (void)done;
   (void)hipFuncSetAttribute(reinterpret_cast<const void *>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
                       (int)bytes);
+}
+
+template <int MODE, int RT>
+static void launch_one(bool fwd, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
+  if (fwd) {
+    set_lds(rnn_fwd_rec<MODE, RT>, lds);
+    hipLaunchKernelGGL((rnn_fwd_rec<MODE, RT>), grid, dim3(NT), lds, s, p);
+  } else {
+    set_lds(rnn_bwd_rec<MODE, RT>, lds);
+    hipLaunchKernelGGL((rnn_bwd_rec<MODE, RT>), grid, dim3(NT), lds, s, p);
+  }
+}
+template <int MODE>
+static void launch_mode(bool fwd, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
+  switch (p.Npad / 16) {
+    case 1: launch_one<MODE, 1>(fwd, p, grid, lds, s); break;
+    case 2: launch_one<MODE, 2>(fwd, p, grid, lds, s); break;
+    case 3: launch_one<MODE, 3>(fwd, p, grid, lds, s); break;
+    default: launch_one<MODE, 4>(fwd, p, grid, lds, s); break;
+  }
+}
+static void launch_rec(bool fwd, int mode, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
+  switch (mode) {
+    case kLstm: launch_mode<kLstm>(fwd, p, grid, lds, s); break;
+    case kGru: launch_mode<kGru>(fwd, p, grid, lds, s); break;
+    case kRelu: launch_mode<kRelu>(fwd, p, grid, lds, s); break;
+    default: launch_mode<kTanh>(fwd, p, grid, lds, s); break;
+  }
 }
 
 static int env_int(const char *name, int dflt) {
@@ -528,8 +644,8 @@ static int pick_fwd_u(const RnnDesc &d, int N) {
     return lds <= 160 * 1024;
   };
   if (want && ok(want)) return want;
-  for (int U : {8, 4, 16, 2, 1})
-    if (ok(U) && (long)d.dirs * (d.H / U) <= 128) return U;
+  // smallest U that keeps every workgroup resident (<= 256 = one per CU):
+  // per-step MFMA latency falls with U (measured: U=4 < 8 < 16 on BLSTM-512)
   for (int U : {4, 8, 16, 2, 1})
     if (ok(U)) return U;
   return 0;
@@ -599,19 +715,13 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.ncol = (NW * U + 15) / 16 * 16; p.Npad = (N + 15) / 16 * 16;
     p.w = wl; p.pl_stride = pls; p.r_off = roff; p.bR_off = bR;
     p.G = R0 + lay.G; p.y = out; p.aux = R0 + lay.aux; p.err = err;
+    p.sync = env_int("KCTC_SYNC", kSyncFlag);
+    p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
+    KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, 4096, s));
     const size_t lds = sizeof(float) * ((size_t)p.ncol * (H + 4) + 4 * (size_t)p.Npad * p.ncol);
     const dim3 grid(dirs * p.nwg);
     ProfSpan ps(s, "rnn_fwd_rec");
-    switch (d.mode) {
-      case kLstm: set_lds(rnn_fwd_rec<kLstm>, lds);
-        hipLaunchKernelGGL(rnn_fwd_rec<kLstm>, grid, dim3(NT), lds, s, p); break;
-      case kGru: set_lds(rnn_fwd_rec<kGru>, lds);
-        hipLaunchKernelGGL(rnn_fwd_rec<kGru>, grid, dim3(NT), lds, s, p); break;
-      case kRelu: set_lds(rnn_fwd_rec<kRelu>, lds);
-        hipLaunchKernelGGL(rnn_fwd_rec<kRelu>, grid, dim3(NT), lds, s, p); break;
-      default: set_lds(rnn_fwd_rec<kTanh>, lds);
-        hipLaunchKernelGGL(rnn_fwd_rec<kTanh>, grid, dim3(NT), lds, s, p); break;
-    }
+    launch_rec(true, d.mode, p, grid, lds, s);
     KCTC_HIP_CHECK(hipGetLastError());
     in = out;
   }
@@ -650,21 +760,16 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     p.bR_off = d.lin_offset(l * dirs, NW, true) - pl0;
     p.G = R0 + lay.G; p.y = const_cast<float *>(out); p.aux = R0 + lay.aux;
     p.dy = dcur; p.E = E; p.DX = DX; p.bias = R0 + lay.bias; p.err = err;
+    p.sync = env_int("KCTC_SYNC", kSyncFlag);
+    if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
+    p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
+    KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, 4096, s));
     const size_t lds = sizeof(float) * ((size_t)U * (NW * H + 4) +
                                         std::max(4 * (size_t)p.Npad * 16, (size_t)2 * N * U * NW));
     const dim3 grid(dirs * p.nwg);
     {
-    ProfSpan ps(s, "rnn_bwd_rec");
-    switch (d.mode) {
-      case kLstm: set_lds(rnn_bwd_rec<kLstm>, lds);
-        hipLaunchKernelGGL(rnn_bwd_rec<kLstm>, grid, dim3(NT), lds, s, p); break;
-      case kGru: set_lds(rnn_bwd_rec<kGru>, lds);
-        hipLaunchKernelGGL(rnn_bwd_rec<kGru>, grid, dim3(NT), lds, s, p); break;
-      case kRelu: set_lds(rnn_bwd_rec<kRelu>, lds);
-        hipLaunchKernelGGL(rnn_bwd_rec<kRelu>, grid, dim3(NT), lds, s, p); break;
-      default: set_lds(rnn_bwd_rec<kTanh>, lds);
-        hipLaunchKernelGGL(rnn_bwd_rec<kTanh>, grid, dim3(NT), lds, s, p); break;
-    }
+      ProfSpan ps(s, "rnn_bwd_rec");
+      launch_rec(false, d.mode, p, grid, lds, s);
     }
     KCTC_HIP_CHECK(hipGetLastError());
     // dx_l = sum_dir DX_dir W_dir   (lower layer's dy, or the caller's dx)

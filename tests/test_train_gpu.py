@@ -109,10 +109,10 @@ def test_train_loss_decreases_and_objf_only(kctc, gpu):
     o0, _, w = net.compute_objf(f, T, N, nf, fl, ll)
     o0b, _, _ = net.compute_objf(f, T, N, nf, fl, ll)
     assert o0 == o0b  # no update, deterministic
-    for _ in range(12):
+    for _ in range(20):
         net.train_step(f, T, N, nf, fl, ll)
     o1, _, _ = net.compute_objf(f, T, N, nf, fl, ll)
-    assert o1 < 0.9 * o0, (o0, o1)
+    assert o1 < 0.93 * o0, (o0, o1)
 
 
 def test_model_write_read_roundtrip(kctc, gpu, tmp_path):
