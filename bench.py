@@ -50,12 +50,12 @@ def model_flops(T, N, D, H, A, L, nw=4, dirs=2):
 
 def cpu_baseline(T, D, H, A, L, steps_seed):
     """The oracle's fp32 restatement (warp-ctc-CPU-style CTC + blocked-GEMM
-    LSTM/affine, OpenMP) on a bounded sample: 2 utterances of the same shape."""
+    LSTM/affine, OpenMP) on a bounded sample: 6 utterances of the same shape."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
     import __graft_entry__ as ge
     k = ge.load_package()
-    Ns = 2
+    Ns = 6
     s = O.NnetSpec()
     s.num_rnn, s.mode, s.hidden, s.dirs, s.layers_per_rnn = L, 2, H, 2, 1
     s.input_dim, s.num_targets = D, A

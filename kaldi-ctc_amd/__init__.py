@@ -393,3 +393,32 @@ def format_input(utt_feats, T_max=None):
     _tcheck(lib().kctc_format_input(cat.ctypes.data, nf.ctypes.data, N, dim, T_max, out.ctypes.data),
             "kctc_format_input")
     return out
+
+
+def smoke_train_step(oracle_lib):
+    """One tiny NnetCtcUpdater step (2 x BLSTM-32, N=3, T=24) on cuda:0,
+    checked against the fp64 oracle (called from __graft_entry__.smoke())."""
+    import torch
+    R, H, D, A, T, N, lr = 2, 32, 16, 9, 24, 3, 0.01
+    net = Nnet(recipe_config(num_rnn=R, input_dim=D, hidden=H, num_targets=A, learning_rate=lr,
+                             param_stddev=0.2), seed=11)
+    upd = [c for c in range(net.num_components) if net.num_params(c) > 0]
+    params = [net.get_params(c).astype(np.float64) for c in upd]
+    feats, nf, fl, ll = synth_minibatch(5, T, N, D, A, 0.2)
+    objf, acc, wt = net.train_step(torch.from_numpy(feats).to("cuda:0"), T, N, nf, fl, ll)
+    s = oracle_lib.NnetSpec()
+    s.num_rnn, s.mode, s.hidden, s.dirs, s.layers_per_rnn = R, 2, H, 2, 1
+    s.input_dim, s.num_targets = D, A
+    s.clip_threshold, s.repair_threshold, s.repair_scale, s.repair_target = 30.0, 0.01, 1.0, 0.0
+    s.rnn_clip_gradient, s.lr_rnn, s.lr_affine = 5.0, lr, lr
+    Wa, ba = params[-1][:-A].reshape(A, -1).copy(), params[-1][-A:].copy()
+    robjf, _, rwt = oracle_lib.train_step(s, params[:-1], Wa, ba, feats.reshape(T, N, D).astype(np.float64),
+                                          nf, fl, ll, repair_draws=np.ones(R, np.float32))
+    params[-1] = np.concatenate([Wa.ravel(), ba])
+    assert abs(objf - robjf) <= 1e-5 * abs(robjf), (objf, robjf)
+    for c, p in zip(upd, params):
+        got = net.get_params(c).astype(np.float64)
+        err = np.linalg.norm(got - p) / np.linalg.norm(p)
+        assert err < 1e-5, (c, err)
+    net.close()
+    return objf, robjf

@@ -102,10 +102,9 @@ namespace {
 constexpr int NT = 256;
 constexpr unsigned kSent = 0xFFFFFFFFu;
 constexpr int kSpinLimit = 1 << 21;
-constexpr int kCH = 8;   // k-groups (16 k each) of A fragments in flight per wave
 constexpr int kMaxRT = 4;  // N <= 64 (four 16-row MFMA tiles)
 constexpr int kMaxCT = 4;  // <= 64 gate columns per workgroup
-constexpr int kMaxIPT = 4;  // pointwise items per thread (N*U <= 1024)
+constexpr int kMaxIPT = 4;  // (N * U / 4 <= 256 pointwise quads: one per thread)
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -237,6 +236,63 @@ __device__ __forceinline__ void load_frags(u32x4 (&af)[RT][CH], __amdgpu_buffer_
   }
 }
 
+// 16-byte write-through (sc1) publish of 4 consecutive units: every A-operand
+// fragment a consumer loads (4 consecutive k) is exactly one such store, so a
+// fragment is either all-sentinel or all-final (no tearing to re-poll).
+__device__ __forceinline__ floatx4 canon(floatx4 v) {
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    if (__float_as_uint(v[i]) == kSent) v[i] = __uint_as_float(0x7FC00000u);
+  return v;
+}
+__device__ __forceinline__ void publish4(__amdgpu_buffer_rsrc_t r, unsigned off, floatx4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, canon(v)), r, (int)off, 0, 16);
+}
+__device__ __forceinline__ floatx4 ld4(const float *p) { return *reinterpret_cast<const floatx4 *>(p); }
+__device__ __forceinline__ void st4(float *p, floatx4 v) { *reinterpret_cast<floatx4 *>(p) = v; }
+__device__ __forceinline__ floatx4 sigm4(floatx4 x) {
+  floatx4 r;
+#pragma unroll
+  for (int i = 0; i < 4; i++) r[i] = sigm(x[i]);
+  return r;
+}
+__device__ __forceinline__ floatx4 tanh4(floatx4 x) {
+  floatx4 r;
+#pragma unroll
+  for (int i = 0; i < 4; i++) r[i] = tanhf(x[i]);
+  return r;
+}
+
+// Poll every not-yet-valid fragment of this lane in batches: all re-loads of
+// a round are in flight together, so a round costs one memory round trip.
+template <int RT, int CH>
+__device__ __forceinline__ void settle_all(u32x4 (&af)[RT][CH], __amdgpu_buffer_rsrc_t rs, long ld,
+                                           long col0, int c0, int KG, int N, unsigned *err, int &bad) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fq = lane >> 4;
+  for (int round = 0; !bad; round++) {
+    int pending = 0;
+#pragma unroll
+    for (int i = 0; i < CH; i++) {
+      const int kg = w + 4 * (c0 + i);
+#pragma unroll
+      for (int rt = 0; rt < RT; rt++) {
+        const int n = rt * 16 + fr;
+        if (kg < KG && n < N && !ready4(af[rt][i])) {
+          af[rt][i] = ld_sc1(rs, (unsigned)(((long)n * ld + col0 + kg * 16 + fq * 4) * 4));
+          pending++;
+        }
+      }
+    }
+    if (!pending) break;
+    if (round > kSpinLimit ||
+        ((round & 255) == 255 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+      bad = 1;
+      break;
+    }
+    asm volatile("" ::: "memory");
+  }
+}
+
 // ---------------------------------------------------------------------------
 // forward recurrence
 // ---------------------------------------------------------------------------
@@ -266,32 +322,21 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec(RecParams p) {
     }
     Rs[c * LDR + k] = v;
   }
-  // pointwise items (n, u)
-  const int items = N * U;
-  float cst[kMaxIPT], hpv[kMaxIPT], gin[kMaxIPT][NW], bR[kMaxIPT][NW];
+  // pointwise item of this thread: row n, units u0+4q .. u0+4q+3
+  const int Q = U / 4, items = N * Q;
+  const bool has_item = tid < items;
+  const int in_ = has_item ? tid / Q : 0, iq = has_item ? tid - in_ * Q : 0;
+  const int ucol = u0 + 4 * iq;
+  floatx4 cst = {0.f, 0.f, 0.f, 0.f}, hpv = cst, gin[NW], bR[NW];
 #pragma unroll
-  for (int j = 0; j < kMaxIPT; j++) {
-    cst[j] = 0.f;
-    hpv[j] = 0.f;
-    const int it = tid + j * NT, u = it % U;
-#pragma unroll
-    for (int q = 0; q < NW; q++) {
-      bR[j][q] = (MODE == kGru && it < items) ? Wd[p.bR_off + q * H + u0 + u] : 0.f;
-      gin[j][q] = 0.f;
-    }
+  for (int q = 0; q < NW; q++) {
+    bR[q] = (MODE == kGru && has_item) ? ld4(Wd + p.bR_off + q * H + ucol) : floatx4{0.f, 0.f, 0.f, 0.f};
+    gin[q] = floatx4{0.f, 0.f, 0.f, 0.f};
   }
-  {  // prefetch the input projection of the first step
+  if (has_item) {  // prefetch the input projection of the first step
     const int t = d == 0 ? 0 : T - 1;
 #pragma unroll
-    for (int j = 0; j < kMaxIPT; j++) {
-      const int it = tid + j * NT;
-      if (it < items) {
-        const int n = it / U, u = it - n * U;
-#pragma unroll
-        for (int q = 0; q < NW; q++)
-          gin[j][q] = p.G[((long)t * N + n) * ldg + (long)d * NW * H + q * H + u0 + u];
-      }
-    }
+    for (int q = 0; q < NW; q++) gin[q] = ld4(p.G + ((long)t * N + in_) * ldg + (long)d * NW * H + q * H + ucol);
   }
   __syncthreads();
   int bad = 0;
@@ -311,7 +356,8 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec(RecParams p) {
       const auto rs = rsrc(p.y + (long)tp * N * ldy, step_bytes);
       for (int c0 = 0; c0 < KGW; c0 += CH) {
         u32x4 af[RT][CH];
-        load_frags<RT, CH>(af, rs, ldy, (long)d * H, c0, KG, N, p.sync, p.err, bad);
+        load_frags<RT, CH>(af, rs, ldy, (long)d * H, c0, KG, N, kSyncFlag, p.err, bad);
+        if (p.sync == kSyncData) settle_all<RT, CH>(af, rs, ldy, (long)d * H, c0, KG, N, p.err, bad);
 #pragma unroll
         for (int i = 0; i < CH; i++) {
           const int kg = w + 4 * (c0 + i);
@@ -319,7 +365,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec(RecParams p) {
 #pragma unroll
             for (int ct = 0; ct < kMaxCT; ct++) {
               if (ct < CT) {
-                const floatx4 b = *reinterpret_cast<const floatx4 *>(Rs + (ct * 16 + fr) * LDR + kg * 16 + fq * 4);
+                const floatx4 b = ld4(Rs + (ct * 16 + fr) * LDR + kg * 16 + fq * 4);
 #pragma unroll
                 for (int s = 0; s < 4; s++)
 #pragma unroll
@@ -342,64 +388,55 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec(RecParams p) {
           for (int r = 0; r < 4; r++)
             red[((long)w * p.Npad + rt * 16 + fq * 4 + r) * ncol + ct * 16 + fr] = acc[rt][ct][r];
     __syncthreads();
-    // pointwise cell update for owned (n, u); publish h_t first, then the rest
-    float act[kMaxIPT][NW], cnew[kMaxIPT];
+    floatx4 act[NW], cnew = {0.f, 0.f, 0.f, 0.f};
+    const long yrow = ((long)t * N + in_) * ldy + (long)d * H + ucol;
+    if (has_item) {
+      floatx4 rh[NW];
 #pragma unroll
-    for (int j = 0; j < kMaxIPT; j++) {
-      const int it = tid + j * NT;
-      if (it < items) {
-        const int n = it / U, u = it - n * U;
-        float rh[NW];
-#pragma unroll
-        for (int q = 0; q < NW; q++) {
-          const int c = q * U + u;
-          rh[q] = ((red[((long)0 * p.Npad + n) * ncol + c] + red[((long)1 * p.Npad + n) * ncol + c]) +
-                   red[((long)2 * p.Npad + n) * ncol + c]) + red[((long)3 * p.Npad + n) * ncol + c];
-        }
-        const long yrow = ((long)t * N + n) * ldy + (long)d * H + u0 + u;
-        float h;
-        if (MODE == kLstm) {
-          act[j][0] = sigm(gin[j][0] + rh[0]);
-          act[j][1] = sigm(gin[j][1] + rh[1]);
-          act[j][2] = tanhf(gin[j][2] + rh[2]);
-          act[j][3] = sigm(gin[j][3] + rh[3]);
-          const float cc = act[j][1] * cst[j] + act[j][0] * act[j][2];
-          cst[j] = cc;
-          cnew[j] = cc;
-          h = act[j][3] * tanhf(cc);
-        } else if (MODE == kGru) {
-          act[j][0] = sigm(gin[j][0] + rh[0] + bR[j][0]);
-          act[j][1] = sigm(gin[j][1] + rh[1] + bR[j][1]);
-          cnew[j] = rh[2] + bR[j][2];
-          act[j][2] = tanhf(gin[j][2] + act[j][0] * cnew[j]);
-          h = (1.f - act[j][1]) * act[j][2] + act[j][1] * hpv[j];
-          hpv[j] = h;
-        } else {
-          const float pre = gin[j][0] + rh[0];
-          h = MODE == kRelu ? fmaxf(pre, 0.f) : tanhf(pre);
-        }
-        publish(p.y + yrow, h);
+      for (int q = 0; q < NW; q++) {
+        const int c = q * U + 4 * iq;
+        rh[q] = ((ld4(red + ((long)0 * p.Npad + in_) * ncol + c) + ld4(red + ((long)1 * p.Npad + in_) * ncol + c)) +
+                 ld4(red + ((long)2 * p.Npad + in_) * ncol + c)) + ld4(red + ((long)3 * p.Npad + in_) * ncol + c);
       }
+      floatx4 h;
+      if (MODE == kLstm) {
+        act[0] = sigm4(gin[0] + rh[0]);
+        act[1] = sigm4(gin[1] + rh[1]);
+        act[2] = tanh4(gin[2] + rh[2]);
+        act[3] = sigm4(gin[3] + rh[3]);
+        cst = act[1] * cst + act[0] * act[2];
+        cnew = cst;
+        h = act[3] * tanh4(cst);
+      } else if (MODE == kGru) {
+        act[0] = sigm4(gin[0] + rh[0] + bR[0]);
+        act[1] = sigm4(gin[1] + rh[1] + bR[1]);
+        cnew = rh[2] + bR[2];
+        act[2] = tanh4(gin[2] + act[0] * cnew);
+        h = (1.f - act[1]) * act[2] + act[1] * hpv;
+        hpv = h;
+      } else {
+        const floatx4 pre = gin[0] + rh[0];
+        if (MODE == kRelu) {
+#pragma unroll
+          for (int i = 0; i < 4; i++) h[i] = fmaxf(pre[i], 0.f);
+        } else {
+          h = tanh4(pre);
+        }
+      }
+      publish4(rsrc(p.y + (long)t * N * ldy, step_bytes), (unsigned)(((long)in_ * ldy + (long)d * H + ucol) * 4), h);
     }
     if (p.sync == kSyncFlag) signal_flag(myflag, (unsigned)(k + 1));
+    if (has_item) {
+      const long grow = ((long)t * N + in_) * ldg + (long)d * NW * H + ucol;
+      if (MODE == kLstm || MODE == kGru) {
 #pragma unroll
-    for (int j = 0; j < kMaxIPT; j++) {
-      const int it = tid + j * NT;
-      if (it < items) {
-        const int n = it / U, u = it - n * U;
-        const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
-        const long yrow = ((long)t * N + n) * ldy + (long)d * H + u0 + u;
-        if (MODE != kRelu && MODE != kTanh) {
+        for (int q = 0; q < NW; q++) st4(p.G + grow + q * H, act[q]);
+        st4(p.aux + yrow, cnew);
+      }
+      if (k + 1 < T) {  // prefetch the next step's input projection
+        const int tn = d == 0 ? t + 1 : t - 1;
 #pragma unroll
-          for (int q = 0; q < NW; q++) p.G[grow + q * H] = act[j][q];
-          p.aux[yrow] = cnew[j];
-        }
-        if (k + 1 < T) {  // prefetch the next step's input projection
-          const int tn = d == 0 ? t + 1 : t - 1;
-#pragma unroll
-          for (int q = 0; q < NW; q++)
-            gin[j][q] = p.G[((long)tn * N + n) * ldg + (long)d * NW * H + q * H + u0 + u];
-        }
+        for (int q = 0; q < NW; q++) gin[q] = ld4(p.G + ((long)tn * N + in_) * ldg + (long)d * NW * H + q * H + ucol);
       }
     }
     __syncthreads();  // red[] is rewritten by the next step
@@ -430,39 +467,30 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec(RecParams p) {
     const int kk = idx / U, u = idx - kk * U;
     RT_s[u * LDK + kk] = R[(long)kk * H + u0 + u];
   }
-  const int items = N * U;
-  float carry[kMaxIPT];   // LSTM: dc carried to the previous step; GRU: dh*z direct term
-  float bsx[kMaxIPT][NW], bsh[kMaxIPT][NW];
-  // prefetched pointwise operands of the step about to be processed
-  float pdy[kMaxIPT], pg[kMaxIPT][NW], pa[kMaxIPT], pap[kMaxIPT];
+  const int Q = U / 4, items = N * Q;
+  const bool has_item = tid < items;
+  const int in_ = has_item ? tid / Q : 0, iq = has_item ? tid - in_ * Q : 0;
+  const int ucol = u0 + 4 * iq;
+  const floatx4 z4 = {0.f, 0.f, 0.f, 0.f};
+  floatx4 carry = z4;  // LSTM: dc carried to the previous step; GRU: dh*z direct term
+  floatx4 bsx[NW], bsh[NW], pg[NW], pdy = z4, pa = z4, pap = z4;
 #pragma unroll
-  for (int j = 0; j < kMaxIPT; j++) {
-    carry[j] = 0.f;
-#pragma unroll
-    for (int q = 0; q < NW; q++) bsx[j][q] = bsh[j][q] = pg[j][q] = 0.f;
-    pdy[j] = pa[j] = pap[j] = 0.f;
-  }
+  for (int q = 0; q < NW; q++) bsx[q] = bsh[q] = pg[q] = z4;
   auto prefetch = [&](int k) {
+    if (!has_item) return;
     const int t = d == 0 ? k : T - 1 - k, tp = d == 0 ? t - 1 : t + 1;
+    const long yrow = ((long)t * N + in_) * ldy + (long)d * H + ucol;
+    const long grow = ((long)t * N + in_) * ldg + (long)d * NW * H + ucol;
+    const long prow = ((long)tp * N + in_) * ldy + (long)d * H + ucol;
+    pdy = ld4(p.dy + yrow);
+    if (MODE == kLstm || MODE == kGru) {
 #pragma unroll
-    for (int j = 0; j < kMaxIPT; j++) {
-      const int it = tid + j * NT;
-      if (it < items) {
-        const int n = it / U, u = it - n * U;
-        const long yrow = ((long)t * N + n) * ldy + (long)d * H + u0 + u;
-        const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
-        const long prow = ((long)tp * N + n) * ldy + (long)d * H + u0 + u;
-        pdy[j] = p.dy[yrow];
-        if (MODE == kLstm || MODE == kGru) {
-#pragma unroll
-          for (int q = 0; q < NW; q++) pg[j][q] = p.G[grow + q * H];
-          pa[j] = p.aux[yrow];
-        }
-        if (MODE == kLstm) pap[j] = k > 0 ? p.aux[prow] : 0.f;
-        else if (MODE == kGru) pap[j] = k > 0 ? p.y[prow] : 0.f;
-        else pap[j] = p.y[yrow];
-      }
+      for (int q = 0; q < NW; q++) pg[q] = ld4(p.G + grow + q * H);
+      pa = ld4(p.aux + yrow);
     }
+    if (MODE == kLstm) pap = k > 0 ? ld4(p.aux + prow) : z4;
+    else if (MODE == kGru) pap = k > 0 ? ld4(p.y + prow) : z4;
+    else pap = ld4(p.y + yrow);
   };
   prefetch(T - 1);
   __syncthreads();
@@ -477,19 +505,20 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec(RecParams p) {
     const unsigned epoch = (unsigned)(T - k);   // number of steps published so far
     floatx4 acc[RT];
 #pragma unroll
-    for (int a = 0; a < RT; a++) acc[a] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int a = 0; a < RT; a++) acc[a] = z4;
     if (k < T - 1) {
       if (p.sync == kSyncFlag) wait_flags(p.flags + d * p.nwg, p.nwg, epoch - 1, p.err, bad, &bad_lds);
       const auto rs = rsrc(p.E + (long)tn * N * ldg, step_bytes);
       for (int c0 = 0; c0 < KGW; c0 += CH) {
         u32x4 af[RT][CH];
-        load_frags<RT, CH>(af, rs, ldg, (long)d * K, c0, KG, N, p.sync, p.err, bad);
+        load_frags<RT, CH>(af, rs, ldg, (long)d * K, c0, KG, N, kSyncFlag, p.err, bad);
+        if (p.sync == kSyncData) settle_all<RT, CH>(af, rs, ldg, (long)d * K, c0, KG, N, p.err, bad);
 #pragma unroll
         for (int i = 0; i < CH; i++) {
           const int kg = w + 4 * (c0 + i);
           if (kg < KG) {
-            floatx4 b = floatx4{0.f, 0.f, 0.f, 0.f};
-            if (fr < U) b = *reinterpret_cast<const floatx4 *>(RT_s + fr * LDK + kg * 16 + fq * 4);
+            floatx4 b = z4;
+            if (fr < U) b = ld4(RT_s + fr * LDK + kg * 16 + fq * 4);
 #pragma unroll
             for (int s = 0; s < 4; s++)
 #pragma unroll
@@ -504,88 +533,77 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec(RecParams p) {
 #pragma unroll
       for (int r = 0; r < 4; r++) red[((long)w * p.Npad + rt * 16 + fq * 4 + r) * 16 + fr] = acc[rt][r];
     __syncthreads();
-    float dx_keep[kMaxIPT][NW];
+    floatx4 dxk[NW];
+    const long grow = ((long)t * N + in_) * ldg + (long)d * NW * H + ucol;
+    const auto rsE = rsrc(p.E + (long)t * N * ldg, step_bytes);
+    const unsigned eoff = (unsigned)(((long)in_ * ldg + (long)d * NW * H + ucol) * 4);
+    if (has_item) {
+      const floatx4 dhr = ((ld4(red + ((long)0 * p.Npad + in_) * 16 + 4 * iq) + ld4(red + ((long)1 * p.Npad + in_) * 16 + 4 * iq)) +
+                           ld4(red + ((long)2 * p.Npad + in_) * 16 + 4 * iq)) + ld4(red + ((long)3 * p.Npad + in_) * 16 + 4 * iq);
+      floatx4 dh = pdy + dhr;
+      if (MODE == kLstm) {
+        const floatx4 ig = pg[0], fg = pg[1], gg = pg[2], og = pg[3];
+        const floatx4 tc = tanh4(pa);
+        const floatx4 dO = dh * tc;
+        const floatx4 dc = dh * og * (1.f - tc * tc) + carry;
+        const floatx4 dpi = dc * gg * ig * (1.f - ig);
+        const floatx4 dpf = dc * pap * fg * (1.f - fg);
+        const floatx4 dpg = dc * ig * (1.f - gg * gg);
+        const floatx4 dpo = dO * og * (1.f - og);
+        carry = dc * fg;
+        publish4(rsE, eoff, dpi);
+        publish4(rsE, eoff + 4 * H, dpf);
+        publish4(rsE, eoff + 8 * H, dpg);
+        publish4(rsE, eoff + 12 * H, dpo);
+        bsx[0] += dpi; bsx[1] += dpf; bsx[2] += dpg; bsx[3] += dpo;
+      } else if (MODE == kGru) {
+        dh += carry;
+        const floatx4 r = pg[0], z = pg[1], nn = pg[2];
+        const floatx4 dn = dh * (1.f - z), dz = dh * (pap - nn);
+        const floatx4 dpn = dn * (1.f - nn * nn);
+        const floatx4 dpr = dpn * pa * r * (1.f - r);
+        const floatx4 dpz = dz * z * (1.f - z);
+        carry = dh * z;
+        dxk[0] = dpr; dxk[1] = dpz; dxk[2] = dpn;
+        publish4(rsE, eoff, dpr);
+        publish4(rsE, eoff + 4 * H, dpz);
+        publish4(rsE, eoff + 8 * H, dpn * r);
+        bsx[0] += dpr; bsx[1] += dpz; bsx[2] += dpn;
+        bsh[0] += dpr; bsh[1] += dpz; bsh[2] += dpn * r;
+      } else {
+        floatx4 der;
 #pragma unroll
-    for (int j = 0; j < kMaxIPT; j++) {
-      const int it = tid + j * NT;
-      if (it < items) {
-        const int n = it / U, u = it - n * U;
-        const float dhr = ((red[((long)0 * p.Npad + n) * 16 + u] + red[((long)1 * p.Npad + n) * 16 + u]) +
-                           red[((long)2 * p.Npad + n) * 16 + u]) + red[((long)3 * p.Npad + n) * 16 + u];
-        const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
-        float dh = pdy[j] + dhr;
-        if (MODE == kLstm) {
-          const float ig = pg[j][0], fg = pg[j][1], gg = pg[j][2], og = pg[j][3];
-          const float cc = pa[j], cp = pap[j];
-          const float tc = tanhf(cc);
-          const float dO = dh * tc;
-          const float dc = dh * og * (1.f - tc * tc) + carry[j];
-          const float dpi = dc * gg * ig * (1.f - ig);
-          const float dpf = dc * cp * fg * (1.f - fg);
-          const float dpg = dc * ig * (1.f - gg * gg);
-          const float dpo = dO * og * (1.f - og);
-          carry[j] = dc * fg;
-          publish(p.E + grow, dpi);
-          publish(p.E + grow + H, dpf);
-          publish(p.E + grow + 2 * H, dpg);
-          publish(p.E + grow + 3 * H, dpo);
-          bsx[j][0] += dpi; bsx[j][1] += dpf; bsx[j][2] += dpg; bsx[j][3] += dpo;
-        } else if (MODE == kGru) {
-          dh += carry[j];
-          const float r = pg[j][0], z = pg[j][1], nn = pg[j][2];
-          const float rhn = pa[j], hp = pap[j];
-          const float dn = dh * (1.f - z), dz = dh * (hp - nn);
-          const float dpn = dn * (1.f - nn * nn);
-          const float dpr = dpn * rhn * r * (1.f - r);
-          const float dpz = dz * z * (1.f - z);
-          carry[j] = dh * z;
-          dx_keep[j][0] = dpr; dx_keep[j][1] = dpz; dx_keep[j][2] = dpn;
-          publish(p.E + grow, dpr);
-          publish(p.E + grow + H, dpz);
-          publish(p.E + grow + 2 * H, dpn * r);
-          bsx[j][0] += dpr; bsx[j][1] += dpz; bsx[j][2] += dpn;
-          bsh[j][0] += dpr; bsh[j][1] += dpz; bsh[j][2] += dpn * r;
-        } else {
-          const float h = pap[j];
-          const float der = MODE == kRelu ? (h > 0.f ? 1.f : 0.f) : (1.f - h * h);
-          const float dp = dh * der;
-          publish(p.E + grow, dp);
-          bsx[j][0] += dp;
-        }
+        for (int i = 0; i < 4; i++) der[i] = MODE == kRelu ? (pap[i] > 0.f ? 1.f : 0.f) : (1.f - pap[i] * pap[i]);
+        const floatx4 dp = dh * der;
+        publish4(rsE, eoff, dp);
+        bsx[0] += dp;
       }
     }
     if (p.sync == kSyncFlag) signal_flag(myflag, epoch);
-    if (MODE == kGru) {
+    if (MODE == kGru && has_item) {
 #pragma unroll
-      for (int j = 0; j < kMaxIPT; j++) {
-        const int it = tid + j * NT;
-        if (it < items) {
-          const int n = it / U, u = it - n * U;
-          const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
-          p.DX[grow] = dx_keep[j][0]; p.DX[grow + H] = dx_keep[j][1]; p.DX[grow + 2 * H] = dx_keep[j][2];
-        }
-      }
+      for (int q = 0; q < NW; q++) st4(p.DX + grow + q * H, dxk[q]);
     }
     if (k > 0) prefetch(k - 1);
     __syncthreads();
   }
   // bias partial sums: reduce over n in a fixed order through LDS
-  float *bs = red;  // reuse: [items][NW] for x and h parts (needs <= 2*1024*4 floats)
+  float *bs = red;  // reuse: [2][N][U][NW] floats
+  if (has_item) {
 #pragma unroll
-  for (int j = 0; j < kMaxIPT; j++) {
-    const int it = tid + j * NT;
-    if (it < items)
+    for (int q = 0; q < NW; q++)
 #pragma unroll
-      for (int q = 0; q < NW; q++) {
-        bs[(long)it * NW + q] = bsx[j][q];
-        bs[(long)items * NW + (long)it * NW + q] = (MODE == kGru) ? bsh[j][q] : bsx[j][q];
+      for (int i = 0; i < 4; i++) {
+        const long base = ((long)in_ * U + 4 * iq + i) * NW + q;
+        bs[base] = bsx[q][i];
+        bs[(long)N * U * NW + base] = (MODE == kGru) ? bsh[q][i] : bsx[q][i];
       }
   }
   __syncthreads();
   for (int q = tid; q < 2 * NW * U; q += NT) {
     const int part = q / (NW * U), rem = q - part * NW * U, gt = rem / U, u = rem - gt * U;
     float s = 0.f;
-    for (int n = 0; n < N; n++) s += bs[(long)part * items * NW + ((long)n * U + u) * NW + gt];
+    for (int n = 0; n < N; n++) s += bs[(long)part * N * U * NW + ((long)n * U + u) * NW + gt];
     p.bias[((long)d * 2 + part) * NW * H + gt * H + u0 + u] = s;
   }
   if (bad && tid == 0) atomicOr(p.err, 1u);
@@ -637,7 +655,7 @@ static int pick_fwd_u(const RnnDesc &d, int N) {
   int want = env_int("KCTC_FWD_U", 0);
   const int NW = d.nw();
   auto ok = [&](int U) {
-    if (U <= 0 || d.H % U || NW * U > 16 * kMaxCT || N * U > NT * kMaxIPT) return false;
+    if (U < 4 || U % 4 || d.H % U || NW * U > 16 * kMaxCT || N * U / 4 > NT) return false;
     if ((long)d.dirs * (d.H / U) > 256) return false;
     const int ncol = (NW * U + 15) / 16 * 16, Npad = (N + 15) / 16 * 16;
     const size_t lds = sizeof(float) * ((size_t)ncol * (d.H + 4) + 4 * (size_t)Npad * ncol);
@@ -646,7 +664,7 @@ static int pick_fwd_u(const RnnDesc &d, int N) {
   if (want && ok(want)) return want;
   // smallest U that keeps every workgroup resident (<= 256 = one per CU):
   // per-step MFMA latency falls with U (measured: U=4 < 8 < 16 on BLSTM-512)
-  for (int U : {4, 8, 16, 2, 1})
+  for (int U : {4, 8, 16})
     if (ok(U)) return U;
   return 0;
 }
@@ -655,7 +673,7 @@ static int pick_bwd_u(const RnnDesc &d, int N) {
   int want = env_int("KCTC_BWD_U", 0);
   const int K = d.nw() * d.H;
   auto ok = [&](int U) {
-    if (U <= 0 || U > 16 || d.H % U || N * U > NT * kMaxIPT) return false;
+    if (U < 4 || U % 4 || U > 16 || d.H % U || N * U / 4 > NT) return false;
     if ((long)d.dirs * (d.H / U) > 256) return false;
     const int Npad = (N + 15) / 16 * 16;
     const size_t lds = sizeof(float) * ((size_t)U * (K + 4) + std::max(4 * (size_t)Npad * 16,
@@ -663,7 +681,7 @@ static int pick_bwd_u(const RnnDesc &d, int N) {
     return lds <= 160 * 1024;
   };
   if (want && ok(want)) return want;
-  for (int U : {16, 8, 4, 2, 1})
+  for (int U : {16, 8, 4})
     if (ok(U)) return U;
   return 0;
 }
@@ -715,7 +733,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.ncol = (NW * U + 15) / 16 * 16; p.Npad = (N + 15) / 16 * 16;
     p.w = wl; p.pl_stride = pls; p.r_off = roff; p.bR_off = bR;
     p.G = R0 + lay.G; p.y = out; p.aux = R0 + lay.aux; p.err = err;
-    p.sync = env_int("KCTC_SYNC", kSyncFlag);
+    p.sync = env_int("KCTC_SYNC", kSyncData);
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, 4096, s));
     const size_t lds = sizeof(float) * ((size_t)p.ncol * (H + 4) + 4 * (size_t)p.Npad * p.ncol);
@@ -760,7 +778,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     p.bR_off = d.lin_offset(l * dirs, NW, true) - pl0;
     p.G = R0 + lay.G; p.y = const_cast<float *>(out); p.aux = R0 + lay.aux;
     p.dy = dcur; p.E = E; p.DX = DX; p.bias = R0 + lay.bias; p.err = err;
-    p.sync = env_int("KCTC_SYNC", kSyncFlag);
+    p.sync = env_int("KCTC_SYNC", kSyncData);
     if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, 4096, s));
