@@ -22,6 +22,13 @@ namespace kctc {
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 32, LDK = BK + 4, NT = 256;
+// LDS image per operand: "k-contiguous" [row][LDK] when the source is
+// k-contiguous (A row-major, B^T row-major), else "row-contiguous" [BK][LDM]
+// so that the 16-B global loads land with one ds_write_b128 instead of four
+// scalar transposing writes; fragments are then read with 4 ds_read_b32
+// (conflict-free: LDM = 132 puts lane groups fq=0/1 on bank halves 0-15/16-31).
+constexpr int LDM = BM + 4;
+constexpr int OPSZ = (BM * LDK > BK * LDM) ? BM * LDK : BK * LDM;
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 struct KParams {
@@ -84,15 +91,21 @@ __device__ __forceinline__ void store_tile(float *__restrict__ S, const floatx4 
       *reinterpret_cast<floatx4 *>(S + r * LDK + k) = reg[i];
     } else {
       int k = (t >> 5) + 8 * i, r = (t & 31) * 4;
-#pragma unroll
-      for (int j = 0; j < 4; j++) S[(r + j) * LDK + k] = reg[i][j];
+      *reinterpret_cast<floatx4 *>(S + k * LDM + r) = reg[i];
     }
   }
 }
 
+template <bool KC>
+__device__ __forceinline__ floatx4 frag(const float *S, int row, int k0) {
+  if (KC) return *reinterpret_cast<const floatx4 *>(S + row * LDK + k0);
+  return floatx4{S[(k0 + 0) * LDM + row], S[(k0 + 1) * LDM + row], S[(k0 + 2) * LDM + row],
+                 S[(k0 + 3) * LDM + row]};
+}
+
 template <bool TA, bool TB>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(KParams p) {
-  __shared__ __attribute__((aligned(16))) float lds[2][(BM + BN) * LDK];
+  __shared__ __attribute__((aligned(16))) float lds[2][2 * OPSZ];
   // XCD-aware bijective remap of the tile index
   const int id = blockIdx.x, tiles = p.tiles;
   const int q = tiles >> 3, rr = tiles & 7, xcd = id & 7, loc = id >> 3;
@@ -125,7 +138,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(KParams p) {
     load_tile<!TA>(Ab, p.lda, arows, 0, kbeg, kend, p.vecA, ra);
     load_tile<TB>(Bb, p.ldb, brows, 0, kbeg, kend, p.vecB, rb);
     store_tile<!TA>(lds[0], ra);
-    store_tile<TB>(lds[0] + BM * LDK, rb);
+    store_tile<TB>(lds[0] + OPSZ, rb);
   }
   __syncthreads();
   for (int kt = 0; kt < nk; kt++) {
@@ -136,16 +149,14 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(KParams p) {
       load_tile<!TA>(Ab, p.lda, arows, 0, k0, kend, p.vecA, ra);
       load_tile<TB>(Bb, p.ldb, brows, 0, k0, kend, p.vecB, rb);
     }
-    const float *sA = lds[cur], *sB = lds[cur] + BM * LDK;
+    const float *sA = lds[cur], *sB = lds[cur] + OPSZ;
 #pragma unroll
     for (int kg = 0; kg < BK / 16; kg++) {
       floatx4 fa[4], fb[4];
 #pragma unroll
-      for (int i = 0; i < 4; i++)
-        fa[i] = *reinterpret_cast<const floatx4 *>(sA + (wm + i * 16 + fr) * LDK + kg * 16 + fq * 4);
+      for (int i = 0; i < 4; i++) fa[i] = frag<!TA>(sA, wm + i * 16 + fr, kg * 16 + fq * 4);
 #pragma unroll
-      for (int j = 0; j < 4; j++)
-        fb[j] = *reinterpret_cast<const floatx4 *>(sB + (wn + j * 16 + fr) * LDK + kg * 16 + fq * 4);
+      for (int j = 0; j < 4; j++) fb[j] = frag<TB>(sB, wn + j * 16 + fr, kg * 16 + fq * 4);
 #pragma unroll
       for (int s = 0; s < 4; s++)
 #pragma unroll
@@ -156,7 +167,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(KParams p) {
     }
     if (more) {
       store_tile<!TA>(lds[cur ^ 1], ra);
-      store_tile<TB>(lds[cur ^ 1] + BM * LDK, rb);
+      store_tile<TB>(lds[cur ^ 1] + OPSZ, rb);
     }
     __syncthreads();
   }
