@@ -25,6 +25,7 @@ struct GemmArgs {
   long strideA = 0, strideB = 0, strideC = 0, strideBias = 0;
   int split_k = 1;
   float *ws = nullptr;
+  int max_blocks = 0;  // > 0: persistent grid of at most this many workgroups
 };
 
 void gemm_f32(hipStream_t stream, const GemmArgs &g);

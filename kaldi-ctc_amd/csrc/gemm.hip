@@ -104,14 +104,14 @@ __device__ __forceinline__ floatx4 frag(const float *S, int row, int k0) {
 }
 
 template <bool TA, bool TB>
-__global__ __launch_bounds__(NT, 2) void gemm_kernel(KParams p) {
-  __shared__ __attribute__((aligned(16))) float lds[2][2 * OPSZ];
-  // XCD-aware bijective remap of the tile index
-  const int id = blockIdx.x, tiles = p.tiles;
-  const int q = tiles >> 3, rr = tiles & 7, xcd = id & 7, loc = id >> 3;
-  const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+__device__ __forceinline__ void gemm_tile(const KParams &p, float (&lds)[2][2 * OPSZ], int id, int total) {
+  // XCD-aware bijective remap of the work index (id & 7 is the XCD as long as
+  // the grid is a multiple of 8 or covers all work items)
+  const int q = total >> 3, rr = total & 7, xcd = id & 7, loc = id >> 3;
+  const int wl = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  const int bz = wl / p.tiles, wg = wl - bz * p.tiles;
   const int tn = wg % p.gx, tm = wg / p.gx;
-  const int bz = blockIdx.z, b = bz % p.batch, ks = bz / p.batch;
+  const int b = bz % p.batch, ks = bz / p.batch;
   const float *A = p.A + (long)b * p.strideA;
   const float *B = p.B + (long)b * p.strideB;
   const int m0 = tm * BM, n0 = tn * BN;
@@ -214,6 +214,16 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(KParams p) {
     }
 }
 
+// One work item = (tile, batch, k-slab).  The grid either covers every item or
+// (max_blocks) is a persistent multiple of 8 that strides over them, leaving
+// CUs free for a concurrently running recurrence.
+template <bool TA, bool TB>
+__global__ __launch_bounds__(NT, 2) void gemm_kernel(KParams p) {
+  __shared__ __attribute__((aligned(16))) float lds[2][2 * OPSZ];
+  const int total = p.tiles * p.batch * p.split;
+  for (int id = blockIdx.x; id < total; id += gridDim.x) gemm_tile<TA, TB>(p, lds, id, total);
+}
+
 __global__ __launch_bounds__(256) void splitk_reduce(KParams p) {
   const long total = (long)p.batch * p.M * p.N;
   const long MN = (long)p.M * p.N;
@@ -282,7 +292,10 @@ void gemm_f32(hipStream_t stream, const GemmArgs &g) {
   };
   p.vecA = aligned(g.A, g.lda, g.strideA);
   p.vecB = aligned(g.B, g.ldb, g.strideB);
-  dim3 grid(p.tiles, 1, p.batch * p.split);
+  const int total = p.tiles * p.batch * p.split;
+  int blocks = total;
+  if (g.max_blocks > 0 && total > g.max_blocks) blocks = std::max(8, g.max_blocks / 8 * 8);
+  dim3 grid(blocks);
   if (!g.transA && !g.transB) hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(NT), 0, stream, p);
   else if (!g.transA && g.transB) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(NT), 0, stream, p);
   else if (g.transA && !g.transB) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, dim3(NT), 0, stream, p);

@@ -28,7 +28,9 @@ DevBuf::~DevBuf() {
 void DevBuf::ensure(size_t b) {
   if (b <= bytes && p) return;
   if (p) {
-    KCTC_HIP_CHECK(hipStreamSynchronize(CuDevice::Instantiate().stream));
+    auto &d = CuDevice::Instantiate();
+    KCTC_HIP_CHECK(hipStreamSynchronize(d.stream));
+    if (d.side) KCTC_HIP_CHECK(hipStreamSynchronize(d.side));
     KCTC_HIP_CHECK(hipFree(p));
     p = nullptr;
   }
@@ -49,8 +51,23 @@ CuDevice &CuDevice::Instantiate() {
   return dev;
 }
 
-void CuDevice::Begin(const char *family) {
+void CuDevice::Fork() {
+  if (!side) return;
+  if (!fork_ev) KCTC_HIP_CHECK(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
+  KCTC_HIP_CHECK(hipEventRecord(fork_ev, stream));
+  KCTC_HIP_CHECK(hipStreamWaitEvent(side, fork_ev, 0));
+}
+
+void CuDevice::Join() {
+  if (!side) return;
+  if (!join_ev) KCTC_HIP_CHECK(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
+  KCTC_HIP_CHECK(hipEventRecord(join_ev, side));
+  KCTC_HIP_CHECK(hipStreamWaitEvent(stream, join_ev, 0));
+}
+
+void CuDevice::Begin(const char *family, hipStream_t s) {
   if (!profiling) return;
+  if (!s) s = stream;
   if (pool.size() < 2) {
     for (int i = 0; i < 64; i++) {
       hipEvent_t e;
@@ -62,14 +79,15 @@ void CuDevice::Begin(const char *family) {
   sp.family = family;
   sp.a = pool.back(); pool.pop_back();
   sp.b = pool.back(); pool.pop_back();
-  KCTC_HIP_CHECK(hipEventRecord(sp.a, stream));
+  sp.s = s;
+  KCTC_HIP_CHECK(hipEventRecord(sp.a, s));
   open.push_back(spans.size());
   spans.push_back(sp);
 }
 
 void CuDevice::End() {
   if (!profiling || open.empty()) return;
-  KCTC_HIP_CHECK(hipEventRecord(spans[open.back()].b, stream));
+  KCTC_HIP_CHECK(hipEventRecord(spans[open.back()].b, spans[open.back()].s));
   open.pop_back();
 }
 
@@ -90,17 +108,17 @@ void CuDevice::Collect() {
 
 void prof_begin(hipStream_t s, const char *family) {
   auto &d = nnet2::CuDevice::Instantiate();
-  if (d.profiling && s == d.stream) d.Begin(family);
+  if (d.profiling && (s == d.stream || (s && s == d.side))) d.Begin(family, s);
 }
 void prof_end(hipStream_t s) {
   auto &d = nnet2::CuDevice::Instantiate();
-  if (d.profiling && s == d.stream) d.End();
+  if (d.profiling && (s == d.stream || (s && s == d.side))) d.End();
 }
 
 namespace nnet2 {
 
 struct ProfScope {
-  explicit ProfScope(const char *f) { CuDevice::Instantiate().Begin(f); }
+  explicit ProfScope(const char *f, hipStream_t s = nullptr) { CuDevice::Instantiate().Begin(f, s); }
   ~ProfScope() { CuDevice::Instantiate().End(); }
 };
 
@@ -387,13 +405,29 @@ void CuDNNRecurrentComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
   if (to_update_in) {
     auto *to_update = dynamic_cast<CuDNNRecurrentComponent *>(to_update_in);
     if (!to_update) throw std::invalid_argument("CuDNNRecurrentComponent: bad to_update");
-    // filter_params_grad_ is zeroed, then cudnnRNNBackwardWeights accumulates
-    KCTC_HIP_CHECK(hipMemsetAsync(to_update->grad_.p, 0, sizeof(float) * NumParameters(), S()));
-    ProfScope ps("layer_rnn_backward_weights");
-    int st = rnn_backward_weights(desc_, S(), T, N, in_value.Data(), out_value.Data(), workspace_.p,
-                                  workspace_.bytes, to_update->grad_.f(), reserve_.p, reserve_.bytes);
+    // filter_params_grad_ is zeroed, then cudnnRNNBackwardWeights accumulates.
+    // On the side stream (when there is one) so the weight GEMMs overlap the
+    // next component's backward recurrence; only this component's reserve,
+    // workspace and gradient are touched there.
+    auto &dev = CuDevice::Instantiate();
+    hipStream_t ws = dev.side ? dev.side : S();
+    dev.Fork();
+    to_update->grad_stream_ = ws;
+    KCTC_HIP_CHECK(hipMemsetAsync(to_update->grad_.p, 0, sizeof(float) * NumParameters(), ws));
+    ProfScope ps("layer_rnn_backward_weights", ws);
+    int st = rnn_backward_weights(desc_, ws, T, N, in_value.Data(), out_value.Data(), workspace_.p,
+                                  workspace_.bytes, to_update->grad_.f(), reserve_.p, reserve_.bytes,
+                                  dev.side ? side_gemm_blocks() : 0);
     if (st) throw std::runtime_error("rnn_backward_weights failed: " + std::to_string(st));
   }
+}
+
+hipStream_t UpdatableComponent::GradStream() const { return grad_stream_ ? grad_stream_ : S(); }
+
+int CuDNNRecurrentComponent::side_gemm_blocks() const {
+  const char *e = getenv("KCTC_SIDE_BLOCKS");
+  if (e && *e) return atoi(e);
+  return 192;
 }
 
 void CuDNNRecurrentComponent::ApplyUpdate() {
@@ -976,11 +1010,12 @@ void NnetCtcUpdater::Backprop(int T, int N) {  // :320-348
     comp.Backprop(chunk_info_[c], chunk_info_[c + 1], in, outv, od, to_update, in_deriv);
     if (comp.IsUpdatable()) {
       auto *u = static_cast<UpdatableComponent *>(&comp);
-      if (exchange_) exchange_->GradReady(c, u->GradData(), u->NumParameters());
+      if (exchange_) exchange_->GradReady(c, u->GradData(), u->NumParameters(), u->GradStream());
       updated.push_back(c);
     }
     if (need_in_deriv && !comp.IsIdentityForward()) std::swap(cur, other);
   }
+  CuDevice::Instantiate().Join();
   if (exchange_) exchange_->Finish();
   for (int c : updated) {
     ProfScope ps("update");

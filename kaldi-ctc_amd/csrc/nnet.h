@@ -93,14 +93,20 @@ struct ChunkInfo {  // src/nnet2/nnet-component.h:72-146 (contiguous case)
 struct CuDevice {
   int device = 0;
   hipStream_t stream = nullptr;
-  // optional per-kernel-family timing (hipEvents on `stream`)
+  // Lower-priority stream for the weight-gradient GEMMs, which then overlap
+  // the next component's backward recurrence (nullptr: everything on `stream`).
+  hipStream_t side = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  void Fork();  // side waits for the work queued so far on stream
+  void Join();  // stream waits for the work queued so far on side
+  // optional per-kernel-family timing (hipEvents on `stream` / `side`)
   bool profiling = false;
-  struct Span { std::string family; hipEvent_t a, b; };
+  struct Span { std::string family; hipEvent_t a, b; hipStream_t s; };
   std::vector<Span> spans;
   std::vector<size_t> open;  // indices of spans begun but not ended (LIFO)
   std::vector<hipEvent_t> pool;
   std::map<std::string, std::pair<double, int>> prof;  // family -> (ms, launches)
-  void Begin(const char *family);
+  void Begin(const char *family, hipStream_t s = nullptr);
   void End();
   void Collect();  // after a stream sync
   static CuDevice &Instantiate();
@@ -150,10 +156,13 @@ class UpdatableComponent : public Component {
   virtual void UnVectorize(const float *host) = 0;
   // gradient produced by the last Backprop (device), in Vectorize order
   virtual float *GradData() = 0;
+  // stream on which GradData() was produced (the exchange waits on it)
+  hipStream_t GradStream() const;
   virtual void ApplyUpdate() = 0;  // params += lr * (clipped) grad
 
  protected:
   float learning_rate_ = 0.001f;
+  hipStream_t grad_stream_ = nullptr;  // nullptr: the device's compute stream
 };
 
 class SpliceComponent : public Component {
@@ -200,6 +209,9 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   float *GradData() override { return grad_.f(); }
   void ApplyUpdate() override;
   unsigned *DeviceError() const { return err_; }
+  // workgroup cap of the side-stream weight GEMMs: the CUs left over by the
+  // backward recurrence (KCTC_SIDE_BLOCKS overrides)
+  int side_gemm_blocks() const;
   const RnnDesc &Desc() const { return desc_; }
   void SetMiniBatch(int n) const { mini_batch_ = n; }  // Init(mini_batch) on change
 
@@ -304,7 +316,7 @@ class Nnet {
 class GradExchange {
  public:
   virtual ~GradExchange() = default;
-  virtual void GradReady(int component, float *grad, long n) = 0;  // on the compute stream
+  virtual void GradReady(int component, float *grad, long n, hipStream_t producer) = 0;
   virtual void Finish() = 0;  // compute stream waits for every launched all-reduce
   virtual int WorldSize() const = 0;
 };

@@ -48,6 +48,6 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
                       size_t ws_bytes, void *reserve, size_t res_bytes, unsigned *err);
 int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *y, void *workspace, size_t ws_bytes, float *dw,
-                         void *reserve, size_t res_bytes);
+                         void *reserve, size_t res_bytes, int max_blocks = 0);
 
 }  // namespace kctc

@@ -104,7 +104,6 @@ constexpr unsigned kSent = 0xFFFFFFFFu;
 constexpr int kSpinLimit = 1 << 21;
 constexpr int kMaxRT = 4;  // N <= 64 (four 16-row MFMA tiles)
 constexpr int kMaxCT = 4;  // <= 64 gate columns per workgroup
-constexpr int kMaxIPT = 4;  // (N * U / 4 <= 256 pointwise quads: one per thread)
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -815,7 +814,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
 // ---------------------------------------------------------------------------
 int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *y, void *workspace, size_t ws_bytes, float *dw,
-                         void *reserve, size_t res_bytes) {
+                         void *reserve, size_t res_bytes, int max_blocks) {
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
   if (res_bytes < sizeof(float) * (size_t)lay.total) return KRNN_BAD_PARAM;
   if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
@@ -843,6 +842,7 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     g.batch = dirs; g.strideA = G4; g.strideB = 0; g.strideC = pls;
     g.split_k = gemm_pick_split(g.M, g.N, g.K, dirs);
     g.ws = ws;
+    g.max_blocks = max_blocks;
     {
       ProfSpan ps(s, "gemm_bwd_w");
       gemm_f32(s, g);
@@ -862,6 +862,7 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       r.strideC = pls;
       r.split_k = gemm_pick_split(r.M, r.N, r.K, dirs);
       r.ws = ws;
+      r.max_blocks = max_blocks;
       ProfSpan ps(s, "gemm_bwd_r");
       gemm_f32(s, r);
     }

@@ -46,8 +46,8 @@ class RcclExchange : public kctc::nnet2::GradExchange {
     (void)hipEventDestroy(ready_);
     (void)hipEventDestroy(done_);
   }
-  void GradReady(int, float *grad, long n) override {
-    KCTC_HIP_CHECK(hipEventRecord(ready_, compute_));
+  void GradReady(int, float *grad, long n, hipStream_t producer) override {
+    KCTC_HIP_CHECK(hipEventRecord(ready_, producer));
     KCTC_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ready_, 0));
     if (ncclAllReduce(grad, grad, (size_t)n, ncclFloat, ncclSum, comm_, comm_stream_) != ncclSuccess)
       throw std::runtime_error("ncclAllReduce failed");
@@ -73,15 +73,33 @@ struct kctcNnetImpl {
   kctc::nnet2::Nnet nnet;
   kctc::nnet2::NnetCtcUpdater trainer{&nnet, true};
   kctc::nnet2::NnetCtcUpdater evaluator{&nnet, false};
+  hipStream_t side = nullptr;
   RcclExchange *dp = nullptr;
   ~kctcNnetImpl() {
     delete dp;
+    if (stream) (void)hipStreamSynchronize(stream);
+    if (side) (void)hipStreamSynchronize(side);
+    auto &d = CuDevice::Instantiate();
+    if (d.stream == stream) d.stream = nullptr;
+    if (d.side == side) d.side = nullptr;
     if (stream) (void)hipStreamDestroy(stream);
+    if (side) (void)hipStreamDestroy(side);
+  }
+  // compute stream at the highest priority (the latency-bound recurrences),
+  // the weight-gradient side stream at the lowest; KCTC_OVERLAP=0 keeps
+  // everything on one stream
+  void create_streams() {
+    int lo = 0, hi = 0;
+    KCTC_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    KCTC_HIP_CHECK(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, hi));
+    const char *e = getenv("KCTC_OVERLAP");
+    if (!(e && *e == '0')) KCTC_HIP_CHECK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, lo));
   }
   void activate() {
     KCTC_HIP_CHECK(hipSetDevice(device));
     CuDevice::Instantiate().device = device;
     CuDevice::Instantiate().stream = stream;
+    CuDevice::Instantiate().side = side;
   }
 };
 
@@ -119,7 +137,7 @@ int kctc_nnet_create(kctcNnet_t *out, const char *config, unsigned long long see
     try {
       n->device = device;
       KCTC_HIP_CHECK(hipSetDevice(device));
-      KCTC_HIP_CHECK(hipStreamCreateWithFlags(&n->stream, hipStreamNonBlocking));
+      n->create_streams();
       n->activate();
       kctc::nnet2::Rng rng(seed);
       n->nnet.Init(config ? config : "", rng);
@@ -258,7 +276,7 @@ int kctc_nnet_read(kctcNnet_t *out, const char *path, int device) {
     try {
       n->device = device;
       KCTC_HIP_CHECK(hipSetDevice(device));
-      KCTC_HIP_CHECK(hipStreamCreateWithFlags(&n->stream, hipStreamNonBlocking));
+      n->create_streams();
       n->activate();
       std::ifstream is(path);
       if (!is) throw std::runtime_error(std::string("cannot open ") + path);
