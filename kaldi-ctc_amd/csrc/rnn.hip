@@ -32,7 +32,10 @@
 // sequences run the full T steps (no masking), weights in the opaque layout of
 // nnet-cudnn-component.cc:327-413 (see RnnDesc::lin_offset).
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
+#include <string>
+#include <vector>
 
 #include "common.h"
 #include "elementwise.h"
@@ -161,7 +164,19 @@ struct RecParams {
   unsigned *flags;  // flag protocol: [dirs][nwg] step epochs, zeroed before launch
   unsigned *err;
   int sync;         // kSyncData / kSyncFlag
+  unsigned long long *trace;  // optional: [kTraceSteps][grid][8] s_memrealtime stamps
 };
+
+// Phase stamps of the first kTraceSteps steps (thread 0 of every workgroup;
+// 100 MHz constant clock), only when the host passes a trace buffer
+// (KCTC_REC_TRACE): 0 step start, 1 flags seen, 2 operand loads landed,
+// 3 MFMA + K reduction done, 4 published (+ flag), 5 step end.
+constexpr int kTraceSteps = 256;
+#define REC_TRACE(kk, ph)                                                                 \
+  do {                                                                                    \
+    if (p.trace && threadIdx.x == 0 && (kk) < kTraceSteps)                                \
+      p.trace[((long)(kk) * gridDim.x + blockIdx.x) * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 
 // Hand-off protocols (selected per launch; both placement-independent):
 //  kSyncData: the payload is the flag (sentinel-filled buffer, sc1 4-B stores,
@@ -350,13 +365,19 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec(RecParams p) {
     for (int a = 0; a < RT; a++)
 #pragma unroll
       for (int b = 0; b < kMaxCT; b++) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+    REC_TRACE(k, 0);
     if (k > 0) {
       if (p.sync == kSyncFlag) wait_flags(p.flags + d * p.nwg, p.nwg, (unsigned)k, p.err, bad, &bad_lds);
+      REC_TRACE(k, 1);
       const auto rs = rsrc(p.y + (long)tp * N * ldy, step_bytes);
       for (int c0 = 0; c0 < KGW; c0 += CH) {
         u32x4 af[RT][CH];
         load_frags<RT, CH>(af, rs, ldy, (long)d * H, c0, KG, N, kSyncFlag, p.err, bad);
         if (p.sync == kSyncData) settle_all<RT, CH>(af, rs, ldy, (long)d * H, c0, KG, N, p.err, bad);
+        if (p.trace) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          REC_TRACE(k, 2);
+        }
 #pragma unroll
         for (int i = 0; i < CH; i++) {
           const int kg = w + 4 * (c0 + i);
@@ -387,6 +408,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec(RecParams p) {
           for (int r = 0; r < 4; r++)
             red[((long)w * p.Npad + rt * 16 + fq * 4 + r) * ncol + ct * 16 + fr] = acc[rt][ct][r];
     __syncthreads();
+    REC_TRACE(k, 3);
     floatx4 act[NW], cnew = {0.f, 0.f, 0.f, 0.f};
     const long yrow = ((long)t * N + in_) * ldy + (long)d * H + ucol;
     if (has_item) {
@@ -425,6 +447,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec(RecParams p) {
       publish4(rsrc(p.y + (long)t * N * ldy, step_bytes), (unsigned)(((long)in_ * ldy + (long)d * H + ucol) * 4), h);
     }
     if (p.sync == kSyncFlag) signal_flag(myflag, (unsigned)(k + 1));
+    REC_TRACE(k, 4);
     if (has_item) {
       const long grow = ((long)t * N + in_) * ldg + (long)d * NW * H + ucol;
       if (MODE == kLstm || MODE == kGru) {
@@ -439,6 +462,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec(RecParams p) {
       }
     }
     __syncthreads();  // red[] is rewritten by the next step
+    REC_TRACE(k, 5);
   }
   if (bad && tid == 0) atomicOr(p.err, 1u);
 }
@@ -505,13 +529,20 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec(RecParams p) {
     floatx4 acc[RT];
 #pragma unroll
     for (int a = 0; a < RT; a++) acc[a] = z4;
+    const int ks = T - 1 - k;
+    REC_TRACE(ks, 0);
     if (k < T - 1) {
       if (p.sync == kSyncFlag) wait_flags(p.flags + d * p.nwg, p.nwg, epoch - 1, p.err, bad, &bad_lds);
+      REC_TRACE(ks, 1);
       const auto rs = rsrc(p.E + (long)tn * N * ldg, step_bytes);
       for (int c0 = 0; c0 < KGW; c0 += CH) {
         u32x4 af[RT][CH];
         load_frags<RT, CH>(af, rs, ldg, (long)d * K, c0, KG, N, kSyncFlag, p.err, bad);
         if (p.sync == kSyncData) settle_all<RT, CH>(af, rs, ldg, (long)d * K, c0, KG, N, p.err, bad);
+        if (p.trace) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          REC_TRACE(ks, 2);
+        }
 #pragma unroll
         for (int i = 0; i < CH; i++) {
           const int kg = w + 4 * (c0 + i);
@@ -532,6 +563,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec(RecParams p) {
 #pragma unroll
       for (int r = 0; r < 4; r++) red[((long)w * p.Npad + rt * 16 + fq * 4 + r) * 16 + fr] = acc[rt][r];
     __syncthreads();
+    REC_TRACE(ks, 3);
     floatx4 dxk[NW];
     const long grow = ((long)t * N + in_) * ldg + (long)d * NW * H + ucol;
     const auto rsE = rsrc(p.E + (long)t * N * ldg, step_bytes);
@@ -579,12 +611,14 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec(RecParams p) {
       }
     }
     if (p.sync == kSyncFlag) signal_flag(myflag, epoch);
+    REC_TRACE(ks, 4);
     if (MODE == kGru && has_item) {
 #pragma unroll
       for (int q = 0; q < NW; q++) st4(p.DX + grow + q * H, dxk[q]);
     }
     if (k > 0) prefetch(k - 1);
     __syncthreads();
+    REC_TRACE(ks, 5);
   }
   // bias partial sums: reduce over n in a fixed order through LDS
   float *bs = red;  // reuse: [2][N][U][NW] floats
@@ -643,6 +677,41 @@ static void launch_rec(bool fwd, int mode, const RecParams &p, dim3 grid, size_t
     default: launch_mode<kTanh>(fwd, p, grid, lds, s); break;
   }
 }
+
+// KCTC_REC_TRACE=<dir>: trace the first forward and the first backward
+// recurrence launch of the process into <dir>/rec_{fwd,bwd}.bin
+// (int32 header {grid, steps, nwg, T} then [steps][grid][8] uint64 stamps).
+struct RecTrace {
+  unsigned long long *dev = nullptr;
+  size_t n = 0;
+  bool arm(const char *tag, int grid) {
+    static bool done_fwd = false, done_bwd = false;
+    const char *dir = getenv("KCTC_REC_TRACE");
+    if (!dir || !*dir) return false;
+    bool &done = tag[0] == 'f' ? done_fwd : done_bwd;
+    if (done) return false;
+    done = true;
+    n = (size_t)kTraceSteps * grid * 8;
+    KCTC_HIP_CHECK(hipMalloc(&dev, n * sizeof(unsigned long long)));
+    KCTC_HIP_CHECK(hipMemset(dev, 0, n * sizeof(unsigned long long)));
+    return true;
+  }
+  void dump(const char *tag, hipStream_t s, int grid, int nwg, int T) {
+    if (!dev) return;
+    KCTC_HIP_CHECK(hipStreamSynchronize(s));
+    std::vector<unsigned long long> h(n);
+    KCTC_HIP_CHECK(hipMemcpy(h.data(), dev, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    (void)hipFree(dev);
+    dev = nullptr;
+    std::string path = std::string(getenv("KCTC_REC_TRACE")) + "/rec_" + tag + ".bin";
+    FILE *f = fopen(path.c_str(), "wb");
+    if (!f) return;
+    int hdr[4] = {grid, kTraceSteps, nwg, T};
+    fwrite(hdr, sizeof(int), 4, f);
+    fwrite(h.data(), sizeof(unsigned long long), n, f);
+    fclose(f);
+  }
+};
 
 static int env_int(const char *name, int dflt) {
   const char *v = getenv(name);
@@ -732,14 +801,19 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.ncol = (NW * U + 15) / 16 * 16; p.Npad = (N + 15) / 16 * 16;
     p.w = wl; p.pl_stride = pls; p.r_off = roff; p.bR_off = bR;
     p.G = R0 + lay.G; p.y = out; p.aux = R0 + lay.aux; p.err = err;
-    p.sync = env_int("KCTC_SYNC", kSyncData);
+    p.sync = env_int("KCTC_SYNC_FWD", env_int("KCTC_SYNC", kSyncData));
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, 4096, s));
     const size_t lds = sizeof(float) * ((size_t)p.ncol * (H + 4) + 4 * (size_t)p.Npad * p.ncol);
     const dim3 grid(dirs * p.nwg);
-    ProfSpan ps(s, "rnn_fwd_rec");
-    launch_rec(true, d.mode, p, grid, lds, s);
+    RecTrace tr;
+    if (tr.arm("fwd", grid.x)) p.trace = tr.dev;
+    {
+      ProfSpan ps(s, "rnn_fwd_rec");
+      launch_rec(true, d.mode, p, grid, lds, s);
+    }
     KCTC_HIP_CHECK(hipGetLastError());
+    tr.dump("fwd", s, grid.x, p.nwg, T);
     in = out;
   }
   return KRNN_OK;
@@ -777,18 +851,21 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     p.bR_off = d.lin_offset(l * dirs, NW, true) - pl0;
     p.G = R0 + lay.G; p.y = const_cast<float *>(out); p.aux = R0 + lay.aux;
     p.dy = dcur; p.E = E; p.DX = DX; p.bias = R0 + lay.bias; p.err = err;
-    p.sync = env_int("KCTC_SYNC", kSyncData);
+    p.sync = env_int("KCTC_SYNC_BWD", env_int("KCTC_SYNC", kSyncFlag));
     if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, 4096, s));
     const size_t lds = sizeof(float) * ((size_t)U * (NW * H + 4) +
                                         std::max(4 * (size_t)p.Npad * 16, (size_t)2 * N * U * NW));
     const dim3 grid(dirs * p.nwg);
+    RecTrace tr;
+    if (tr.arm("bwd", grid.x)) p.trace = tr.dev;
     {
       ProfSpan ps(s, "rnn_bwd_rec");
       launch_rec(false, d.mode, p, grid, lds, s);
     }
     KCTC_HIP_CHECK(hipGetLastError());
+    tr.dump("bwd", s, grid.x, p.nwg, T);
     // dx_l = sum_dir DX_dir W_dir   (lower layer's dy, or the caller's dx)
     float *dxl = (l == 0) ? dx : res + lay.per_layer * (l - 1) + lay.dout;
     if (dxl) {

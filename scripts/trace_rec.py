@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""Summarise a KCTC_REC_TRACE recurrence trace (rec_fwd.bin / rec_bwd.bin).
+
+Per phase: median over steps 8..steps-1 and over workgroups of the phase
+duration (us, 100 MHz stamps); plus the hand-off latency = consumer
+'flags seen' minus the LAST producer's 'published' of the previous step."""
+import sys
+import numpy as np
+
+def main(path):
+    raw = open(path, "rb").read()
+    grid, steps, nwg, T = np.frombuffer(raw[:16], dtype=np.int32)
+    tr = np.frombuffer(raw[16:], dtype=np.uint64).reshape(steps, grid, 8).astype(np.int64)
+    steps = min(steps, T)
+    tr = tr[:steps]
+    us = 1e-2  # 100 MHz
+    names = ["start->flags", "flags->loads", "loads->reduced", "reduced->published", "published->end"]
+    sl = slice(8, steps)
+    print(f"{path}: grid={grid} nwg={nwg} T={T} steps traced={steps}")
+    for i, nm in enumerate(names):
+        d = (tr[sl, :, i + 1] - tr[sl, :, i]) * us
+        print(f"  {nm:22s} median {np.median(d):7.3f}  p90 {np.percentile(d, 90):7.3f}")
+    step = (tr[9:steps, :, 0] - tr[8:steps - 1, :, 0]) * us
+    print(f"  step period            median {np.median(step):7.3f}  p90 {np.percentile(step, 90):7.3f}")
+    dirs = grid // nwg
+    lat = []
+    for d in range(dirs):
+        wg = slice(d * nwg, (d + 1) * nwg)
+        last_pub = tr[8:steps - 1, wg, 4].max(axis=1)
+        first_pub = tr[8:steps - 1, wg, 4].min(axis=1)
+        seen = tr[9:steps, wg, 1]
+        lat.append((seen - last_pub[:, None]) * us)
+        skew = (last_pub - first_pub) * us
+        print(f"  dir {d}: publish skew (last-first producer) median {np.median(skew):.3f}")
+    lat = np.concatenate([l.ravel() for l in lat])
+    print(f"  handoff last-publish->seen median {np.median(lat):7.3f}  p10 {np.percentile(lat, 10):7.3f}  p90 {np.percentile(lat, 90):7.3f}")
+
+if __name__ == "__main__":
+    for p in sys.argv[1:]:
+        main(p)
