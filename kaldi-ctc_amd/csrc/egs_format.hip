@@ -1,0 +1,109 @@
+// egs_format.hip -- FormatNnetInput on the GPU: CompressedMatrix decode of
+// every example of a minibatch straight into the time-major network input
+// [T_max*N][feat_dim + spk_dim] (row t*N+n, zero rows for t >= T_n).
+//
+// Reference: FormatNnetInput (src/ctc/ctc-nnet-update.cc:351-424) decodes on
+// the CPU in the background thread (CompressedMatrix::CopyToMat,
+// src/matrix/compressed-matrix.cc:438-481) and then copies ~5 MB per
+// minibatch host->device; here the ~4x smaller compressed bytes travel and the
+// decode is one HBM-bound launch.
+//
+// Grid (ceil(T_max/R), N): a workgroup decodes R frames of one example.
+// Format 1 (column-major bytes + per-column percentiles): each wave reads 64
+// consecutive bytes of one column (coalesced), decodes with the column's
+// percentiles (LDS) into an LDS tile [R][cols+1], then the tile is written
+// out row-major (contiguous rows).  Format 2 (uint16 row-major) decodes in
+// place.  The arithmetic is the reference's to the bit: float products and
+// sums rounded separately (no contraction), the byte ramps in double.
+#include "common.h"
+#include "egs.h"
+
+#pragma clang fp contract(off)
+
+namespace kctc {
+namespace egs {
+namespace {
+
+__device__ __forceinline__ float dev_from_u16(float mn, float range, unsigned v) {
+  const float a = range * 1.52590218966964e-05F;
+  return mn + a * (float)v;
+}
+
+__device__ __forceinline__ float dev_from_u8(float p0, float p25, float p75, float p100, unsigned v) {
+  if (v <= 64) return (float)((double)p0 + (double)((p25 - p0) * (float)v) * (1 / 64.0));
+  if (v <= 192) return (float)((double)p25 + (double)((p75 - p25) * (float)(v - 64)) * (1 / 128.0));
+  return (float)((double)p75 + (double)((p100 - p75) * (float)(v - 192)) * (1 / 63.0));
+}
+
+__global__ __launch_bounds__(256) void egs_format_kernel(const uint8_t *__restrict__ blob, int N, int T_max,
+                                                         int Df, int Ds, int R, float *__restrict__ out) {
+  extern __shared__ float lds[];
+  const int n = blockIdx.y, t0 = blockIdx.x * R, tid = threadIdx.x;
+  const EgDesc d = reinterpret_cast<const EgDesc *>(blob)[n];
+  const int Dt = Df + Ds, LD = Df + 1;
+  const int rows_here = min(R, T_max - t0);
+  const int valid = max(0, min(rows_here, d.frames - t0));  // rows of this tile with data
+  const uint8_t *body = blob + d.off;
+  float *pc = lds;              // [4][Df]
+  float *tile = lds + 4 * Df;   // [R][LD]
+  if (valid > 0) {
+    if (d.format == 1) {
+      const uint16_t *ph = reinterpret_cast<const uint16_t *>(body);
+      for (int c = tid; c < Df; c += 256) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) pc[q * Df + c] = dev_from_u16(d.min_value, d.range, ph[4 * c + q]);
+      }
+      __syncthreads();
+      const uint8_t *bytes = body + 8 * (long)Df + d.first + t0;
+      for (int idx = tid; idx < Df * R; idx += 256) {
+        const int c = idx / R, j = idx - c * R;
+        if (j < valid)
+          tile[j * LD + c] = dev_from_u8(pc[c], pc[Df + c], pc[2 * Df + c], pc[3 * Df + c],
+                                         bytes[(long)c * d.rows + j]);
+      }
+    } else {
+      const uint16_t *v = reinterpret_cast<const uint16_t *>(body) + (long)(d.first + t0) * Df;
+      for (int idx = tid; idx < Df * valid; idx += 256) {
+        const int j = idx / Df, c = idx - j * Df;
+        tile[j * LD + c] = dev_from_u16(d.min_value, d.range, v[idx]);
+      }
+    }
+  }
+  __syncthreads();
+  const float *spk = d.spk_off >= 0 ? reinterpret_cast<const float *>(blob + d.spk_off) : nullptr;
+  for (int idx = tid; idx < rows_here * Dt; idx += 256) {
+    const int j = idx / Dt, c = idx - j * Dt;
+    float v = 0.f;
+    if (j < valid) v = c < Df ? tile[j * LD + c] : spk[c - Df];
+    out[((long)(t0 + j) * N + n) * Dt + c] = v;
+  }
+}
+
+int pick_rows(int Df) {
+  int R = 64;
+  while (R > 1 && (size_t)(4 * Df + R * (Df + 1)) * 4 > 64 * 1024) R >>= 1;
+  return R;
+}
+
+}  // namespace
+
+size_t format_scratch_bytes(const Minibatch &mb) { return align_up(mb.blob.size(), 256); }
+
+void format_on_device(Minibatch &mb, float *out, void *scratch, size_t scratch_bytes, hipStream_t stream) {
+  if (mb.N <= 0) return;
+  if (scratch_bytes < mb.blob.size()) throw std::invalid_argument("format: scratch too small");
+  if (mb.feat_dim <= 0 || mb.feat_dim > 4096) throw std::invalid_argument("format: unsupported feature dim");
+  KCTC_HIP_CHECK(hipMemcpyAsync(scratch, mb.blob.data(), mb.blob.size(), hipMemcpyHostToDevice, stream));
+  if (!mb.done) KCTC_HIP_CHECK(hipEventCreateWithFlags(&mb.done, hipEventDisableTiming));
+  KCTC_HIP_CHECK(hipEventRecord(mb.done, stream));
+  if (mb.T_max <= 0) return;
+  const int R = pick_rows(mb.feat_dim);
+  const size_t lds = (size_t)(4 * mb.feat_dim + R * (mb.feat_dim + 1)) * 4;
+  dim3 grid(ceil_div(mb.T_max, R), mb.N);
+  hipLaunchKernelGGL(egs_format_kernel, grid, dim3(256), lds, stream, static_cast<const uint8_t *>(scratch),
+                     mb.N, mb.T_max, mb.feat_dim, mb.spk_dim, R, out);
+  KCTC_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace egs
+}  // namespace kctc

@@ -165,6 +165,7 @@ struct RecParams {
   unsigned *err;
   int sync;         // kSyncData / kSyncFlag
   unsigned long long *trace;  // optional: [kTraceSteps][grid][8] s_memrealtime stamps
+  int allow_local;  // v4: hand off through the shared L2 when placement allows it
 };
 
 // Phase stamps of the first kTraceSteps steps (thread 0 of every workgroup;
@@ -642,6 +643,426 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec(RecParams p) {
   if (bad && tid == 0) atomicOr(p.err, 1u);
 }
 
+
+// ---------------------------------------------------------------------------
+// v4: XCD-local recurrences
+// ---------------------------------------------------------------------------
+// Grid = 8 * nwg; block b works as (dir = b & 7, g = b >> 3) when b & 7 < dirs,
+// the others exit at once.  Under the observed round-robin dispatch the nwg
+// (<= 32) workgroups of one direction then share one XCD and its L2, so the
+// per-step all-gather of h (or dGates) is served by that L2 instead of the
+// fabric.  This is checked, never assumed: every workgroup publishes its
+// HW_REG_XCC_ID through the placement-independent form, and only when ALL
+// workgroups of a direction read one id does that direction hand off through
+// its L2 (plain payload and flag stores, which stay in the shared L2; sc1
+// loads, which bypass the reading CU's L1).  Otherwise it uses the
+// placement-independent form throughout (sc1 write-through payload and flag
+// stores after every storing wave's vmcnt(0) and a barrier, sc1 loads:
+// MI355X_MICROARCH.md "Valid forms", row 1).  Either way a step is
+//   wait for the direction's nwg epoch flags (one sc1 poll per lane, wave 0)
+//   -> sc1 16-B loads of the previous step straight into MFMA A registers
+//   -> v_mfma_f32_16x16x4_f32 over the LDS-resident R slice (K split over
+//      the 4 waves, reduced through LDS)
+//   -> pointwise cell math, one (n, unit) element per thread
+//   -> payload stores -> vmcnt(0) -> barrier -> lane 0 epoch flag.
+// Epoch 1 is the placement probe; step k publishes epoch k + 2.
+
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v & 0xfu;
+}
+
+__device__ __forceinline__ float fsigm(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float ftanh(float x) { return 2.f * fsigm(2.f * x) - 1.f; }
+
+__device__ __forceinline__ void put(float *q, float v, int local) {
+  if (local) {
+    __hip_atomic_store(reinterpret_cast<unsigned *>(q), __float_as_uint(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_WORKGROUP);
+  } else {
+    __hip_atomic_store(reinterpret_cast<unsigned *>(q), __float_as_uint(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__device__ __forceinline__ void signal_epoch(unsigned *flag, unsigned epoch, int local) {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // every storing wave drains
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (local) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Placement probe: returns 1 iff every workgroup of direction d is on this XCD.
+__device__ int probe_local(const RecParams &p, int d, int g, unsigned *myflag, int &bad, int *bad_lds,
+                           int *loc_lds) {
+  unsigned *xt = p.flags + 512 + d * p.nwg;
+  const unsigned me = xcc_id() + 1u;
+  if (threadIdx.x == 0) __hip_atomic_store(xt + g, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  signal_epoch(myflag, 1u, 0);
+  wait_flags(p.flags + d * p.nwg, p.nwg, 1u, p.err, bad, bad_lds);
+  if (threadIdx.x < 64) {
+    bool ok = true;
+    for (int i = threadIdx.x; i < p.nwg; i += 64)
+      ok &= __hip_atomic_load(xt + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == me;
+    const bool all = __all(ok);
+    if (threadIdx.x == 0) *loc_lds = (all && p.allow_local) ? 1 : 0;
+  }
+  __syncthreads();
+  return *loc_lds;
+}
+
+constexpr int kMaxEPT = 4;  // (n, unit) elements per thread: N * U <= 1024
+
+template <int MODE, int RT>
+__global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
+  constexpr int NW = MODE == kLstm ? 4 : MODE == kGru ? 3 : 1;
+  constexpr int CH = 32 / RT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ int bad_lds, loc_lds;
+  const int d = blockIdx.x & 7, g = blockIdx.x >> 3;
+  if (d >= p.dirs || g >= p.nwg) return;
+  const int H = p.H, U = p.U, N = p.N, T = p.T, ncol = p.ncol;
+  const int LDR = H + 4;
+  const int u0 = g * U;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  const int CT = ncol / 16;
+  const long ldy = (long)p.dirs * H, ldg = (long)p.dirs * NW * H;
+  float *Rs = smem;                      // [ncol][LDR]
+  float *red = Rs + (long)ncol * LDR;    // [4][Npad][ncol]
+  const float *Wd = p.w + d * p.pl_stride;
+  const float *R = Wd + p.r_off;
+  if (tid == 0) bad_lds = 0;
+  for (int idx = tid; idx < ncol * H; idx += NT) {
+    const int c = idx / H, k = idx - c * H;
+    float v = 0.f;
+    if (c < NW * U) {
+      const int gt = c / U, u = c - gt * U;
+      v = R[(long)(gt * H + u0 + u) * H + k];
+    }
+    Rs[c * LDR + k] = v;
+  }
+  const int items = N * U;
+  float cst[kMaxEPT], hpv[kMaxEPT], gin[kMaxEPT][NW], bR[kMaxEPT][NW];
+#pragma unroll
+  for (int j = 0; j < kMaxEPT; j++) {
+    cst[j] = hpv[j] = 0.f;
+    const int e = tid + j * NT, n = e / U, u = e - n * U;
+#pragma unroll
+    for (int q = 0; q < NW; q++) {
+      bR[j][q] = (MODE == kGru && e < items) ? Wd[p.bR_off + q * H + u0 + u] : 0.f;
+      gin[j][q] = 0.f;
+      if (e < items) {
+        const int t = d == 0 ? 0 : T - 1;
+        gin[j][q] = p.G[((long)t * N + n) * ldg + (long)d * NW * H + q * H + u0 + u];
+      }
+    }
+  }
+  int bad = 0;
+  unsigned *myflag = p.flags + d * p.nwg + g;
+  const int local = probe_local(p, d, g, myflag, bad, &bad_lds, &loc_lds);
+  const int KG = H / 16;
+  const int KGW = (KG + 3) / 4;
+  const unsigned step_bytes = (unsigned)((long)N * ldy * sizeof(float));
+  for (int k = 0; k < T && !bad; k++) {
+    const int t = d == 0 ? k : T - 1 - k, tp = d == 0 ? t - 1 : t + 1;
+    floatx4 acc[RT][kMaxCT];
+#pragma unroll
+    for (int a = 0; a < RT; a++)
+#pragma unroll
+      for (int b = 0; b < kMaxCT; b++) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+    REC_TRACE(k, 0);
+    if (k > 0) {
+      wait_flags(p.flags + d * p.nwg, p.nwg, (unsigned)(k + 1), p.err, bad, &bad_lds);
+      REC_TRACE(k, 1);
+      const auto rs = rsrc(p.y + (long)tp * N * ldy, step_bytes);
+      for (int c0 = 0; c0 < KGW; c0 += CH) {
+        u32x4 af[RT][CH];
+        load_frags<RT, CH>(af, rs, ldy, (long)d * H, c0, KG, N, kSyncFlag, p.err, bad);
+        if (p.trace) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          REC_TRACE(k, 2);
+        }
+#pragma unroll
+        for (int i = 0; i < CH; i++) {
+          const int kg = w + 4 * (c0 + i);
+          if (kg < KG) {
+#pragma unroll
+            for (int ct = 0; ct < kMaxCT; ct++) {
+              if (ct < CT) {
+                const floatx4 b = ld4(Rs + (ct * 16 + fr) * LDR + kg * 16 + fq * 4);
+#pragma unroll
+                for (int s = 0; s < 4; s++)
+#pragma unroll
+                  for (int rt = 0; rt < RT; rt++)
+                    acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[rt][i][s]), b[s],
+                                                                       acc[rt][ct], 0, 0, 0);
+              }
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+      for (int ct = 0; ct < kMaxCT; ct++)
+        if (ct < CT)
+#pragma unroll
+          for (int r = 0; r < 4; r++)
+            red[((long)w * p.Npad + rt * 16 + fq * 4 + r) * ncol + ct * 16 + fr] = acc[rt][ct][r];
+    __syncthreads();
+    REC_TRACE(k, 3);
+    float act[kMaxEPT][NW], cnew[kMaxEPT];
+#pragma unroll
+    for (int j = 0; j < kMaxEPT; j++) {
+      const int e = tid + j * NT;
+      cnew[j] = 0.f;
+      if (e >= items) continue;
+      const int n = e / U, u = e - n * U;
+      float rh[NW];
+#pragma unroll
+      for (int q = 0; q < NW; q++) {
+        const int c = q * U + u;
+        rh[q] = ((red[((long)0 * p.Npad + n) * ncol + c] + red[((long)1 * p.Npad + n) * ncol + c]) +
+                 red[((long)2 * p.Npad + n) * ncol + c]) + red[((long)3 * p.Npad + n) * ncol + c];
+      }
+      float h;
+      if (MODE == kLstm) {
+        act[j][0] = fsigm(gin[j][0] + rh[0]);
+        act[j][1] = fsigm(gin[j][1] + rh[1]);
+        act[j][2] = ftanh(gin[j][2] + rh[2]);
+        act[j][3] = fsigm(gin[j][3] + rh[3]);
+        cst[j] = act[j][1] * cst[j] + act[j][0] * act[j][2];
+        cnew[j] = cst[j];
+        h = act[j][3] * ftanh(cst[j]);
+      } else if (MODE == kGru) {
+        act[j][0] = fsigm(gin[j][0] + rh[0] + bR[j][0]);
+        act[j][1] = fsigm(gin[j][1] + rh[1] + bR[j][1]);
+        cnew[j] = rh[2] + bR[j][2];
+        act[j][2] = ftanh(gin[j][2] + act[j][0] * cnew[j]);
+        h = (1.f - act[j][1]) * act[j][2] + act[j][1] * hpv[j];
+        hpv[j] = h;
+      } else {
+        const float pre = gin[j][0] + rh[0];
+        h = MODE == kRelu ? fmaxf(pre, 0.f) : ftanh(pre);
+      }
+      put(p.y + ((long)t * N + n) * ldy + (long)d * H + u0 + u, h, local);
+    }
+    signal_epoch(myflag, (unsigned)(k + 2), local);
+    REC_TRACE(k, 4);
+#pragma unroll
+    for (int j = 0; j < kMaxEPT; j++) {
+      const int e = tid + j * NT;
+      if (e >= items) continue;
+      const int n = e / U, u = e - n * U;
+      if (MODE == kLstm || MODE == kGru) {
+        const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
+#pragma unroll
+        for (int q = 0; q < NW; q++) p.G[grow + q * H] = act[j][q];
+        p.aux[((long)t * N + n) * ldy + (long)d * H + u0 + u] = cnew[j];
+      }
+      if (k + 1 < T) {  // prefetch the next step's input projection
+        const int tn = d == 0 ? t + 1 : t - 1;
+#pragma unroll
+        for (int q = 0; q < NW; q++) gin[j][q] = p.G[((long)tn * N + n) * ldg + (long)d * NW * H + q * H + u0 + u];
+      }
+    }
+    __syncthreads();  // red[] is rewritten by the next step
+    REC_TRACE(k, 5);
+  }
+  if (bad && tid == 0) atomicOr(p.err, 1u);
+}
+
+template <int MODE, int RT>
+__global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
+  constexpr int NW = MODE == kLstm ? 4 : MODE == kGru ? 3 : 1;
+  constexpr int CH = 32 / RT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ int bad_lds, loc_lds;
+  const int d = blockIdx.x & 7, g = blockIdx.x >> 3;
+  if (d >= p.dirs || g >= p.nwg) return;
+  const int H = p.H, U = p.U, N = p.N, T = p.T;
+  const int K = NW * H, LDK = K + 4;
+  const int u0 = g * U;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  const long ldy = (long)p.dirs * H, ldg = (long)p.dirs * NW * H;
+  float *RT_s = smem;                       // [U][LDK]: RT_s[u][kk] = R[kk][u0+u]
+  float *red = RT_s + (long)U * LDK;        // [4][Npad][16]
+  const float *Wd = p.w + d * p.pl_stride;
+  const float *R = Wd + p.r_off;
+  if (tid == 0) bad_lds = 0;
+  for (int idx = tid; idx < U * K; idx += NT) {
+    const int kk = idx / U, u = idx - kk * U;
+    RT_s[u * LDK + kk] = R[(long)kk * H + u0 + u];
+  }
+  const int items = N * U;
+  float carry[kMaxEPT], bsx[kMaxEPT][NW], bsh[kMaxEPT][NW];
+  float pg[kMaxEPT][NW], pdy[kMaxEPT], pa[kMaxEPT], pap[kMaxEPT];
+#pragma unroll
+  for (int j = 0; j < kMaxEPT; j++) {
+    carry[j] = pdy[j] = pa[j] = pap[j] = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; q++) bsx[j][q] = bsh[j][q] = pg[j][q] = 0.f;
+  }
+  auto prefetch = [&](int k) {
+    const int t = d == 0 ? k : T - 1 - k, tp = d == 0 ? t - 1 : t + 1;
+#pragma unroll
+    for (int j = 0; j < kMaxEPT; j++) {
+      const int e = tid + j * NT;
+      if (e >= items) continue;
+      const int n = e / U, u = e - n * U;
+      const long yrow = ((long)t * N + n) * ldy + (long)d * H + u0 + u;
+      const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
+      const long prow = ((long)tp * N + n) * ldy + (long)d * H + u0 + u;
+      pdy[j] = p.dy[yrow];
+      if (MODE == kLstm || MODE == kGru) {
+#pragma unroll
+        for (int q = 0; q < NW; q++) pg[j][q] = p.G[grow + q * H];
+        pa[j] = p.aux[yrow];
+      }
+      if (MODE == kLstm) pap[j] = k > 0 ? p.aux[prow] : 0.f;
+      else if (MODE == kGru) pap[j] = k > 0 ? p.y[prow] : 0.f;
+      else pap[j] = p.y[yrow];
+    }
+  };
+  prefetch(T - 1);
+  int bad = 0;
+  unsigned *myflag = p.flags + d * p.nwg + g;
+  const int local = probe_local(p, d, g, myflag, bad, &bad_lds, &loc_lds);
+  const int KG = K / 16;
+  const int KGW = (KG + 3) / 4;
+  const unsigned step_bytes = (unsigned)((long)N * ldg * sizeof(float));
+  for (int k = T - 1; k >= 0 && !bad; k--) {
+    const int t = d == 0 ? k : T - 1 - k;
+    const int tn = d == 0 ? t + 1 : t - 1;
+    const int ks = T - 1 - k;             // steps done before this one
+    floatx4 acc[RT];
+#pragma unroll
+    for (int a = 0; a < RT; a++) acc[a] = floatx4{0.f, 0.f, 0.f, 0.f};
+    REC_TRACE(ks, 0);
+    if (ks > 0) {
+      wait_flags(p.flags + d * p.nwg, p.nwg, (unsigned)(ks + 1), p.err, bad, &bad_lds);
+      REC_TRACE(ks, 1);
+      const auto rs = rsrc(p.E + (long)tn * N * ldg, step_bytes);
+      for (int c0 = 0; c0 < KGW; c0 += CH) {
+        u32x4 af[RT][CH];
+        load_frags<RT, CH>(af, rs, ldg, (long)d * K, c0, KG, N, kSyncFlag, p.err, bad);
+        if (p.trace) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          REC_TRACE(ks, 2);
+        }
+#pragma unroll
+        for (int i = 0; i < CH; i++) {
+          const int kg = w + 4 * (c0 + i);
+          if (kg < KG) {
+            floatx4 b = floatx4{0.f, 0.f, 0.f, 0.f};
+            if (fr < U) b = ld4(RT_s + fr * LDK + kg * 16 + fq * 4);
+#pragma unroll
+            for (int s = 0; s < 4; s++)
+#pragma unroll
+              for (int rt = 0; rt < RT; rt++)
+                acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[rt][i][s]), b[s], acc[rt], 0, 0, 0);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) red[((long)w * p.Npad + rt * 16 + fq * 4 + r) * 16 + fr] = acc[rt][r];
+    __syncthreads();
+    REC_TRACE(ks, 3);
+    float dxk[kMaxEPT][NW];
+#pragma unroll
+    for (int j = 0; j < kMaxEPT; j++) {
+      const int e = tid + j * NT;
+      if (e >= items) continue;
+      const int n = e / U, u = e - n * U;
+      const float dhr = ((red[((long)0 * p.Npad + n) * 16 + u] + red[((long)1 * p.Npad + n) * 16 + u]) +
+                         red[((long)2 * p.Npad + n) * 16 + u]) + red[((long)3 * p.Npad + n) * 16 + u];
+      float dh = pdy[j] + dhr;
+      float *Erow = p.E + ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
+      if (MODE == kLstm) {
+        const float ig = pg[j][0], fg = pg[j][1], gg = pg[j][2], og = pg[j][3];
+        const float tc = ftanh(pa[j]);
+        const float dO = dh * tc;
+        const float dc = dh * og * (1.f - tc * tc) + carry[j];
+        const float dpi = dc * gg * ig * (1.f - ig);
+        const float dpf = dc * pap[j] * fg * (1.f - fg);
+        const float dpg = dc * ig * (1.f - gg * gg);
+        const float dpo = dO * og * (1.f - og);
+        carry[j] = dc * fg;
+        put(Erow, dpi, local);
+        put(Erow + H, dpf, local);
+        put(Erow + 2 * H, dpg, local);
+        put(Erow + 3 * H, dpo, local);
+        bsx[j][0] += dpi; bsx[j][1] += dpf; bsx[j][2] += dpg; bsx[j][3] += dpo;
+      } else if (MODE == kGru) {
+        dh += carry[j];
+        const float r = pg[j][0], z = pg[j][1], nn = pg[j][2];
+        const float dn = dh * (1.f - z), dz = dh * (pap[j] - nn);
+        const float dpn = dn * (1.f - nn * nn);
+        const float dpr = dpn * pa[j] * r * (1.f - r);
+        const float dpz = dz * z * (1.f - z);
+        carry[j] = dh * z;
+        dxk[j][0] = dpr; dxk[j][1] = dpz; dxk[j][2] = dpn;
+        put(Erow, dpr, local);
+        put(Erow + H, dpz, local);
+        put(Erow + 2 * H, dpn * r, local);
+        bsx[j][0] += dpr; bsx[j][1] += dpz; bsx[j][2] += dpn;
+        bsh[j][0] += dpr; bsh[j][1] += dpz; bsh[j][2] += dpn * r;
+      } else {
+        const float der = MODE == kRelu ? (pap[j] > 0.f ? 1.f : 0.f) : (1.f - pap[j] * pap[j]);
+        const float dp = dh * der;
+        put(Erow, dp, local);
+        bsx[j][0] += dp;
+      }
+    }
+    signal_epoch(myflag, (unsigned)(ks + 2), local);
+    REC_TRACE(ks, 4);
+    if (MODE == kGru) {
+#pragma unroll
+      for (int j = 0; j < kMaxEPT; j++) {
+        const int e = tid + j * NT;
+        if (e >= items) continue;
+        const int n = e / U, u = e - n * U;
+        const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
+#pragma unroll
+        for (int q = 0; q < NW; q++) p.DX[grow + q * H] = dxk[j][q];
+      }
+    }
+    if (k > 0) prefetch(k - 1);
+    __syncthreads();
+    REC_TRACE(ks, 5);
+  }
+  // bias partial sums: reduce over n in a fixed order through LDS
+  float *bs = red;  // reuse: [2][N][U][NW] floats (fits: see lds sizing)
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kMaxEPT; j++) {
+    const int e = tid + j * NT;
+    if (e >= items) continue;
+    const int n = e / U, u = e - n * U;
+#pragma unroll
+    for (int q = 0; q < NW; q++) {
+      const long base = ((long)n * U + u) * NW + q;
+      bs[base] = bsx[j][q];
+      bs[(long)N * U * NW + base] = (MODE == kGru) ? bsh[j][q] : bsx[j][q];
+    }
+  }
+  __syncthreads();
+  for (int q = tid; q < 2 * NW * U; q += NT) {
+    const int part = q / (NW * U), rem = q - part * NW * U, gt = rem / U, u = rem - gt * U;
+    float s = 0.f;
+    for (int n = 0; n < N; n++) s += bs[(long)part * N * U * NW + ((long)n * U + u) * NW + gt];
+    p.bias[((long)d * 2 + part) * NW * H + gt * H + u0 + u] = s;
+  }
+  if (bad && tid == 0) atomicOr(p.err, 1u);
+}
+
 template <typename F>
 static void set_lds(F f, size_t bytes) {
   static size_t done[8] = {0};
@@ -651,7 +1072,17 @@ static void set_lds(F f, size_t bytes) {
 }
 
 template <int MODE, int RT>
-static void launch_one(bool fwd, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
+static void launch_one(bool fwd, const RecParams &p, dim3 grid, size_t lds, hipStream_t s, int ver) {
+  if (ver == 4) {
+    if (fwd) {
+      set_lds(rnn_fwd_rec4<MODE, RT>, lds);
+      hipLaunchKernelGGL((rnn_fwd_rec4<MODE, RT>), grid, dim3(NT), lds, s, p);
+    } else {
+      set_lds(rnn_bwd_rec4<MODE, RT>, lds);
+      hipLaunchKernelGGL((rnn_bwd_rec4<MODE, RT>), grid, dim3(NT), lds, s, p);
+    }
+    return;
+  }
   if (fwd) {
     set_lds(rnn_fwd_rec<MODE, RT>, lds);
     hipLaunchKernelGGL((rnn_fwd_rec<MODE, RT>), grid, dim3(NT), lds, s, p);
@@ -661,26 +1092,27 @@ static void launch_one(bool fwd, const RecParams &p, dim3 grid, size_t lds, hipS
   }
 }
 template <int MODE>
-static void launch_mode(bool fwd, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
+static void launch_mode(bool fwd, const RecParams &p, dim3 grid, size_t lds, hipStream_t s, int ver) {
   switch (p.Npad / 16) {
-    case 1: launch_one<MODE, 1>(fwd, p, grid, lds, s); break;
-    case 2: launch_one<MODE, 2>(fwd, p, grid, lds, s); break;
-    case 3: launch_one<MODE, 3>(fwd, p, grid, lds, s); break;
-    default: launch_one<MODE, 4>(fwd, p, grid, lds, s); break;
+    case 1: launch_one<MODE, 1>(fwd, p, grid, lds, s, ver); break;
+    case 2: launch_one<MODE, 2>(fwd, p, grid, lds, s, ver); break;
+    case 3: launch_one<MODE, 3>(fwd, p, grid, lds, s, ver); break;
+    default: launch_one<MODE, 4>(fwd, p, grid, lds, s, ver); break;
   }
 }
-static void launch_rec(bool fwd, int mode, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
+static void launch_rec(bool fwd, int mode, const RecParams &p, dim3 grid, size_t lds, hipStream_t s,
+                       int ver) {
   switch (mode) {
-    case kLstm: launch_mode<kLstm>(fwd, p, grid, lds, s); break;
-    case kGru: launch_mode<kGru>(fwd, p, grid, lds, s); break;
-    case kRelu: launch_mode<kRelu>(fwd, p, grid, lds, s); break;
-    default: launch_mode<kTanh>(fwd, p, grid, lds, s); break;
+    case kLstm: launch_mode<kLstm>(fwd, p, grid, lds, s, ver); break;
+    case kGru: launch_mode<kGru>(fwd, p, grid, lds, s, ver); break;
+    case kRelu: launch_mode<kRelu>(fwd, p, grid, lds, s, ver); break;
+    default: launch_mode<kTanh>(fwd, p, grid, lds, s, ver); break;
   }
 }
 
 // KCTC_REC_TRACE=<dir>: trace the first forward and the first backward
 // recurrence launch of the process into <dir>/rec_{fwd,bwd}.bin
-// (int32 header {grid, steps, nwg, T} then [steps][grid][8] uint64 stamps).
+// (int32 header {grid, steps, nwg, T, dirs, version} then [steps][grid][8] uint64 stamps).
 struct RecTrace {
   unsigned long long *dev = nullptr;
   size_t n = 0;
@@ -696,7 +1128,7 @@ struct RecTrace {
     KCTC_HIP_CHECK(hipMemset(dev, 0, n * sizeof(unsigned long long)));
     return true;
   }
-  void dump(const char *tag, hipStream_t s, int grid, int nwg, int T) {
+  void dump(const char *tag, hipStream_t s, int grid, int nwg, int T, int dirs, int ver) {
     if (!dev) return;
     KCTC_HIP_CHECK(hipStreamSynchronize(s));
     std::vector<unsigned long long> h(n);
@@ -706,8 +1138,8 @@ struct RecTrace {
     std::string path = std::string(getenv("KCTC_REC_TRACE")) + "/rec_" + tag + ".bin";
     FILE *f = fopen(path.c_str(), "wb");
     if (!f) return;
-    int hdr[4] = {grid, kTraceSteps, nwg, T};
-    fwrite(hdr, sizeof(int), 4, f);
+    int hdr[6] = {grid, kTraceSteps, nwg, T, dirs, ver};
+    fwrite(hdr, sizeof(int), 6, f);
     fwrite(h.data(), sizeof(unsigned long long), n, f);
     fclose(f);
   }
@@ -734,6 +1166,37 @@ static int pick_fwd_u(const RnnDesc &d, int N) {
   // per-step MFMA latency falls with U (measured: U=4 < 8 < 16 on BLSTM-512)
   for (int U : {4, 8, 16})
     if (ok(U)) return U;
+  return 0;
+}
+
+// v4 (XCD-local): nwg = H/U <= kCusPerXcd workgroups per direction, one XCD each.
+constexpr int kCusPerXcd = 32;
+static size_t fwd_lds_bytes(const RnnDesc &d, int N, int U) {
+  const int ncol = (d.nw() * U + 15) / 16 * 16, Npad = (N + 15) / 16 * 16;
+  return sizeof(float) * ((size_t)ncol * (d.H + 4) + 4 * (size_t)Npad * ncol);
+}
+static size_t bwd_lds_bytes(const RnnDesc &d, int N, int U) {
+  const int Npad = (N + 15) / 16 * 16;
+  return sizeof(float) * ((size_t)U * (d.nw() * d.H + 4) +
+                          std::max(4 * (size_t)Npad * 16, (size_t)2 * N * U * d.nw()));
+}
+static int rec_version() { return env_int("KCTC_REC", 4); }
+static int pick_fwd_u4(const RnnDesc &d, int N) {
+  if (rec_version() != 4 || d.dirs > 8) return 0;
+  for (int U = 1; U <= d.H; U++) {
+    if (d.H % U || d.H / U > kCusPerXcd) continue;
+    if (d.nw() * U > 16 * kMaxCT || N * U > kMaxEPT * NT) return 0;
+    return fwd_lds_bytes(d, N, U) <= 160 * 1024 ? U : 0;
+  }
+  return 0;
+}
+static int pick_bwd_u4(const RnnDesc &d, int N) {
+  if (rec_version() != 4 || d.dirs > 8) return 0;
+  for (int U = 1; U <= 16; U++) {
+    if (d.H % U || d.H / U > kCusPerXcd) continue;
+    if (N * U > kMaxEPT * NT) return 0;
+    return bwd_lds_bytes(d, N, U) <= 160 * 1024 ? U : 0;
+  }
   return 0;
 }
 
@@ -766,7 +1229,9 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
   if (res_bytes < sizeof(float) * (size_t)lay.total) return KRNN_BAD_PARAM;
   if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
-  const int U = pick_fwd_u(d, N);
+  const int U4 = pick_fwd_u4(d, N);
+  const int ver = U4 ? 4 : 3;
+  const int U = U4 ? U4 : pick_fwd_u(d, N);
   if (!U) return KRNN_NOT_SUPPORTED;
   const int NW = d.nw(), H = d.H, dirs = d.dirs;
   const long TN = (long)T * N;
@@ -782,7 +1247,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     const long bW = d.lin_offset(l * dirs, 0, true) - pl0;
     const long bR = d.lin_offset(l * dirs, NW, true) - pl0;
     const long roff = d.lin_offset(l * dirs, NW, false) - pl0;
-    KCTC_HIP_CHECK(hipMemsetAsync(out, 0xFF, sizeof(float) * TN * dirs * H, s));
+    if (ver == 3) KCTC_HIP_CHECK(hipMemsetAsync(out, 0xFF, sizeof(float) * TN * dirs * H, s));
     GemmArgs g;
     g.transA = false; g.transB = true;
     g.M = (int)TN; g.N = NW * H; g.K = Din;
@@ -801,19 +1266,20 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.ncol = (NW * U + 15) / 16 * 16; p.Npad = (N + 15) / 16 * 16;
     p.w = wl; p.pl_stride = pls; p.r_off = roff; p.bR_off = bR;
     p.G = R0 + lay.G; p.y = out; p.aux = R0 + lay.aux; p.err = err;
-    p.sync = env_int("KCTC_SYNC_FWD", env_int("KCTC_SYNC", kSyncData));
+    p.sync = ver == 4 ? kSyncFlag : env_int("KCTC_SYNC_FWD", env_int("KCTC_SYNC", kSyncData));
+    p.allow_local = env_int("KCTC_LOCAL", 1);
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, 4096, s));
-    const size_t lds = sizeof(float) * ((size_t)p.ncol * (H + 4) + 4 * (size_t)p.Npad * p.ncol);
-    const dim3 grid(dirs * p.nwg);
+    const size_t lds = fwd_lds_bytes(d, N, U);
+    const dim3 grid(ver == 4 ? 8 * p.nwg : dirs * p.nwg);
     RecTrace tr;
     if (tr.arm("fwd", grid.x)) p.trace = tr.dev;
     {
       ProfSpan ps(s, "rnn_fwd_rec");
-      launch_rec(true, d.mode, p, grid, lds, s);
+      launch_rec(true, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
-    tr.dump("fwd", s, grid.x, p.nwg, T);
+    tr.dump("fwd", s, grid.x, p.nwg, T, dirs, ver);
     in = out;
   }
   return KRNN_OK;
@@ -828,7 +1294,9 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
   if (T <= 0 || N <= 0 || N > 16 * kMaxRT || d.H % 16) return KRNN_NOT_SUPPORTED;
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
   if (res_bytes < sizeof(float) * (size_t)lay.total) return KRNN_BAD_PARAM;
-  const int U = pick_bwd_u(d, N);
+  const int U4 = pick_bwd_u4(d, N);
+  const int ver = U4 ? 4 : 3;
+  const int U = U4 ? U4 : pick_bwd_u(d, N);
   if (!U) return KRNN_NOT_SUPPORTED;
   const int NW = d.nw(), H = d.H, dirs = d.dirs;
   const long TN = (long)T * N;
@@ -843,7 +1311,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     const long pls = d.pl_size(l);
     float *E = R0 + lay.E;
     float *DX = d.mode == kGru ? R0 + lay.DX : E;
-    KCTC_HIP_CHECK(hipMemsetAsync(E, 0xFF, sizeof(float) * TN * dirs * NW * H, s));
+    if (ver == 3) KCTC_HIP_CHECK(hipMemsetAsync(E, 0xFF, sizeof(float) * TN * dirs * NW * H, s));
     RecParams p{};
     p.T = T; p.N = N; p.H = H; p.dirs = dirs; p.U = U; p.nwg = H / U;
     p.ncol = 16; p.Npad = (N + 15) / 16 * 16;
@@ -851,21 +1319,21 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     p.bR_off = d.lin_offset(l * dirs, NW, true) - pl0;
     p.G = R0 + lay.G; p.y = const_cast<float *>(out); p.aux = R0 + lay.aux;
     p.dy = dcur; p.E = E; p.DX = DX; p.bias = R0 + lay.bias; p.err = err;
-    p.sync = env_int("KCTC_SYNC_BWD", env_int("KCTC_SYNC", kSyncFlag));
+    p.sync = ver == 4 ? kSyncFlag : env_int("KCTC_SYNC_BWD", env_int("KCTC_SYNC", kSyncFlag));
+    p.allow_local = env_int("KCTC_LOCAL", 1);
     if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, 4096, s));
-    const size_t lds = sizeof(float) * ((size_t)U * (NW * H + 4) +
-                                        std::max(4 * (size_t)p.Npad * 16, (size_t)2 * N * U * NW));
-    const dim3 grid(dirs * p.nwg);
+    const size_t lds = bwd_lds_bytes(d, N, U);
+    const dim3 grid(ver == 4 ? 8 * p.nwg : dirs * p.nwg);
     RecTrace tr;
     if (tr.arm("bwd", grid.x)) p.trace = tr.dev;
     {
       ProfSpan ps(s, "rnn_bwd_rec");
-      launch_rec(false, d.mode, p, grid, lds, s);
+      launch_rec(false, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
-    tr.dump("bwd", s, grid.x, p.nwg, T);
+    tr.dump("bwd", s, grid.x, p.nwg, T, dirs, ver);
     // dx_l = sum_dir DX_dir W_dir   (lower layer's dy, or the caller's dx)
     float *dxl = (l == 0) ? dx : res + lay.per_layer * (l - 1) + lay.dout;
     if (dxl) {

@@ -67,6 +67,8 @@ class RcclExchange : public kctc::nnet2::GradExchange {
 
 }  // namespace
 
+void kctc_set_error(const char *msg) { g_err = msg ? msg : ""; }
+
 struct kctcNnetImpl {
   int device = 0;
   hipStream_t stream = nullptr;

@@ -7,33 +7,40 @@ duration (us, 100 MHz stamps); plus the hand-off latency = consumer
 import sys
 import numpy as np
 
+
 def main(path):
     raw = open(path, "rb").read()
-    grid, steps, nwg, T = np.frombuffer(raw[:16], dtype=np.int32)
-    tr = np.frombuffer(raw[16:], dtype=np.uint64).reshape(steps, grid, 8).astype(np.int64)
+    grid, steps, nwg, T, dirs, ver = np.frombuffer(raw[:24], dtype=np.int32)
+    tr = np.frombuffer(raw[24:], dtype=np.uint64).reshape(steps, grid, 8).astype(np.int64)
     steps = min(steps, T)
     tr = tr[:steps]
+    if ver == 4:
+        members = [[b for b in range(grid) if b % 8 == d] for d in range(dirs)]
+    else:
+        members = [list(range(d * nwg, (d + 1) * nwg)) for d in range(dirs)]
+    active = sorted(b for m in members for b in m)
+    tr = tr[:, active, :]
+    idx = {b: i for i, b in enumerate(active)}
     us = 1e-2  # 100 MHz
     names = ["start->flags", "flags->loads", "loads->reduced", "reduced->published", "published->end"]
     sl = slice(8, steps)
-    print(f"{path}: grid={grid} nwg={nwg} T={T} steps traced={steps}")
+    print(f"{path}: v{ver} grid={grid} nwg={nwg} dirs={dirs} T={T} steps traced={steps}")
     for i, nm in enumerate(names):
         d = (tr[sl, :, i + 1] - tr[sl, :, i]) * us
         print(f"  {nm:22s} median {np.median(d):7.3f}  p90 {np.percentile(d, 90):7.3f}")
     step = (tr[9:steps, :, 0] - tr[8:steps - 1, :, 0]) * us
     print(f"  step period            median {np.median(step):7.3f}  p90 {np.percentile(step, 90):7.3f}")
-    dirs = grid // nwg
     lat = []
-    for d in range(dirs):
-        wg = slice(d * nwg, (d + 1) * nwg)
-        last_pub = tr[8:steps - 1, wg, 4].max(axis=1)
-        first_pub = tr[8:steps - 1, wg, 4].min(axis=1)
-        seen = tr[9:steps, wg, 1]
-        lat.append((seen - last_pub[:, None]) * us)
-        skew = (last_pub - first_pub) * us
-        print(f"  dir {d}: publish skew (last-first producer) median {np.median(skew):.3f}")
+    for d, m in enumerate(members):
+        cols = [idx[b] for b in m]
+        pub = tr[8:steps - 1][:, cols, 4]
+        seen = tr[9:steps][:, cols, 1]
+        lat.append((seen - pub.max(axis=1)[:, None]) * us)
+        print(f"  dir {d}: publish skew (last-first producer) median {np.median((pub.max(1) - pub.min(1)) * us):.3f}")
     lat = np.concatenate([l.ravel() for l in lat])
-    print(f"  handoff last-publish->seen median {np.median(lat):7.3f}  p10 {np.percentile(lat, 10):7.3f}  p90 {np.percentile(lat, 90):7.3f}")
+    print(f"  handoff last-publish->seen median {np.median(lat):7.3f}  p10 {np.percentile(lat, 10):7.3f}  "
+          f"p90 {np.percentile(lat, 90):7.3f}")
+
 
 if __name__ == "__main__":
     for p in sys.argv[1:]:
