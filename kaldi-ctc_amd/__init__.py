@@ -10,6 +10,10 @@ libkaldictc_amd.so (built from csrc/ by the Makefile next to this file):
   * nnet2 trainer ABI (include/kaldi_ctc_train.h) -- the NnetCtcUpdater /
     TrainNnetSimple step (src/ctc/ctc-nnet-update.cc:94-128,
     src/ctc/ctc-nnet-train.cc:181-284) on device buffers.
+  * egs ABI (include/kaldi_ctc_egs.h) -- NnetCtcExample archives, the
+    CompressedMatrix codec, NnetCtcExampleBackgroundReader and FormatNnetInput
+    decoded on the GPU (src/ctc/ctc-nnet-example.cc, ctc-nnet-train.cc:31-183,
+    ctc-nnet-update.cc:351-424, src/matrix/compressed-matrix.cc).
 
 torch is used only as plumbing (device memory, streams, torch.distributed
 rendezvous).  Every entry point fails loudly when the HIP library is missing;
@@ -422,3 +426,131 @@ def smoke_train_step(oracle_lib):
         assert err < 1e-5, (c, err)
     net.close()
     return objf, robjf
+
+
+# ---------------------------------------------------------------------------
+# egs: NnetCtcExample archives, CompressedMatrix, background reader, GPU format
+# ---------------------------------------------------------------------------
+def cm_compress(m):
+    """CompressedMatrix::CopyFromMat of a float32 [rows, cols] matrix -> bytes
+    (the in-memory image: 20-byte GlobalHeader + body)."""
+    m = np.ascontiguousarray(m, dtype=np.float32)
+    rows, cols = m.shape
+    L = lib()
+    out = np.zeros(max(L.kctc_cm_compressed_bytes(rows, cols), 0), dtype=np.uint8)
+    if out.size == 0:
+        return out
+    _tcheck(L.kctc_cm_compress(m.ctypes.data, rows, cols, out.ctypes.data), "kctc_cm_compress")
+    return out
+
+
+def cm_decompress(img):
+    """CompressedMatrix::CopyToMat of an image from cm_compress -> float32 [rows, cols]."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    hdr = np.frombuffer(img[:20].tobytes(), dtype=np.int32)
+    rows, cols = int(hdr[3]), int(hdr[4])
+    out = np.empty((rows, cols), dtype=np.float32)
+    _tcheck(lib().kctc_cm_decompress(img.ctypes.data, out.ctypes.data), "kctc_cm_decompress")
+    return out
+
+
+class EgsWriter:
+    """NnetCtcExampleWriter over a binary Kaldi archive (features compressed)."""
+
+    def __init__(self, wspecifier):
+        self._h = ctypes.c_void_p()
+        _tcheck(lib().kctc_egs_writer_open(ctypes.byref(self._h), wspecifier.encode()), "kctc_egs_writer_open")
+
+    def write(self, key, feats, labels, left_context=0, spk_info=None):
+        f = np.ascontiguousarray(feats, dtype=np.float32)
+        lab = np.ascontiguousarray(labels, dtype=np.int32)
+        spk = None if spk_info is None else np.ascontiguousarray(spk_info, dtype=np.float32)
+        _tcheck(lib().kctc_egs_write(self._h, key.encode(), f.ctypes.data, f.shape[0], f.shape[1],
+                                     lab.ctypes.data, lab.size, left_context,
+                                     None if spk is None else spk.ctypes.data, 0 if spk is None else spk.size),
+                "kctc_egs_write")
+
+    def close(self):
+        if self._h:
+            _tcheck(lib().kctc_egs_writer_close(self._h), "kctc_egs_writer_close")
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+class Minibatch:
+    """One minibatch from EgsReader (still compressed until format())."""
+
+    def __init__(self, handle):
+        self._h = handle
+        L = lib()
+        N, T, D, tl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_long()
+        _tcheck(L.kctc_minibatch_info(handle, ctypes.byref(N), ctypes.byref(T), ctypes.byref(D), ctypes.byref(tl)),
+                "kctc_minibatch_info")
+        self.N, self.T_max, self.input_dim, self.total_labels = N.value, T.value, D.value, tl.value
+        self.num_frames = np.zeros(self.N, dtype=np.int32)
+        self.label_lengths = np.zeros(self.N, dtype=np.int32)
+        self.flat_labels = np.zeros(max(self.total_labels, 1), dtype=np.int32)
+        _tcheck(L.kctc_minibatch_labels(handle, self.num_frames.ctypes.data, self.label_lengths.ctypes.data,
+                                        self.flat_labels.ctypes.data), "kctc_minibatch_labels")
+        self.flat_labels = self.flat_labels[:self.total_labels]
+        self.keys = [L.kctc_minibatch_key(handle, n).decode() for n in range(self.N)]
+
+    def scratch_bytes(self):
+        return int(lib().kctc_minibatch_scratch_bytes(self._h))
+
+    def format(self, out, scratch, stream=None):
+        """Stream-ordered FormatNnetInput on the GPU into out [T_max*N, input_dim] (device)."""
+        _tcheck(lib().kctc_minibatch_format(self._h, _ptr(out), _ptr(scratch), int(scratch.numel()),
+                                            ctypes.c_void_p(_stream_handle(stream))), "kctc_minibatch_format")
+
+    def free(self):
+        if self._h:
+            lib().kctc_minibatch_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class EgsReader:
+    """SequentialNnetCtcExampleReader + NnetCtcExampleBackgroundReader: iterate
+    minibatches (skip rules of ctc-nnet-train.cc:84-95)."""
+
+    def __init__(self, rspecifier, minibatch_size, max_frames=100000, nnet_left_context=0, nnet_right_context=0):
+        self._h = ctypes.c_void_p()
+        _tcheck(lib().kctc_egs_reader_open(ctypes.byref(self._h), rspecifier.encode(), minibatch_size, max_frames,
+                                           nnet_left_context, nnet_right_context), "kctc_egs_reader_open")
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        mb = ctypes.c_void_p()
+        _tcheck(lib().kctc_egs_reader_next(self._h, ctypes.byref(mb)), "kctc_egs_reader_next")
+        if not mb.value:
+            raise StopIteration
+        return Minibatch(mb)
+
+    def stats(self):
+        r, k = ctypes.c_long(), ctypes.c_long()
+        _tcheck(lib().kctc_egs_reader_stats(self._h, ctypes.byref(r), ctypes.byref(k)), "kctc_egs_reader_stats")
+        return r.value, k.value
+
+    def close(self):
+        if self._h:
+            lib().kctc_egs_reader_close(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

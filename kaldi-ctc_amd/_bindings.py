@@ -53,6 +53,23 @@ SIGS = {
     "kctc_nnet_enable_dp": (ci, [vp, vp, ci, ci]),
     "kctc_format_input": (ci, [vp, vp, ci, ci, ci, vp]),
     "kctc_synth_minibatch": (cl, [ctypes.c_ulonglong, ci, ci, ci, ci, cd, vp, vp, vp, vp]),
+    # include/kaldi_ctc_egs.h
+    "kctc_cm_compressed_bytes": (cl, [ci, ci]),
+    "kctc_cm_compress": (ci, [vp, ci, ci, vp]),
+    "kctc_cm_decompress": (ci, [vp, vp]),
+    "kctc_egs_writer_open": (ci, [ctypes.POINTER(vp), ctypes.c_char_p]),
+    "kctc_egs_write": (ci, [vp, ctypes.c_char_p, vp, ci, ci, vp, ci, ci, vp, ci]),
+    "kctc_egs_writer_close": (ci, [vp]),
+    "kctc_egs_reader_open": (ci, [ctypes.POINTER(vp), ctypes.c_char_p, ci, ci, ci, ci]),
+    "kctc_egs_reader_next": (ci, [vp, ctypes.POINTER(vp)]),
+    "kctc_egs_reader_stats": (ci, [vp, ctypes.POINTER(cl), ctypes.POINTER(cl)]),
+    "kctc_egs_reader_close": (ci, [vp]),
+    "kctc_minibatch_info": (ci, [vp, ip, ip, ip, ctypes.POINTER(cl)]),
+    "kctc_minibatch_labels": (ci, [vp, vp, vp, vp]),
+    "kctc_minibatch_key": (ctypes.c_char_p, [vp, ci]),
+    "kctc_minibatch_scratch_bytes": (cl, [vp]),
+    "kctc_minibatch_format": (ci, [vp, vp, vp, cl, vp]),
+    "kctc_minibatch_free": (ci, [vp]),
 }
 
 

@@ -158,3 +158,56 @@ def train_step(spec, rnn_params, affine_W, affine_b, feats, num_frames, flat_lab
         draws.ctypes.data if draws is not None else None, cnc, cc,
         ctypes.byref(acc), ctypes.byref(wt))
     return tot, acc.value, wt.value
+
+
+# ---- CompressedMatrix / FormatNnetInput restatement (oracle/oracle_egs.c) ----
+def _egs_bind(L):
+    if getattr(L, "_egs_bound", False):
+        return
+    L.oracle_cm_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.oracle_cm_bytes.restype = ctypes.c_long
+    L.oracle_cm_compress.argtypes = [f32p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    L.oracle_cm_compress.restype = ctypes.c_long
+    L.oracle_cm_decompress.argtypes = [ctypes.c_void_p, f32p]
+    L.oracle_cm_decompress.restype = None
+    L.oracle_format_input_cm.argtypes = [ctypes.c_void_p, i32p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, f32p]
+    L.oracle_format_input_cm.restype = None
+    L._egs_bound = True
+
+
+def cm_compress(m):
+    L = lib()
+    _egs_bind(L)
+    m = np.ascontiguousarray(m, dtype=np.float32)
+    rows, cols = m.shape
+    out = np.zeros(max(L.oracle_cm_bytes(rows, cols), 0), dtype=np.uint8)
+    if out.size:
+        L.oracle_cm_compress(m, rows, cols, out.ctypes.data)
+    return out
+
+
+def cm_decompress(img):
+    L = lib()
+    _egs_bind(L)
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    hdr = np.frombuffer(img[:20].tobytes(), dtype=np.int32)
+    out = np.empty((int(hdr[3]), int(hdr[4])), dtype=np.float32)
+    L.oracle_cm_decompress(img.ctypes.data, out)
+    return out
+
+
+def format_input_cm(images, ignore, spk, T_max):
+    """FormatNnetInput over compressed images -> [T_max*N, dim+spk_dim]."""
+    L = lib()
+    _egs_bind(L)
+    N = len(images)
+    imgs = [np.ascontiguousarray(i, dtype=np.uint8) for i in images]
+    arr = (ctypes.c_void_p * N)(*[i.ctypes.data for i in imgs])
+    hdr = np.frombuffer(imgs[0][:20].tobytes(), dtype=np.int32)
+    spk = np.ascontiguousarray(spk, dtype=np.float32) if spk is not None else np.zeros((N, 0), np.float32)
+    sd = spk.shape[1]
+    out = np.empty((T_max * N, int(hdr[4]) + sd), dtype=np.float32)
+    L.oracle_format_input_cm(ctypes.cast(arr, ctypes.c_void_p), np.ascontiguousarray(ignore, dtype=np.int32),
+                             spk.ctypes.data if sd else None, sd, N, T_max, out)
+    return out
