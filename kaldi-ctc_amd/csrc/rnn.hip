@@ -716,6 +716,12 @@ __device__ int probe_local(const RecParams &p, int d, int g, unsigned *myflag, i
 
 constexpr int kMaxEPT = 4;  // (n, unit) elements per thread: N * U <= 1024
 
+// Operand hand-off loads are the critical path of a step, and a wave's vector
+// memory operations complete in issue order (s_waitcnt vmcnt), so everything
+// else a step reads from or writes to HBM -- next step's input projection /
+// dy / saved activations, this step's G / aux stores -- is issued right AFTER
+// the step's hand-off loads have landed (behind the MFMA loop), never in
+// front of the next step's hand-off loads.
 template <int MODE, int RT>
 __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
   constexpr int NW = MODE == kLstm ? 4 : MODE == kGru ? 3 : 1;
@@ -745,27 +751,51 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
     Rs[c * LDR + k] = v;
   }
   const int items = N * U;
-  float cst[kMaxEPT], hpv[kMaxEPT], gin[kMaxEPT][NW], bR[kMaxEPT][NW];
+  float cst[kMaxEPT], hpv[kMaxEPT], gin[kMaxEPT][NW], gnx[kMaxEPT][NW], bR[kMaxEPT][NW];
+  float act[kMaxEPT][NW], cnew[kMaxEPT];
+  auto gin_load = [&](int t, float (&dst)[kMaxEPT][NW]) {
+#pragma unroll
+    for (int j = 0; j < kMaxEPT; j++) {
+      const int e = tid + j * NT, n = e / U, u = e - n * U;
+      if (e < items) {
+#pragma unroll
+        for (int q = 0; q < NW; q++) dst[j][q] = p.G[((long)t * N + n) * ldg + (long)d * NW * H + q * H + u0 + u];
+      }
+    }
+  };
+  // saved activations for the backward pass (G rows overwritten in place, aux)
+  auto act_store = [&](int t) {
+    if (MODE != kLstm && MODE != kGru) return;
+#pragma unroll
+    for (int j = 0; j < kMaxEPT; j++) {
+      const int e = tid + j * NT, n = e / U, u = e - n * U;
+      if (e < items) {
+        const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
+#pragma unroll
+        for (int q = 0; q < NW; q++) p.G[grow + q * H] = act[j][q];
+        p.aux[((long)t * N + n) * ldy + (long)d * H + u0 + u] = cnew[j];
+      }
+    }
+  };
 #pragma unroll
   for (int j = 0; j < kMaxEPT; j++) {
-    cst[j] = hpv[j] = 0.f;
+    cst[j] = hpv[j] = cnew[j] = 0.f;
     const int e = tid + j * NT, n = e / U, u = e - n * U;
 #pragma unroll
     for (int q = 0; q < NW; q++) {
       bR[j][q] = (MODE == kGru && e < items) ? Wd[p.bR_off + q * H + u0 + u] : 0.f;
-      gin[j][q] = 0.f;
-      if (e < items) {
-        const int t = d == 0 ? 0 : T - 1;
-        gin[j][q] = p.G[((long)t * N + n) * ldg + (long)d * NW * H + q * H + u0 + u];
-      }
+      gin[j][q] = gnx[j][q] = act[j][q] = 0.f;
     }
+    (void)n;
   }
+  gin_load(d == 0 ? 0 : T - 1, gin);
   int bad = 0;
   unsigned *myflag = p.flags + d * p.nwg + g;
   const int local = probe_local(p, d, g, myflag, bad, &bad_lds, &loc_lds);
   const int KG = H / 16;
   const int KGW = (KG + 3) / 4;
   const unsigned step_bytes = (unsigned)((long)N * ldy * sizeof(float));
+  int t_prev = -1;
   for (int k = 0; k < T && !bad; k++) {
     const int t = d == 0 ? k : T - 1 - k, tp = d == 0 ? t - 1 : t + 1;
     floatx4 acc[RT][kMaxCT];
@@ -805,6 +835,11 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
         }
       }
     }
+    asm volatile("" ::: "memory");
+    // behind the hand-off loads: previous step's saved activations, next
+    // step's input projection
+    if (t_prev >= 0) act_store(t_prev);
+    if (k + 1 < T) gin_load(d == 0 ? t + 1 : t - 1, gnx);
 #pragma unroll
     for (int rt = 0; rt < RT; rt++)
 #pragma unroll
@@ -815,11 +850,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
             red[((long)w * p.Npad + rt * 16 + fq * 4 + r) * ncol + ct * 16 + fr] = acc[rt][ct][r];
     __syncthreads();
     REC_TRACE(k, 3);
-    float act[kMaxEPT][NW], cnew[kMaxEPT];
 #pragma unroll
     for (int j = 0; j < kMaxEPT; j++) {
       const int e = tid + j * NT;
-      cnew[j] = 0.f;
       if (e >= items) continue;
       const int n = e / U, u = e - n * U;
       float rh[NW];
@@ -854,25 +887,14 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
     signal_epoch(myflag, (unsigned)(k + 2), local);
     REC_TRACE(k, 4);
 #pragma unroll
-    for (int j = 0; j < kMaxEPT; j++) {
-      const int e = tid + j * NT;
-      if (e >= items) continue;
-      const int n = e / U, u = e - n * U;
-      if (MODE == kLstm || MODE == kGru) {
-        const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
+    for (int j = 0; j < kMaxEPT; j++)
 #pragma unroll
-        for (int q = 0; q < NW; q++) p.G[grow + q * H] = act[j][q];
-        p.aux[((long)t * N + n) * ldy + (long)d * H + u0 + u] = cnew[j];
-      }
-      if (k + 1 < T) {  // prefetch the next step's input projection
-        const int tn = d == 0 ? t + 1 : t - 1;
-#pragma unroll
-        for (int q = 0; q < NW; q++) gin[j][q] = p.G[((long)tn * N + n) * ldg + (long)d * NW * H + q * H + u0 + u];
-      }
-    }
+      for (int q = 0; q < NW; q++) gin[j][q] = gnx[j][q];
+    t_prev = t;
     __syncthreads();  // red[] is rewritten by the next step
     REC_TRACE(k, 5);
   }
+  if (t_prev >= 0 && !bad) act_store(t_prev);
   if (bad && tid == 0) atomicOr(p.err, 1u);
 }
 
@@ -899,15 +921,17 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
     RT_s[u * LDK + kk] = R[(long)kk * H + u0 + u];
   }
   const int items = N * U;
-  float carry[kMaxEPT], bsx[kMaxEPT][NW], bsh[kMaxEPT][NW];
-  float pg[kMaxEPT][NW], pdy[kMaxEPT], pa[kMaxEPT], pap[kMaxEPT];
+  // per element: current step's operands (c*) and the next step's (n*)
+  float carry[kMaxEPT], bsx[kMaxEPT][NW], bsh[kMaxEPT][NW], dxk[kMaxEPT][NW];
+  float cg[kMaxEPT][NW], cdy[kMaxEPT], ca[kMaxEPT], cap[kMaxEPT];
+  float ng[kMaxEPT][NW], ndy[kMaxEPT], na[kMaxEPT], nap[kMaxEPT];
 #pragma unroll
   for (int j = 0; j < kMaxEPT; j++) {
-    carry[j] = pdy[j] = pa[j] = pap[j] = 0.f;
+    carry[j] = cdy[j] = ca[j] = cap[j] = ndy[j] = na[j] = nap[j] = 0.f;
 #pragma unroll
-    for (int q = 0; q < NW; q++) bsx[j][q] = bsh[j][q] = pg[j][q] = 0.f;
+    for (int q = 0; q < NW; q++) bsx[j][q] = bsh[j][q] = cg[j][q] = ng[j][q] = dxk[j][q] = 0.f;
   }
-  auto prefetch = [&](int k) {
+  auto prefetch = [&](int k) {  // operands of forward-order step k into n*
     const int t = d == 0 ? k : T - 1 - k, tp = d == 0 ? t - 1 : t + 1;
 #pragma unroll
     for (int j = 0; j < kMaxEPT; j++) {
@@ -917,24 +941,45 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
       const long yrow = ((long)t * N + n) * ldy + (long)d * H + u0 + u;
       const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
       const long prow = ((long)tp * N + n) * ldy + (long)d * H + u0 + u;
-      pdy[j] = p.dy[yrow];
+      ndy[j] = p.dy[yrow];
       if (MODE == kLstm || MODE == kGru) {
 #pragma unroll
-        for (int q = 0; q < NW; q++) pg[j][q] = p.G[grow + q * H];
-        pa[j] = p.aux[yrow];
+        for (int q = 0; q < NW; q++) ng[j][q] = p.G[grow + q * H];
+        na[j] = p.aux[yrow];
       }
-      if (MODE == kLstm) pap[j] = k > 0 ? p.aux[prow] : 0.f;
-      else if (MODE == kGru) pap[j] = k > 0 ? p.y[prow] : 0.f;
-      else pap[j] = p.y[yrow];
+      if (MODE == kLstm) nap[j] = k > 0 ? p.aux[prow] : 0.f;
+      else if (MODE == kGru) nap[j] = k > 0 ? p.y[prow] : 0.f;
+      else nap[j] = p.y[yrow];
+    }
+  };
+  auto rotate = [&]() {
+#pragma unroll
+    for (int j = 0; j < kMaxEPT; j++) {
+      cdy[j] = ndy[j]; ca[j] = na[j]; cap[j] = nap[j];
+#pragma unroll
+      for (int q = 0; q < NW; q++) cg[j][q] = ng[j][q];
+    }
+  };
+  auto dx_store = [&](int t) {  // GRU: input-side dGates of step t
+#pragma unroll
+    for (int j = 0; j < kMaxEPT; j++) {
+      const int e = tid + j * NT;
+      if (e >= items) continue;
+      const int n = e / U, u = e - n * U;
+      const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
+#pragma unroll
+      for (int q = 0; q < NW; q++) p.DX[grow + q * H] = dxk[j][q];
     }
   };
   prefetch(T - 1);
+  rotate();
   int bad = 0;
   unsigned *myflag = p.flags + d * p.nwg + g;
   const int local = probe_local(p, d, g, myflag, bad, &bad_lds, &loc_lds);
   const int KG = K / 16;
   const int KGW = (KG + 3) / 4;
   const unsigned step_bytes = (unsigned)((long)N * ldg * sizeof(float));
+  int t_prev = -1;
   for (int k = T - 1; k >= 0 && !bad; k--) {
     const int t = d == 0 ? k : T - 1 - k;
     const int tn = d == 0 ? t + 1 : t - 1;
@@ -969,13 +1014,16 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
         }
       }
     }
+    asm volatile("" ::: "memory");
+    // behind the hand-off loads: next step's operands, last step's GRU dx
+    if (k > 0) prefetch(k - 1);
+    if (MODE == kGru && t_prev >= 0) dx_store(t_prev);
 #pragma unroll
     for (int rt = 0; rt < RT; rt++)
 #pragma unroll
       for (int r = 0; r < 4; r++) red[((long)w * p.Npad + rt * 16 + fq * 4 + r) * 16 + fr] = acc[rt][r];
     __syncthreads();
     REC_TRACE(ks, 3);
-    float dxk[kMaxEPT][NW];
 #pragma unroll
     for (int j = 0; j < kMaxEPT; j++) {
       const int e = tid + j * NT;
@@ -983,15 +1031,15 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
       const int n = e / U, u = e - n * U;
       const float dhr = ((red[((long)0 * p.Npad + n) * 16 + u] + red[((long)1 * p.Npad + n) * 16 + u]) +
                          red[((long)2 * p.Npad + n) * 16 + u]) + red[((long)3 * p.Npad + n) * 16 + u];
-      float dh = pdy[j] + dhr;
+      float dh = cdy[j] + dhr;
       float *Erow = p.E + ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
       if (MODE == kLstm) {
-        const float ig = pg[j][0], fg = pg[j][1], gg = pg[j][2], og = pg[j][3];
-        const float tc = ftanh(pa[j]);
+        const float ig = cg[j][0], fg = cg[j][1], gg = cg[j][2], og = cg[j][3];
+        const float tc = ftanh(ca[j]);
         const float dO = dh * tc;
         const float dc = dh * og * (1.f - tc * tc) + carry[j];
         const float dpi = dc * gg * ig * (1.f - ig);
-        const float dpf = dc * pap[j] * fg * (1.f - fg);
+        const float dpf = dc * cap[j] * fg * (1.f - fg);
         const float dpg = dc * ig * (1.f - gg * gg);
         const float dpo = dO * og * (1.f - og);
         carry[j] = dc * fg;
@@ -1002,10 +1050,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
         bsx[j][0] += dpi; bsx[j][1] += dpf; bsx[j][2] += dpg; bsx[j][3] += dpo;
       } else if (MODE == kGru) {
         dh += carry[j];
-        const float r = pg[j][0], z = pg[j][1], nn = pg[j][2];
-        const float dn = dh * (1.f - z), dz = dh * (pap[j] - nn);
+        const float r = cg[j][0], z = cg[j][1], nn = cg[j][2];
+        const float dn = dh * (1.f - z), dz = dh * (cap[j] - nn);
         const float dpn = dn * (1.f - nn * nn);
-        const float dpr = dpn * pa[j] * r * (1.f - r);
+        const float dpr = dpn * ca[j] * r * (1.f - r);
         const float dpz = dz * z * (1.f - z);
         carry[j] = dh * z;
         dxk[j][0] = dpr; dxk[j][1] = dpz; dxk[j][2] = dpn;
@@ -1015,7 +1063,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
         bsx[j][0] += dpr; bsx[j][1] += dpz; bsx[j][2] += dpn;
         bsh[j][0] += dpr; bsh[j][1] += dpz; bsh[j][2] += dpn * r;
       } else {
-        const float der = MODE == kRelu ? (pap[j] > 0.f ? 1.f : 0.f) : (1.f - pap[j] * pap[j]);
+        const float der = MODE == kRelu ? (cap[j] > 0.f ? 1.f : 0.f) : (1.f - cap[j] * cap[j]);
         const float dp = dh * der;
         put(Erow, dp, local);
         bsx[j][0] += dp;
@@ -1023,21 +1071,12 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
     }
     signal_epoch(myflag, (unsigned)(ks + 2), local);
     REC_TRACE(ks, 4);
-    if (MODE == kGru) {
-#pragma unroll
-      for (int j = 0; j < kMaxEPT; j++) {
-        const int e = tid + j * NT;
-        if (e >= items) continue;
-        const int n = e / U, u = e - n * U;
-        const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
-#pragma unroll
-        for (int q = 0; q < NW; q++) p.DX[grow + q * H] = dxk[j][q];
-      }
-    }
-    if (k > 0) prefetch(k - 1);
+    rotate();
+    t_prev = t;
     __syncthreads();
     REC_TRACE(ks, 5);
   }
+  if (MODE == kGru && t_prev >= 0 && !bad) dx_store(t_prev);
   // bias partial sums: reduce over n in a fixed order through LDS
   float *bs = red;  // reuse: [2][N][U][NW] floats (fits: see lds sizing)
   __syncthreads();
