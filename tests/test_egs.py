@@ -158,7 +158,7 @@ def _make_egs(rng, n, dim=40, T=(30, 200), spk_dim=0, left_context=0):
     egs = []
     for i in range(n):
         t = int(rng.integers(*T))
-        L = int(rng.integers(0, max(1, (t - 1) // 2)))
+        L = min(int(rng.integers(0, max(1, (t - 1) // 2))), 639)  # readable: <= 639 labels
         feats = rng.standard_normal((t, dim)).astype(np.float32)
         labels = rng.integers(1, 41, size=L).astype(np.int32)
         spk = rng.standard_normal(spk_dim).astype(np.float32) if spk_dim else None
