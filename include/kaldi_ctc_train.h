@@ -79,6 +79,22 @@ int kctc_nnet_read(kctcNnet_t *nnet, const char *path, int device);
 int kctc_dp_unique_id(void *uid128);
 int kctc_nnet_enable_dp(kctcNnet_t nnet, const void *uid128, int rank, int world_size);
 
+/* TrainNnetSimple momentum (src/ctc/ctc-nnet-train.cc:194-245, config
+ * ctc-nnet-train.h:33-66): with m != 0 every update goes to a delta copy
+ * (delta += lr * clip(grad); params += delta; delta *= m) and ClipGradient
+ * counters accumulate in the delta copy.  0 (default) = plain SGD. */
+int kctc_nnet_set_momentum(kctcNnet_t nnet, float momentum);
+
+/* TrainNnetSimple (src/ctc/ctc-nnet-train.cc:185-284) over a background egs
+ * reader (include/kaldi_ctc_egs.h, opened with the trainer's minibatch_size /
+ * max_allow_frames): every minibatch is formatted on the GPU and trained with
+ * DoBackprop until the archive is exhausted or max_minibatches (> 0) have run.
+ * Outputs (may be NULL): examples processed, total weight (labels), total
+ * objective, total accuracy. */
+struct kctcEgsReader_;
+int kctc_nnet_train_simple(kctcNnet_t nnet, struct kctcEgsReader_ *reader, long max_minibatches,
+                           long *num_egs, double *tot_weight, double *tot_objf, double *tot_accuracy);
+
 /* FormatNnetInput: pack per-utterance [T_n][dim] host matrices (concatenated
  * in `feats`, row offsets by num_frames) into [T_max*N][dim], row t*N+n,
  * zero padded.  out must hold T_max*N*dim floats (host). */

@@ -363,6 +363,16 @@ class Nnet:
         _tcheck(lib().kctc_nnet_profile(self.h, family.encode(), ctypes.byref(ms), ctypes.byref(n)), "profile")
         return ms.value, n.value
 
+    def set_momentum(self, m):
+        _tcheck(lib().kctc_nnet_set_momentum(self.h, float(m)), "set_momentum")
+
+    def train_simple(self, reader, max_minibatches=0):
+        """TrainNnetSimple over an EgsReader -> dict(num_egs, tot_weight, tot_objf, tot_accuracy)."""
+        ne, w, o, a = ctypes.c_long(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        _tcheck(lib().kctc_nnet_train_simple(self.h, reader._h, int(max_minibatches), ctypes.byref(ne),
+                                             ctypes.byref(w), ctypes.byref(o), ctypes.byref(a)), "train_simple")
+        return {"num_egs": ne.value, "tot_weight": w.value, "tot_objf": o.value, "tot_accuracy": a.value}
+
     def enable_dp(self, uid, rank, world):
         buf = ctypes.create_string_buffer(bytes(uid), 128)
         _tcheck(lib().kctc_nnet_enable_dp(self.h, buf, rank, world), "enable_dp")

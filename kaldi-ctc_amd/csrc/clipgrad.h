@@ -21,6 +21,10 @@ size_t clipgrad_scratch_bytes(long rows);
 // clipped-proportion part is evaluated on the device.
 void clipgrad_backprop(hipStream_t s, float *d, const float *in_value, long rows, int dim,
                        float threshold, bool norm_based, bool try_repair, float repair_threshold,
-                       float repair_target, float repair_scale, ClipState *st, void *scratch);
+                       float repair_target, float repair_scale, ClipState *st, void *scratch,
+                       const ClipState *decide = nullptr);
+// st accumulates the counters; decide (default st) supplies the clipped
+// proportion of the repair decision: the backpropped component's own stats,
+// which differ from to_update's under momentum (ctc-nnet-train.cc:194-202).
 
 }  // namespace kctc

@@ -75,14 +75,14 @@ __device__ double block_sum(double v) {
   return r;
 }
 
-__global__ __launch_bounds__(256) void k_decide(State *st, const double *__restrict__ part, int nb,
-                                                long rows, float threshold, float scale) {
+__global__ __launch_bounds__(256) void k_decide(State *st, const State *dec, const double *__restrict__ part,
+                                                int nb, long rows, float threshold, float scale) {
   double a = 0, b = 0;
   for (int i = threadIdx.x; i < nb; i += 256) { a += part[2 * i]; b += part[2 * i + 1]; }
   a = block_sum(a);
   b = block_sum(b);
   if (threadIdx.x == 0) {
-    const double prop = st->count > 0 ? st->num_clipped / st->count : 0.0;
+    const double prop = dec->count > 0 ? dec->num_clipped / dec->count : 0.0;
     st->active = prop > (double)threshold;
     st->dn = a;
     st->rn = b;
@@ -137,7 +137,9 @@ size_t clipgrad_scratch_bytes(long rows) { return sizeof(double) * 2 * (size_t)(
 
 void clipgrad_backprop(hipStream_t s, float *d, const float *in_value, long rows, int dim,
                        float threshold, bool norm_based, bool try_repair, float repair_threshold,
-                       float repair_target, float repair_scale, ClipState *st, void *scratch) {
+                       float repair_target, float repair_scale, ClipState *st, void *scratch,
+                       const ClipState *decide) {
+  if (!decide) decide = st;
   if (rows <= 0 || !(threshold > 0.f)) return;
   if (norm_based) {
     rownorm_clip(s, d, rows, dim, threshold, &st->step_clipped);
@@ -152,7 +154,7 @@ void clipgrad_backprop(hipStream_t s, float *d, const float *in_value, long rows
   const int nb = ceil_div(rows, 4);
   hipLaunchKernelGGL(k_norms, dim3(nb), dim3(256), 0, s, d, in_value, rows, dim, repair_target, 1,
                      part);
-  hipLaunchKernelGGL(k_decide, dim3(1), dim3(256), 0, s, st, part, nb, rows,
+  hipLaunchKernelGGL(k_decide, dim3(1), dim3(256), 0, s, st, decide, part, nb, rows,
                      repair_threshold, repair_scale);
   hipLaunchKernelGGL(k_apply, dim3(nb), dim3(256), 0, s, d, in_value, rows, dim, repair_target, st,
                      part);

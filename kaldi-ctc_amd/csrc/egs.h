@@ -147,3 +147,9 @@ void format_on_device(Minibatch &mb, float *out, void *scratch, size_t scratch_b
 
 }  // namespace egs
 }  // namespace kctc
+
+// opaque handles of include/kaldi_ctc_egs.h (shared by egs_api.cpp and train_api.cpp)
+struct kctcEgsReader_ {
+  kctc::egs::BackgroundReader r;
+  kctcEgsReader_(const char *spec, int mb, int max_frames, int l, int rc) : r(spec, mb, max_frames, l, rc) {}
+};

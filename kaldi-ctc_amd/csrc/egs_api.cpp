@@ -13,10 +13,6 @@ struct kctcEgsWriter_ {
   ArchiveWriter w;
   explicit kctcEgsWriter_(const char *spec) : w(spec) {}
 };
-struct kctcEgsReader_ {
-  BackgroundReader r;
-  kctcEgsReader_(const char *spec, int mb, int max_frames, int l, int rc) : r(spec, mb, max_frames, l, rc) {}
-};
 struct kctcMinibatch_ {
   std::unique_ptr<Minibatch> mb;
 };

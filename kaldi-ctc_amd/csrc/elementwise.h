@@ -8,6 +8,10 @@ namespace kctc {
 
 // w += lr * clamp(dw, -clip, clip)   (clip <= 0: no clamp)
 void clip_sgd_update(hipStream_t s, float *w, const float *dw, long n, float lr, float clip);
+// momentum form (TrainNnetSimple with a delta nnet, ctc-nnet-train.cc:194-245):
+// delta += lr * clamp(dw); w += delta; delta *= m
+void momentum_update(hipStream_t s, float *w, float *delta, const float *dw, long n, float lr, float clip,
+                     float m);
 // ClipGradientComponent norm-based backprop: rows with |row| >= thr scaled to
 // norm thr; *nclipped (device int) += number of such rows.
 void rownorm_clip(hipStream_t s, float *d, long rows, int dim, float thr, int *nclipped);

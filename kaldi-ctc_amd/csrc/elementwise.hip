@@ -147,6 +147,24 @@ static int grid_for(long n, int per = 256) {
   return (int)std::max<long>(1, std::min<long>(b, 4096));
 }
 
+__global__ __launch_bounds__(256) void k_momentum(float *__restrict__ w, float *__restrict__ delta,
+                                                  const float *__restrict__ dw, long n, float lr, float clip,
+                                                  float m) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    float g = dw[i];
+    if (clip > 0.f) g = fminf(fmaxf(g, -clip), clip);
+    const float dl = delta[i] + lr * g;
+    w[i] += dl;
+    delta[i] = m * dl;
+  }
+}
+
+void momentum_update(hipStream_t s, float *w, float *delta, const float *dw, long n, float lr, float clip,
+                     float m) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_momentum, dim3(grid_for(n)), dim3(256), 0, s, w, delta, dw, n, lr, clip, m);
+}
+
 void clip_sgd_update(hipStream_t s, float *w, const float *dw, long n, float lr, float clip) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_clip_sgd, dim3(grid_for((n + 3) / 4)), dim3(256), 0, s, w, dw, n, lr, clip);

@@ -424,6 +424,22 @@ void CuDNNRecurrentComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
 
 hipStream_t UpdatableComponent::GradStream() const { return grad_stream_ ? grad_stream_ : S(); }
 
+void UpdatableComponent::SetMomentum(float m) {
+  if (!(m >= 0.f && m < 1.f)) throw std::invalid_argument("momentum must be in [0, 1)");
+  momentum_ = m;
+  if (m != 0.f) {  // delta_nnet->SetZero(false): a fresh zero delta
+    delta_.ensure(sizeof(float) * NumParameters());
+    KCTC_HIP_CHECK(hipMemsetAsync(delta_.p, 0, sizeof(float) * NumParameters(), S()));
+  }
+}
+
+void UpdatableComponent::UpdateWith(float *params, const float *grad, float clip) {
+  if (momentum_ == 0.f)
+    clip_sgd_update(S(), params, grad, NumParameters(), learning_rate_, clip);
+  else
+    momentum_update(S(), params, delta_.f(), grad, NumParameters(), learning_rate_, clip, momentum_);
+}
+
 int CuDNNRecurrentComponent::side_gemm_blocks() const {
   const char *e = getenv("KCTC_SIDE_BLOCKS");
   if (e && *e) return atoi(e);
@@ -432,7 +448,7 @@ int CuDNNRecurrentComponent::side_gemm_blocks() const {
 
 void CuDNNRecurrentComponent::ApplyUpdate() {
   // ApplyFloor(-clip) / ApplyCeiling(clip) then filter_params_ += lr * grad
-  clip_sgd_update(S(), params_.f(), grad_.f(), NumParameters(), learning_rate_, clip_gradient_);
+  UpdateWith(params_.f(), grad_.f(), clip_gradient_);
 }
 
 void CuDNNRecurrentComponent::Vectorize(float *host) const {
@@ -485,7 +501,30 @@ ClipGradientComponent::ClipGradientComponent() {
   KCTC_HIP_CHECK(hipMemset(dev_, 0, sizeof(ClipState)));
 }
 ClipGradientComponent::~ClipGradientComponent() {
+  delete shadow_;
   if (dev_) (void)hipFree(dev_);
+}
+
+// delta_nnet = new Nnet(*nnet): the copy starts with this component's
+// configuration and counters (ctc-nnet-train.cc:194-202)
+void ClipGradientComponent::EnableShadow(bool on) {
+  delete shadow_;
+  shadow_ = nullptr;
+  if (!on) return;
+  auto *c = new ClipGradientComponent();
+  c->dim_ = dim_;
+  c->clipping_threshold_ = clipping_threshold_;
+  c->norm_based_clipping_ = norm_based_clipping_;
+  c->self_repair_clipped_proportion_threshold_ = self_repair_clipped_proportion_threshold_;
+  c->self_repair_target_ = self_repair_target_;
+  c->self_repair_scale_ = self_repair_scale_;
+  SyncStats();
+  c->num_clipped_ = num_clipped_;
+  c->count_ = count_;
+  c->num_self_repaired_ = num_self_repaired_;
+  c->num_backpropped_ = num_backpropped_;
+  KCTC_HIP_CHECK(hipMemcpyAsync(c->dev_, dev_, sizeof(ClipState), hipMemcpyDeviceToDevice, S()));
+  shadow_ = c;
 }
 
 void ClipGradientComponent::InitFromString(std::string args, Rng &) {
@@ -546,7 +585,7 @@ void ClipGradientComponent::Backprop(const ChunkInfo &, const ChunkInfo &, const
   bool try_repair = false;
   if (to_update) {
     to_update->num_backpropped_ += 1;
-    const double count_after = count_ + (norm_based_clipping_ ? rows : 0);
+    const double count_after = count_ + ((norm_based_clipping_ && to_update == this) ? rows : 0);
     if (!(self_repair_clipped_proportion_threshold_ >= 1.0f || self_repair_scale_ == 0.0f ||
           count_after == 0))
       try_repair = !(next_draw_ > 0.5f);
@@ -557,7 +596,7 @@ void ClipGradientComponent::Backprop(const ChunkInfo &, const ChunkInfo &, const
   clipgrad_backprop(S(), in_deriv->Data(), in_value.Data(), rows, dim_, clipping_threshold_,
                     norm_based_clipping_, try_repair, self_repair_clipped_proportion_threshold_,
                     self_repair_target_, self_repair_scale_, (to_update ? to_update : this)->dev_,
-                    scratch_.p);
+                    scratch_.p, dev_);
 }
 
 void ClipGradientComponent::SyncStats() const {
@@ -701,7 +740,7 @@ void AffineComponent::Backprop(const ChunkInfo &, const ChunkInfo &, const CuMat
 }
 
 void AffineComponent::ApplyUpdate() {
-  clip_sgd_update(S(), params_.f(), grad_.f(), NumParameters(), learning_rate_, 0.f);
+  UpdateWith(params_.f(), grad_.f(), 0.f);
 }
 void AffineComponent::Vectorize(float *host) const {
   auto v = d2h(params_.f(), NumParameters());
@@ -799,6 +838,15 @@ int Nnet::FirstUpdatableComponent() const {  // nnet-nnet.cc:838-845
 
 void Nnet::ZeroStats() {
   for (auto *c : components_) c->ZeroStats();
+}
+
+void Nnet::SetMomentum(float m) {
+  if (!(m >= 0.f && m < 1.f)) throw std::invalid_argument("momentum must be in [0, 1)");
+  momentum_ = m;
+  for (auto *c : components_) {
+    if (c->IsUpdatable()) static_cast<UpdatableComponent *>(c)->SetMomentum(m);
+    if (auto *cg = dynamic_cast<ClipGradientComponent *>(c)) cg->EnableShadow(m != 0.f);
+  }
 }
 
 void Nnet::SetLearningRate(float lr) {
@@ -1005,6 +1053,7 @@ void NnetCtcUpdater::Backprop(int T, int N) {  // :320-348
     if (auto *cg = dynamic_cast<ClipGradientComponent *>(&comp)) {
       // RandUniform() for RepairGradients, one stream per updater
       cg->next_draw_ = (float)repair_rng_.uniform();
+      if (cg->Shadow()) to_update = cg->Shadow();  // momentum: delta_nnet's copy
     }
     const CuMatrixBase od(cur->Data(), rows, comp.OutputDim());
     comp.Backprop(chunk_info_[c], chunk_info_[c + 1], in, outv, od, to_update, in_deriv);

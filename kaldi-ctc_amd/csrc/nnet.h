@@ -159,10 +159,18 @@ class UpdatableComponent : public Component {
   // stream on which GradData() was produced (the exchange waits on it)
   hipStream_t GradStream() const;
   virtual void ApplyUpdate() = 0;  // params += lr * (clipped) grad
+  // TrainNnetSimple momentum (ctc-nnet-train.cc:194-245): the update goes to
+  // a delta copy (delta += lr * clip(grad)), then params += delta and
+  // delta *= momentum.  0 = plain SGD (the recipe's default).
+  void SetMomentum(float m);
+  float Momentum() const { return momentum_; }
 
  protected:
+  void UpdateWith(float *params, const float *grad, float clip);
   float learning_rate_ = 0.001f;
   hipStream_t grad_stream_ = nullptr;  // nullptr: the device's compute stream
+  float momentum_ = 0.f;
+  DevBuf delta_;
 };
 
 class SpliceComponent : public Component {
@@ -252,6 +260,10 @@ class ClipGradientComponent : public Component {
   double Count() const { return count_; }
   // one RandUniform() per Backprop, drawn by the updater (glibc rand() in the reference)
   mutable float next_draw_ = 1.0f;
+  // momentum training passes delta_nnet's copy as to_update: counters go to
+  // the copy, the repair decision reads this component's own counters
+  void EnableShadow(bool on);
+  ClipGradientComponent *Shadow() const { return shadow_; }
 
 
  private:
@@ -263,6 +275,7 @@ class ClipGradientComponent : public Component {
   mutable double num_clipped_ = 0, count_ = 0, num_self_repaired_ = 0, num_backpropped_ = 0;
   ClipState *dev_ = nullptr;
   mutable DevBuf scratch_;
+  ClipGradientComponent *shadow_ = nullptr;
 };
 
 class AffineComponent : public UpdatableComponent {
@@ -305,11 +318,14 @@ class Nnet {
   int OutputDim() const { return components_.back()->OutputDim(); }
   void ZeroStats();
   void SetLearningRate(float lr);
+  void SetMomentum(float m);
+  float Momentum() const { return momentum_; }
   void Write(std::ostream &os) const;
   void Read(std::istream &is);
 
  private:
   std::vector<Component *> components_;
+  float momentum_ = 0.f;
 };
 
 // Data-parallel gradient exchange (RCCL over xGMI); implemented in dp.cpp.

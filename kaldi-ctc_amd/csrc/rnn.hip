@@ -168,7 +168,7 @@ struct RecParams {
   int allow_local;  // v4: hand off through the shared L2 when placement allows it
 };
 
-// Phase stamps of the first kTraceSteps steps (thread 0 of every workgroup;
+// Phase stamps of the first kTraceSteps steps ([steps][grid][16]; thread 0 of every workgroup;
 // 100 MHz constant clock), only when the host passes a trace buffer
 // (KCTC_REC_TRACE): 0 step start, 1 flags seen, 2 operand loads landed,
 // 3 MFMA + K reduction done, 4 published (+ flag), 5 step end.
@@ -176,7 +176,14 @@ constexpr int kTraceSteps = 256;
 #define REC_TRACE(kk, ph)                                                                 \
   do {                                                                                    \
     if (p.trace && threadIdx.x == 0 && (kk) < kTraceSteps)                                \
-      p.trace[((long)(kk) * gridDim.x + blockIdx.x) * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); \
+      p.trace[((long)(kk) * gridDim.x + blockIdx.x) * 16 + (ph)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+// per-wave stamps (lane 0 of every wave): slot 6 + w loads landed, 10 + w MFMA done
+#define REC_TRACE_W(kk, ph)                                                               \
+  do {                                                                                    \
+    if (p.trace && (threadIdx.x & 63) == 0 && (kk) < kTraceSteps)                         \
+      p.trace[((long)(kk) * gridDim.x + blockIdx.x) * 16 + (ph) + (threadIdx.x >> 6)] =   \
+          __builtin_amdgcn_s_memrealtime();                                               \
   } while (0)
 
 // Hand-off protocols (selected per launch; both placement-independent):
@@ -814,6 +821,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
         if (p.trace) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           REC_TRACE(k, 2);
+          REC_TRACE_W(k, 6);
         }
 #pragma unroll
         for (int i = 0; i < CH; i++) {
@@ -848,6 +856,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
 #pragma unroll
           for (int r = 0; r < 4; r++)
             red[((long)w * p.Npad + rt * 16 + fq * 4 + r) * ncol + ct * 16 + fr] = acc[rt][ct][r];
+    if (p.trace) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      REC_TRACE_W(k, 10);
+    }
     __syncthreads();
     REC_TRACE(k, 3);
 #pragma unroll
@@ -998,6 +1010,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
         if (p.trace) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           REC_TRACE(ks, 2);
+          REC_TRACE_W(ks, 6);
         }
 #pragma unroll
         for (int i = 0; i < CH; i++) {
@@ -1022,6 +1035,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
     for (int rt = 0; rt < RT; rt++)
 #pragma unroll
       for (int r = 0; r < 4; r++) red[((long)w * p.Npad + rt * 16 + fq * 4 + r) * 16 + fr] = acc[rt][r];
+    if (p.trace) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      REC_TRACE_W(ks, 10);
+    }
     __syncthreads();
     REC_TRACE(ks, 3);
 #pragma unroll
@@ -1162,7 +1179,7 @@ struct RecTrace {
     bool &done = tag[0] == 'f' ? done_fwd : done_bwd;
     if (done) return false;
     done = true;
-    n = (size_t)kTraceSteps * grid * 8;
+    n = (size_t)kTraceSteps * grid * 16;
     KCTC_HIP_CHECK(hipMalloc(&dev, n * sizeof(unsigned long long)));
     KCTC_HIP_CHECK(hipMemset(dev, 0, n * sizeof(unsigned long long)));
     return true;

@@ -12,6 +12,7 @@
 #include <string>
 
 #include "common.h"
+#include "egs.h"
 #include "nnet.h"
 
 using kctc::nnet2::CuDevice;
@@ -77,6 +78,7 @@ struct kctcNnetImpl {
   kctc::nnet2::NnetCtcUpdater evaluator{&nnet, false};
   hipStream_t side = nullptr;
   RcclExchange *dp = nullptr;
+  kctc::nnet2::DevBuf egs_feats, egs_scratch;  // TrainNnetSimple staging
   ~kctcNnetImpl() {
     delete dp;
     if (stream) (void)hipStreamSynchronize(stream);
@@ -310,6 +312,45 @@ int kctc_nnet_enable_dp(kctcNnet_t n, const void *uid128, int rank, int world_si
       n->dp = new RcclExchange(uid128, rank, world_size, n->stream);
       n->trainer.SetExchange(n->dp);
     }
+  });
+}
+
+int kctc_nnet_set_momentum(kctcNnet_t n, float momentum) {
+  return guarded([&] {
+    KCTC_REQUIRE(n, "null nnet");
+    n->activate();
+    n->nnet.SetMomentum(momentum);
+  });
+}
+
+int kctc_nnet_train_simple(kctcNnet_t n, struct kctcEgsReader_ *r, long max_minibatches, long *num_egs,
+                           double *tot_weight, double *tot_objf, double *tot_accuracy) {
+  return guarded([&] {
+    KCTC_REQUIRE(n && r, "kctc_nnet_train_simple: null argument");
+    n->activate();
+    long egs = 0, mbs = 0;
+    double w = 0, objf = 0, acc = 0;
+    while (max_minibatches <= 0 || mbs < max_minibatches) {
+      std::unique_ptr<kctc::egs::Minibatch> mb = r->r.Next();  // GetNextMinibatch
+      if (!mb) break;
+      if (mb->InputDim() != n->nnet.InputDim())
+        throw std::invalid_argument("egs input dim " + std::to_string(mb->InputDim()) + " != nnet input dim " +
+                                    std::to_string(n->nnet.InputDim()));
+      n->egs_feats.ensure(sizeof(float) * (size_t)mb->T_max * mb->N * mb->InputDim());
+      n->egs_scratch.ensure(kctc::egs::format_scratch_bytes(*mb));
+      kctc::egs::format_on_device(*mb, n->egs_feats.f(), n->egs_scratch.p, n->egs_scratch.bytes, n->stream);
+      const auto st = n->trainer.ComputeForMinibatch(n->egs_feats.f(), mb->T_max, mb->N, mb->num_frames.data(),
+                                                     mb->labels.data(), mb->label_lengths.data());
+      objf += st.tot_objf;
+      acc += st.tot_accuracy;
+      w += st.tot_weight;
+      egs += mb->N;
+      mbs++;
+    }
+    if (num_egs) *num_egs = egs;
+    if (tot_weight) *tot_weight = w;
+    if (tot_objf) *tot_objf = objf;
+    if (tot_accuracy) *tot_accuracy = acc;
   });
 }
 

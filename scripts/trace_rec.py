@@ -11,7 +11,7 @@ import numpy as np
 def main(path):
     raw = open(path, "rb").read()
     grid, steps, nwg, T, dirs, ver = np.frombuffer(raw[:24], dtype=np.int32)
-    tr = np.frombuffer(raw[24:], dtype=np.uint64).reshape(steps, grid, 8).astype(np.int64)
+    tr = np.frombuffer(raw[24:], dtype=np.uint64).reshape(steps, grid, 16).astype(np.int64)
     steps = min(steps, T)
     tr = tr[:steps]
     if ver == 4:
@@ -28,6 +28,11 @@ def main(path):
     for i, nm in enumerate(names):
         d = (tr[sl, :, i + 1] - tr[sl, :, i]) * us
         print(f"  {nm:22s} median {np.median(d):7.3f}  p90 {np.percentile(d, 90):7.3f}")
+    if ver == 4 and tr[sl, :, 6].min() > 0:
+        for w in range(4):
+            ld = (tr[sl, :, 6 + w] - tr[sl, :, 1]) * us
+            mf = (tr[sl, :, 10 + w] - tr[sl, :, 6 + w]) * us
+            print(f"  wave {w}: flags->loads {np.median(ld):7.3f}  loads->mfma-done {np.median(mf):7.3f}")
     step = (tr[9:steps, :, 0] - tr[8:steps - 1, :, 0]) * us
     print(f"  step period            median {np.median(step):7.3f}  p90 {np.percentile(step, 90):7.3f}")
     lat = []
