@@ -723,6 +723,63 @@ __device__ int probe_local(const RecParams &p, int d, int g, unsigned *myflag, i
 
 constexpr int kMaxEPT = 4;  // (n, unit) elements per thread: N * U <= 1024
 
+// Branch-free MFMA bodies with compile-time trip counts (the generic loops'
+// per-iteration guards made the compiler drain vmcnt/lgkmcnt and shuttle the
+// accumulators between AGPRs and VGPRs around every 4-MFMA group).
+// A fragments: all KGW of this wave's k-groups loaded in one pass.
+template <int RT, int CT, int KGW>
+__device__ __forceinline__ void fwd_mfma(floatx4 (&acc)[RT][kMaxCT], const u32x4 (&af)[RT][32 / RT],
+                                         const float *Rs, int LDR, int w, int fr, int fq) {
+#pragma unroll
+  for (int i = 0; i < KGW; i++) {
+    const int kg = w + 4 * i;
+    floatx4 b[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ct++) b[ct] = ld4(Rs + (ct * 16 + fr) * LDR + kg * 16 + fq * 4);
+#pragma unroll
+    for (int s = 0; s < 4; s++)
+#pragma unroll
+      for (int ct = 0; ct < CT; ct++)
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++)
+          acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[rt][i][s]), b[ct][s], acc[rt][ct],
+                                                             0, 0, 0);
+  }
+}
+
+// backward: one 16-column tile; NA accumulator sets (by k-group parity) break
+// the dependent MFMA chain, summed in a fixed order at the end.
+template <int RT, int KGW>
+__device__ __forceinline__ void bwd_mfma(floatx4 (&acc)[RT], const u32x4 (&af)[RT][32 / RT], const float *RT_s,
+                                         int LDK, int U, int w, int fr, int fq) {
+  constexpr int NA = (KGW % 4 == 0) ? 4 : (KGW % 2 == 0 ? 2 : 1);
+  floatx4 part[NA][RT];
+#pragma unroll
+  for (int a = 0; a < NA; a++)
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++) part[a][rt] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const float *brow = RT_s + (fr < U ? fr : 0) * LDK + fq * 4;
+  const float bmask = fr < U ? 1.f : 0.f;
+#pragma unroll
+  for (int i = 0; i < KGW; i++) {
+    const int kg = w + 4 * i;
+    const floatx4 b = ld4(brow + kg * 16) * bmask;
+#pragma unroll
+    for (int s = 0; s < 4; s++)
+#pragma unroll
+      for (int rt = 0; rt < RT; rt++)
+        part[i % NA][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[rt][i][s]), b[s], part[i % NA][rt],
+                                                                0, 0, 0);
+  }
+#pragma unroll
+  for (int rt = 0; rt < RT; rt++) {
+    floatx4 t = part[0][rt];
+#pragma unroll
+    for (int a = 1; a < NA; a++) t += part[a][rt];
+    acc[rt] = t;
+  }
+}
+
 // Operand hand-off loads are the critical path of a step, and a wave's vector
 // memory operations complete in issue order (s_waitcnt vmcnt), so everything
 // else a step reads from or writes to HBM -- next step's input projection /
@@ -802,6 +859,8 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
   const int KG = H / 16;
   const int KGW = (KG + 3) / 4;
   const unsigned step_bytes = (unsigned)((long)N * ldy * sizeof(float));
+  // compile-time MFMA body: CT column tiles x KGW k-groups per wave (KG % 4 == 0)
+  const int fast = (KG % 4 == 0 && KGW <= CH && (KGW == 8 || KGW == 4)) ? CT * 100 + KGW / 2 : 0;
   int t_prev = -1;
   for (int k = 0; k < T && !bad; k++) {
     const int t = d == 0 ? k : T - 1 - k, tp = d == 0 ? t - 1 : t + 1;
@@ -815,6 +874,26 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
       wait_flags(p.flags + d * p.nwg, p.nwg, (unsigned)(k + 1), p.err, bad, &bad_lds);
       REC_TRACE(k, 1);
       const auto rs = rsrc(p.y + (long)tp * N * ldy, step_bytes);
+      if (fast) {
+        u32x4 af[RT][CH];
+        load_frags<RT, CH>(af, rs, ldy, (long)d * H, 0, KG, N, kSyncFlag, p.err, bad);
+        if (p.trace) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          REC_TRACE(k, 2);
+          REC_TRACE_W(k, 6);
+        }
+        switch (fast) {
+          case 104: fwd_mfma<RT, 1, 8>(acc, af, Rs, LDR, w, fr, fq); break;
+          case 204: fwd_mfma<RT, 2, 8>(acc, af, Rs, LDR, w, fr, fq); break;
+          case 304: fwd_mfma<RT, 3, 8>(acc, af, Rs, LDR, w, fr, fq); break;
+          case 404: fwd_mfma<RT, 4, 8>(acc, af, Rs, LDR, w, fr, fq); break;
+          case 102: fwd_mfma<RT, 1, 4>(acc, af, Rs, LDR, w, fr, fq); break;
+          case 202: fwd_mfma<RT, 2, 4>(acc, af, Rs, LDR, w, fr, fq); break;
+          case 302: fwd_mfma<RT, 3, 4>(acc, af, Rs, LDR, w, fr, fq); break;
+          case 402: fwd_mfma<RT, 4, 4>(acc, af, Rs, LDR, w, fr, fq); break;
+          default: break;
+        }
+      } else
       for (int c0 = 0; c0 < KGW; c0 += CH) {
         u32x4 af[RT][CH];
         load_frags<RT, CH>(af, rs, ldy, (long)d * H, c0, KG, N, kSyncFlag, p.err, bad);
@@ -991,6 +1070,8 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
   const int KG = K / 16;
   const int KGW = (KG + 3) / 4;
   const unsigned step_bytes = (unsigned)((long)N * ldg * sizeof(float));
+  const int fast = (KG % 4 == 0 && KGW <= CH &&
+                    (KGW == 32 || KGW == 24 || KGW == 16 || KGW == 12 || KGW == 8 || KGW == 4)) ? KGW : 0;
   int t_prev = -1;
   for (int k = T - 1; k >= 0 && !bad; k--) {
     const int t = d == 0 ? k : T - 1 - k;
@@ -1004,6 +1085,24 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
       wait_flags(p.flags + d * p.nwg, p.nwg, (unsigned)(ks + 1), p.err, bad, &bad_lds);
       REC_TRACE(ks, 1);
       const auto rs = rsrc(p.E + (long)tn * N * ldg, step_bytes);
+      if (fast) {
+        u32x4 af[RT][CH];
+        load_frags<RT, CH>(af, rs, ldg, (long)d * K, 0, KG, N, kSyncFlag, p.err, bad);
+        if (p.trace) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          REC_TRACE(ks, 2);
+          REC_TRACE_W(ks, 6);
+        }
+        switch (fast) {
+          case 32: bwd_mfma<RT, 32>(acc, af, RT_s, LDK, U, w, fr, fq); break;
+          case 24: bwd_mfma<RT, 24>(acc, af, RT_s, LDK, U, w, fr, fq); break;
+          case 16: bwd_mfma<RT, 16>(acc, af, RT_s, LDK, U, w, fr, fq); break;
+          case 12: bwd_mfma<RT, 12>(acc, af, RT_s, LDK, U, w, fr, fq); break;
+          case 8: bwd_mfma<RT, 8>(acc, af, RT_s, LDK, U, w, fr, fq); break;
+          case 4: bwd_mfma<RT, 4>(acc, af, RT_s, LDK, U, w, fr, fq); break;
+          default: break;
+        }
+      } else
       for (int c0 = 0; c0 < KGW; c0 += CH) {
         u32x4 af[RT][CH];
         load_frags<RT, CH>(af, rs, ldg, (long)d * K, c0, KG, N, kSyncFlag, p.err, bad);
