@@ -166,6 +166,7 @@ struct RecParams {
   int sync;         // kSyncData / kSyncFlag
   unsigned long long *trace;  // optional: [kTraceSteps][grid][8] s_memrealtime stamps
   int allow_local;  // v4: hand off through the shared L2 when placement allows it
+  int xpd;          // v4: XCD slots per direction (nwg = 32 * xpd workgroups)
 };
 
 // Phase stamps of the first kTraceSteps steps ([steps][grid][16]; thread 0 of every workgroup;
@@ -175,10 +176,14 @@ struct RecParams {
 constexpr int kTraceSteps = 256;
 #define REC_TRACE(kk, ph)                                                                 \
   do {                                                                                    \
-    if (p.trace && threadIdx.x == 0 && (kk) < kTraceSteps)                                \
-      p.trace[((long)(kk) * gridDim.x + blockIdx.x) * 16 + (ph)] = __builtin_amdgcn_s_memrealtime(); \
+    if (p.trace && threadIdx.x == 0 && (kk) < kTraceSteps) {                              \
+      unsigned long long *tr_ = p.trace + ((long)(kk) * gridDim.x + blockIdx.x) * 16;     \
+      tr_[(ph)] = __builtin_amdgcn_s_memrealtime();                                       \
+      if ((ph) == 2 || (ph) == 3) tr_[12 + (ph)] = __builtin_amdgcn_s_memtime();          \
+    }                                                                                     \
   } while (0)
-// per-wave stamps (lane 0 of every wave): slot 6 + w loads landed, 10 + w MFMA done
+// per-wave stamps (lane 0 of every wave): slot 6 + w loads landed, 10 + w MFMA done;
+// slots 14/15: shader-clock counter (s_memtime) at phases 2/3 (clock estimate)
 #define REC_TRACE_W(kk, ph)                                                               \
   do {                                                                                    \
     if (p.trace && (threadIdx.x & 63) == 0 && (kk) < kTraceSteps)                         \
@@ -792,7 +797,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
   constexpr int CH = 32 / RT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int bad_lds, loc_lds;
-  const int d = blockIdx.x & 7, g = blockIdx.x >> 3;
+  const int slot = blockIdx.x & 7, d = slot / p.xpd, g = (blockIdx.x >> 3) * p.xpd + slot % p.xpd;
   if (d >= p.dirs || g >= p.nwg) return;
   const int H = p.H, U = p.U, N = p.N, T = p.T, ncol = p.ncol;
   const int LDR = H + 4;
@@ -995,7 +1000,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
   constexpr int CH = 32 / RT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int bad_lds, loc_lds;
-  const int d = blockIdx.x & 7, g = blockIdx.x >> 3;
+  const int slot = blockIdx.x & 7, d = slot / p.xpd, g = (blockIdx.x >> 3) * p.xpd + slot % p.xpd;
   if (d >= p.dirs || g >= p.nwg) return;
   const int H = p.H, U = p.U, N = p.N, T = p.T;
   const int K = NW * H, LDK = K + 4;
@@ -1267,7 +1272,7 @@ static void launch_rec(bool fwd, int mode, const RecParams &p, dim3 grid, size_t
 
 // KCTC_REC_TRACE=<dir>: trace the first forward and the first backward
 // recurrence launch of the process into <dir>/rec_{fwd,bwd}.bin
-// (int32 header {grid, steps, nwg, T, dirs, version} then [steps][grid][8] uint64 stamps).
+// (int32 header {grid, steps, nwg, T, dirs, version, xpd, 0} then [steps][grid][16] uint64 stamps).
 struct RecTrace {
   unsigned long long *dev = nullptr;
   size_t n = 0;
@@ -1283,7 +1288,7 @@ struct RecTrace {
     KCTC_HIP_CHECK(hipMemset(dev, 0, n * sizeof(unsigned long long)));
     return true;
   }
-  void dump(const char *tag, hipStream_t s, int grid, int nwg, int T, int dirs, int ver) {
+  void dump(const char *tag, hipStream_t s, int grid, int nwg, int T, int dirs, int ver, int xpd = 1) {
     if (!dev) return;
     KCTC_HIP_CHECK(hipStreamSynchronize(s));
     std::vector<unsigned long long> h(n);
@@ -1293,8 +1298,8 @@ struct RecTrace {
     std::string path = std::string(getenv("KCTC_REC_TRACE")) + "/rec_" + tag + ".bin";
     FILE *f = fopen(path.c_str(), "wb");
     if (!f) return;
-    int hdr[6] = {grid, kTraceSteps, nwg, T, dirs, ver};
-    fwrite(hdr, sizeof(int), 6, f);
+    int hdr[8] = {grid, kTraceSteps, nwg, T, dirs, ver, xpd, 0};
+    fwrite(hdr, sizeof(int), 8, f);
     fwrite(h.data(), sizeof(unsigned long long), n, f);
     fclose(f);
   }
@@ -1336,22 +1341,36 @@ static size_t bwd_lds_bytes(const RnnDesc &d, int N, int U) {
                           std::max(4 * (size_t)Npad * 16, (size_t)2 * N * U * d.nw()));
 }
 static int rec_version() { return env_int("KCTC_REC", 4); }
+// XCD slots one direction spans for U units per workgroup (0: not a v4 shape)
+static int v4_xpd(const RnnDesc &d, int U) {
+  if (U <= 0 || d.H % U) return 0;
+  const int nwg = d.H / U;
+  if (nwg % kCusPerXcd) return nwg < kCusPerXcd && d.dirs <= 8 ? 1 : 0;
+  const int x = nwg / kCusPerXcd;
+  return (x == 1 || x == 2 || x == 4 || x == 8) && x * d.dirs <= 8 ? x : 0;
+}
 static int pick_fwd_u4(const RnnDesc &d, int N) {
   if (rec_version() != 4 || d.dirs > 8) return 0;
-  for (int U = 1; U <= d.H; U++) {
-    if (d.H % U || d.H / U > kCusPerXcd) continue;
-    if (d.nw() * U > 16 * kMaxCT || N * U > kMaxEPT * NT) return 0;
-    return fwd_lds_bytes(d, N, U) <= 160 * 1024 ? U : 0;
-  }
+  auto ok = [&](int U) {
+    return U >= 4 && U % 4 == 0 && v4_xpd(d, U) && d.nw() * U <= 16 * kMaxCT && N * U <= kMaxEPT * NT &&
+           fwd_lds_bytes(d, N, U) <= 160 * 1024;
+  };
+  const int want = env_int("KCTC_FWD_U", 0);
+  if (want) return ok(want) ? want : 0;
+  for (int U : {16, 8, 4, 32})
+    if (ok(U)) return U;
   return 0;
 }
 static int pick_bwd_u4(const RnnDesc &d, int N) {
   if (rec_version() != 4 || d.dirs > 8) return 0;
-  for (int U = 1; U <= 16; U++) {
-    if (d.H % U || d.H / U > kCusPerXcd) continue;
-    if (N * U > kMaxEPT * NT) return 0;
-    return bwd_lds_bytes(d, N, U) <= 160 * 1024 ? U : 0;
-  }
+  auto ok = [&](int U) {
+    return U >= 4 && U <= 16 && U % 4 == 0 && v4_xpd(d, U) && N * U <= kMaxEPT * NT &&
+           bwd_lds_bytes(d, N, U) <= 160 * 1024;
+  };
+  const int want = env_int("KCTC_BWD_U", 0);
+  if (want) return ok(want) ? want : 0;
+  for (int U : {16, 8, 4})
+    if (ok(U)) return U;
   return 0;
 }
 
@@ -1426,7 +1445,8 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, 4096, s));
     const size_t lds = fwd_lds_bytes(d, N, U);
-    const dim3 grid(ver == 4 ? 8 * p.nwg : dirs * p.nwg);
+    p.xpd = ver == 4 ? v4_xpd(d, U) : 1;
+    const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : dirs * p.nwg);
     RecTrace tr;
     if (tr.arm("fwd", grid.x)) p.trace = tr.dev;
     {
@@ -1434,7 +1454,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       launch_rec(true, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
-    tr.dump("fwd", s, grid.x, p.nwg, T, dirs, ver);
+    tr.dump("fwd", s, grid.x, p.nwg, T, dirs, ver, p.xpd);
     in = out;
   }
   return KRNN_OK;
@@ -1480,7 +1500,8 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, 4096, s));
     const size_t lds = bwd_lds_bytes(d, N, U);
-    const dim3 grid(ver == 4 ? 8 * p.nwg : dirs * p.nwg);
+    p.xpd = ver == 4 ? v4_xpd(d, U) : 1;
+    const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : dirs * p.nwg);
     RecTrace tr;
     if (tr.arm("bwd", grid.x)) p.trace = tr.dev;
     {
@@ -1488,7 +1509,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
       launch_rec(false, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
-    tr.dump("bwd", s, grid.x, p.nwg, T, dirs, ver);
+    tr.dump("bwd", s, grid.x, p.nwg, T, dirs, ver, p.xpd);
     // dx_l = sum_dir DX_dir W_dir   (lower layer's dy, or the caller's dx)
     float *dxl = (l == 0) ? dx : res + lay.per_layer * (l - 1) + lay.dout;
     if (dxl) {

@@ -10,12 +10,13 @@ import numpy as np
 
 def main(path):
     raw = open(path, "rb").read()
-    grid, steps, nwg, T, dirs, ver = np.frombuffer(raw[:24], dtype=np.int32)
-    tr = np.frombuffer(raw[24:], dtype=np.uint64).reshape(steps, grid, 16).astype(np.int64)
+    grid, steps, nwg, T, dirs, ver, xpd, _ = np.frombuffer(raw[:32], dtype=np.int32)
+    tr = np.frombuffer(raw[32:], dtype=np.uint64).reshape(steps, grid, 16).astype(np.int64)
     steps = min(steps, T)
     tr = tr[:steps]
     if ver == 4:
-        members = [[b for b in range(grid) if b % 8 == d] for d in range(dirs)]
+        members = [[b for b in range(grid) if (b % 8) // xpd == d and (b // 8) * xpd + (b % 8) % xpd < nwg]
+                   for d in range(dirs)]
     else:
         members = [list(range(d * nwg, (d + 1) * nwg)) for d in range(dirs)]
     active = sorted(b for m in members for b in m)
@@ -24,7 +25,12 @@ def main(path):
     us = 1e-2  # 100 MHz
     names = ["start->flags", "flags->loads", "loads->reduced", "reduced->published", "published->end"]
     sl = slice(8, steps)
-    print(f"{path}: v{ver} grid={grid} nwg={nwg} dirs={dirs} T={T} steps traced={steps}")
+    print(f"{path}: v{ver} grid={grid} nwg={nwg} xpd={xpd} dirs={dirs} T={T} steps traced={steps}")
+    m = (tr[sl, :, 15] - tr[sl, :, 14]).astype(np.float64)
+    r = (tr[sl, :, 3] - tr[sl, :, 2]).astype(np.float64) * 1e-8
+    ok = (r > 0) & (m > 0)
+    if ok.any():
+        print(f"  shader clock (s_memtime / s_memrealtime) ~{np.median(m[ok] / r[ok]) / 1e9:.2f} GHz")
     for i, nm in enumerate(names):
         d = (tr[sl, :, i + 1] - tr[sl, :, i]) * us
         print(f"  {nm:22s} median {np.median(d):7.3f}  p90 {np.percentile(d, 90):7.3f}")
