@@ -98,7 +98,14 @@ static long drec_split_floats(const RnnDesc &d, int T, int N) {
 static size_t flags_offset(const RnnDesc &d, int T, int N) {
   return sizeof(float) * (size_t)al64(drec_split_floats(d, T, N));
 }
-size_t rnn_workspace_bytes(const RnnDesc &d, int T, int N) { return flags_offset(d, T, N) + 4096; }
+// then the v4 exchange images (one layer at a time; forward and backward of a
+// layer never overlap): T * dirs * max(H, nW*H) * Npad floats
+static size_t xch_offset(const RnnDesc &d, int T, int N) { return flags_offset(d, T, N) + 4096; }
+static size_t xch_bytes(const RnnDesc &d, int T, int N) {
+  const long Npad = (N + 15) / 16 * 16;
+  return sizeof(float) * (size_t)T * d.dirs * d.nw() * d.H * Npad;
+}
+size_t rnn_workspace_bytes(const RnnDesc &d, int T, int N) { return xch_offset(d, T, N) + xch_bytes(d, T, N); }
 
 namespace {
 
@@ -167,6 +174,7 @@ struct RecParams {
   unsigned long long *trace;  // optional: [kTraceSteps][grid][8] s_memrealtime stamps
   int allow_local;  // v4: hand off through the shared L2 when placement allows it
   int xpd;          // v4: XCD slots per direction (nwg = 32 * xpd workgroups)
+  float *xch;       // v4: per-step exchange images [T][dirs][KG][Npad][16] (workspace)
 };
 
 // Phase stamps of the first kTraceSteps steps ([steps][grid][16]; thread 0 of every workgroup;
@@ -728,13 +736,30 @@ __device__ int probe_local(const RecParams &p, int d, int g, unsigned *myflag, i
 
 constexpr int kMaxEPT = 4;  // (n, unit) elements per thread: N * U <= 1024
 
-// Branch-free MFMA bodies with compile-time trip counts (the generic loops'
-// per-iteration guards made the compiler drain vmcnt/lgkmcnt and shuttle the
-// accumulators between AGPRs and VGPRs around every 4-MFMA group).
-// A fragments: all KGW of this wave's k-groups loaded in one pass.
+// Exchange image of one step, fragment-major: [dirs][KG][Npad][16] floats
+// (KG = 16-wide k-groups).  One MFMA A fragment (16 rows x 16 k) is 1 KB of
+// contiguous memory, so every hand-off load instruction moves whole 128-B
+// lines; producers write 16 consecutive units of a row as 64 contiguous bytes.
+// The row-major copies the rest of the layer needs (y, E) are written with
+// plain stores off the critical path.
+__device__ __forceinline__ long xoff(int d, int kg, int n, int j, int KG, int Npad) {
+  return (((long)d * KG + kg) * Npad + n) * 16 + j;
+}
+
+// Hand-off loads + MFMA body of one step with compile-time trip counts: all
+// loads first, then the MFMAs consume them in issue order, so the in-order
+// vmcnt lets the first k-groups compute while the rest are in flight.
+// Forward: acc[RT][CT] += h_{t-1}[rows][k] * R_slice^T[k][cols], K split over
+// the 4 waves (wave w: k-groups w, w+4, ...).
 template <int RT, int CT, int KGW>
-__device__ __forceinline__ void fwd_mfma(floatx4 (&acc)[RT][kMaxCT], const u32x4 (&af)[RT][32 / RT],
-                                         const float *Rs, int LDR, int w, int fr, int fq) {
+__device__ __forceinline__ void fwd_step_mfma(floatx4 (&acc)[RT][kMaxCT], __amdgpu_buffer_rsrc_t rs, long dbase,
+                                              int Npad, const float *Rs, int LDR, int w, int fr, int fq) {
+  u32x4 af[KGW][RT];
+#pragma unroll
+  for (int i = 0; i < KGW; i++)
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++)
+      af[i][rt] = ld_sc1(rs, (unsigned)((dbase + ((long)(w + 4 * i) * Npad + rt * 16 + fr) * 16 + fq * 4) * 4));
 #pragma unroll
   for (int i = 0; i < KGW; i++) {
     const int kg = w + 4 * i;
@@ -747,34 +772,43 @@ __device__ __forceinline__ void fwd_mfma(floatx4 (&acc)[RT][kMaxCT], const u32x4
       for (int ct = 0; ct < CT; ct++)
 #pragma unroll
         for (int rt = 0; rt < RT; rt++)
-          acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[rt][i][s]), b[ct][s], acc[rt][ct],
+          acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[i][rt][s]), b[ct][s], acc[rt][ct],
                                                              0, 0, 0);
   }
 }
 
-// backward: one 16-column tile; NA accumulator sets (by k-group parity) break
-// the dependent MFMA chain, summed in a fixed order at the end.
+// Backward: acc[RT] = dG_{t+1}[rows][kk] * R^T_slice[kk][units] over all nW*H
+// kk (wave w: k-groups w, w+4, ...); NA accumulator sets interleaved so no
+// MFMA waits on its predecessor, summed in a fixed order.
 template <int RT, int KGW>
-__device__ __forceinline__ void bwd_mfma(floatx4 (&acc)[RT], const u32x4 (&af)[RT][32 / RT], const float *RT_s,
-                                         int LDK, int U, int w, int fr, int fq) {
+__device__ __forceinline__ void bwd_step_mfma(floatx4 (&acc)[RT], __amdgpu_buffer_rsrc_t rs, long dbase, int Npad,
+                                              const float *RT_s, int LDK, int w, int fr, int fq) {
   constexpr int NA = (KGW % 4 == 0) ? 4 : (KGW % 2 == 0 ? 2 : 1);
+  u32x4 af[KGW][RT];
+#pragma unroll
+  for (int i = 0; i < KGW; i++)
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++)
+      af[i][rt] = ld_sc1(rs, (unsigned)((dbase + ((long)(w + 4 * i) * Npad + rt * 16 + fr) * 16 + fq * 4) * 4));
   floatx4 part[NA][RT];
 #pragma unroll
   for (int a = 0; a < NA; a++)
 #pragma unroll
     for (int rt = 0; rt < RT; rt++) part[a][rt] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const float *brow = RT_s + (fr < U ? fr : 0) * LDK + fq * 4;
-  const float bmask = fr < U ? 1.f : 0.f;
+  const float *brow = RT_s + fr * LDK + fq * 4;
 #pragma unroll
-  for (int i = 0; i < KGW; i++) {
-    const int kg = w + 4 * i;
-    const floatx4 b = ld4(brow + kg * 16) * bmask;
+  for (int i0 = 0; i0 < KGW; i0 += NA) {
+    floatx4 b[NA];
+#pragma unroll
+    for (int a = 0; a < NA; a++) b[a] = ld4(brow + (w + 4 * (i0 + a)) * 16);
 #pragma unroll
     for (int s = 0; s < 4; s++)
 #pragma unroll
-      for (int rt = 0; rt < RT; rt++)
-        part[i % NA][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[rt][i][s]), b[s], part[i % NA][rt],
-                                                                0, 0, 0);
+      for (int a = 0; a < NA; a++)
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++)
+          part[a][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[i0 + a][rt][s]), b[a][s],
+                                                             part[a][rt], 0, 0, 0);
   }
 #pragma unroll
   for (int rt = 0; rt < RT; rt++) {
@@ -785,26 +819,65 @@ __device__ __forceinline__ void bwd_mfma(floatx4 (&acc)[RT], const u32x4 (&af)[R
   }
 }
 
-// Operand hand-off loads are the critical path of a step, and a wave's vector
-// memory operations complete in issue order (s_waitcnt vmcnt), so everything
-// else a step reads from or writes to HBM -- next step's input projection /
-// dy / saved activations, this step's G / aux stores -- is issued right AFTER
-// the step's hand-off loads have landed (behind the MFMA loop), never in
-// front of the next step's hand-off loads.
+// generic (runtime trip count) versions of the same bodies
+template <int RT>
+__device__ __forceinline__ void fwd_step_generic(floatx4 (&acc)[RT][kMaxCT], __amdgpu_buffer_rsrc_t rs, long dbase,
+                                                 int Npad, int KG, int CT, const float *Rs, int LDR, int w, int fr,
+                                                 int fq) {
+  for (int kg = w; kg < KG; kg += 4) {
+    u32x4 af[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++)
+      af[rt] = ld_sc1(rs, (unsigned)((dbase + ((long)kg * Npad + rt * 16 + fr) * 16 + fq * 4) * 4));
+#pragma unroll
+    for (int ct = 0; ct < kMaxCT; ct++) {
+      if (ct < CT) {
+        const floatx4 b = ld4(Rs + (ct * 16 + fr) * LDR + kg * 16 + fq * 4);
+#pragma unroll
+        for (int s = 0; s < 4; s++)
+#pragma unroll
+          for (int rt = 0; rt < RT; rt++)
+            acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[rt][s]), b[s], acc[rt][ct], 0, 0, 0);
+      }
+    }
+  }
+}
+template <int RT>
+__device__ __forceinline__ void bwd_step_generic(floatx4 (&acc)[RT], __amdgpu_buffer_rsrc_t rs, long dbase, int Npad,
+                                                 int KG, const float *RT_s, int LDK, int w, int fr, int fq) {
+  for (int kg = w; kg < KG; kg += 4) {
+    u32x4 af[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++)
+      af[rt] = ld_sc1(rs, (unsigned)((dbase + ((long)kg * Npad + rt * 16 + fr) * 16 + fq * 4) * 4));
+    const floatx4 b = ld4(RT_s + fr * LDK + kg * 16 + fq * 4);
+#pragma unroll
+    for (int s = 0; s < 4; s++)
+#pragma unroll
+      for (int rt = 0; rt < RT; rt++)
+        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[rt][s]), b[s], acc[rt], 0, 0, 0);
+  }
+}
+
+// Everything else a step reads from or writes to HBM (next step's input
+// projection / dy / saved activations, the row-major y / E copies) is issued
+// right AFTER the step's hand-off loads have been consumed, never in front of
+// them: a wave's vector memory operations complete in issue order.
 template <int MODE, int RT>
 __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
   constexpr int NW = MODE == kLstm ? 4 : MODE == kGru ? 3 : 1;
-  constexpr int CH = 32 / RT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int bad_lds, loc_lds;
   const int slot = blockIdx.x & 7, d = slot / p.xpd, g = (blockIdx.x >> 3) * p.xpd + slot % p.xpd;
   if (d >= p.dirs || g >= p.nwg) return;
-  const int H = p.H, U = p.U, N = p.N, T = p.T, ncol = p.ncol;
+  const int H = p.H, U = p.U, N = p.N, T = p.T, ncol = p.ncol, Npad = p.Npad;
   const int LDR = H + 4;
   const int u0 = g * U;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
   const int CT = ncol / 16;
   const long ldy = (long)p.dirs * H, ldg = (long)p.dirs * NW * H;
+  const int KG = H / 16;
+  const long xstep = (long)p.dirs * KG * Npad * 16;  // floats of one step's exchange image
   float *Rs = smem;                      // [ncol][LDR]
   float *red = Rs + (long)ncol * LDR;    // [4][Npad][ncol]
   const float *Wd = p.w + d * p.pl_stride;
@@ -821,7 +894,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
   }
   const int items = N * U;
   float cst[kMaxEPT], hpv[kMaxEPT], gin[kMaxEPT][NW], gnx[kMaxEPT][NW], bR[kMaxEPT][NW];
-  float act[kMaxEPT][NW], cnew[kMaxEPT];
+  float act[kMaxEPT][NW], cnew[kMaxEPT], hval[kMaxEPT];
   auto gin_load = [&](int t, float (&dst)[kMaxEPT][NW]) {
 #pragma unroll
     for (int j = 0; j < kMaxEPT; j++) {
@@ -832,40 +905,40 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
       }
     }
   };
-  // saved activations for the backward pass (G rows overwritten in place, aux)
-  auto act_store = [&](int t) {
-    if (MODE != kLstm && MODE != kGru) return;
+  // row-major outputs of step t: y, and for the backward pass G (activations,
+  // overwritten in place) and aux
+  auto out_store = [&](int t) {
 #pragma unroll
     for (int j = 0; j < kMaxEPT; j++) {
       const int e = tid + j * NT, n = e / U, u = e - n * U;
       if (e < items) {
-        const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
+        p.y[((long)t * N + n) * ldy + (long)d * H + u0 + u] = hval[j];
+        if (MODE == kLstm || MODE == kGru) {
+          const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
 #pragma unroll
-        for (int q = 0; q < NW; q++) p.G[grow + q * H] = act[j][q];
-        p.aux[((long)t * N + n) * ldy + (long)d * H + u0 + u] = cnew[j];
+          for (int q = 0; q < NW; q++) p.G[grow + q * H] = act[j][q];
+          p.aux[((long)t * N + n) * ldy + (long)d * H + u0 + u] = cnew[j];
+        }
       }
     }
   };
 #pragma unroll
   for (int j = 0; j < kMaxEPT; j++) {
-    cst[j] = hpv[j] = cnew[j] = 0.f;
-    const int e = tid + j * NT, n = e / U, u = e - n * U;
+    cst[j] = hpv[j] = cnew[j] = hval[j] = 0.f;
+    const int e = tid + j * NT, u = e % U;
 #pragma unroll
     for (int q = 0; q < NW; q++) {
       bR[j][q] = (MODE == kGru && e < items) ? Wd[p.bR_off + q * H + u0 + u] : 0.f;
       gin[j][q] = gnx[j][q] = act[j][q] = 0.f;
     }
-    (void)n;
   }
   gin_load(d == 0 ? 0 : T - 1, gin);
   int bad = 0;
   unsigned *myflag = p.flags + d * p.nwg + g;
   const int local = probe_local(p, d, g, myflag, bad, &bad_lds, &loc_lds);
-  const int KG = H / 16;
-  const int KGW = (KG + 3) / 4;
-  const unsigned step_bytes = (unsigned)((long)N * ldy * sizeof(float));
-  // compile-time MFMA body: CT column tiles x KGW k-groups per wave (KG % 4 == 0)
-  const int fast = (KG % 4 == 0 && KGW <= CH && (KGW == 8 || KGW == 4)) ? CT * 100 + KGW / 2 : 0;
+  const int KGW = KG / 4;
+  const int fast = (KG % 4 == 0 && KGW * RT <= 32 && (KGW == 8 || KGW == 4)) ? CT * 100 + KGW / 2 : 0;
+  const long dbase = (long)d * KG * Npad * 16;
   int t_prev = -1;
   for (int k = 0; k < T && !bad; k++) {
     const int t = d == 0 ? k : T - 1 - k, tp = d == 0 ? t - 1 : t + 1;
@@ -878,59 +951,23 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
     if (k > 0) {
       wait_flags(p.flags + d * p.nwg, p.nwg, (unsigned)(k + 1), p.err, bad, &bad_lds);
       REC_TRACE(k, 1);
-      const auto rs = rsrc(p.y + (long)tp * N * ldy, step_bytes);
-      if (fast) {
-        u32x4 af[RT][CH];
-        load_frags<RT, CH>(af, rs, ldy, (long)d * H, 0, KG, N, kSyncFlag, p.err, bad);
-        if (p.trace) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          REC_TRACE(k, 2);
-          REC_TRACE_W(k, 6);
-        }
-        switch (fast) {
-          case 104: fwd_mfma<RT, 1, 8>(acc, af, Rs, LDR, w, fr, fq); break;
-          case 204: fwd_mfma<RT, 2, 8>(acc, af, Rs, LDR, w, fr, fq); break;
-          case 304: fwd_mfma<RT, 3, 8>(acc, af, Rs, LDR, w, fr, fq); break;
-          case 404: fwd_mfma<RT, 4, 8>(acc, af, Rs, LDR, w, fr, fq); break;
-          case 102: fwd_mfma<RT, 1, 4>(acc, af, Rs, LDR, w, fr, fq); break;
-          case 202: fwd_mfma<RT, 2, 4>(acc, af, Rs, LDR, w, fr, fq); break;
-          case 302: fwd_mfma<RT, 3, 4>(acc, af, Rs, LDR, w, fr, fq); break;
-          case 402: fwd_mfma<RT, 4, 4>(acc, af, Rs, LDR, w, fr, fq); break;
-          default: break;
-        }
-      } else
-      for (int c0 = 0; c0 < KGW; c0 += CH) {
-        u32x4 af[RT][CH];
-        load_frags<RT, CH>(af, rs, ldy, (long)d * H, c0, KG, N, kSyncFlag, p.err, bad);
-        if (p.trace) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          REC_TRACE(k, 2);
-          REC_TRACE_W(k, 6);
-        }
-#pragma unroll
-        for (int i = 0; i < CH; i++) {
-          const int kg = w + 4 * (c0 + i);
-          if (kg < KG) {
-#pragma unroll
-            for (int ct = 0; ct < kMaxCT; ct++) {
-              if (ct < CT) {
-                const floatx4 b = ld4(Rs + (ct * 16 + fr) * LDR + kg * 16 + fq * 4);
-#pragma unroll
-                for (int s = 0; s < 4; s++)
-#pragma unroll
-                  for (int rt = 0; rt < RT; rt++)
-                    acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[rt][i][s]), b[s],
-                                                                       acc[rt][ct], 0, 0, 0);
-              }
-            }
-          }
-        }
+      const auto rs = rsrc(p.xch + (long)tp * xstep, (unsigned)(xstep * 4));
+      switch (fast) {
+        case 104: fwd_step_mfma<RT, 1, 8>(acc, rs, dbase, Npad, Rs, LDR, w, fr, fq); break;
+        case 204: fwd_step_mfma<RT, 2, 8>(acc, rs, dbase, Npad, Rs, LDR, w, fr, fq); break;
+        case 304: fwd_step_mfma<RT, 3, 8>(acc, rs, dbase, Npad, Rs, LDR, w, fr, fq); break;
+        case 404: fwd_step_mfma<RT, 4, 8>(acc, rs, dbase, Npad, Rs, LDR, w, fr, fq); break;
+        case 102: fwd_step_mfma<RT, 1, 4>(acc, rs, dbase, Npad, Rs, LDR, w, fr, fq); break;
+        case 202: fwd_step_mfma<RT, 2, 4>(acc, rs, dbase, Npad, Rs, LDR, w, fr, fq); break;
+        case 302: fwd_step_mfma<RT, 3, 4>(acc, rs, dbase, Npad, Rs, LDR, w, fr, fq); break;
+        case 402: fwd_step_mfma<RT, 4, 4>(acc, rs, dbase, Npad, Rs, LDR, w, fr, fq); break;
+        default: fwd_step_generic<RT>(acc, rs, dbase, Npad, KG, CT, Rs, LDR, w, fr, fq); break;
       }
     }
     asm volatile("" ::: "memory");
-    // behind the hand-off loads: previous step's saved activations, next
-    // step's input projection
-    if (t_prev >= 0) act_store(t_prev);
+    // behind the hand-off loads: last step's row-major outputs, next step's
+    // input projection
+    if (t_prev >= 0) out_store(t_prev);
     if (k + 1 < T) gin_load(d == 0 ? t + 1 : t - 1, gnx);
 #pragma unroll
     for (int rt = 0; rt < RT; rt++)
@@ -939,13 +976,14 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
         if (ct < CT)
 #pragma unroll
           for (int r = 0; r < 4; r++)
-            red[((long)w * p.Npad + rt * 16 + fq * 4 + r) * ncol + ct * 16 + fr] = acc[rt][ct][r];
+            red[((long)w * Npad + rt * 16 + fq * 4 + r) * ncol + ct * 16 + fr] = acc[rt][ct][r];
     if (p.trace) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       REC_TRACE_W(k, 10);
     }
     __syncthreads();
     REC_TRACE(k, 3);
+    float *xt = p.xch + (long)t * xstep;
 #pragma unroll
     for (int j = 0; j < kMaxEPT; j++) {
       const int e = tid + j * NT;
@@ -955,8 +993,8 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
 #pragma unroll
       for (int q = 0; q < NW; q++) {
         const int c = q * U + u;
-        rh[q] = ((red[((long)0 * p.Npad + n) * ncol + c] + red[((long)1 * p.Npad + n) * ncol + c]) +
-                 red[((long)2 * p.Npad + n) * ncol + c]) + red[((long)3 * p.Npad + n) * ncol + c];
+        rh[q] = ((red[((long)0 * Npad + n) * ncol + c] + red[((long)1 * Npad + n) * ncol + c]) +
+                 red[((long)2 * Npad + n) * ncol + c]) + red[((long)3 * Npad + n) * ncol + c];
       }
       float h;
       if (MODE == kLstm) {
@@ -978,7 +1016,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
         const float pre = gin[j][0] + rh[0];
         h = MODE == kRelu ? fmaxf(pre, 0.f) : ftanh(pre);
       }
-      put(p.y + ((long)t * N + n) * ldy + (long)d * H + u0 + u, h, local);
+      hval[j] = h;
+      const int uu = u0 + u;
+      put(xt + xoff(d, uu >> 4, n, uu & 15, KG, Npad), h, local);
     }
     signal_epoch(myflag, (unsigned)(k + 2), local);
     REC_TRACE(k, 4);
@@ -990,42 +1030,44 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
     __syncthreads();  // red[] is rewritten by the next step
     REC_TRACE(k, 5);
   }
-  if (t_prev >= 0 && !bad) act_store(t_prev);
+  if (t_prev >= 0 && !bad) out_store(t_prev);
   if (bad && tid == 0) atomicOr(p.err, 1u);
 }
 
 template <int MODE, int RT>
 __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
   constexpr int NW = MODE == kLstm ? 4 : MODE == kGru ? 3 : 1;
-  constexpr int CH = 32 / RT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int bad_lds, loc_lds;
   const int slot = blockIdx.x & 7, d = slot / p.xpd, g = (blockIdx.x >> 3) * p.xpd + slot % p.xpd;
   if (d >= p.dirs || g >= p.nwg) return;
-  const int H = p.H, U = p.U, N = p.N, T = p.T;
+  const int H = p.H, U = p.U, N = p.N, T = p.T, Npad = p.Npad;
   const int K = NW * H, LDK = K + 4;
+  const int KG = K / 16;
+  const long xstep = (long)p.dirs * KG * Npad * 16;
   const int u0 = g * U;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
   const long ldy = (long)p.dirs * H, ldg = (long)p.dirs * NW * H;
-  float *RT_s = smem;                       // [U][LDK]: RT_s[u][kk] = R[kk][u0+u]
-  float *red = RT_s + (long)U * LDK;        // [4][Npad][16]
+  float *RT_s = smem;                       // [16][LDK]: RT_s[u][kk] = R[kk][u0+u], rows >= U zero
+  float *red = RT_s + (long)16 * LDK;       // [4][Npad][16]
   const float *Wd = p.w + d * p.pl_stride;
   const float *R = Wd + p.r_off;
   if (tid == 0) bad_lds = 0;
-  for (int idx = tid; idx < U * K; idx += NT) {
-    const int kk = idx / U, u = idx - kk * U;
-    RT_s[u * LDK + kk] = R[(long)kk * H + u0 + u];
+  for (int idx = tid; idx < 16 * K; idx += NT) {
+    const int kk = idx / 16, u = idx - kk * 16;
+    RT_s[u * LDK + kk] = u < U ? R[(long)kk * H + u0 + u] : 0.f;
   }
   const int items = N * U;
-  // per element: current step's operands (c*) and the next step's (n*)
-  float carry[kMaxEPT], bsx[kMaxEPT][NW], bsh[kMaxEPT][NW], dxk[kMaxEPT][NW];
+  // per element: current step's operands (c*), the next step's (n*), and the
+  // row-major dGates of the previous step waiting to be stored (e*, dxk)
+  float carry[kMaxEPT], bsx[kMaxEPT][NW], bsh[kMaxEPT][NW], dxk[kMaxEPT][NW], eg[kMaxEPT][NW];
   float cg[kMaxEPT][NW], cdy[kMaxEPT], ca[kMaxEPT], cap[kMaxEPT];
   float ng[kMaxEPT][NW], ndy[kMaxEPT], na[kMaxEPT], nap[kMaxEPT];
 #pragma unroll
   for (int j = 0; j < kMaxEPT; j++) {
     carry[j] = cdy[j] = ca[j] = cap[j] = ndy[j] = na[j] = nap[j] = 0.f;
 #pragma unroll
-    for (int q = 0; q < NW; q++) bsx[j][q] = bsh[j][q] = cg[j][q] = ng[j][q] = dxk[j][q] = 0.f;
+    for (int q = 0; q < NW; q++) bsx[j][q] = bsh[j][q] = cg[j][q] = ng[j][q] = dxk[j][q] = eg[j][q] = 0.f;
   }
   auto prefetch = [&](int k) {  // operands of forward-order step k into n*
     const int t = d == 0 ? k : T - 1 - k, tp = d == 0 ? t - 1 : t + 1;
@@ -1056,7 +1098,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
       for (int q = 0; q < NW; q++) cg[j][q] = ng[j][q];
     }
   };
-  auto dx_store = [&](int t) {  // GRU: input-side dGates of step t
+  auto e_store = [&](int t) {  // row-major dGates of step t (E; GRU also DX)
 #pragma unroll
     for (int j = 0; j < kMaxEPT; j++) {
       const int e = tid + j * NT;
@@ -1064,7 +1106,11 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
       const int n = e / U, u = e - n * U;
       const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
 #pragma unroll
-      for (int q = 0; q < NW; q++) p.DX[grow + q * H] = dxk[j][q];
+      for (int q = 0; q < NW; q++) p.E[grow + q * H] = eg[j][q];
+      if (MODE == kGru) {
+#pragma unroll
+        for (int q = 0; q < NW; q++) p.DX[grow + q * H] = dxk[j][q];
+      }
     }
   };
   prefetch(T - 1);
@@ -1072,11 +1118,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
   int bad = 0;
   unsigned *myflag = p.flags + d * p.nwg + g;
   const int local = probe_local(p, d, g, myflag, bad, &bad_lds, &loc_lds);
-  const int KG = K / 16;
-  const int KGW = (KG + 3) / 4;
-  const unsigned step_bytes = (unsigned)((long)N * ldg * sizeof(float));
-  const int fast = (KG % 4 == 0 && KGW <= CH &&
+  const int KGW = KG / 4;
+  const int fast = (KG % 4 == 0 && KGW * RT <= 32 &&
                     (KGW == 32 || KGW == 24 || KGW == 16 || KGW == 12 || KGW == 8 || KGW == 4)) ? KGW : 0;
+  const long dbase = (long)d * KG * Npad * 16;
   int t_prev = -1;
   for (int k = T - 1; k >= 0 && !bad; k--) {
     const int t = d == 0 ? k : T - 1 - k;
@@ -1089,86 +1134,51 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
     if (ks > 0) {
       wait_flags(p.flags + d * p.nwg, p.nwg, (unsigned)(ks + 1), p.err, bad, &bad_lds);
       REC_TRACE(ks, 1);
-      const auto rs = rsrc(p.E + (long)tn * N * ldg, step_bytes);
-      if (fast) {
-        u32x4 af[RT][CH];
-        load_frags<RT, CH>(af, rs, ldg, (long)d * K, 0, KG, N, kSyncFlag, p.err, bad);
-        if (p.trace) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          REC_TRACE(ks, 2);
-          REC_TRACE_W(ks, 6);
-        }
-        switch (fast) {
-          case 32: bwd_mfma<RT, 32>(acc, af, RT_s, LDK, U, w, fr, fq); break;
-          case 24: bwd_mfma<RT, 24>(acc, af, RT_s, LDK, U, w, fr, fq); break;
-          case 16: bwd_mfma<RT, 16>(acc, af, RT_s, LDK, U, w, fr, fq); break;
-          case 12: bwd_mfma<RT, 12>(acc, af, RT_s, LDK, U, w, fr, fq); break;
-          case 8: bwd_mfma<RT, 8>(acc, af, RT_s, LDK, U, w, fr, fq); break;
-          case 4: bwd_mfma<RT, 4>(acc, af, RT_s, LDK, U, w, fr, fq); break;
-          default: break;
-        }
-      } else
-      for (int c0 = 0; c0 < KGW; c0 += CH) {
-        u32x4 af[RT][CH];
-        load_frags<RT, CH>(af, rs, ldg, (long)d * K, c0, KG, N, kSyncFlag, p.err, bad);
-        if (p.trace) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          REC_TRACE(ks, 2);
-          REC_TRACE_W(ks, 6);
-        }
-#pragma unroll
-        for (int i = 0; i < CH; i++) {
-          const int kg = w + 4 * (c0 + i);
-          if (kg < KG) {
-            floatx4 b = floatx4{0.f, 0.f, 0.f, 0.f};
-            if (fr < U) b = ld4(RT_s + fr * LDK + kg * 16 + fq * 4);
-#pragma unroll
-            for (int s = 0; s < 4; s++)
-#pragma unroll
-              for (int rt = 0; rt < RT; rt++)
-                acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[rt][i][s]), b[s], acc[rt], 0, 0, 0);
-          }
-        }
+      const auto rs = rsrc(p.xch + (long)tn * xstep, (unsigned)(xstep * 4));
+      switch (fast) {
+        case 32: bwd_step_mfma<RT, 32>(acc, rs, dbase, Npad, RT_s, LDK, w, fr, fq); break;
+        case 24: bwd_step_mfma<RT, 24>(acc, rs, dbase, Npad, RT_s, LDK, w, fr, fq); break;
+        case 16: bwd_step_mfma<RT, 16>(acc, rs, dbase, Npad, RT_s, LDK, w, fr, fq); break;
+        case 12: bwd_step_mfma<RT, 12>(acc, rs, dbase, Npad, RT_s, LDK, w, fr, fq); break;
+        case 8: bwd_step_mfma<RT, 8>(acc, rs, dbase, Npad, RT_s, LDK, w, fr, fq); break;
+        case 4: bwd_step_mfma<RT, 4>(acc, rs, dbase, Npad, RT_s, LDK, w, fr, fq); break;
+        default: bwd_step_generic<RT>(acc, rs, dbase, Npad, KG, RT_s, LDK, w, fr, fq); break;
       }
     }
     asm volatile("" ::: "memory");
-    // behind the hand-off loads: next step's operands, last step's GRU dx
+    // behind the hand-off loads: next step's operands, last step's row-major dGates
     if (k > 0) prefetch(k - 1);
-    if (MODE == kGru && t_prev >= 0) dx_store(t_prev);
+    if (t_prev >= 0) e_store(t_prev);
 #pragma unroll
     for (int rt = 0; rt < RT; rt++)
 #pragma unroll
-      for (int r = 0; r < 4; r++) red[((long)w * p.Npad + rt * 16 + fq * 4 + r) * 16 + fr] = acc[rt][r];
+      for (int r = 0; r < 4; r++) red[((long)w * Npad + rt * 16 + fq * 4 + r) * 16 + fr] = acc[rt][r];
     if (p.trace) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       REC_TRACE_W(ks, 10);
     }
     __syncthreads();
     REC_TRACE(ks, 3);
+    float *xt = p.xch + (long)t * xstep;
 #pragma unroll
     for (int j = 0; j < kMaxEPT; j++) {
       const int e = tid + j * NT;
       if (e >= items) continue;
       const int n = e / U, u = e - n * U;
-      const float dhr = ((red[((long)0 * p.Npad + n) * 16 + u] + red[((long)1 * p.Npad + n) * 16 + u]) +
-                         red[((long)2 * p.Npad + n) * 16 + u]) + red[((long)3 * p.Npad + n) * 16 + u];
+      const float dhr = ((red[((long)0 * Npad + n) * 16 + u] + red[((long)1 * Npad + n) * 16 + u]) +
+                         red[((long)2 * Npad + n) * 16 + u]) + red[((long)3 * Npad + n) * 16 + u];
       float dh = cdy[j] + dhr;
-      float *Erow = p.E + ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
+      const int uu = u0 + u;
       if (MODE == kLstm) {
         const float ig = cg[j][0], fg = cg[j][1], gg = cg[j][2], og = cg[j][3];
         const float tc = ftanh(ca[j]);
         const float dO = dh * tc;
         const float dc = dh * og * (1.f - tc * tc) + carry[j];
-        const float dpi = dc * gg * ig * (1.f - ig);
-        const float dpf = dc * cap[j] * fg * (1.f - fg);
-        const float dpg = dc * ig * (1.f - gg * gg);
-        const float dpo = dO * og * (1.f - og);
+        eg[j][0] = dc * gg * ig * (1.f - ig);
+        eg[j][1] = dc * cap[j] * fg * (1.f - fg);
+        eg[j][2] = dc * ig * (1.f - gg * gg);
+        eg[j][3] = dO * og * (1.f - og);
         carry[j] = dc * fg;
-        put(Erow, dpi, local);
-        put(Erow + H, dpf, local);
-        put(Erow + 2 * H, dpg, local);
-        put(Erow + 3 * H, dpo, local);
-        bsx[j][0] += dpi; bsx[j][1] += dpf; bsx[j][2] += dpg; bsx[j][3] += dpo;
       } else if (MODE == kGru) {
         dh += carry[j];
         const float r = cg[j][0], z = cg[j][1], nn = cg[j][2];
@@ -1178,16 +1188,17 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
         const float dpz = dz * z * (1.f - z);
         carry[j] = dh * z;
         dxk[j][0] = dpr; dxk[j][1] = dpz; dxk[j][2] = dpn;
-        put(Erow, dpr, local);
-        put(Erow + H, dpz, local);
-        put(Erow + 2 * H, dpn * r, local);
-        bsx[j][0] += dpr; bsx[j][1] += dpz; bsx[j][2] += dpn;
+        eg[j][0] = dpr; eg[j][1] = dpz; eg[j][2] = dpn * r;
         bsh[j][0] += dpr; bsh[j][1] += dpz; bsh[j][2] += dpn * r;
       } else {
         const float der = MODE == kRelu ? (cap[j] > 0.f ? 1.f : 0.f) : (1.f - cap[j] * cap[j]);
-        const float dp = dh * der;
-        put(Erow, dp, local);
-        bsx[j][0] += dp;
+        eg[j][0] = dh * der;
+      }
+#pragma unroll
+      for (int q = 0; q < NW; q++) {
+        const int kk = q * H + uu;
+        put(xt + xoff(d, kk >> 4, n, kk & 15, KG, Npad), eg[j][q], local);
+        bsx[j][q] += (MODE == kGru) ? dxk[j][q] : eg[j][q];
       }
     }
     signal_epoch(myflag, (unsigned)(ks + 2), local);
@@ -1197,7 +1208,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
     __syncthreads();
     REC_TRACE(ks, 5);
   }
-  if (MODE == kGru && t_prev >= 0 && !bad) dx_store(t_prev);
+  if (t_prev >= 0 && !bad) e_store(t_prev);
   // bias partial sums: reduce over n in a fixed order through LDS
   float *bs = red;  // reuse: [2][N][U][NW] floats (fits: see lds sizing)
   __syncthreads();
@@ -1335,9 +1346,9 @@ static size_t fwd_lds_bytes(const RnnDesc &d, int N, int U) {
   const int ncol = (d.nw() * U + 15) / 16 * 16, Npad = (N + 15) / 16 * 16;
   return sizeof(float) * ((size_t)ncol * (d.H + 4) + 4 * (size_t)Npad * ncol);
 }
-static size_t bwd_lds_bytes(const RnnDesc &d, int N, int U) {
+static size_t bwd_lds_bytes(const RnnDesc &d, int N, int U, int ver = 3) {
   const int Npad = (N + 15) / 16 * 16;
-  return sizeof(float) * ((size_t)U * (d.nw() * d.H + 4) +
+  return sizeof(float) * ((size_t)(ver == 4 ? 16 : U) * (d.nw() * d.H + 4) +
                           std::max(4 * (size_t)Npad * 16, (size_t)2 * N * U * d.nw()));
 }
 static int rec_version() { return env_int("KCTC_REC", 4); }
@@ -1365,7 +1376,7 @@ static int pick_bwd_u4(const RnnDesc &d, int N) {
   if (rec_version() != 4 || d.dirs > 8) return 0;
   auto ok = [&](int U) {
     return U >= 4 && U <= 16 && U % 4 == 0 && v4_xpd(d, U) && N * U <= kMaxEPT * NT &&
-           bwd_lds_bytes(d, N, U) <= 160 * 1024;
+           bwd_lds_bytes(d, N, U, 4) <= 160 * 1024;
   };
   const int want = env_int("KCTC_BWD_U", 0);
   if (want) return ok(want) ? want : 0;
@@ -1446,6 +1457,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, 4096, s));
     const size_t lds = fwd_lds_bytes(d, N, U);
     p.xpd = ver == 4 ? v4_xpd(d, U) : 1;
+    p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
     const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : dirs * p.nwg);
     RecTrace tr;
     if (tr.arm("fwd", grid.x)) p.trace = tr.dev;
@@ -1499,8 +1511,9 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, 4096, s));
-    const size_t lds = bwd_lds_bytes(d, N, U);
+    const size_t lds = bwd_lds_bytes(d, N, U, ver);
     p.xpd = ver == 4 ? v4_xpd(d, U) : 1;
+    p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
     const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : dirs * p.nwg);
     RecTrace tr;
     if (tr.arm("bwd", grid.x)) p.trace = tr.dev;
