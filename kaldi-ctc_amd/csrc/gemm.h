@@ -26,6 +26,10 @@ struct GemmArgs {
   int split_k = 1;
   float *ws = nullptr;
   int max_blocks = 0;  // > 0: persistent grid of at most this many workgroups
+  // optional: zeroed device int -> dynamic tile scheduling (blocks pull work
+  // items from this counter; blocks that start late, e.g. on CUs a concurrent
+  // persistent kernel holds, find the work done and exit)
+  int *tile_counter = nullptr;
 };
 
 void gemm_f32(hipStream_t stream, const GemmArgs &g);

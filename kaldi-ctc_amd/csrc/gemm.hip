@@ -41,6 +41,7 @@ struct KParams {
   float alpha, beta;
   float *ws;
   int vecA, vecB;
+  int *counter;
 };
 
 // Load one operand tile (rows r0.., k0..) into 4 float4 registers.
@@ -104,11 +105,13 @@ __device__ __forceinline__ floatx4 frag(const float *S, int row, int k0) {
 }
 
 template <bool TA, bool TB>
-__device__ __forceinline__ void gemm_tile(const KParams &p, float (&lds)[2][2 * OPSZ], int id, int total) {
+__device__ __forceinline__ void gemm_tile(const KParams &p, float (&lds)[2][2 * OPSZ], int id, int total,
+                                          bool remap) {
   // XCD-aware bijective remap of the work index (id & 7 is the XCD as long as
-  // the grid is a multiple of 8 or covers all work items)
+  // the grid is a multiple of 8 or covers all work items); dynamic ids are
+  // handed out in time order and used as they are
   const int q = total >> 3, rr = total & 7, xcd = id & 7, loc = id >> 3;
-  const int wl = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  const int wl = remap ? (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc : id;
   const int bz = wl / p.tiles, wg = wl - bz * p.tiles;
   const int tn = wg % p.gx, tm = wg / p.gx;
   const int b = bz % p.batch, ks = bz / p.batch;
@@ -220,8 +223,20 @@ __device__ __forceinline__ void gemm_tile(const KParams &p, float (&lds)[2][2 * 
 template <bool TA, bool TB>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(KParams p) {
   __shared__ __attribute__((aligned(16))) float lds[2][2 * OPSZ];
+  __shared__ int next;
   const int total = p.tiles * p.batch * p.split;
-  for (int id = blockIdx.x; id < total; id += gridDim.x) gemm_tile<TA, TB>(p, lds, id, total);
+  if (p.counter) {
+    while (true) {
+      if (threadIdx.x == 0) next = atomicAdd(p.counter, 1);
+      __syncthreads();
+      const int id = next;
+      __syncthreads();
+      if (id >= total) break;
+      gemm_tile<TA, TB>(p, lds, id, total, false);
+    }
+    return;
+  }
+  for (int id = blockIdx.x; id < total; id += gridDim.x) gemm_tile<TA, TB>(p, lds, id, total, true);
 }
 
 __global__ __launch_bounds__(256) void splitk_reduce(KParams p) {
@@ -295,6 +310,8 @@ void gemm_f32(hipStream_t stream, const GemmArgs &g) {
   const int total = p.tiles * p.batch * p.split;
   int blocks = total;
   if (g.max_blocks > 0 && total > g.max_blocks) blocks = std::max(8, g.max_blocks / 8 * 8);
+  p.counter = g.tile_counter;
+  if (p.counter) KCTC_HIP_CHECK(hipMemsetAsync(p.counter, 0, sizeof(int), stream));
   dim3 grid(blocks);
   if (!g.transA && !g.transB) hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(NT), 0, stream, p);
   else if (!g.transA && g.transB) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(NT), 0, stream, p);

@@ -443,7 +443,7 @@ void UpdatableComponent::UpdateWith(float *params, const float *grad, float clip
 int CuDNNRecurrentComponent::side_gemm_blocks() const {
   const char *e = getenv("KCTC_SIDE_BLOCKS");
   if (e && *e) return atoi(e);
-  return 192;
+  return 512;  // dynamic tile scheduling: two per CU, late starters exit
 }
 
 void CuDNNRecurrentComponent::ApplyUpdate() {

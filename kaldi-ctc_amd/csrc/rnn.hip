@@ -1452,7 +1452,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.w = wl; p.pl_stride = pls; p.r_off = roff; p.bR_off = bR;
     p.G = R0 + lay.G; p.y = out; p.aux = R0 + lay.aux; p.err = err;
     p.sync = ver == 4 ? kSyncFlag : env_int("KCTC_SYNC_FWD", env_int("KCTC_SYNC", kSyncData));
-    p.allow_local = env_int("KCTC_LOCAL", 1);
+    p.allow_local = env_int("KCTC_LOCAL", 0);
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, 4096, s));
     const size_t lds = fwd_lds_bytes(d, N, U);
@@ -1507,7 +1507,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     p.G = R0 + lay.G; p.y = const_cast<float *>(out); p.aux = R0 + lay.aux;
     p.dy = dcur; p.E = E; p.DX = DX; p.bias = R0 + lay.bias; p.err = err;
     p.sync = ver == 4 ? kSyncFlag : env_int("KCTC_SYNC_BWD", env_int("KCTC_SYNC", kSyncFlag));
-    p.allow_local = env_int("KCTC_LOCAL", 1);
+    p.allow_local = env_int("KCTC_LOCAL", 0);
     if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, 4096, s));
@@ -1577,6 +1577,10 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     g.split_k = gemm_pick_split(g.M, g.N, g.K, dirs);
     g.ws = ws;
     g.max_blocks = max_blocks;
+    // flag words 1008..1009 of the workspace: dynamic tile counters (the
+    // recurrences of this layer, which use the other flag words, are done)
+    unsigned *fl = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
+    if (max_blocks > 0) g.tile_counter = reinterpret_cast<int *>(fl + 1008);
     {
       ProfSpan ps(s, "gemm_bwd_w");
       gemm_f32(s, g);
@@ -1597,6 +1601,7 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       r.split_k = gemm_pick_split(r.M, r.N, r.K, dirs);
       r.ws = ws;
       r.max_blocks = max_blocks;
+      if (max_blocks > 0) r.tile_counter = reinterpret_cast<int *>(fl + 1009);
       ProfSpan ps(s, "gemm_bwd_r");
       gemm_f32(s, r);
     }
