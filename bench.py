@@ -48,6 +48,23 @@ def model_flops(T, N, D, H, A, L, nw=4, dirs=2):
     return f, launches
 
 
+def pmc_traffic(kernel):
+    """HBM-side bytes per launch of `kernel` from the newest committed rocprofv3
+    PMC pass (profiles/*_pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE; produced by
+    scripts/gpu_bench_prof.sh on this workload).  bench.py cannot read counters
+    itself; None when no measurement of this kernel is committed."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if kernel in d and "traffic_bytes_per_launch" in d[kernel]:
+            return d[kernel]["traffic_bytes_per_launch"], os.path.basename(f)
+    return None, None
+
+
 def cpu_baseline(T, D, H, A, L, steps_seed):
     """The oracle's fp32 restatement (warp-ctc-CPU-style CTC + blocked-GEMM
     LSTM/affine, OpenMP) on a bounded sample: 6 utterances of the same shape."""
@@ -164,8 +181,10 @@ def main():
         avg_s = ms / n / 1e3
         flops_per_launch = fam_flops[dom] / (n / args.steps)
         achieved = flops_per_launch / avg_s / 1e12
+        traffic, tsrc = pmc_traffic(dom)
         roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None, "kernel": dom,
+                "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic, "traffic_source": tsrc,
+                "kernel": dom,
                 "avg_launch_ms": round(ms / n, 4),
                 "flops_per_launch": flops_per_launch,
                 "families_ms_per_step": {f: round(prof[f][0] / args.steps, 3) for f in prof}}
