@@ -34,6 +34,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -1234,6 +1235,260 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
   if (bad && tid == 0) atomicOr(p.err, 1u);
 }
 
+// ---------------------------------------------------------------------------
+// v5 backward: reduce-scatter hand-off
+// ---------------------------------------------------------------------------
+// WG (dir, g) owns units u0..u0+U-1 and the nW*U rows of R that feed those
+// units' gates.  Per step it (1) sums the partial dh of its units from every
+// producer, (2) does the pointwise cell backward of its (n, unit) elements,
+// (3) multiplies its dGates [Npad x nW*U] by its R rows [nW*U x H] on the
+// MFMAs -- every wave owns a quarter of the H output columns, so there is no
+// cross-wave reduction -- and publishes that partial dh of ALL units in the
+// MFMA C-fragment layout [tile][row tile][lane][4] (1 KB per 16 x 16 tile).
+// Consumers read only the tile positions of their own units from every
+// producer and sum them in a fixed order.  Per WG and step: 32 KB read and
+// 32 KB written (BLSTM-512, N=16) instead of the 128 KB dGates all-gather of
+// v4.  Hand-off as v4 (sc1 payload, vmcnt(0), barrier, sc1 epoch flag; sc1
+// loads), into a per-step image that is never reused within a launch.
+template <int MODE, int RT>
+__global__ __launch_bounds__(NT, 1) void rnn_bwd_rec5(RecParams p) {
+  constexpr int NW = MODE == kLstm ? 4 : MODE == kGru ? 3 : 1;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ int bad_lds, loc_lds;
+  const int slot = blockIdx.x & 7, d = slot / p.xpd, g = (blockIdx.x >> 3) * p.xpd + slot % p.xpd;
+  if (d >= p.dirs || g >= p.nwg) return;
+  constexpr int Npad = RT * 16;
+  const int H = p.H, U = p.U, N = p.N, T = p.T, nwg = p.nwg;
+  const int K = NW * U, KQ = (K + 15) / 16, Kp = KQ * 16, K4 = Kp + 4;
+  const int CTT = H / 16, CTW = CTT / 4;
+  const int u0 = g * U, ct_own = u0 >> 4, fr0 = u0 & 15;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  const long ldy = (long)p.dirs * H, ldg = (long)p.dirs * NW * H;
+  const long xstep = (long)p.dirs * nwg * H * Npad;  // floats of one step's partial image
+  float *Rk = smem;                           // [H][K4]: Rk[col][q*U+u] = R[q*H+u0+u][col]
+  float *Ads = Rk + (long)H * K4;             // [Npad][K4]: this step's dGates (recurrent part)
+  float *red = Ads + (long)Npad * K4;         // [256][4]: per-(group, position) partial sums
+  const float *Wd = p.w + d * p.pl_stride;
+  const float *R = Wd + p.r_off;
+  if (tid == 0) bad_lds = 0;
+  for (int idx = tid; idx < Kp * H; idx += NT) {
+    const int k = idx / H, col = idx - k * H;
+    float v = 0.f;
+    if (k < K) {
+      const int q = k / U, u = k - q * U;
+      v = R[(long)(q * H + u0 + u) * H + col];
+    }
+    Rk[col * K4 + k] = v;
+  }
+  for (int idx = tid; idx < Npad * K4; idx += NT) Ads[idx] = 0.f;
+  // consumer positions: 16-B chunks (rt, fq, unit) of the own tile, Pn of
+  // them per producer; G thread groups split the producers
+  const int Pn = RT * 4 * U, G = NT / Pn, NL = nwg / G;
+  const int pos = tid % Pn, grp = tid / Pn;
+  const int prt = pos / (4 * U), prem = pos - prt * 4 * U, pfq = prem / U, pu = prem - pfq * U;
+  const long pos_off = (((long)ct_own * RT + prt) * 64 + pfq * 16 + fr0 + pu) * 4;  // within a producer block
+  const long prod_stride = (long)CTT * RT * 64 * 4;                                 // floats per producer
+  const int items = N * U;
+  float carry[kMaxEPT], bsx[kMaxEPT][NW], bsh[kMaxEPT][NW], dxk[kMaxEPT][NW], eg[kMaxEPT][NW];
+  float cg[kMaxEPT][NW], cdy[kMaxEPT], ca[kMaxEPT], cap[kMaxEPT];
+  float ng[kMaxEPT][NW], ndy[kMaxEPT], na[kMaxEPT], nap[kMaxEPT];
+#pragma unroll
+  for (int j = 0; j < kMaxEPT; j++) {
+    carry[j] = cdy[j] = ca[j] = cap[j] = ndy[j] = na[j] = nap[j] = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; q++) bsx[j][q] = bsh[j][q] = cg[j][q] = ng[j][q] = dxk[j][q] = eg[j][q] = 0.f;
+  }
+  auto prefetch = [&](int k) {  // operands of forward-order step k into n*
+    const int t = d == 0 ? k : T - 1 - k, tp = d == 0 ? t - 1 : t + 1;
+#pragma unroll
+    for (int j = 0; j < kMaxEPT; j++) {
+      const int e = tid + j * NT;
+      if (e >= items) continue;
+      const int n = e / U, u = e - n * U;
+      const long yrow = ((long)t * N + n) * ldy + (long)d * H + u0 + u;
+      const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
+      const long prow = ((long)tp * N + n) * ldy + (long)d * H + u0 + u;
+      ndy[j] = p.dy[yrow];
+      if (MODE == kLstm || MODE == kGru) {
+#pragma unroll
+        for (int q = 0; q < NW; q++) ng[j][q] = p.G[grow + q * H];
+        na[j] = p.aux[yrow];
+      }
+      if (MODE == kLstm) nap[j] = k > 0 ? p.aux[prow] : 0.f;
+      else if (MODE == kGru) nap[j] = k > 0 ? p.y[prow] : 0.f;
+      else nap[j] = p.y[yrow];
+    }
+  };
+  auto rotate = [&]() {
+#pragma unroll
+    for (int j = 0; j < kMaxEPT; j++) {
+      cdy[j] = ndy[j]; ca[j] = na[j]; cap[j] = nap[j];
+#pragma unroll
+      for (int q = 0; q < NW; q++) cg[j][q] = ng[j][q];
+    }
+  };
+  auto e_store = [&](int t) {  // row-major dGates of step t (E; GRU also DX)
+#pragma unroll
+    for (int j = 0; j < kMaxEPT; j++) {
+      const int e = tid + j * NT;
+      if (e >= items) continue;
+      const int n = e / U, u = e - n * U;
+      const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
+#pragma unroll
+      for (int q = 0; q < NW; q++) p.E[grow + q * H] = eg[j][q];
+      if (MODE == kGru) {
+#pragma unroll
+        for (int q = 0; q < NW; q++) p.DX[grow + q * H] = dxk[j][q];
+      }
+    }
+  };
+  prefetch(T - 1);
+  rotate();
+  int bad = 0;
+  unsigned *myflag = p.flags + d * nwg + g;
+  (void)probe_local(p, d, g, myflag, bad, &bad_lds, &loc_lds);
+  int t_prev = -1;
+  for (int k = T - 1; k >= 0 && !bad; k--) {
+    const int t = d == 0 ? k : T - 1 - k;
+    const int ks = T - 1 - k;  // steps done before this one
+    REC_TRACE(ks, 0);
+    if (ks > 0) {
+      wait_flags(p.flags + d * nwg, nwg, (unsigned)(ks + 1), p.err, bad, &bad_lds);
+      REC_TRACE(ks, 1);
+      // the own units' partial dh from every producer (published at step ks-1)
+      const auto rs = rsrc(p.xch + (long)(ks - 1) * xstep, (unsigned)(xstep * 4));
+      const long base = (long)d * nwg * prod_stride + pos_off;
+      floatx4 sum = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (grp < G) {
+        if (NL == 8 * RT) {  // H = 512: compile-time count, all loads in flight
+          u32x4 v[8 * RT];
+#pragma unroll
+          for (int i = 0; i < 8 * RT; i++)
+            v[i] = ld_sc1(rs, (unsigned)((base + (long)(grp + G * i) * prod_stride) * 4));
+#pragma unroll
+          for (int i = 0; i < 8 * RT; i++) sum += __builtin_bit_cast(floatx4, v[i]);
+        } else {
+          for (int i = 0; i < NL; i++)
+            sum += __builtin_bit_cast(floatx4, ld_sc1(rs, (unsigned)((base + (long)(grp + G * i) * prod_stride) * 4)));
+        }
+        *reinterpret_cast<floatx4 *>(red + (long)(grp * Pn + pos) * 4) = sum;
+      }
+      REC_TRACE(ks, 2);
+    }
+    asm volatile("" ::: "memory");
+    // behind the hand-off loads: next step's operands, last step's row-major dGates
+    if (k > 0) prefetch(k - 1);
+    if (t_prev >= 0) e_store(t_prev);
+    __syncthreads();
+    REC_TRACE(ks, 3);
+#pragma unroll
+    for (int j = 0; j < kMaxEPT; j++) {
+      const int e = tid + j * NT;
+      if (e >= items) continue;
+      const int n = e / U, u = e - n * U;
+      float dhr = 0.f;
+      if (ks > 0) {
+        const int rt = n >> 4, nf = (n & 15) >> 2, r = n & 3;
+        const int ps = rt * 4 * U + nf * U + u;
+        for (int gg = 0; gg < G; gg++) dhr += red[(long)(gg * Pn + ps) * 4 + r];
+      }
+      float dh = cdy[j] + dhr;
+      if (MODE == kLstm) {
+        const float ig = cg[j][0], fg = cg[j][1], gg = cg[j][2], og = cg[j][3];
+        const float tc = ftanh(ca[j]);
+        const float dO = dh * tc;
+        const float dc = dh * og * (1.f - tc * tc) + carry[j];
+        eg[j][0] = dc * gg * ig * (1.f - ig);
+        eg[j][1] = dc * cap[j] * fg * (1.f - fg);
+        eg[j][2] = dc * ig * (1.f - gg * gg);
+        eg[j][3] = dO * og * (1.f - og);
+        carry[j] = dc * fg;
+      } else if (MODE == kGru) {
+        dh += carry[j];
+        const float r = cg[j][0], z = cg[j][1], nn = cg[j][2];
+        const float dn = dh * (1.f - z), dz = dh * (cap[j] - nn);
+        const float dpn = dn * (1.f - nn * nn);
+        const float dpr = dpn * ca[j] * r * (1.f - r);
+        const float dpz = dz * z * (1.f - z);
+        carry[j] = dh * z;
+        dxk[j][0] = dpr; dxk[j][1] = dpz; dxk[j][2] = dpn;
+        eg[j][0] = dpr; eg[j][1] = dpz; eg[j][2] = dpn * r;
+        bsh[j][0] += dpr; bsh[j][1] += dpz; bsh[j][2] += dpn * r;
+      } else {
+        const float der = MODE == kRelu ? (cap[j] > 0.f ? 1.f : 0.f) : (1.f - cap[j] * cap[j]);
+        eg[j][0] = dh * der;
+      }
+#pragma unroll
+      for (int q = 0; q < NW; q++) {
+        Ads[(long)n * K4 + q * U + u] = eg[j][q];
+        bsx[j][q] += (MODE == kGru) ? dxk[j][q] : eg[j][q];
+      }
+    }
+    __syncthreads();
+    if (k > 0) {  // partial dh of all units for the next step
+      floatx4 acc[RT][8];
+#pragma unroll
+      for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+        for (int c = 0; c < 8; c++) acc[rt][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int kq = 0; kq < KQ; kq++) {
+        floatx4 a[RT], b[8];
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++) a[rt] = ld4(Ads + (long)(rt * 16 + fr) * K4 + kq * 16 + fq * 4);
+#pragma unroll
+        for (int c = 0; c < 8; c++)
+          if (c < CTW) b[c] = ld4(Rk + (long)((w * CTW + c) * 16 + fr) * K4 + kq * 16 + fq * 4);
+#pragma unroll
+        for (int s = 0; s < 4; s++)
+#pragma unroll
+          for (int c = 0; c < 8; c++)
+            if (c < CTW)
+#pragma unroll
+              for (int rt = 0; rt < RT; rt++)
+                acc[rt][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rt][s], b[c][s], acc[rt][c], 0, 0, 0);
+      }
+      const auto ro = rsrc(p.xch + (long)ks * xstep, (unsigned)(xstep * 4));
+      const long obase = (long)(d * nwg + g) * prod_stride;
+#pragma unroll
+      for (int c = 0; c < 8; c++)
+        if (c < CTW)
+#pragma unroll
+          for (int rt = 0; rt < RT; rt++)
+            publish4(ro, (unsigned)((obase + (((long)(w * CTW + c) * RT + rt) * 64 + lane) * 4) * 4), acc[rt][c]);
+      REC_TRACE_W(ks, 10);
+    }
+    signal_epoch(myflag, (unsigned)(ks + 2), 0);
+    REC_TRACE(ks, 4);
+    rotate();
+    t_prev = t;
+    REC_TRACE(ks, 5);
+  }
+  if (t_prev >= 0 && !bad) e_store(t_prev);
+  // bias partial sums: reduce over n in a fixed order (Rk region is free now)
+  float *bs = Rk;  // [2][N][U][NW]
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kMaxEPT; j++) {
+    const int e = tid + j * NT;
+    if (e >= items) continue;
+    const int n = e / U, u = e - n * U;
+#pragma unroll
+    for (int q = 0; q < NW; q++) {
+      const long b0 = ((long)n * U + u) * NW + q;
+      bs[b0] = bsx[j][q];
+      bs[(long)N * U * NW + b0] = (MODE == kGru) ? bsh[j][q] : bsx[j][q];
+    }
+  }
+  __syncthreads();
+  for (int q = tid; q < 2 * NW * U; q += NT) {
+    const int part = q / (NW * U), rem = q - part * NW * U, gt = rem / U, u = rem - gt * U;
+    float s2 = 0.f;
+    for (int n = 0; n < N; n++) s2 += bs[(long)part * N * U * NW + ((long)n * U + u) * NW + gt];
+    p.bias[((long)d * 2 + part) * NW * H + gt * H + u0 + u] = s2;
+  }
+  if (bad && tid == 0) atomicOr(p.err, 1u);
+}
+
 template <typename F>
 static void set_lds(F f, size_t bytes) {
   static size_t done[8] = {0};
@@ -1244,6 +1499,11 @@ static void set_lds(F f, size_t bytes) {
 
 template <int MODE, int RT>
 static void launch_one(bool fwd, const RecParams &p, dim3 grid, size_t lds, hipStream_t s, int ver) {
+  if (ver == 5) {
+    set_lds(rnn_bwd_rec5<MODE, RT>, lds);
+    hipLaunchKernelGGL((rnn_bwd_rec5<MODE, RT>), grid, dim3(NT), lds, s, p);
+    return;
+  }
   if (ver == 4) {
     if (fwd) {
       set_lds(rnn_fwd_rec4<MODE, RT>, lds);
@@ -1387,6 +1647,68 @@ static int pick_bwd_u4(const RnnDesc &d, int N) {
   return 0;
 }
 
+// v5 backward (reduce-scatter): U in {16, 8}, H % 64 == 0, Npad in {16, 32, 64}
+static size_t bwd5_lds_bytes(const RnnDesc &d, int N, int U) {
+  const int K = d.nw() * U, Kp = (K + 15) / 16 * 16, K4 = Kp + 4;
+  const int Npad = (N + 15) / 16 * 16;
+  return sizeof(float) * ((size_t)d.H * K4 + (size_t)Npad * K4 + 256 * 4);
+}
+static int pick_bwd_u5(const RnnDesc &d, int N) {
+  if (env_int("KCTC_BWD_REC", 5) != 5 || rec_version() != 4 || d.dirs > 8 || d.H % 64) return 0;
+  const int Npad = (N + 15) / 16 * 16;
+  if (Npad != 16 && Npad != 32 && Npad != 64) return 0;
+  auto ok = [&](int U) {
+    if (!v4_xpd(d, U) || N * U > kMaxEPT * NT || (Npad / 16) * 4 * U > NT) return false;
+    if ((long)2 * N * U * d.nw() > (long)d.H * (d.nw() * U + 4)) return false;  // bias scratch in Rk
+    return bwd5_lds_bytes(d, N, U) <= 160 * 1024;
+  };
+  const int want = env_int("KCTC_BWD_U", 0);
+  if (want) return ok(want) ? want : 0;
+  for (int U : {16, 8})
+    if (ok(U)) return U;
+  return 0;
+}
+
+// Per-device exchange pool of the v5 backward: one step image per time step,
+// never reused within a launch (T x dirs x nwg x H x Npad floats, 4.2 GB for
+// BLSTM-512 N=16 T=2000).  Library-owned so that the components of a network
+// share it; launches on one device are ordered through its event.
+namespace {
+struct XchPool {
+  void *p = nullptr;
+  size_t bytes = 0;
+  hipEvent_t ev = nullptr;
+};
+std::mutex g_xch_mu;
+XchPool g_xch[64];
+}  // namespace
+
+static float *xch_acquire(size_t bytes, hipStream_t s) {
+  int dev = 0;
+  KCTC_HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_xch_mu);
+  XchPool &x = g_xch[dev & 63];
+  if (x.ev) KCTC_HIP_CHECK(hipStreamWaitEvent(s, x.ev, 0));
+  if (bytes > x.bytes) {
+    if (x.p) {
+      KCTC_HIP_CHECK(hipDeviceSynchronize());
+      KCTC_HIP_CHECK(hipFree(x.p));
+      x.p = nullptr;
+    }
+    KCTC_HIP_CHECK(hipMalloc(&x.p, bytes));
+    x.bytes = bytes;
+  }
+  return static_cast<float *>(x.p);
+}
+static void xch_release(hipStream_t s) {
+  int dev = 0;
+  KCTC_HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_xch_mu);
+  XchPool &x = g_xch[dev & 63];
+  if (!x.ev) KCTC_HIP_CHECK(hipEventCreateWithFlags(&x.ev, hipEventDisableTiming));
+  KCTC_HIP_CHECK(hipEventRecord(x.ev, s));
+}
+
 static int pick_bwd_u(const RnnDesc &d, int N) {
   int want = env_int("KCTC_BWD_U", 0);
   const int K = d.nw() * d.H;
@@ -1483,9 +1805,10 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
   if (T <= 0 || N <= 0 || N > 16 * kMaxRT || d.H % 16) return KRNN_NOT_SUPPORTED;
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
   if (res_bytes < sizeof(float) * (size_t)lay.total) return KRNN_BAD_PARAM;
-  const int U4 = pick_bwd_u4(d, N);
-  const int ver = U4 ? 4 : 3;
-  const int U = U4 ? U4 : pick_bwd_u(d, N);
+  const int U5 = pick_bwd_u5(d, N);
+  const int U4 = U5 ? 0 : pick_bwd_u4(d, N);
+  const int ver = U5 ? 5 : U4 ? 4 : 3;
+  const int U = U5 ? U5 : U4 ? U4 : pick_bwd_u(d, N);
   if (!U) return KRNN_NOT_SUPPORTED;
   const int NW = d.nw(), H = d.H, dirs = d.dirs;
   const long TN = (long)T * N;
@@ -1508,15 +1831,18 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     p.bR_off = d.lin_offset(l * dirs, NW, true) - pl0;
     p.G = R0 + lay.G; p.y = const_cast<float *>(out); p.aux = R0 + lay.aux;
     p.dy = dcur; p.E = E; p.DX = DX; p.bias = R0 + lay.bias; p.err = err;
-    p.sync = ver == 4 ? kSyncFlag : env_int("KCTC_SYNC_BWD", env_int("KCTC_SYNC", kSyncFlag));
+    p.sync = ver >= 4 ? kSyncFlag : env_int("KCTC_SYNC_BWD", env_int("KCTC_SYNC", kSyncFlag));
     p.allow_local = env_int("KCTC_LOCAL", 0);
     if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, 4096, s));
-    const size_t lds = bwd_lds_bytes(d, N, U, ver);
-    p.xpd = ver == 4 ? v4_xpd(d, U) : 1;
-    p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
-    const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : dirs * p.nwg);
+    const size_t lds = ver == 5 ? bwd5_lds_bytes(d, N, U) : bwd_lds_bytes(d, N, U, ver);
+    p.xpd = ver >= 4 ? v4_xpd(d, U) : 1;
+    if (ver == 5)
+      p.xch = xch_acquire(sizeof(float) * (size_t)T * dirs * p.nwg * H * p.Npad, s);
+    else
+      p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
+    const dim3 grid(ver >= 4 ? 8 * ceil_div(p.nwg, p.xpd) : dirs * p.nwg);
     RecTrace tr;
     if (tr.arm("bwd", grid.x)) p.trace = tr.dev;
     {
@@ -1524,6 +1850,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
       launch_rec(false, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
+    if (ver == 5) xch_release(s);
     tr.dump("bwd", s, grid.x, p.nwg, T, dirs, ver, p.xpd);
     // dx_l = sum_dir DX_dir W_dir   (lower layer's dy, or the caller's dx)
     float *dxl = (l == 0) ? dx : res + lay.per_layer * (l - 1) + lay.dout;

@@ -14,7 +14,7 @@ def main(path):
     tr = np.frombuffer(raw[32:], dtype=np.uint64).reshape(steps, grid, 16).astype(np.int64)
     steps = min(steps, T)
     tr = tr[:steps]
-    if ver == 4:
+    if ver >= 4:
         members = [[b for b in range(grid) if (b % 8) // xpd == d and (b // 8) * xpd + (b % 8) % xpd < nwg]
                    for d in range(dirs)]
     else:
@@ -34,7 +34,7 @@ def main(path):
     for i, nm in enumerate(names):
         d = (tr[sl, :, i + 1] - tr[sl, :, i]) * us
         print(f"  {nm:22s} median {np.median(d):7.3f}  p90 {np.percentile(d, 90):7.3f}")
-    if ver == 4 and tr[sl, :, 6].min() > 0:
+    if ver >= 4 and tr[sl, :, 6].min() > 0:
         for w in range(4):
             ld = (tr[sl, :, 6 + w] - tr[sl, :, 1]) * us
             mf = (tr[sl, :, 10 + w] - tr[sl, :, 6 + w]) * us
