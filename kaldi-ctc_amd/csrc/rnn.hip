@@ -1654,7 +1654,7 @@ static size_t bwd5_lds_bytes(const RnnDesc &d, int N, int U) {
   return sizeof(float) * ((size_t)d.H * K4 + (size_t)Npad * K4 + 256 * 4);
 }
 static int pick_bwd_u5(const RnnDesc &d, int N) {
-  if (env_int("KCTC_BWD_REC", 5) != 5 || rec_version() != 4 || d.dirs > 8 || d.H % 64) return 0;
+  if (env_int("KCTC_BWD_REC", 4) != 5 || rec_version() != 4 || d.dirs > 8 || d.H % 64) return 0;
   const int Npad = (N + 15) / 16 * 16;
   if (Npad != 16 && Npad != 32 && Npad != 64) return 0;
   auto ok = [&](int U) {

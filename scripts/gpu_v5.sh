@@ -2,9 +2,9 @@
 # v5 backward validation: parity tests, trace, bench variants.
 set -o pipefail
 mkdir -p gpurun_out/tr5
-timeout -k 10 600 python -m pytest tests/test_rnn_gpu.py tests/test_train_gpu.py tests/test_egs.py tests/test_train_egs_gpu.py -x -q > gpurun_out/tests_v5.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/tests_v5.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_rnn_gpu.py tests/test_train_gpu.py tests/test_egs.py tests/test_train_egs_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/tests_v5.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/tests_v5.log; exit 1; }
 tail -2 gpurun_out/tests_v5.log
-KCTC_BWD_U=8 timeout -k 10 300 python -m pytest tests/test_rnn_gpu.py -x -q > gpurun_out/tests_v5u8.log 2>&1 || { echo TESTS_U8_FAILED; tail -40 gpurun_out/tests_v5u8.log; exit 1; }
+KCTC_BWD_U=8 timeout -k 10 300 python -u -m pytest tests/test_rnn_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/tests_v5u8.log 2>&1 || { echo TESTS_U8_FAILED; tail -40 gpurun_out/tests_v5u8.log; exit 1; }
 tail -1 gpurun_out/tests_v5u8.log
 KCTC_REC_TRACE=gpurun_out/tr5 timeout -k 10 300 python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-profile > gpurun_out/tr5.log 2>&1 || { echo TRACE_FAILED; tail -5 gpurun_out/tr5.log; exit 1; }
 python scripts/trace_rec.py gpurun_out/tr5/rec_bwd.bin
