@@ -1236,226 +1236,262 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
 }
 
 // ---------------------------------------------------------------------------
-// v5 backward: reduce-scatter hand-off
+// v6 backward: reduce-scatter hand-off, split-fp16 MFMA
 // ---------------------------------------------------------------------------
-// WG (dir, g) owns units u0..u0+U-1 and the nW*U rows of R that feed those
-// units' gates.  Per step it (1) sums the partial dh of its units from every
-// producer, (2) does the pointwise cell backward of its (n, unit) elements,
-// (3) multiplies its dGates [Npad x nW*U] by its R rows [nW*U x H] on the
-// MFMAs -- every wave owns a quarter of the H output columns, so there is no
-// cross-wave reduction -- and publishes that partial dh of ALL units in the
-// MFMA C-fragment layout [tile][row tile][lane][4] (1 KB per 16 x 16 tile).
-// Consumers read only the tile positions of their own units from every
-// producer and sum them in a fixed order.  Per WG and step: 32 KB read and
-// 32 KB written (BLSTM-512, N=16) instead of the 128 KB dGates all-gather of
-// v4.  Hand-off as v4 (sc1 payload, vmcnt(0), barrier, sc1 epoch flag; sc1
-// loads), into a per-step image that is never reused within a launch.
-template <int MODE, int RT>
-__global__ __launch_bounds__(NT, 1) void rnn_bwd_rec5(RecParams p) {
-  constexpr int NW = MODE == kLstm ? 4 : MODE == kGru ? 3 : 1;
+// WG (dir, g) owns units u0..u0+U-1 and the K = nW*U rows of R that feed those
+// units' gates.  Per step it
+//   (1) sums the partial dh of its units from every producer WG of its
+//       direction (published the step before; fixed summation order),
+//   (2) does the pointwise cell backward of its (n, unit) elements (one per
+//       thread) -> dGates [N x K],
+//   (3) multiplies dGates [16 x K] by its R rows [K x H] on the matrix cores,
+//       every wave owning H/4 output columns (no cross-wave reduction), and
+//   (4) publishes that partial dh of ALL H units, fp32, in the MFMA C-fragment
+//       layout [producer][col tile][lane][4] (1 KB per 16 x 16 tile).
+// Per WG and step 32 KB are read and 32 KB written (BLSTM-512, N=16) instead of
+// the 128 KB dGates all-gather of v4.
+//
+// Split-fp16 products ("fp16x3"): both operands are scaled by powers of two
+// (R slice: one exponent per WG, from its max |R|; dGates: one exponent per
+// row, from the row's max over the WG's K columns) so the largest magnitude
+// lands in [2^13, 2^14), and split as x = hi + lo with hi = fp16(x),
+// lo = fp16(x - hi).  acc += hi_a hi_b + hi_a lo_b + lo_a hi_b on
+// v_mfma_f32_16x16x32_f16 (products exact, fp32 accumulation), then the exact
+// power-of-two unscale.  Each operand keeps 22 significant bits relative to
+// its row / slice maximum; the dropped lo*lo term is 2^-22 of it -- the same
+// order as fp32 rounding of the accumulated terms.  5.3x fewer MFMA cycles
+// than v_mfma_f32_16x16x4_f32 for the same product.
+//
+// R lives in registers for the whole launch (the B fragments of the wave's
+// H/64 column tiles, hi and lo); dGates goes through a 4.5 KB LDS image.
+// Hand-off as v4 (sc1 payload stores, vmcnt(0), barrier, sc1 epoch flag;
+// sc1 loads) into a per-step image that is never rewritten within a launch.
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float wave_max16(float v, int width) {
+  // max over groups of `width` (8 or 16) consecutive lanes
+  v = fmaxf(v, __shfl_xor(v, 1));
+  v = fmaxf(v, __shfl_xor(v, 2));
+  v = fmaxf(v, __shfl_xor(v, 4));
+  if (width > 8) v = fmaxf(v, __shfl_xor(v, 8));
+  return v;
+}
+
+// exponent s with max * 2^s in [2^13, 2^14) (s = 14 for max == 0)
+__device__ __forceinline__ int split_exp(float mx) {
+  int e = 0;
+  (void)frexpf(mx, &e);
+  return 14 - e;
+}
+
+__device__ __forceinline__ void split16(float x, _Float16 &hi, _Float16 &lo) {
+  hi = (_Float16)x;
+  lo = (_Float16)(x - (float)hi);
+}
+
+template <int MODE, int U, int CTW>
+__global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
+  constexpr int NW = MODE == kLstm ? 4 : 3;
+  constexpr int K = NW * U, KB = (K + 31) / 32, AP = KB * 32 + 8;  // A image row pitch (halves)
+  constexpr int H = CTW * 64, CTT = H / 16, NWG = H / U;
+  constexpr int POS = 4 * U;       // 16-B chunks of the own column tile per producer
+  constexpr int NGRP = NT / POS;   // producer groups
+  constexpr int PER = NWG / NGRP;  // producers summed per group
+  static_assert(NWG % NGRP == 0, "producer groups");
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ int bad_lds, loc_lds;
-  const int slot = blockIdx.x & 7, d = slot / p.xpd, g = (blockIdx.x >> 3) * p.xpd + slot % p.xpd;
-  if (d >= p.dirs || g >= p.nwg) return;
-  constexpr int Npad = RT * 16;
-  const int H = p.H, U = p.U, N = p.N, T = p.T, nwg = p.nwg;
-  const int K = NW * U, KQ = (K + 15) / 16, Kp = KQ * 16, K4 = Kp + 4;
-  const int CTT = H / 16, CTW = CTT / 4;
+  __shared__ int bad_lds;
+  __shared__ int rowexp[16];
+  __shared__ float wmax[4];
+  const int d = blockIdx.x % p.dirs, g = blockIdx.x / p.dirs;
+  if (g >= NWG) return;
+  const int N = p.N, T = p.T;
   const int u0 = g * U, ct_own = u0 >> 4, fr0 = u0 & 15;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
   const long ldy = (long)p.dirs * H, ldg = (long)p.dirs * NW * H;
-  const long xstep = (long)p.dirs * nwg * H * Npad;  // floats of one step's partial image
-  float *Rk = smem;                           // [H][K4]: Rk[col][q*U+u] = R[q*H+u0+u][col]
-  float *Ads = Rk + (long)H * K4;             // [Npad][K4]: this step's dGates (recurrent part)
-  float *red = Ads + (long)Npad * K4;         // [256][4]: per-(group, position) partial sums
+  constexpr long PSTR = (long)CTT * 64 * 4;   // floats per producer block (16 x H)
+  const long xstep = (long)p.dirs * NWG * PSTR;
+  _Float16 *Ahi = reinterpret_cast<_Float16 *>(smem);  // [16][AP]
+  _Float16 *Alo = Ahi + 16 * AP;
+  float *red = reinterpret_cast<float *>(Alo + 16 * AP);  // [NGRP][POS][4]
   const float *Wd = p.w + d * p.pl_stride;
   const float *R = Wd + p.r_off;
   if (tid == 0) bad_lds = 0;
-  for (int idx = tid; idx < Kp * H; idx += NT) {
-    const int k = idx / H, col = idx - k * H;
-    float v = 0.f;
-    if (k < K) {
-      const int q = k / U, u = k - q * U;
-      v = R[(long)(q * H + u0 + u) * H + col];
-    }
-    Rk[col * K4 + k] = v;
-  }
-  for (int idx = tid; idx < Npad * K4; idx += NT) Ads[idx] = 0.f;
-  // consumer positions: 16-B chunks (rt, fq, unit) of the own tile, Pn of
-  // them per producer; G thread groups split the producers
-  const int Pn = RT * 4 * U, G = NT / Pn, NL = nwg / G;
-  const int pos = tid % Pn, grp = tid / Pn;
-  const int prt = pos / (4 * U), prem = pos - prt * 4 * U, pfq = prem / U, pu = prem - pfq * U;
-  const long pos_off = (((long)ct_own * RT + prt) * 64 + pfq * 16 + fr0 + pu) * 4;  // within a producer block
-  const long prod_stride = (long)CTT * RT * 64 * 4;                                 // floats per producer
-  const int items = N * U;
-  float carry[kMaxEPT], bsx[kMaxEPT][NW], bsh[kMaxEPT][NW], dxk[kMaxEPT][NW], eg[kMaxEPT][NW];
-  float cg[kMaxEPT][NW], cdy[kMaxEPT], ca[kMaxEPT], cap[kMaxEPT];
-  float ng[kMaxEPT][NW], ndy[kMaxEPT], na[kMaxEPT], nap[kMaxEPT];
+  for (int i = tid; i < 32 * AP; i += NT) Ahi[i] = (_Float16)0.f;  // Ahi and Alo, padding included
+  // ---- R slice -> scaled hi/lo B fragments in registers ----
+  auto rval = [&](int kk, int col) -> float {
+    if (kk >= K) return 0.f;
+    const int q = kk / U, u = kk - q * U;
+    return R[(long)(q * H + u0 + u) * H + col];
+  };
+  float mx = 0.f;
 #pragma unroll
-  for (int j = 0; j < kMaxEPT; j++) {
-    carry[j] = cdy[j] = ca[j] = cap[j] = ndy[j] = na[j] = nap[j] = 0.f;
+  for (int c = 0; c < CTW; c++)
 #pragma unroll
-    for (int q = 0; q < NW; q++) bsx[j][q] = bsh[j][q] = cg[j][q] = ng[j][q] = dxk[j][q] = eg[j][q] = 0.f;
-  }
-  auto prefetch = [&](int k) {  // operands of forward-order step k into n*
-    const int t = d == 0 ? k : T - 1 - k, tp = d == 0 ? t - 1 : t + 1;
+    for (int kb = 0; kb < KB; kb++)
 #pragma unroll
-    for (int j = 0; j < kMaxEPT; j++) {
-      const int e = tid + j * NT;
-      if (e >= items) continue;
-      const int n = e / U, u = e - n * U;
-      const long yrow = ((long)t * N + n) * ldy + (long)d * H + u0 + u;
-      const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
-      const long prow = ((long)tp * N + n) * ldy + (long)d * H + u0 + u;
-      ndy[j] = p.dy[yrow];
-      if (MODE == kLstm || MODE == kGru) {
+      for (int j = 0; j < 8; j++) mx = fmaxf(mx, fabsf(rval(kb * 32 + fq * 8 + j, (w * CTW + c) * 16 + fr)));
 #pragma unroll
-        for (int q = 0; q < NW; q++) ng[j][q] = p.G[grow + q * H];
-        na[j] = p.aux[yrow];
+  for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if (lane == 0) wmax[w] = mx;
+  __syncthreads();
+  const int sB = split_exp(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3])));
+  halfx8 bhi[CTW][KB], blo[CTW][KB];
+#pragma unroll
+  for (int c = 0; c < CTW; c++)
+#pragma unroll
+    for (int kb = 0; kb < KB; kb++)
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        _Float16 h, l;
+        split16(ldexpf(rval(kb * 32 + fq * 8 + j, (w * CTW + c) * 16 + fr), sB), h, l);
+        bhi[c][kb][j] = h;
+        blo[c][kb][j] = l;
       }
-      if (MODE == kLstm) nap[j] = k > 0 ? p.aux[prow] : 0.f;
-      else if (MODE == kGru) nap[j] = k > 0 ? p.y[prow] : 0.f;
-      else nap[j] = p.y[yrow];
-    }
+  // ---- per-element state: thread tid <-> (n = tid / U, u = tid % U) ----
+  const bool has_e = tid < 16 * U;
+  const int en = tid / U, eu = tid - en * U;
+  const bool live = has_e && en < N;
+  float carry = 0.f, bsx[NW], bsh[NW], dxk[NW], eg[NW], cg[NW], ng[NW];
+  float cdy = 0.f, ca = 0.f, cap = 0.f, ndy = 0.f, na = 0.f, nap = 0.f;
+#pragma unroll
+  for (int q = 0; q < NW; q++) bsx[q] = bsh[q] = dxk[q] = eg[q] = cg[q] = ng[q] = 0.f;
+  auto prefetch = [&](int k) {  // operands of forward-order step k into n*
+    if (!live) return;
+    const int t = d == 0 ? k : T - 1 - k, tp = d == 0 ? t - 1 : t + 1;
+    const long yrow = ((long)t * N + en) * ldy + (long)d * H + u0 + eu;
+    const long grow = ((long)t * N + en) * ldg + (long)d * NW * H + u0 + eu;
+    const long prow = ((long)tp * N + en) * ldy + (long)d * H + u0 + eu;
+    ndy = p.dy[yrow];
+#pragma unroll
+    for (int q = 0; q < NW; q++) ng[q] = p.G[grow + q * H];
+    na = p.aux[yrow];
+    if (MODE == kLstm) nap = k > 0 ? p.aux[prow] : 0.f;
+    else nap = k > 0 ? p.y[prow] : 0.f;
   };
   auto rotate = [&]() {
+    cdy = ndy; ca = na; cap = nap;
 #pragma unroll
-    for (int j = 0; j < kMaxEPT; j++) {
-      cdy[j] = ndy[j]; ca[j] = na[j]; cap[j] = nap[j];
-#pragma unroll
-      for (int q = 0; q < NW; q++) cg[j][q] = ng[j][q];
-    }
+    for (int q = 0; q < NW; q++) cg[q] = ng[q];
   };
   auto e_store = [&](int t) {  // row-major dGates of step t (E; GRU also DX)
+    if (!live) return;
+    const long grow = ((long)t * N + en) * ldg + (long)d * NW * H + u0 + eu;
 #pragma unroll
-    for (int j = 0; j < kMaxEPT; j++) {
-      const int e = tid + j * NT;
-      if (e >= items) continue;
-      const int n = e / U, u = e - n * U;
-      const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + u;
+    for (int q = 0; q < NW; q++) p.E[grow + q * H] = eg[q];
+    if (MODE == kGru) {
 #pragma unroll
-      for (int q = 0; q < NW; q++) p.E[grow + q * H] = eg[j][q];
-      if (MODE == kGru) {
-#pragma unroll
-        for (int q = 0; q < NW; q++) p.DX[grow + q * H] = dxk[j][q];
-      }
+      for (int q = 0; q < NW; q++) p.DX[grow + q * H] = dxk[q];
     }
   };
+  // consumer chunk of this thread: position pos (lane of the own column tile)
+  // of producers grp, grp + NGRP, ...
+  const int pos = tid % POS, grp = tid / POS;
+  const int pln = U == 16 ? pos : (pos >> 3) * 16 + fr0 + (pos & 7);
+  const long coff = (long)d * NWG * PSTR + ((long)ct_own * 64 + pln) * 4 + (long)grp * PSTR;
+  // where element (en, eu) finds its sum: chunk of lane (en/4)*16 + fr0 + eu, register en % 4
+  const int epos = U == 16 ? (en >> 2) * 16 + eu : (en >> 2) * 8 + eu;
   prefetch(T - 1);
   rotate();
   int bad = 0;
-  unsigned *myflag = p.flags + d * nwg + g;
-  (void)probe_local(p, d, g, myflag, bad, &bad_lds, &loc_lds);
+  unsigned *myflag = p.flags + d * NWG + g;
   int t_prev = -1;
   for (int k = T - 1; k >= 0 && !bad; k--) {
     const int t = d == 0 ? k : T - 1 - k;
     const int ks = T - 1 - k;  // steps done before this one
     REC_TRACE(ks, 0);
     if (ks > 0) {
-      wait_flags(p.flags + d * nwg, nwg, (unsigned)(ks + 1), p.err, bad, &bad_lds);
+      wait_flags(p.flags + d * NWG, NWG, (unsigned)(ks + 1), p.err, bad, &bad_lds);
       REC_TRACE(ks, 1);
-      // the own units' partial dh from every producer (published at step ks-1)
       const auto rs = rsrc(p.xch + (long)(ks - 1) * xstep, (unsigned)(xstep * 4));
-      const long base = (long)d * nwg * prod_stride + pos_off;
-      floatx4 sum = floatx4{0.f, 0.f, 0.f, 0.f};
-      if (grp < G) {
-        if (NL == 8 * RT) {  // H = 512: compile-time count, all loads in flight
-          u32x4 v[8 * RT];
+      u32x4 v[PER];
 #pragma unroll
-          for (int i = 0; i < 8 * RT; i++)
-            v[i] = ld_sc1(rs, (unsigned)((base + (long)(grp + G * i) * prod_stride) * 4));
+      for (int i = 0; i < PER; i++) v[i] = ld_sc1(rs, (unsigned)((coff + (long)i * NGRP * PSTR) * 4));
+      floatx4 s = __builtin_bit_cast(floatx4, v[0]);
 #pragma unroll
-          for (int i = 0; i < 8 * RT; i++) sum += __builtin_bit_cast(floatx4, v[i]);
-        } else {
-          for (int i = 0; i < NL; i++)
-            sum += __builtin_bit_cast(floatx4, ld_sc1(rs, (unsigned)((base + (long)(grp + G * i) * prod_stride) * 4)));
-        }
-        *reinterpret_cast<floatx4 *>(red + (long)(grp * Pn + pos) * 4) = sum;
-      }
+      for (int i = 1; i < PER; i++) s += __builtin_bit_cast(floatx4, v[i]);
+      st4(red + (long)(grp * POS + pos) * 4, s);
       REC_TRACE(ks, 2);
     }
     asm volatile("" ::: "memory");
     // behind the hand-off loads: next step's operands, last step's row-major dGates
-    if (k > 0) prefetch(k - 1);
     if (t_prev >= 0) e_store(t_prev);
+    if (k > 0) prefetch(k - 1);
     __syncthreads();
-    REC_TRACE(ks, 3);
-#pragma unroll
-    for (int j = 0; j < kMaxEPT; j++) {
-      const int e = tid + j * NT;
-      if (e >= items) continue;
-      const int n = e / U, u = e - n * U;
+    if (has_e) {
       float dhr = 0.f;
       if (ks > 0) {
-        const int rt = n >> 4, nf = (n & 15) >> 2, r = n & 3;
-        const int ps = rt * 4 * U + nf * U + u;
-        for (int gg = 0; gg < G; gg++) dhr += red[(long)(gg * Pn + ps) * 4 + r];
+#pragma unroll
+        for (int gg = 0; gg < NGRP; gg++) dhr += red[(long)(gg * POS + epos) * 4 + (en & 3)];
       }
-      float dh = cdy[j] + dhr;
+      float dh = cdy + dhr;
       if (MODE == kLstm) {
-        const float ig = cg[j][0], fg = cg[j][1], gg = cg[j][2], og = cg[j][3];
-        const float tc = ftanh(ca[j]);
+        const float ig = cg[0], fg = cg[1], gg = cg[2], og = cg[3];
+        const float tc = ftanh(ca);
         const float dO = dh * tc;
-        const float dc = dh * og * (1.f - tc * tc) + carry[j];
-        eg[j][0] = dc * gg * ig * (1.f - ig);
-        eg[j][1] = dc * cap[j] * fg * (1.f - fg);
-        eg[j][2] = dc * ig * (1.f - gg * gg);
-        eg[j][3] = dO * og * (1.f - og);
-        carry[j] = dc * fg;
-      } else if (MODE == kGru) {
-        dh += carry[j];
-        const float r = cg[j][0], z = cg[j][1], nn = cg[j][2];
-        const float dn = dh * (1.f - z), dz = dh * (cap[j] - nn);
-        const float dpn = dn * (1.f - nn * nn);
-        const float dpr = dpn * ca[j] * r * (1.f - r);
-        const float dpz = dz * z * (1.f - z);
-        carry[j] = dh * z;
-        dxk[j][0] = dpr; dxk[j][1] = dpz; dxk[j][2] = dpn;
-        eg[j][0] = dpr; eg[j][1] = dpz; eg[j][2] = dpn * r;
-        bsh[j][0] += dpr; bsh[j][1] += dpz; bsh[j][2] += dpn * r;
+        const float dc = dh * og * (1.f - tc * tc) + carry;
+        eg[0] = dc * gg * ig * (1.f - ig);
+        eg[1] = dc * cap * fg * (1.f - fg);
+        eg[2] = dc * ig * (1.f - gg * gg);
+        eg[3] = dO * og * (1.f - og);
+        carry = dc * fg;
       } else {
-        const float der = MODE == kRelu ? (cap[j] > 0.f ? 1.f : 0.f) : (1.f - cap[j] * cap[j]);
-        eg[j][0] = dh * der;
+        dh += carry;
+        const float r = cg[0], z = cg[1], nn = cg[2];
+        const float dn = dh * (1.f - z), dz = dh * (cap - nn);
+        const float dpn = dn * (1.f - nn * nn);
+        const float dpr = dpn * ca * r * (1.f - r);
+        const float dpz = dz * z * (1.f - z);
+        carry = dh * z;
+        dxk[0] = dpr; dxk[1] = dpz; dxk[2] = dpn;
+        eg[0] = dpr; eg[1] = dpz; eg[2] = dpn * r;
+        bsh[0] += dpr; bsh[1] += dpz; bsh[2] += dpn * r;
       }
+      float m = 0.f;
 #pragma unroll
       for (int q = 0; q < NW; q++) {
-        Ads[(long)n * K4 + q * U + u] = eg[j][q];
-        bsx[j][q] += (MODE == kGru) ? dxk[j][q] : eg[j][q];
+        bsx[q] += (MODE == kGru) ? dxk[q] : eg[q];
+        m = fmaxf(m, fabsf(eg[q]));
       }
+      const int se = split_exp(wave_max16(m, U));
+#pragma unroll
+      for (int q = 0; q < NW; q++) {
+        _Float16 h, l;
+        split16(ldexpf(eg[q], se), h, l);
+        Ahi[en * AP + q * U + eu] = h;
+        Alo[en * AP + q * U + eu] = l;
+      }
+      if (eu == 0) rowexp[en] = se + sB;
     }
     __syncthreads();
+    REC_TRACE(ks, 3);
     if (k > 0) {  // partial dh of all units for the next step
-      floatx4 acc[RT][8];
+      floatx4 acc[CTW];
 #pragma unroll
-      for (int rt = 0; rt < RT; rt++)
+      for (int c = 0; c < CTW; c++) acc[c] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int c = 0; c < 8; c++) acc[rt][c] = floatx4{0.f, 0.f, 0.f, 0.f};
-      for (int kq = 0; kq < KQ; kq++) {
-        floatx4 a[RT], b[8];
+      for (int kb = 0; kb < KB; kb++) {
+        const halfx8 ah = *reinterpret_cast<const halfx8 *>(Ahi + fr * AP + kb * 32 + fq * 8);
+        const halfx8 al = *reinterpret_cast<const halfx8 *>(Alo + fr * AP + kb * 32 + fq * 8);
 #pragma unroll
-        for (int rt = 0; rt < RT; rt++) a[rt] = ld4(Ads + (long)(rt * 16 + fr) * K4 + kq * 16 + fq * 4);
+        for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bhi[c][kb], acc[c], 0, 0, 0);
 #pragma unroll
-        for (int c = 0; c < 8; c++)
-          if (c < CTW) b[c] = ld4(Rk + (long)((w * CTW + c) * 16 + fr) * K4 + kq * 16 + fq * 4);
+        for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, blo[c][kb], acc[c], 0, 0, 0);
 #pragma unroll
-        for (int s = 0; s < 4; s++)
-#pragma unroll
-          for (int c = 0; c < 8; c++)
-            if (c < CTW)
-#pragma unroll
-              for (int rt = 0; rt < RT; rt++)
-                acc[rt][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rt][s], b[c][s], acc[rt][c], 0, 0, 0);
+        for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bhi[c][kb], acc[c], 0, 0, 0);
       }
+      int ex[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) ex[i] = -rowexp[fq * 4 + i];
       const auto ro = rsrc(p.xch + (long)ks * xstep, (unsigned)(xstep * 4));
-      const long obase = (long)(d * nwg + g) * prod_stride;
+      const long obase = (long)(d * NWG + g) * PSTR;
 #pragma unroll
-      for (int c = 0; c < 8; c++)
-        if (c < CTW)
+      for (int c = 0; c < CTW; c++) {
+        floatx4 o;
 #pragma unroll
-          for (int rt = 0; rt < RT; rt++)
-            publish4(ro, (unsigned)((obase + (((long)(w * CTW + c) * RT + rt) * 64 + lane) * 4) * 4), acc[rt][c]);
-      REC_TRACE_W(ks, 10);
+        for (int i = 0; i < 4; i++) o[i] = ldexpf(acc[c][i], ex[i]);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ro,
+                                               (int)((obase + ((long)(w * CTW + c) * 64 + lane) * 4) * 4), 0, 16);
+      }
     }
     signal_epoch(myflag, (unsigned)(ks + 2), 0);
     REC_TRACE(ks, 4);
@@ -1464,26 +1500,22 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec5(RecParams p) {
     REC_TRACE(ks, 5);
   }
   if (t_prev >= 0 && !bad) e_store(t_prev);
-  // bias partial sums: reduce over n in a fixed order (Rk region is free now)
-  float *bs = Rk;  // [2][N][U][NW]
+  // bias partial sums: reduce over n in a fixed order through LDS
+  float *bs = red;  // [2][16][U][NW] floats
   __syncthreads();
-#pragma unroll
-  for (int j = 0; j < kMaxEPT; j++) {
-    const int e = tid + j * NT;
-    if (e >= items) continue;
-    const int n = e / U, u = e - n * U;
+  if (has_e) {
 #pragma unroll
     for (int q = 0; q < NW; q++) {
-      const long b0 = ((long)n * U + u) * NW + q;
-      bs[b0] = bsx[j][q];
-      bs[(long)N * U * NW + b0] = (MODE == kGru) ? bsh[j][q] : bsx[j][q];
+      const long b0 = ((long)en * U + eu) * NW + q;
+      bs[b0] = live ? bsx[q] : 0.f;
+      bs[(long)16 * U * NW + b0] = live ? ((MODE == kGru) ? bsh[q] : bsx[q]) : 0.f;
     }
   }
   __syncthreads();
   for (int q = tid; q < 2 * NW * U; q += NT) {
     const int part = q / (NW * U), rem = q - part * NW * U, gt = rem / U, u = rem - gt * U;
     float s2 = 0.f;
-    for (int n = 0; n < N; n++) s2 += bs[(long)part * N * U * NW + ((long)n * U + u) * NW + gt];
+    for (int n = 0; n < N; n++) s2 += bs[(long)part * 16 * U * NW + ((long)n * U + u) * NW + gt];
     p.bias[((long)d * 2 + part) * NW * H + gt * H + u0 + u] = s2;
   }
   if (bad && tid == 0) atomicOr(p.err, 1u);
@@ -1499,11 +1531,6 @@ static void set_lds(F f, size_t bytes) {
 
 template <int MODE, int RT>
 static void launch_one(bool fwd, const RecParams &p, dim3 grid, size_t lds, hipStream_t s, int ver) {
-  if (ver == 5) {
-    set_lds(rnn_bwd_rec5<MODE, RT>, lds);
-    hipLaunchKernelGGL((rnn_bwd_rec5<MODE, RT>), grid, dim3(NT), lds, s, p);
-    return;
-  }
   if (ver == 4) {
     if (fwd) {
       set_lds(rnn_fwd_rec4<MODE, RT>, lds);
@@ -1529,6 +1556,28 @@ static void launch_mode(bool fwd, const RecParams &p, dim3 grid, size_t lds, hip
     case 2: launch_one<MODE, 2>(fwd, p, grid, lds, s, ver); break;
     case 3: launch_one<MODE, 3>(fwd, p, grid, lds, s, ver); break;
     default: launch_one<MODE, 4>(fwd, p, grid, lds, s, ver); break;
+  }
+}
+template <int MODE, int U, int CTW>
+static void launch6_one(const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
+  set_lds(rnn_bwd_rec6<MODE, U, CTW>, lds);
+  hipLaunchKernelGGL((rnn_bwd_rec6<MODE, U, CTW>), grid, dim3(NT), lds, s, p);
+}
+template <int MODE, int U>
+static void launch6_u(const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
+  switch (p.H / 64) {
+    case 4: launch6_one<MODE, U, 4>(p, grid, lds, s); break;
+    case 5: launch6_one<MODE, U, 5>(p, grid, lds, s); break;
+    default: launch6_one<MODE, U, 8>(p, grid, lds, s); break;
+  }
+}
+static void launch_rec6(int mode, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
+  if (mode == kLstm) {
+    if (p.U == 16) launch6_u<kLstm, 16>(p, grid, lds, s);
+    else launch6_u<kLstm, 8>(p, grid, lds, s);
+  } else {
+    if (p.U == 16) launch6_u<kGru, 16>(p, grid, lds, s);
+    else launch6_u<kGru, 8>(p, grid, lds, s);
   }
 }
 static void launch_rec(bool fwd, int mode, const RecParams &p, dim3 grid, size_t lds, hipStream_t s,
@@ -1647,21 +1696,20 @@ static int pick_bwd_u4(const RnnDesc &d, int N) {
   return 0;
 }
 
-// v5 backward (reduce-scatter): U in {16, 8}, H % 64 == 0, Npad in {16, 32, 64}
-static size_t bwd5_lds_bytes(const RnnDesc &d, int N, int U) {
-  const int K = d.nw() * U, Kp = (K + 15) / 16 * 16, K4 = Kp + 4;
-  const int Npad = (N + 15) / 16 * 16;
-  return sizeof(float) * ((size_t)d.H * K4 + (size_t)Npad * K4 + 256 * 4);
+// v6 backward (reduce-scatter, split-fp16 MFMA): LSTM/GRU, N <= 16,
+// H in {256, 320, 512}, U in {16, 8}
+static size_t bwd6_lds_bytes(const RnnDesc &d, int U) {
+  const int K = d.nw() * U, KB = (K + 31) / 32, AP = KB * 32 + 8;
+  const size_t img = 2 * 16 * (size_t)AP * 2;
+  const size_t red = sizeof(float) * std::max((size_t)NT * 4, (size_t)2 * 16 * U * d.nw());
+  // at least 96 KB so that no other workgroup (a side-stream GEMM block)
+  // shares the CU with a recurrence workgroup
+  return std::max(img + red, (size_t)96 * 1024);
 }
-static int pick_bwd_u5(const RnnDesc &d, int N) {
-  if (env_int("KCTC_BWD_REC", 4) != 5 || rec_version() != 4 || d.dirs > 8 || d.H % 64) return 0;
-  const int Npad = (N + 15) / 16 * 16;
-  if (Npad != 16 && Npad != 32 && Npad != 64) return 0;
-  auto ok = [&](int U) {
-    if (!v4_xpd(d, U) || N * U > kMaxEPT * NT || (Npad / 16) * 4 * U > NT) return false;
-    if ((long)2 * N * U * d.nw() > (long)d.H * (d.nw() * U + 4)) return false;  // bias scratch in Rk
-    return bwd5_lds_bytes(d, N, U) <= 160 * 1024;
-  };
+static int pick_bwd_u6(const RnnDesc &d, int N) {
+  if (env_int("KCTC_BWD_REC", 6) != 6 || rec_version() != 4) return 0;
+  if ((d.mode != kLstm && d.mode != kGru) || N > 16 || (d.H != 256 && d.H != 320 && d.H != 512)) return 0;
+  auto ok = [&](int U) { return d.H % U == 0 && (long)d.dirs * (d.H / U) <= 256 && (d.H / U) % (NT / (4 * U)) == 0; };
   const int want = env_int("KCTC_BWD_U", 0);
   if (want) return ok(want) ? want : 0;
   for (int U : {16, 8})
@@ -1669,7 +1717,7 @@ static int pick_bwd_u5(const RnnDesc &d, int N) {
   return 0;
 }
 
-// Per-device exchange pool of the v5 backward: one step image per time step,
+// Per-device exchange pool of the v6 backward: one step image per time step,
 // never reused within a launch (T x dirs x nwg x H x Npad floats, 4.2 GB for
 // BLSTM-512 N=16 T=2000).  Library-owned so that the components of a network
 // share it; launches on one device are ordered through its event.
@@ -1805,10 +1853,10 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
   if (T <= 0 || N <= 0 || N > 16 * kMaxRT || d.H % 16) return KRNN_NOT_SUPPORTED;
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
   if (res_bytes < sizeof(float) * (size_t)lay.total) return KRNN_BAD_PARAM;
-  const int U5 = pick_bwd_u5(d, N);
-  const int U4 = U5 ? 0 : pick_bwd_u4(d, N);
-  const int ver = U5 ? 5 : U4 ? 4 : 3;
-  const int U = U5 ? U5 : U4 ? U4 : pick_bwd_u(d, N);
+  const int U6 = pick_bwd_u6(d, N);
+  const int U4 = U6 ? 0 : pick_bwd_u4(d, N);
+  const int ver = U6 ? 6 : U4 ? 4 : 3;
+  const int U = U6 ? U6 : U4 ? U4 : pick_bwd_u(d, N);
   if (!U) return KRNN_NOT_SUPPORTED;
   const int NW = d.nw(), H = d.H, dirs = d.dirs;
   const long TN = (long)T * N;
@@ -1836,22 +1884,23 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, 4096, s));
-    const size_t lds = ver == 5 ? bwd5_lds_bytes(d, N, U) : bwd_lds_bytes(d, N, U, ver);
-    p.xpd = ver >= 4 ? v4_xpd(d, U) : 1;
-    if (ver == 5)
-      p.xch = xch_acquire(sizeof(float) * (size_t)T * dirs * p.nwg * H * p.Npad, s);
+    const size_t lds = ver == 6 ? bwd6_lds_bytes(d, U) : bwd_lds_bytes(d, N, U, ver);
+    p.xpd = ver == 4 ? v4_xpd(d, U) : 1;
+    if (ver == 6)
+      p.xch = xch_acquire(sizeof(float) * (size_t)T * dirs * p.nwg * 16 * H, s);
     else
       p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
-    const dim3 grid(ver >= 4 ? 8 * ceil_div(p.nwg, p.xpd) : dirs * p.nwg);
+    const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : dirs * p.nwg);
     RecTrace tr;
     if (tr.arm("bwd", grid.x)) p.trace = tr.dev;
     {
       ProfSpan ps(s, "rnn_bwd_rec");
-      launch_rec(false, d.mode, p, grid, lds, s, ver);
+      if (ver == 6) launch_rec6(d.mode, p, grid, lds, s);
+      else launch_rec(false, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
-    if (ver == 5) xch_release(s);
-    tr.dump("bwd", s, grid.x, p.nwg, T, dirs, ver, p.xpd);
+    if (ver == 6) xch_release(s);
+    tr.dump("bwd", s, grid.x, p.nwg, T, dirs, ver, ver == 6 ? 0 : p.xpd);
     // dx_l = sum_dir DX_dir W_dir   (lower layer's dy, or the caller's dx)
     float *dxl = (l == 0) ? dx : res + lay.per_layer * (l - 1) + lay.dout;
     if (dxl) {

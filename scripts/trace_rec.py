@@ -14,7 +14,9 @@ def main(path):
     tr = np.frombuffer(raw[32:], dtype=np.uint64).reshape(steps, grid, 16).astype(np.int64)
     steps = min(steps, T)
     tr = tr[:steps]
-    if ver >= 4:
+    if xpd == 0:  # v6: block b -> (dir b % dirs, g b / dirs)
+        members = [[b for b in range(grid) if b % dirs == d and b // dirs < nwg] for d in range(dirs)]
+    elif ver >= 4:
         members = [[b for b in range(grid) if (b % 8) // xpd == d and (b // 8) * xpd + (b % 8) % xpd < nwg]
                    for d in range(dirs)]
     else:
