@@ -1521,6 +1521,212 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
   if (bad && tid == 0) atomicOr(p.err, 1u);
 }
 
+// ---------------------------------------------------------------------------
+// v6 forward: split-fp16 MFMA over an fp16 hi/lo all-gather of h
+// ---------------------------------------------------------------------------
+// WG (dir, g) owns units u0..u0+U-1; per step it multiplies h_{t-1} [16 x H]
+// by its R slice (the nW*U gate rows of its units) on
+// v_mfma_f32_16x16x32_f16 with the split-fp16 products of the v6 backward
+// (R scaled per WG, h scaled by 2^14: |h| <= 1 for LSTM / GRU), K split over
+// the 4 waves and reduced through LDS in a fixed order, then does the cell
+// update of its (n, unit) elements and publishes h_t as the fp16 hi/lo pair
+// of its units.  The exchange image of a step is A-fragment-major:
+// [dir][kb = k/32][hi|lo][16 rows][32 k] halves (1 KB per fragment), the same
+// 64 KB per step as the fp32 image of v4; a consumer lane loads 16 B of hi
+// and 16 B of lo per 32-k block.  The R slice lives in registers (B
+// fragments) for the whole launch.  Hand-off as v4 (sc1 stores, vmcnt(0),
+// barrier, sc1 epoch flag; sc1 loads).
+template <int MODE, int U, int H>
+__global__ __launch_bounds__(NT, 1) void rnn_fwd_rec6(RecParams p) {
+  constexpr int NW = MODE == kLstm ? 4 : 3;
+  constexpr int NC = NW * U, CT = (NC + 15) / 16, RP = CT * 16 + 1;  // red row pitch (floats)
+  constexpr int KB = H / 32, KBW = (KB + 3) / 4, NWG = H / U;
+  constexpr int CH = U / 8;  // 16-B chunks of a published row
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ int bad_lds;
+  __shared__ float wmax[4];
+  const int d = blockIdx.x % p.dirs, g = blockIdx.x / p.dirs;
+  if (g >= NWG) return;
+  const int N = p.N, T = p.T;
+  const int u0 = g * U;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  const long ldy = (long)p.dirs * H, ldg = (long)p.dirs * NW * H;
+  constexpr long XS = 2L * KB * 2 * 16 * 32;  // halves per step image (dirs <= 2)
+  float *red = smem;                                                     // [4][16][RP]
+  _Float16 *stg = reinterpret_cast<_Float16 *>(smem + 4 * 16 * RP + 3);  // [2][16][U], 16-B aligned below
+  stg = reinterpret_cast<_Float16 *>((reinterpret_cast<uintptr_t>(stg) + 15) & ~uintptr_t(15));
+  const float *Wd = p.w + d * p.pl_stride;
+  const float *R = Wd + p.r_off;
+  _Float16 *xch = reinterpret_cast<_Float16 *>(p.xch);
+  if (tid == 0) bad_lds = 0;
+  // ---- R slice -> scaled hi/lo B fragments: B[k][c] = R[q*H + u0 + u][k], c = q*U + u ----
+  auto rrow = [&](int c) -> const float * {
+    const int q = c / U, u = c - q * U;
+    return R + (long)(q * H + u0 + u) * H;
+  };
+  float mx = 0.f;
+#pragma unroll
+  for (int ct = 0; ct < CT; ct++) {
+    const int c = ct * 16 + fr;
+    if (c < NC) {
+      const float *rr = rrow(c);
+#pragma unroll
+      for (int i = 0; i < KBW; i++) {
+        const int kb = w + 4 * i;
+        if (kb < KB) {
+#pragma unroll
+          for (int j = 0; j < 8; j++) mx = fmaxf(mx, fabsf(rr[kb * 32 + fq * 8 + j]));
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if (lane == 0) wmax[w] = mx;
+  __syncthreads();
+  const int sB = split_exp(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3])));
+  const int sOut = -(sB + 14);
+  halfx8 bhi[CT][KBW], blo[CT][KBW];
+#pragma unroll
+  for (int ct = 0; ct < CT; ct++) {
+    const int c = ct * 16 + fr;
+#pragma unroll
+    for (int i = 0; i < KBW; i++) {
+      const int kb = w + 4 * i;
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const float v = (c < NC && kb < KB) ? rrow(c)[kb * 32 + fq * 8 + j] : 0.f;
+        _Float16 h, l;
+        split16(ldexpf(v, sB), h, l);
+        bhi[ct][i][j] = h;
+        blo[ct][i][j] = l;
+      }
+    }
+  }
+  // ---- per-element state: thread tid <-> (n = tid / U, u = tid % U) ----
+  const bool has_e = tid < 16 * U;
+  const int en = tid / U, eu = tid - en * U;
+  const bool live = has_e && en < N;
+  float cst = 0.f, hpv = 0.f, cnew = 0.f, hval = 0.f;
+  float gin[NW], gnx[NW], bR[NW], act[NW];
+#pragma unroll
+  for (int q = 0; q < NW; q++) {
+    gin[q] = gnx[q] = act[q] = 0.f;
+    bR[q] = (MODE == kGru && has_e) ? Wd[p.bR_off + q * H + u0 + eu] : 0.f;
+  }
+  auto gin_load = [&](int t, float (&dst)[NW]) {
+    if (!live) return;
+#pragma unroll
+    for (int q = 0; q < NW; q++) dst[q] = p.G[((long)t * N + en) * ldg + (long)d * NW * H + q * H + u0 + eu];
+  };
+  auto out_store = [&](int t) {  // row-major y, activations (in place of G), aux of step t
+    if (!live) return;
+    p.y[((long)t * N + en) * ldy + (long)d * H + u0 + eu] = hval;
+    const long grow = ((long)t * N + en) * ldg + (long)d * NW * H + u0 + eu;
+#pragma unroll
+    for (int q = 0; q < NW; q++) p.G[grow + q * H] = act[q];
+    p.aux[((long)t * N + en) * ldy + (long)d * H + u0 + eu] = cnew;
+  };
+  gin_load(d == 0 ? 0 : T - 1, gin);
+  int bad = 0;
+  unsigned *myflag = p.flags + d * NWG + g;
+  // publish geometry: store thread s < 32 * CH: part = s / (16 CH), row, chunk
+  const int sp = tid / (16 * CH), sn = (tid / CH) % 16, sch = tid % CH;
+  const int kb0 = u0 >> 5, koff = (u0 & 31) + sch * 8;
+  int t_prev = -1;
+  for (int k = 0; k < T && !bad; k++) {
+    const int t = d == 0 ? k : T - 1 - k, tp = d == 0 ? t - 1 : t + 1;
+    floatx4 acc[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ct++) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+    REC_TRACE(k, 0);
+    if (k > 0) {
+      wait_flags(p.flags + d * NWG, NWG, (unsigned)(k + 1), p.err, bad, &bad_lds);
+      REC_TRACE(k, 1);
+      const auto rs = rsrc(xch + (long)tp * XS, (unsigned)(XS * 2));
+      u32x4 ah[KBW], al[KBW];
+#pragma unroll
+      for (int i = 0; i < KBW; i++) {
+        const int kb = w + 4 * i;
+        if (kb < KB) {
+          const long o = ((((long)d * KB + kb) * 2) * 16 + fr) * 32 + fq * 8;
+          ah[i] = ld_sc1(rs, (unsigned)(o * 2));
+          al[i] = ld_sc1(rs, (unsigned)((o + 16 * 32) * 2));
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < KBW; i++) {
+        if (w + 4 * i < KB) {
+          const halfx8 a0 = __builtin_bit_cast(halfx8, ah[i]), a1 = __builtin_bit_cast(halfx8, al[i]);
+#pragma unroll
+          for (int ct = 0; ct < CT; ct++) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bhi[ct][i], acc[ct], 0, 0, 0);
+#pragma unroll
+          for (int ct = 0; ct < CT; ct++) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, blo[ct][i], acc[ct], 0, 0, 0);
+#pragma unroll
+          for (int ct = 0; ct < CT; ct++) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bhi[ct][i], acc[ct], 0, 0, 0);
+        }
+      }
+    }
+    asm volatile("" ::: "memory");
+    // behind the hand-off loads: last step's row-major outputs, next step's input projection
+    if (t_prev >= 0) out_store(t_prev);
+    if (k + 1 < T) gin_load(d == 0 ? t + 1 : t - 1, gnx);
+#pragma unroll
+    for (int ct = 0; ct < CT; ct++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) red[(w * 16 + fq * 4 + i) * RP + ct * 16 + fr] = acc[ct][i];
+    __syncthreads();
+    REC_TRACE(k, 3);
+    if (has_e) {
+      float rh[NW];
+#pragma unroll
+      for (int q = 0; q < NW; q++) {
+        const int c = q * U + eu;
+        rh[q] = ldexpf(((red[(0 * 16 + en) * RP + c] + red[(1 * 16 + en) * RP + c]) + red[(2 * 16 + en) * RP + c]) +
+                           red[(3 * 16 + en) * RP + c],
+                       sOut);
+      }
+      float h;
+      if (MODE == kLstm) {
+        act[0] = fsigm(gin[0] + rh[0]);
+        act[1] = fsigm(gin[1] + rh[1]);
+        act[2] = ftanh(gin[2] + rh[2]);
+        act[3] = fsigm(gin[3] + rh[3]);
+        cst = act[1] * cst + act[0] * act[2];
+        cnew = cst;
+        h = act[3] * ftanh(cst);
+      } else {
+        act[0] = fsigm(gin[0] + rh[0] + bR[0]);
+        act[1] = fsigm(gin[1] + rh[1] + bR[1]);
+        cnew = rh[2] + bR[2];
+        act[2] = ftanh(gin[2] + act[0] * cnew);
+        h = (1.f - act[1]) * act[2] + act[1] * hpv;
+        hpv = h;
+      }
+      if (!live) h = 0.f;
+      hval = h;
+      _Float16 hh, hl;
+      split16(h * 16384.f, hh, hl);
+      stg[en * U + eu] = hh;
+      stg[(16 + en) * U + eu] = hl;
+    }
+    __syncthreads();
+    if (tid < 32 * CH) {
+      const u32x4 v = *reinterpret_cast<const u32x4 *>(stg + (sp * 16 + sn) * U + sch * 8);
+      const long o = ((((long)d * KB + kb0) * 2 + sp) * 16 + sn) * 32 + koff;
+      __builtin_amdgcn_raw_buffer_store_b128(v, rsrc(xch + (long)t * XS, (unsigned)(XS * 2)), (int)(o * 2), 0, 16);
+    }
+    signal_epoch(myflag, (unsigned)(k + 2), 0);
+    REC_TRACE(k, 4);
+#pragma unroll
+    for (int q = 0; q < NW; q++) gin[q] = gnx[q];
+    t_prev = t;
+    REC_TRACE(k, 5);
+  }
+  if (t_prev >= 0 && !bad) out_store(t_prev);
+  if (bad && tid == 0) atomicOr(p.err, 1u);
+}
+
 template <typename F>
 static void set_lds(F f, size_t bytes) {
   static size_t done[8] = {0};
@@ -1578,6 +1784,26 @@ static void launch_rec6(int mode, const RecParams &p, dim3 grid, size_t lds, hip
   } else {
     if (p.U == 16) launch6_u<kGru, 16>(p, grid, lds, s);
     else launch6_u<kGru, 8>(p, grid, lds, s);
+  }
+}
+template <int MODE, int U>
+static void launchf6_u(const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
+  switch (p.H) {
+    case 256: set_lds(rnn_fwd_rec6<MODE, U, 256>, lds);
+      hipLaunchKernelGGL((rnn_fwd_rec6<MODE, U, 256>), grid, dim3(NT), lds, s, p); break;
+    case 320: set_lds(rnn_fwd_rec6<MODE, U, 320>, lds);
+      hipLaunchKernelGGL((rnn_fwd_rec6<MODE, U, 320>), grid, dim3(NT), lds, s, p); break;
+    default: set_lds(rnn_fwd_rec6<MODE, U, 512>, lds);
+      hipLaunchKernelGGL((rnn_fwd_rec6<MODE, U, 512>), grid, dim3(NT), lds, s, p); break;
+  }
+}
+static void launch_fwd6(int mode, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
+  if (mode == kLstm) {
+    if (p.U == 16) launchf6_u<kLstm, 16>(p, grid, lds, s);
+    else launchf6_u<kLstm, 8>(p, grid, lds, s);
+  } else {
+    if (p.U == 16) launchf6_u<kGru, 16>(p, grid, lds, s);
+    else launchf6_u<kGru, 8>(p, grid, lds, s);
   }
 }
 static void launch_rec(bool fwd, int mode, const RecParams &p, dim3 grid, size_t lds, hipStream_t s,
@@ -1696,6 +1922,25 @@ static int pick_bwd_u4(const RnnDesc &d, int N) {
   return 0;
 }
 
+// v6 forward (split-fp16 MFMA, fp16 hi/lo h all-gather): LSTM/GRU, N <= 16,
+// H in {256, 320, 512}, U in {8, 16}
+static size_t fwd6_lds_bytes(const RnnDesc &d, int U) {
+  const int CT = (d.nw() * U + 15) / 16;
+  const size_t b = sizeof(float) * (4 * 16 * (size_t)(CT * 16 + 1) + 8) + 2 * 16 * (size_t)U * 2;
+  return std::max(b, (size_t)96 * 1024);  // one recurrence workgroup per CU
+}
+static int pick_fwd_u6(const RnnDesc &d, int N) {
+  if (env_int("KCTC_FWD_REC", 6) != 6 || rec_version() != 4) return 0;
+  if ((d.mode != kLstm && d.mode != kGru) || N > 16 || (d.H != 256 && d.H != 320 && d.H != 512)) return 0;
+  auto ok = [&](int U) { return d.H % U == 0 && (long)d.dirs * (d.H / U) <= 256; };
+  const int want = env_int("KCTC_FWD_U", 0);
+  if (want) return ok(want) ? want : 0;
+  // measured on BLSTM-512 N=16: U=16 34.2 ms/step of forward recurrence, U=8 37.1
+  for (int U : {16, 8})
+    if (ok(U)) return U;
+  return 0;
+}
+
 // v6 backward (reduce-scatter, split-fp16 MFMA): LSTM/GRU, N <= 16,
 // H in {256, 320, 512}, U in {16, 8}
 static size_t bwd6_lds_bytes(const RnnDesc &d, int U) {
@@ -1786,9 +2031,10 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
   if (res_bytes < sizeof(float) * (size_t)lay.total) return KRNN_BAD_PARAM;
   if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
-  const int U4 = pick_fwd_u4(d, N);
-  const int ver = U4 ? 4 : 3;
-  const int U = U4 ? U4 : pick_fwd_u(d, N);
+  const int U6 = pick_fwd_u6(d, N);
+  const int U4 = U6 ? 0 : pick_fwd_u4(d, N);
+  const int ver = U6 ? 6 : U4 ? 4 : 3;
+  const int U = U6 ? U6 : U4 ? U4 : pick_fwd_u(d, N);
   if (!U) return KRNN_NOT_SUPPORTED;
   const int NW = d.nw(), H = d.H, dirs = d.dirs;
   const long TN = (long)T * N;
@@ -1827,7 +2073,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.allow_local = env_int("KCTC_LOCAL", 0);
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, 4096, s));
-    const size_t lds = fwd_lds_bytes(d, N, U);
+    const size_t lds = ver == 6 ? fwd6_lds_bytes(d, U) : fwd_lds_bytes(d, N, U);
     p.xpd = ver == 4 ? v4_xpd(d, U) : 1;
     p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
     const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : dirs * p.nwg);
@@ -1835,10 +2081,11 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     if (tr.arm("fwd", grid.x)) p.trace = tr.dev;
     {
       ProfSpan ps(s, "rnn_fwd_rec");
-      launch_rec(true, d.mode, p, grid, lds, s, ver);
+      if (ver == 6) launch_fwd6(d.mode, p, grid, lds, s);
+      else launch_rec(true, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
-    tr.dump("fwd", s, grid.x, p.nwg, T, dirs, ver, p.xpd);
+    tr.dump("fwd", s, grid.x, p.nwg, T, dirs, ver, ver == 6 ? 0 : p.xpd);
     in = out;
   }
   return KRNN_OK;

@@ -49,6 +49,11 @@ CASES = [
     (1, 15, 4, 12, 32, 1, True),     # TANH
     (2, 9, 40, 32, 64, 1, True),     # N > 16: several MFMA row tiles
     (2, 40, 16, 256, 512, 1, True),  # BLSTM-512 width (U=8 / U=16 partitions)
+    # v6 (split-fp16 MFMA) shapes: H in {256, 320, 512}, N <= 16, LSTM and GRU
+    (3, 21, 7, 64, 256, 1, True),    # GRU H=256, padded rows
+    (2, 16, 5, 48, 320, 1, False),   # uni LSTM H=320 (the recipe's cell dim)
+    (3, 12, 16, 40, 512, 2, True),   # stacked BGRU-512
+    (2, 30, 1, 40, 256, 1, True),    # a single utterance
 ]
 
 
