@@ -4,14 +4,15 @@
 //
 // Three launches per call, all stream-ordered:
 //   K1 ctc_logz        one wave per frame row: logZ[t,n] = logsumexp_a act[t,n,a]
-//                      (fully parallel, HBM-bound: 4*A B read per row).
+//                      and lp[t,n,a] = act - logZ (fully parallel, HBM-bound:
+//                      4*A B read + 4*A B written per row).
 //   K2 ctc_alpha_beta  one 256-thread workgroup per (utterance, direction):
 //                      log-space alpha (forward) or beta (backward) recursion,
 //                      serial over T with ONE workgroup barrier per frame.  The
 //                      extended (blank-interleaved) label sequence lives in
 //                      registers, the previous frame's column in double-buffered
-//                      LDS, the emission log-probs are prefetched PD frames ahead
-//                      into registers.  Each frame is renormalised by the max of
+//                      LDS, the emission log-probs (normalised by K1) are
+//                      gathered into LDS a chunk of frames ahead by LDS-DMA.  Each frame is renormalised by the max of
 //                      the previous column (wave max via DPP/shfl, then LDS) and
 //                      the running offset is kept in fp64, so exp(alpha+beta-logp)
 //                      keeps ~1e-7 relative accuracy at T=2000 (plain fp32 log
@@ -21,6 +22,7 @@
 //                      gamma_t(k) = sum_{s: l'_s = k} exp(a~+b~+off), then
 //                      grad = softmax - gamma; padding / infeasible rows get 0.
 //                      Deterministic (fixed summation order, no atomics).
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -32,9 +34,10 @@ namespace kctc {
 namespace ctcimpl {
 
 constexpr int kMaxLabel = 639;  // MAX_WARPCTC_LABEL_LENGTH, src/ctc/ctc-nnet-train.cc:25-26
-constexpr int kThreads = 256;
-constexpr int kSPT = (2 * kMaxLabel + 1 + kThreads - 1) / kThreads;  // states per thread (5)
-constexpr int kPD = 8;   // emission prefetch depth (frames)
+constexpr int kThreads = 256;  // K3
+constexpr int kABThreads = 512;  // K2: 8 waves, 2 per SIMD, <= 3 states per thread
+constexpr int kABWaves = kABThreads / 64;
+constexpr int kSPT = (2 * kMaxLabel + 1 + kABThreads - 1) / kABThreads;  // states per thread (3)
 constexpr int kFR = 8;   // frames per K3 workgroup
 
 struct UttDesc {
@@ -44,7 +47,7 @@ struct UttDesc {
 };
 
 struct Layout {
-  size_t desc, labels, costs, logz, spill, offs, total;
+  size_t desc, labels, costs, logz, lp, spill, offs, total;
   int T_max;
   long long spill_floats, off_doubles;
 };
@@ -76,6 +79,7 @@ static bool make_layout(const int *label_lengths, const int *input_lengths, int 
   l.labels = p; p = align_up(p + sizeof(int) * (nlab > 0 ? nlab : 1), 256);
   l.costs = p;  p = align_up(p + sizeof(double) * N, 256);
   l.logz = p;   p = align_up(p + sizeof(float) * (size_t)T_max * N + 4, 256);
+  l.lp = p;     p = align_up(p + sizeof(float) * (size_t)T_max * N * A + 4, 256);
   l.spill = p;  p = align_up(p + sizeof(float) * (size_t)spill, 256);
   l.offs = p;   p = align_up(p + sizeof(double) * (size_t)offs, 256);
   l.total = p;
@@ -89,7 +93,7 @@ static bool make_layout(const int *label_lengths, const int *input_lengths, int 
 // K1: per-frame log normaliser.  One wave per row, 4 rows per workgroup.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void ctc_logz(const float *__restrict__ acts, int A, long rows,
-                                                float *__restrict__ logz) {
+                                                float *__restrict__ logz, float *__restrict__ lp) {
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -100,33 +104,66 @@ __global__ __launch_bounds__(256) void ctc_logz(const float *__restrict__ acts, 
   float s = 0.f;
   for (int a = lane; a < A; a += kWave) s += expf(r[a] - m);
   s = wave_sum(s);
-  if (lane == 0) logz[row] = m + logf(s);
+  const float z = m + logf(s);
+  if (lane == 0) logz[row] = z;
+  for (int a = lane; a < A; a += kWave) lp[row * A + a] = r[a] - z;  // normalised log-probs (K2 input)
 }
 
 // log(e^a + e^b + e^c) as max + log1p(sum of the two smaller terms): the
 // dominant term contributes exactly 1, so log1p keeps full relative precision
-// of the small ones (logf(1 + x) would round x to the ulp of 1).
+// of the small ones (logf(1 + x) would round x to the ulp of 1).  log1p(x) is
+// evaluated as log(u) * x / (u - 1) with u = fl(1 + x) (the rounding of u
+// cancels to first order), on the hardware v_log_f32 / v_exp_f32.
+__device__ __forceinline__ float fast_log1p(float x) {
+  const float u = 1.f + x;
+  if (u == 1.f) return x;
+  return __logf(u) * __fdividef(x, u - 1.f);
+}
 __device__ __forceinline__ float lse3(float a, float b, float c) {
   const float m = fmaxf(a, fmaxf(b, c));
   if (m == -INFINITY) return -INFINITY;
   const float lo = fminf(a, fminf(b, c));
   const float md = fmaxf(fminf(a, b), fminf(fmaxf(a, b), c));  // median, exact
-  return m + log1pf(expf(md - m) + expf(lo - m));
+  return m + fast_log1p(__expf(md - m) + __expf(lo - m));
 }
 
 // ---------------------------------------------------------------------------
 // K2: alpha (blockIdx.x < N) and beta (blockIdx.x >= N) recursions.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads) void ctc_alpha_beta(
-    const float *__restrict__ acts, const float *__restrict__ logz, int N, int A, int blank,
-    UttDesc *__restrict__ descs, const int *__restrict__ labels, float *__restrict__ spill,
-    double *__restrict__ offs, double *__restrict__ costs, int write_spill) {
+// The emission log-probs lp[t, n, l'_s] of the next chunk of F frames are
+// gathered into LDS by LDS-DMA (global_load_lds, one 4-byte gather per lane
+// and state block) while the current chunk is processed, so the serial frame
+// loop itself issues no global load: per frame it reads LDS, computes, spills
+// its column and meets ONE raw s_barrier (lgkmcnt only -- a __syncthreads()
+// would drain the in-flight DMA).  The chunk's DMA is waited for once, at the
+// chunk boundary.  All LDS is one dynamic array (a second __shared__ object
+// makes hipcc wait vmcnt(0) before LDS reads while a DMA is in flight):
+//   emit[2][F][SP] | col[2][CP] | wmax[2][8] | feasible flag
+struct AbLds {
+  int F, SP, CP;
+  __device__ __host__ size_t floats() const { return 2 * (size_t)F * SP + 2 * (size_t)CP + 2 * kABWaves + 4; }
+};
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <bool SPILL>
+__global__ __launch_bounds__(kABThreads) void ctc_alpha_beta(
+    const float *__restrict__ lp, int N, int A, int blank, UttDesc *__restrict__ descs,
+    const int *__restrict__ labels, float *__restrict__ spill, double *__restrict__ offs,
+    double *__restrict__ costs, AbLds lay) {
   const bool is_beta = blockIdx.x >= (unsigned)N;
   const int n = is_beta ? blockIdx.x - N : blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  __shared__ float col[2][2 * kMaxLabel + 4];
-  __shared__ float wmax[2][kThreads / kWave];
-  __shared__ int sh_feasible;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int F = lay.F, SP = lay.SP, CP = lay.CP;
+  float *emit = lds;                       // [2][F][SP]
+  float *colb = emit + 2 * (size_t)F * SP;  // [2][CP]
+  float *wmax = colb + 2 * CP;             // [2][kABWaves]
+  int *sh_feasible = reinterpret_cast<int *>(wmax + 2 * kABWaves);
 
   UttDesc d = descs[n];
   const int T = d.T, L = d.L, S = d.S;
@@ -134,137 +171,137 @@ __global__ __launch_bounds__(kThreads) void ctc_alpha_beta(
   if (tid == 0) {
     int rep = 0;
     for (int i = 1; i < L; i++) rep += (lab[i] == lab[i - 1]);
-    sh_feasible = (T > 0 && L + rep <= T);
+    *sh_feasible = (T > 0 && L + rep <= T);
   }
   __syncthreads();
-  const int feasible = sh_feasible;
+  const int feasible = *sh_feasible;
   if (!is_beta && tid == 0) {
     descs[n].feasible = feasible;
     if (!feasible) costs[n] = 0.0;
   }
   if (!feasible) return;
 
-  // extended label of each owned state, and its skip permission
+  // extended label of each owned state s = tid + 256 i, and its skip permission
   int ext[kSPT];
   bool skip[kSPT];
 #pragma unroll
   for (int i = 0; i < kSPT; i++) {
-    int s = tid + i * kThreads;
+    int s = tid + i * kABThreads;
     ext[i] = (s < S) ? ((s & 1) ? lab[(s - 1) >> 1] : blank) : blank;
     skip[i] = false;
     if (s < S && (s & 1)) {
       if (!is_beta) skip[i] = (s >= 2) && (lab[(s - 1) >> 1] != lab[(s - 3) >> 1]);
       else skip[i] = (s + 2 < S) && (lab[(s + 1) >> 1] != lab[(s - 1) >> 1]);
-    } else if (s < S && is_beta) {
-      skip[i] = false;  // blank -> blank+2 is never a skip target (l'_{s+2} is blank)
     }
   }
   // beta: transition s -> s+2 allowed iff l'_{s+2} != blank and != l'_s; for
   // odd s that is lab[(s+1)/2] != lab[(s-1)/2]; for even s, l'_{s+2} is blank.
 
-  const float *arow = acts + (long)n * A;        // + t*N*A
-  const float *zrow = logz + n;                  // + t*N
   const long tstride = (long)N * A;
+  const float *lrow = lp + (long)n * A;  // + t * N * A
   float *sp = spill + d.ab_off + (is_beta ? (long long)T * S : 0);
   double *op = offs + d.off_off + (is_beta ? T : 0);
-
-  // emission prefetch ring: pf[k][i] = act[t_k, n, ext_i], pz[k] = logZ[t_k, n]
-  float pf[kPD][kSPT];
-  float pz[kPD];
   auto tframe = [&](int k) { return is_beta ? T - 1 - k : k; };  // k-th processed frame
+  const int nblk = (S + 63) / 64;  // 64-state blocks; wave w gathers blocks w, w + 8, ...
+  auto issue = [&](int c, int b) {
+    float *dst = emit + (size_t)b * F * SP;
+    for (int f = 0; f < F; f++) {
+      const int k = c * F + f;
+      if (k >= T) break;
+      const float *src = lrow + (long)tframe(k) * tstride;
 #pragma unroll
-  for (int k = 0; k < kPD; k++) {
-    if (k < T) {
-      int t = tframe(k);
-#pragma unroll
-      for (int i = 0; i < kSPT; i++) pf[k][i] = arow[t * tstride + ext[i]];
-      pz[k] = zrow[(long)t * N];
+      for (int i = 0; i < kSPT; i++) {
+        const int sb = wid + kABWaves * i;
+        if (sb < nblk) __builtin_amdgcn_global_load_lds(src + ext[i], dst + (size_t)f * SP + sb * 64, 4, 0, 0);
+      }
     }
-  }
+  };
 
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
   double off = 0.0;
   int cur = 0;
-  for (int k0 = 0; k0 < T; k0 += kPD) {
+  const int nchunk = (T + F - 1) / F;
+  for (int c = 0; c < nchunk; c++) {
+    if (c + 1 < nchunk) issue(c + 1, (c + 1) & 1);
+    const float *em = emit + (size_t)(c & 1) * F * SP;
+    const int fend = min(F, T - c * F);
+    for (int f = 0; f < fend; f++) {
+      const int k = c * F + f;
+      const int t = tframe(k);
+      float ly[kSPT];
 #pragma unroll
-    for (int kk = 0; kk < kPD; kk++) {
-      const int k = k0 + kk;
-      if (k < T) {
-        const int t = tframe(k);
-        float ly[kSPT];
+      for (int i = 0; i < kSPT; i++) ly[i] = (tid + i * kABThreads < S) ? em[(size_t)f * SP + tid + i * kABThreads] : 0.f;
+      float *cc = colb + cur * CP;
+      float lmax = -INFINITY;
+      if (k == 0) {
+        // init: alpha_0(0)=ly(blank), alpha_0(1)=ly(l1); beta_{T-1}(S-1)=beta(S-2)=0,
+        // stored as q = beta + ly (the next step's input)
 #pragma unroll
-        for (int i = 0; i < kSPT; i++) ly[i] = pf[kk][i] - pz[kk];
-        // issue the prefetch for frame k + PD into the slot just consumed
-        if (k + kPD < T) {
-          int tn = tframe(k + kPD);
-#pragma unroll
-          for (int i = 0; i < kSPT; i++) pf[kk][i] = arow[tn * tstride + ext[i]];
-          pz[kk] = zrow[(long)tn * N];
+        for (int i = 0; i < kSPT; i++) {
+          int s = tid + i * kABThreads;
+          if (s < S) {
+            float v;
+            if (!is_beta) v = (s <= 1) ? ly[i] : -INFINITY;
+            else v = (s >= S - 2) ? 0.f : -INFINITY;
+            if (SPILL) sp[(long)t * S + s] = v;
+            float q = is_beta ? v + ly[i] : v;
+            cc[s] = q;
+            lmax = fmaxf(lmax, q);
+          }
         }
-        float lmax = -INFINITY;
-        if (k == 0) {
-          // init: alpha_0(0)=ly(blank), alpha_0(1)=ly(l1); beta_{T-1}(S-1)=beta(S-2)=0,
-          // stored as q = beta + ly (the next step's input)
+      } else {
+        const float *wm = wmax + (cur ^ 1) * kABWaves;
+        float mu = wm[0];
 #pragma unroll
-          for (int i = 0; i < kSPT; i++) {
-            int s = tid + i * kThreads;
-            if (s < S) {
-              float v;
-              if (!is_beta) v = (s <= 1) ? ly[i] : -INFINITY;
-              else v = (s >= S - 2) ? 0.f : -INFINITY;
-              if (write_spill) sp[(long)t * S + s] = v;
-              float q = is_beta ? v + ly[i] : v;
-              col[cur][s] = q;
+        for (int w = 1; w < kABWaves; w++) mu = fmaxf(mu, wm[w]);
+        const float *pv = colb + (cur ^ 1) * CP;
+#pragma unroll
+        for (int i = 0; i < kSPT; i++) {
+          int s = tid + i * kABThreads;
+          if (s < S) {
+            float v;
+            if (!is_beta) {
+              float a = pv[s];
+              float b = s >= 1 ? pv[s - 1] : -INFINITY;
+              float c2 = skip[i] ? pv[s - 2] : -INFINITY;
+              v = lse3(a - mu, b - mu, c2 - mu);
+              v = (v == -INFINITY) ? v : v + ly[i];
+              if (SPILL) sp[(long)t * S + s] = v;
+              cc[s] = v;
+              lmax = fmaxf(lmax, v);
+            } else {
+              float a = pv[s];
+              float b = s + 1 < S ? pv[s + 1] : -INFINITY;
+              float c2 = skip[i] ? pv[s + 2] : -INFINITY;
+              v = lse3(a - mu, b - mu, c2 - mu);
+              if (SPILL) sp[(long)t * S + s] = v;
+              float q = (v == -INFINITY) ? v : v + ly[i];
+              cc[s] = q;
               lmax = fmaxf(lmax, q);
             }
           }
-        } else {
-          float mu = wmax[cur ^ 1][0];
-#pragma unroll
-          for (int w = 1; w < kThreads / kWave; w++) mu = fmaxf(mu, wmax[cur ^ 1][w]);
-          const float *pv = col[cur ^ 1];
-#pragma unroll
-          for (int i = 0; i < kSPT; i++) {
-            int s = tid + i * kThreads;
-            if (s < S) {
-              float v;
-              if (!is_beta) {
-                float a = pv[s];
-                float b = s >= 1 ? pv[s - 1] : -INFINITY;
-                float c = skip[i] ? pv[s - 2] : -INFINITY;
-                v = lse3(a - mu, b - mu, c - mu);
-                v = (v == -INFINITY) ? v : v + ly[i];
-                if (write_spill) sp[(long)t * S + s] = v;
-                col[cur][s] = v;
-                lmax = fmaxf(lmax, v);
-              } else {
-                float a = pv[s];
-                float b = s + 1 < S ? pv[s + 1] : -INFINITY;
-                float c = skip[i] ? pv[s + 2] : -INFINITY;
-                v = lse3(a - mu, b - mu, c - mu);
-                if (write_spill) sp[(long)t * S + s] = v;
-                float q = (v == -INFINITY) ? v : v + ly[i];
-                col[cur][s] = q;
-                lmax = fmaxf(lmax, q);
-              }
-            }
-          }
-          off += (double)mu;
         }
-        lmax = wave_max(lmax);
-        if (lane == 0) wmax[cur][wid] = lmax;
-        if (tid == 0 && write_spill) op[t] = off;
-        __syncthreads();
-        cur ^= 1;
+        off += (double)mu;
       }
+      lmax = wave_max_l63(lmax);
+      if (lane == 63) wmax[cur * kABWaves + wid] = lmax;
+      if (tid == 0 && SPILL) op[t] = off;
+      lds_barrier();
+      cur ^= 1;
     }
+    // the next chunk's gathers have landed; every wave is done with this chunk's buffer
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
   }
   if (!is_beta && tid == 0) {
     // log p = O_{T-1} + lse(alpha~_{T-1}(S-1), alpha~_{T-1}(S-2))
-    const float *pv = col[cur ^ 1];
+    const float *pv = colb + (cur ^ 1) * CP;
     float a = pv[S - 1], b = S > 1 ? pv[S - 2] : -INFINITY;
     float m = fmaxf(a, b);
-    double lp = off + (double)m + log((double)expf(a - m) + (double)expf(b - m));
-    costs[n] = -lp;
+    double lpv = off + (double)m + log((double)expf(a - m) + (double)expf(b - m));
+    costs[n] = -lpv;
   }
 }
 
@@ -417,16 +454,34 @@ static ctcStatus_t launch(const float *acts, float *grads, const int *flat_label
   float *d_spill = reinterpret_cast<float *>(ws + lay.spill);
   double *d_offs = reinterpret_cast<double *>(ws + lay.offs);
   const long rows = (long)lay.T_max * N;
+  float *d_lp = reinterpret_cast<float *>(ws + lay.lp);
   if (rows > 0) {
     ProfSpan ps(stream, "ctc_logz");
     hipLaunchKernelGGL(ctc_logz, dim3(ceil_div(rows, 4)), dim3(256), 0, stream, acts, A, rows,
-                       d_logz);
+                       d_logz, d_lp);
   }
   const int want = grads != nullptr;
   {
-  ProfSpan ps(stream, "ctc_alpha_beta");
-  hipLaunchKernelGGL(ctc_alpha_beta, dim3(want ? 2 * N : N), dim3(kThreads), 0, stream, acts,
-                     d_logz, N, A, blank, d_desc, d_lab, d_spill, d_offs, costs_dev, want);
+    int Smax = 1;
+    for (int n = 0; n < N; n++) Smax = 2 * label_lengths[n] + 1 > Smax ? 2 * label_lengths[n] + 1 : Smax;
+    AbLds al;
+    al.SP = (Smax + 63) / 64 * 64;
+    al.CP = (Smax + 4 + 3) / 4 * 4;
+    // chunk depth: as many frames as fit 96 KB of double-buffered emissions (4..32)
+    al.F = (int)std::min<size_t>(32, std::max<size_t>(4, (size_t)96 * 1024 / (2 * sizeof(float) * al.SP)));
+    const size_t shm = sizeof(float) * al.floats();
+    if (shm > 160 * 1024) return CTC_STATUS_INVALID_VALUE;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(ctc_alpha_beta<true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(ctc_alpha_beta<false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    ProfSpan ps(stream, "ctc_alpha_beta");
+    if (want)
+      hipLaunchKernelGGL(ctc_alpha_beta<true>, dim3(2 * N), dim3(kABThreads), shm, stream, d_lp, N, A, blank,
+                         d_desc, d_lab, d_spill, d_offs, costs_dev, al);
+    else
+      hipLaunchKernelGGL(ctc_alpha_beta<false>, dim3(N), dim3(kABThreads), shm, stream, d_lp, N, A, blank,
+                         d_desc, d_lab, d_spill, d_offs, costs_dev, al);
   }
   if (want && lay.T_max > 0) {
     int Lmax = 0;

@@ -36,6 +36,21 @@ void gemm_f32(hipStream_t stream, const GemmArgs &g);
 // Heuristic split-K so that tiles * split fill the chip; returns 1 if not needed.
 int gemm_pick_split(int M, int N, int K, int batch);
 
+// Split-fp16 ("x3") GEMM, same contract as gemm_f32 (fp32-class results, see
+// gemm.hip).  Operand scaling: per A row (M index) / per B column (N index)
+// max |x| as float bits (absmax_f32), or, when the array is null, a constant
+// bound on |x| (e.g. 1 for an LSTM/GRU output).
+struct X3Scales {
+  const unsigned *amaxA = nullptr, *amaxB = nullptr;
+  long strideA = 0, strideB = 0;  // per batch
+  float boundA = 1.f, boundB = 1.f;
+};
+void gemm_x3(hipStream_t stream, const GemmArgs &g, const X3Scales &s);
+int split_exp_host(float bound);
+// max |X| per row (rmax[b][r]) and per column (cmax[b][c]) as float bits; either may be null
+void absmax_f32(hipStream_t stream, const float *X, long ldx, int rows, int cols, unsigned *rmax, unsigned *cmax,
+                int batch = 1, long strideX = 0, long strideR = 0, long strideC = 0);
+
 // column sums: out[b][j] (+)= alpha * sum_i X[b][i*ldx + j], i < rows  (accumulate if beta=1)
 void colsum_f32(hipStream_t stream, const float *X, long ldx, int rows, int cols, float alpha,
                 float beta, float *out, int batch = 1, long strideX = 0, long strideOut = 0);

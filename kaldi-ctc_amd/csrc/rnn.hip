@@ -1270,11 +1270,7 @@ typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ float wave_max16(float v, int width) {
   // max over groups of `width` (8 or 16) consecutive lanes
-  v = fmaxf(v, __shfl_xor(v, 1));
-  v = fmaxf(v, __shfl_xor(v, 2));
-  v = fmaxf(v, __shfl_xor(v, 4));
-  if (width > 8) v = fmaxf(v, __shfl_xor(v, 8));
-  return v;
+  return width > 8 ? group_max16(v) : group_max8(v);
 }
 
 // exponent s with max * 2^s in [2^13, 2^14) (s = 14 for max == 0)
