@@ -240,6 +240,19 @@ def add_mat_mat(C, A, B, transA=False, transB=False, alpha=1.0, beta=0.0, stream
         raise KctcError(f"kcm_add_mat_mat failed ({st})")
 
 
+def add_mat_mat_x3(C, A, B, transA=False, transB=False, alpha=1.0, beta=0.0, stream=None):
+    """add_mat_mat on the split-fp16 matrix-core path (kcm_add_mat_mat_x3)."""
+    import torch
+    M, N = C.shape
+    K = A.shape[0] if transA else A.shape[1]
+    ws = torch.empty(M + N, dtype=torch.int32, device=C.device)
+    st = lib().kcm_add_mat_mat_x3(_stream_handle(stream), int(transA), int(transB), M, N, K, alpha,
+                                  _ptr(A), A.stride(0), _ptr(B), B.stride(0), beta, _ptr(C), C.stride(0),
+                                  _ptr(ws))
+    if st != 0:
+        raise KctcError(f"kcm_add_mat_mat_x3 failed ({st})")
+
+
 # ---------------------------------------------------------------------------
 # nnet2 trainer (include/kaldi_ctc_train.h)
 # ---------------------------------------------------------------------------

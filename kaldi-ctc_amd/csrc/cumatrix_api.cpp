@@ -23,6 +23,31 @@ int kcm_add_mat_mat(struct ihipStream_t *stream, int transA, int transB, int M, 
   }
 }
 
+int kcm_add_mat_mat_x3(struct ihipStream_t *stream, int transA, int transB, int M, int N, int K,
+                       float alpha, const float *A, long lda, const float *B, long ldb, float beta,
+                       float *C, long ldc, unsigned *ws) {
+  if (M < 0 || N < 0 || K < 0 || !C || !ws) return 1;
+  try {
+    kctc::GemmArgs g;
+    g.transA = transA != 0; g.transB = transB != 0;
+    g.M = M; g.N = N; g.K = K; g.alpha = alpha; g.beta = beta;
+    g.A = A; g.lda = lda; g.B = B; g.ldb = ldb; g.C = C; g.ldc = ldc;
+    kctc::X3Scales s;
+    s.amaxA = ws;
+    s.amaxB = ws + M;
+    // op(A) rows: rows of A (row-major M x K) or columns of A^T (K x M)
+    if (!transA) kctc::absmax_f32(stream, A, lda, M, K, ws, nullptr);
+    else kctc::absmax_f32(stream, A, lda, K, M, nullptr, ws);
+    // op(B) columns: columns of B (K x N) or rows of B^T (N x K)
+    if (!transB) kctc::absmax_f32(stream, B, ldb, K, N, nullptr, ws + M);
+    else kctc::absmax_f32(stream, B, ldb, N, K, ws + M, nullptr);
+    kctc::gemm_x3(stream, g, s);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+  } catch (...) {
+    return 3;
+  }
+}
+
 int kcm_find_row_max_id(struct ihipStream_t *stream, const float *m, long rows, int cols, int *ids) {
   if (!m || !ids || cols <= 0) return 1;
   kctc::row_argmax(stream, m, rows, cols, ids);

@@ -33,6 +33,7 @@
 // nnet-cudnn-component.cc:327-413 (see RnnDesc::lin_offset).
 #include <algorithm>
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <mutex>
 #include <string>
@@ -106,7 +107,49 @@ static size_t xch_bytes(const RnnDesc &d, int T, int N) {
   const long Npad = (N + 15) / 16 * 16;
   return sizeof(float) * (size_t)T * d.dirs * d.nw() * d.H * Npad;
 }
-size_t rnn_workspace_bytes(const RnnDesc &d, int T, int N) { return xch_offset(d, T, N) + xch_bytes(d, T, N); }
+// then the split-fp16 GEMM scales (per stacked layer): max |x| of the GEMM
+// operands' rows / columns (float bits), see X3Lay
+struct X3Lay {
+  long rin, wrow, wcol, dxr, dxc, ec, xcol, yc, per_layer;
+};
+static X3Lay x3_layout(const RnnDesc &d, int T, int N) {
+  X3Lay x;
+  const long TN = (long)T * N, G = (long)d.dirs * d.nw() * d.H, Dm = std::max(d.D, d.dirs * d.H);
+  long p = 0;
+  x.rin = p;  p += al64(TN);               // rows of the layer input
+  x.wrow = p; p += al64(G);                // rows of W (gate rows), per direction
+  x.wcol = p; p += al64((long)d.dirs * Dm);  // columns of W (input dims), per direction
+  x.dxr = p;  p += al64((long)d.dirs * TN);  // rows of dGates (frames), per direction
+  x.dxc = p;  p += al64(G);                // columns of dGates (input part)
+  x.ec = p;   p += al64(G);                // columns of dGates (recurrent part; GRU)
+  x.xcol = p; p += al64(Dm);               // columns of the layer input
+  x.yc = p;   p += al64((long)d.dirs * d.H);  // columns of the layer output
+  x.per_layer = p;
+  return x;
+}
+static size_t x3_offset(const RnnDesc &d, int T, int N) { return align_up(xch_offset(d, T, N) + xch_bytes(d, T, N), 256); }
+size_t rnn_workspace_bytes(const RnnDesc &d, int T, int N) {
+  return x3_offset(d, T, N) + sizeof(unsigned) * (size_t)x3_layout(d, T, N).per_layer * d.layers;
+}
+static unsigned *x3_base(void *ws, const RnnDesc &d, int T, int N, int l) {
+  return reinterpret_cast<unsigned *>(static_cast<char *>(ws) + x3_offset(d, T, N)) +
+         (long)x3_layout(d, T, N).per_layer * l;
+}
+// The RNN GEMMs run on the split-fp16 matrix-core path unless KCTC_GEMM=f32
+// (or the contraction is too short to pay for the scale pass).
+static bool use_x3(int K) {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("KCTC_GEMM");
+    v = (e && !strcmp(e, "f32")) ? 0 : 1;
+  }
+  return v && K >= 128;
+}
+static void absmax_span(hipStream_t s, const float *X, long ldx, int rows, int cols, unsigned *rmax, unsigned *cmax,
+                        int batch = 1, long strideX = 0, long strideR = 0, long strideC = 0) {
+  ProfSpan ps(s, "x3_scales");
+  absmax_f32(s, X, ldx, rows, cols, rmax, cmax, batch, strideX, strideR, strideC);
+}
 
 namespace {
 
@@ -2056,7 +2099,22 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     g.bias = wl + bW;
     g.bias2 = (d.mode == kGru) ? nullptr : wl + bR;
     g.batch = dirs; g.strideA = 0; g.strideB = pls; g.strideC = (long)NW * H; g.strideBias = pls;
-    {
+    if (use_x3(Din)) {
+      unsigned *x3 = x3_base(workspace, d, T, N, l);
+      const X3Lay xl = x3_layout(d, T, N);
+      X3Scales sc;
+      // the layer input: a lower stacked layer's LSTM/GRU/TANH output is in
+      // [-1, 1]; the component input (layer 0) and RELU outputs get row maxima
+      if (l == 0 || d.mode == kRelu) {
+        absmax_span(s, in, Din, (int)TN, Din, x3 + xl.rin, nullptr);
+        sc.amaxA = x3 + xl.rin;
+      }
+      absmax_span(s, wl, Din, NW * H, Din, x3 + xl.wrow, nullptr, dirs, pls, (long)NW * H);
+      sc.amaxB = x3 + xl.wrow;
+      sc.strideB = (long)NW * H;
+      ProfSpan ps(s, "gemm_fwd_proj");
+      gemm_x3(s, g, sc);
+    } else {
       ProfSpan ps(s, "gemm_fwd_proj");
       gemm_f32(s, g);
     }
@@ -2146,7 +2204,21 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     tr.dump("bwd", s, grid.x, p.nwg, T, dirs, ver, ver == 6 ? 0 : p.xpd);
     // dx_l = sum_dir DX_dir W_dir   (lower layer's dy, or the caller's dx)
     float *dxl = (l == 0) ? dx : res + lay.per_layer * (l - 1) + lay.dout;
+    const bool x3 = use_x3(NW * H);
+    unsigned *x3b = x3_base(workspace, d, T, N, l);
+    const X3Lay xl = x3_layout(d, T, N);
+    if (x3) {
+      // scales of dGates for this GEMM (frame rows) and for the weight
+      // GEMMs on the side stream (gate columns; GRU: also the recurrent part E)
+      const long G4 = (long)NW * H;
+      absmax_span(s, DX, (long)dirs * G4, (int)TN, (int)G4, dxl ? x3b + xl.dxr : nullptr, x3b + xl.dxc, dirs, G4,
+                  TN, G4);
+      if (d.mode == kGru) absmax_span(s, E, (long)dirs * G4, (int)TN, (int)G4, nullptr, x3b + xl.ec, dirs, G4, 0, G4);
+    }
     if (dxl) {
+      if (x3)
+        for (int dir = 0; dir < dirs; dir++)
+          absmax_span(s, wl + dir * pls, Din, NW * H, Din, nullptr, x3b + xl.wcol + (long)dir * Din);
       for (int dir = 0; dir < dirs; dir++) {
         GemmArgs g;
         g.transA = false; g.transB = false;
@@ -2156,7 +2228,14 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
         g.C = dxl; g.ldc = Din;
         g.beta = dir == 0 ? 0.f : 1.f;
         ProfSpan ps(s, "gemm_bwd_data");
-        gemm_f32(s, g);
+        if (x3) {
+          X3Scales sc;
+          sc.amaxA = x3b + xl.dxr + (long)dir * TN;
+          sc.amaxB = x3b + xl.wcol + (long)dir * Din;
+          gemm_x3(s, g, sc);
+        } else {
+          gemm_f32(s, g);
+        }
       }
     }
     dcur = dxl;
@@ -2202,7 +2281,20 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     // recurrences of this layer, which use the other flag words, are done)
     unsigned *fl = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     if (max_blocks > 0) g.tile_counter = reinterpret_cast<int *>(fl + 1008);
-    {
+    const bool x3 = use_x3((int)TN) && Din >= 64;
+    unsigned *x3b = x3_base(workspace, d, T, N, l);
+    const X3Lay xl = x3_layout(d, T, N);
+    if (x3) {
+      X3Scales sc;
+      sc.amaxA = x3b + xl.dxc;  // dGates columns (from rnn_backward_data)
+      sc.strideA = G4;
+      if (l == 0 || d.mode == kRelu) {
+        absmax_span(s, in, Din, (int)TN, Din, nullptr, x3b + xl.xcol);
+        sc.amaxB = x3b + xl.xcol;
+      }
+      ProfSpan ps(s, "gemm_bwd_w");
+      gemm_x3(s, g, sc);
+    } else {
       ProfSpan ps(s, "gemm_bwd_w");
       gemm_f32(s, g);
     }
@@ -2223,8 +2315,21 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       r.ws = ws;
       r.max_blocks = max_blocks;
       if (max_blocks > 0) r.tile_counter = reinterpret_cast<int *>(fl + 1009);
-      ProfSpan ps(s, "gemm_bwd_r");
-      gemm_f32(s, r);
+      if (x3) {
+        X3Scales sc;
+        sc.amaxA = x3b + (d.mode == kGru ? xl.ec : xl.dxc);
+        sc.strideA = G4;
+        if (d.mode == kRelu) {
+          absmax_span(s, out, ldy, (int)TN, (int)ldy, nullptr, x3b + xl.yc);
+          sc.amaxB = x3b + xl.yc;
+          sc.strideB = H;
+        }
+        ProfSpan ps(s, "gemm_bwd_r");
+        gemm_x3(s, r, sc);
+      } else {
+        ProfSpan ps(s, "gemm_bwd_r");
+        gemm_f32(s, r);
+      }
     }
     // biases: dbW += sum dGx, dbR += sum dGh (partials from the recurrence)
     const long bW = d.lin_offset(l * dirs, 0, true) - pl0;

@@ -166,3 +166,30 @@ def test_gemm_matches_numpy(kctc, gpu, ta, tb, M, N, K):
     torch.cuda.synchronize()
     ref = 0.5 * ((A.T if ta else A).astype(np.float64) @ (B.T if tb else B).astype(np.float64)) - 1.5 * C0
     assert rel_err(C.cpu().numpy(), ref) < 1e-6
+
+
+@pytest.mark.parametrize("ta,tb,M,N,K", [(0, 0, 77, 41, 40), (0, 1, 300, 130, 257), (1, 0, 64, 96, 1000),
+                                         (1, 1, 33, 17, 9), (0, 1, 1024, 1024, 1024), (1, 0, 512, 256, 4000)])
+def test_gemm_x3_matches_numpy(kctc, gpu, ta, tb, M, N, K):
+    """Split-fp16 GEMM: fp32-class accuracy, also for rows / columns whose
+    magnitudes differ by many orders (per-row / per-column power-of-two scaling)."""
+    import torch
+    rng = np.random.default_rng(M * 7 + N + K)
+    A = rng.standard_normal((K, M) if ta else (M, K)).astype(np.float32)
+    B = rng.standard_normal((N, K) if tb else (K, N)).astype(np.float32)
+    # op(A) rows and op(B) columns spanning 1e-12 .. 1e6
+    ra = (10.0 ** rng.uniform(-12, 6, M)).astype(np.float32)
+    cb = (10.0 ** rng.uniform(-12, 6, N)).astype(np.float32)
+    A = A * (ra[None, :] if ta else ra[:, None])
+    B = B * (cb[:, None] if tb else cb[None, :])
+    C0 = rng.standard_normal((M, N)).astype(np.float32)
+    C = torch.from_numpy(C0).to(gpu)
+    kctc.add_mat_mat_x3(C, torch.from_numpy(A).to(gpu), torch.from_numpy(B).to(gpu), bool(ta), bool(tb),
+                        alpha=0.5, beta=0.0)
+    torch.cuda.synchronize()
+    ref = 0.5 * ((A.T if ta else A).astype(np.float64) @ (B.T if tb else B).astype(np.float64))
+    out = C.cpu().numpy().astype(np.float64)
+    # element-wise, relative to the scale of the row of op(A) times the column of op(B)
+    scale = np.abs(A.T if ta else A).max(axis=1)[:, None] * np.abs(B.T if tb else B).max(axis=0)[None, :] * K
+    assert np.max(np.abs(out - ref) / scale) < 2e-7
+    assert rel_err(out, ref) < 1e-6
