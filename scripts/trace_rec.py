@@ -33,8 +33,11 @@ def main(path):
     ok = (r > 0) & (m > 0)
     if ok.any():
         print(f"  shader clock (s_memtime / s_memrealtime) ~{np.median(m[ok] / r[ok]) / 1e9:.2f} GHz")
-    for i, nm in enumerate(names):
-        d = (tr[sl, :, i + 1] - tr[sl, :, i]) * us
+    stamps = [i for i in range(6) if tr[sl, :, i].min() > 0]  # phases this kernel records
+    pnames = {0: "start", 1: "flags", 2: "loads", 3: "reduced", 4: "published", 5: "end"}
+    for a, b in zip(stamps[:-1], stamps[1:]):
+        d = (tr[sl, :, b] - tr[sl, :, a]) * us
+        nm = f"{pnames[a]}->{pnames[b]}"
         print(f"  {nm:22s} median {np.median(d):7.3f}  p90 {np.percentile(d, 90):7.3f}")
     if ver >= 4 and tr[sl, :, 6].min() > 0:
         for w in range(4):
