@@ -102,7 +102,10 @@ static size_t flags_offset(const RnnDesc &d, int T, int N) {
 }
 // then the v4 exchange images (one layer at a time; forward and backward of a
 // layer never overlap): T * dirs * max(H, nW*H) * Npad floats
-static size_t xch_offset(const RnnDesc &d, int T, int N) { return flags_offset(d, T, N) + 4096; }
+// flag region: words 0..1023 (v3/v4 flags, placement ids, GEMM tile counters
+// at 1008/1009), then one 128-B line per (direction, workgroup) for v6
+constexpr size_t kFlagBytes = 4096 + 2 * 64 * 128;
+static size_t xch_offset(const RnnDesc &d, int T, int N) { return flags_offset(d, T, N) + kFlagBytes; }
 static size_t xch_bytes(const RnnDesc &d, int T, int N) {
   const long Npad = (N + 15) / 16 * 16;
   return sizeof(float) * (size_t)T * d.dirs * d.nw() * d.H * Npad;
@@ -1316,6 +1319,54 @@ __device__ __forceinline__ float wave_max16(float v, int width) {
   return width > 8 ? group_max16(v) : group_max8(v);
 }
 
+// v6 flag words: one 128-B line per (direction, workgroup), so that the
+// producers' flag stores and the consumers' polls spread over L2 / memory
+// channels instead of hammering one line.
+constexpr int kFlagStride = 32;  // words
+__device__ __forceinline__ unsigned *flag6(const RecParams &p, int d, int g, int nwg) {
+  return p.flags + 1024 + ((long)d * nwg + g) * kFlagStride;
+}
+__device__ __forceinline__ void wait_flags6(const unsigned *f0, int nwg, unsigned epoch, unsigned *err, int &bad,
+                                            int *bad_lds) {
+  if (threadIdx.x < 64) {
+    int spins = 0;
+    while (true) {
+      bool ok = true;
+      for (int i = threadIdx.x; i < nwg; i += 64)
+        ok &= __hip_atomic_load(f0 + (long)i * kFlagStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= epoch;
+      if (__all(ok)) break;
+      if (++spins > kSpinLimit ||
+          ((spins & 255) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        bad = 1;
+        if (threadIdx.x == 0) *bad_lds = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  if (*bad_lds) bad = 1;
+}
+// Placement probe of a v6 launch in XCD-slot mapping: 1 iff every workgroup of
+// direction d reads the same HW_REG_XCC_ID (then the hand-off may stay in that
+// XCD's L2: plain payload and flag stores, sc1 loads).  Publishes epoch 1.
+__device__ int probe6(const RecParams &p, int d, int g, int nwg, int &bad, int *bad_lds, int *loc_lds) {
+  unsigned *ids = p.flags + 512 + d * nwg;
+  const unsigned me = xcc_id() + 1u;
+  if (threadIdx.x == 0) __hip_atomic_store(ids + g, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  signal_epoch(flag6(p, d, g, nwg), 1u, 0);
+  wait_flags6(flag6(p, d, 0, nwg), nwg, 1u, p.err, bad, bad_lds);
+  if (threadIdx.x < 64) {
+    bool ok = true;
+    for (int i = threadIdx.x; i < nwg; i += 64)
+      ok &= __hip_atomic_load(ids + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == me;
+    const bool all = __all(ok);
+    if (threadIdx.x == 0) *loc_lds = all ? 1 : 0;
+  }
+  __syncthreads();
+  return *loc_lds;
+}
+
 // exponent s with max * 2^s in [2^13, 2^14) (s = 14 for max == 0)
 __device__ __forceinline__ int split_exp(float mx) {
   int e = 0;
@@ -1338,16 +1389,22 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
   constexpr int PER = NWG / NGRP;  // producers summed per group
   static_assert(NWG % NGRP == 0, "producer groups");
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ int bad_lds;
+  __shared__ int bad_lds, loc_lds;
   __shared__ int rowexp[16];
   __shared__ float wmax[4];
-  const int d = blockIdx.x % p.dirs, g = blockIdx.x / p.dirs;
-  if (g >= NWG) return;
+  // xpd = 1: XCD-slot mapping (block b -> direction b & 7, so a direction's 32
+  // workgroups share one XCD under round-robin dispatch; checked by probe6);
+  // else block b -> direction b % dirs
+  const int d = p.xpd ? (blockIdx.x & 7) : blockIdx.x % p.dirs;
+  const int g = p.xpd ? (blockIdx.x >> 3) : blockIdx.x / p.dirs;
+  if (d >= p.dirs || g >= NWG) return;
   const int N = p.N, T = p.T;
   const int u0 = g * U, ct_own = u0 >> 4, fr0 = u0 & 15;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
   const long ldy = (long)p.dirs * H, ldg = (long)p.dirs * NW * H;
-  constexpr long PSTR = (long)CTT * 64 * 4;   // floats per producer block (16 x H)
+  // floats per producer block (16 x H) + 256 B, so that the 1-KB chunks a
+  // consumer reads from consecutive producers fall in different L2 channels
+  constexpr long PSTR = (long)CTT * 64 * 4 + 64;
   const long xstep = (long)p.dirs * NWG * PSTR;
   _Float16 *Ahi = reinterpret_cast<_Float16 *>(smem);  // [16][AP]
   _Float16 *Alo = Ahi + 16 * AP;
@@ -1432,14 +1489,16 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
   prefetch(T - 1);
   rotate();
   int bad = 0;
-  unsigned *myflag = p.flags + d * NWG + g;
+  unsigned *myflag = flag6(p, d, g, NWG);
+  if (tid == 0) loc_lds = 0;
+  const int local = (p.xpd && p.allow_local) ? probe6(p, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
   int t_prev = -1;
   for (int k = T - 1; k >= 0 && !bad; k--) {
     const int t = d == 0 ? k : T - 1 - k;
     const int ks = T - 1 - k;  // steps done before this one
     REC_TRACE(ks, 0);
     if (ks > 0) {
-      wait_flags(p.flags + d * NWG, NWG, (unsigned)(ks + 1), p.err, bad, &bad_lds);
+      wait_flags6(flag6(p, d, 0, NWG), NWG, (unsigned)(ks + 1), p.err, bad, &bad_lds);
       REC_TRACE(ks, 1);
       const auto rs = rsrc(p.xch + (long)(ks - 1) * xstep, (unsigned)(xstep * 4));
       u32x4 v[PER];
@@ -1528,11 +1587,14 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
         floatx4 o;
 #pragma unroll
         for (int i = 0; i < 4; i++) o[i] = ldexpf(acc[c][i], ex[i]);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ro,
-                                               (int)((obase + ((long)(w * CTW + c) * 64 + lane) * 4) * 4), 0, 16);
+        const int off = (int)((obase + ((long)(w * CTW + c) * 64 + lane) * 4) * 4);
+        // write-through (sc1) payload in either mode: the stored lines leave
+        // the XCD's L2, so the consumers' sc1 loads read them from the
+        // Infinity Cache; only the flag stays in the shared L2 when local
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ro, off, 0, 16);
       }
     }
-    signal_epoch(myflag, (unsigned)(ks + 2), 0);
+    signal_epoch(myflag, (unsigned)(ks + 2), local);
     REC_TRACE(ks, 4);
     rotate();
     t_prev = t;
@@ -1668,7 +1730,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec6(RecParams p) {
   };
   gin_load(d == 0 ? 0 : T - 1, gin);
   int bad = 0;
-  unsigned *myflag = p.flags + d * NWG + g;
+  unsigned *myflag = flag6(p, d, g, NWG);
   // publish geometry: store thread s < 32 * CH: part = s / (16 CH), row, chunk
   const int sp = tid / (16 * CH), sn = (tid / CH) % 16, sch = tid % CH;
   const int kb0 = u0 >> 5, koff = (u0 & 31) + sch * 8;
@@ -1680,7 +1742,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec6(RecParams p) {
     for (int ct = 0; ct < CT; ct++) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
     REC_TRACE(k, 0);
     if (k > 0) {
-      wait_flags(p.flags + d * NWG, NWG, (unsigned)(k + 1), p.err, bad, &bad_lds);
+      wait_flags6(flag6(p, d, 0, NWG), NWG, (unsigned)(k + 1), p.err, bad, &bad_lds);
       REC_TRACE(k, 1);
       const auto rs = rsrc(xch + (long)tp * XS, (unsigned)(XS * 2));
       u32x4 ah[KBW], al[KBW];
@@ -2126,7 +2188,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.sync = ver == 4 ? kSyncFlag : env_int("KCTC_SYNC_FWD", env_int("KCTC_SYNC", kSyncData));
     p.allow_local = env_int("KCTC_LOCAL", 0);
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
-    KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, 4096, s));
+    KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, kFlagBytes, s));
     const size_t lds = ver == 6 ? fwd6_lds_bytes(d, U) : fwd_lds_bytes(d, N, U);
     p.xpd = ver == 4 ? v4_xpd(d, U) : 1;
     p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
@@ -2184,14 +2246,21 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     p.allow_local = env_int("KCTC_LOCAL", 0);
     if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
-    KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, 4096, s));
+    KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, kFlagBytes, s));
     const size_t lds = ver == 6 ? bwd6_lds_bytes(d, U) : bwd_lds_bytes(d, N, U, ver);
     p.xpd = ver == 4 ? v4_xpd(d, U) : 1;
-    if (ver == 6)
-      p.xch = xch_acquire(sizeof(float) * (size_t)T * dirs * p.nwg * 16 * H, s);
-    else
+    if (ver == 6) {
+      // XCD-slot mapping when a direction's workgroups fit one XCD
+      // (measured slower, 37.2 vs 33.6 ms/step of backward recurrence: the 32
+      // workgroups of a direction then load 1 MB per step through ONE XCD's
+      // fabric port; spread over the XCDs they use four)
+      p.xpd = (p.nwg == kCusPerXcd && dirs <= 8 && env_int("KCTC_XCD6", 0)) ? 1 : 0;
+      p.allow_local = env_int("KCTC_LOCAL", 1);
+      p.xch = xch_acquire(sizeof(float) * (size_t)T * dirs * p.nwg * (16 * H + 64), s);
+    } else {
       p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
-    const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : dirs * p.nwg);
+    }
+    const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : ver == 6 && p.xpd ? 8 * p.nwg : dirs * p.nwg);
     RecTrace tr;
     if (tr.arm("bwd", grid.x)) p.trace = tr.dev;
     {
@@ -2201,7 +2270,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     }
     KCTC_HIP_CHECK(hipGetLastError());
     if (ver == 6) xch_release(s);
-    tr.dump("bwd", s, grid.x, p.nwg, T, dirs, ver, ver == 6 ? 0 : p.xpd);
+    tr.dump("bwd", s, grid.x, p.nwg, T, dirs, ver, ver == 6 ? (p.xpd ? 1 : 0) : p.xpd);
     // dx_l = sum_dir DX_dir W_dir   (lower layer's dy, or the caller's dx)
     float *dxl = (l == 0) ? dx : res + lay.per_layer * (l - 1) + lay.dout;
     const bool x3 = use_x3(NW * H);
