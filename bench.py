@@ -30,6 +30,7 @@ sys.path.insert(0, ROOT)
 METRIC = "CTC-train frames/sec, 5×BLSTM-512 mb=16, at 1/2/4/8 MI355X; loss match"
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix = FP32 vector peak (dense)
 PEAK_HBM_GBS = 8000.0
+PEAK_F16_TFLOPS = 2500.0   # dense f16/bf16 MFMA
 
 
 def model_flops(T, N, D, H, A, L, nw=4, dirs=2):
@@ -169,8 +170,8 @@ def main():
     fam_flops, _ = model_flops(T, N, D, H, A, L)
     prof = {}
     if profile:
-        for fam in list(fam_flops) + ["ctc_logz", "ctc_alpha_beta", "ctc_grad", "affine", "clip_gradient",
-                                      "update", "argmax", "scale"]:
+        for fam in list(fam_flops) + ["x3_scales", "ctc_logz", "ctc_alpha_beta", "ctc_grad", "affine",
+                                      "clip_gradient", "update", "argmax", "scale"]:
             ms, n = net.profile(fam)
             if n:
                 prof[fam] = (ms, n)
@@ -188,6 +189,31 @@ def main():
                 "avg_launch_ms": round(ms / n, 4),
                 "flops_per_launch": flops_per_launch,
                 "families_ms_per_step": {f: round(prof[f][0] / args.steps, 3) for f in prof}}
+        # secondary rooflines named by north_star: the gate GEMMs (input
+        # projections; split-fp16 MFMA: 3 f16 MFMAs per fp32-class product, so
+        # the matrix-core issue rate is 3x the algorithmic rate against the
+        # 2.5 PF dense f16 peak) and the CTC alpha/beta recursion (HBM bytes:
+        # gathered emissions read + alpha/beta columns spilled, fp64 offsets)
+        aux = {}
+        if "gemm_fwd_proj" in prof:
+            ms_g, n_g = prof["gemm_fwd_proj"]
+            tf = fam_flops["gemm_fwd_proj"] * args.steps / (ms_g / 1e3) / 1e12
+            aux["gate_gemm"] = {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_FP32_TFLOPS,
+                                "unit": "TFLOP/s", "frac": round(tf / PEAK_FP32_TFLOPS, 4),
+                                "mfma_issue_frac_f16": round(3 * tf / PEAK_F16_TFLOPS, 4)}
+        if "ctc_alpha_beta" in prof:
+            ms_c, n_c = prof["ctc_alpha_beta"]
+            byts = 0.0
+            for step in range(args.warmup, total):
+                _, nf, fl, ll = batches[step]
+                S = 2 * np.asarray(ll, np.float64) + 1
+                byts += float(np.sum(2 * (8.0 * np.asarray(nf) * S + 8.0 * np.asarray(nf))))
+            gbs = byts / (ms_c / 1e3) / 1e9
+            aux["ctc_alpha_beta"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
+                                     "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
+                                     "ms_per_launch": round(ms_c / n_c, 4),
+                                     "note": "serial over T (one barrier per frame): latency-bound"}
+        roof["secondary"] = aux
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
