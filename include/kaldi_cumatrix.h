@@ -7,6 +7,8 @@
 #ifndef KALDI_CTC_AMD_KALDI_CUMATRIX_H_
 #define KALDI_CTC_AMD_KALDI_CUMATRIX_H_
 
+#include <stddef.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -21,12 +23,13 @@ int kcm_add_mat_mat(struct ihipStream_t *stream, int transA, int transB, int M, 
                     float *C, long ldc);
 /* The same product on the split-fp16 matrix-core path (fp32-class: every row
  * of op(A) and column of op(B) is scaled by a power of two and carried as an
- * fp16 hi + lo pair, hi*hi + hi*lo + lo*hi accumulated in fp32; gemm.hip).
- * ws: device scratch of at least M + N unsigned ints (per-row / per-column
- * max |x|). */
+ * fp16 hi + lo pair, hi*hi + hi*lo + lo*hi accumulated in fp32; both operands
+ * are first packed along K, gemm_x3p.hip).  ws: device scratch of at least
+ * kcm_add_mat_mat_x3_workspace(M, N, K) bytes. */
+size_t kcm_add_mat_mat_x3_workspace(int M, int N, int K);
 int kcm_add_mat_mat_x3(struct ihipStream_t *stream, int transA, int transB, int M, int N, int K,
                        float alpha, const float *A, long lda, const float *B, long ldb, float beta,
-                       float *C, long ldc, unsigned *ws);
+                       float *C, long ldc, void *ws);
 /* ids[r] = argmax_c m[r][c], first maximum wins.  Replaces CuMatrix::FindRowMaxId
  * (src/cudamatrix/cu-matrix.cc:1612-1645). */
 int kcm_find_row_max_id(struct ihipStream_t *stream, const float *m, long rows, int cols, int *ids);

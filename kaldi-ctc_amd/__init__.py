@@ -245,7 +245,7 @@ def add_mat_mat_x3(C, A, B, transA=False, transB=False, alpha=1.0, beta=0.0, str
     import torch
     M, N = C.shape
     K = A.shape[0] if transA else A.shape[1]
-    ws = torch.empty(M + N, dtype=torch.int32, device=C.device)
+    ws = torch.empty(lib().kcm_add_mat_mat_x3_workspace(M, N, K), dtype=torch.uint8, device=C.device)
     st = lib().kcm_add_mat_mat_x3(_stream_handle(stream), int(transA), int(transB), M, N, K, alpha,
                                   _ptr(A), A.stride(0), _ptr(B), B.stride(0), beta, _ptr(C), C.stride(0),
                                   _ptr(ws))

@@ -1,6 +1,8 @@
 // cumatrix_api.cpp -- C ABI of include/kaldi_cumatrix.h.
 #include "kaldi_cumatrix.h"
 
+#include <algorithm>
+
 #include "common.h"
 #include "elementwise.h"
 #include "gemm.h"
@@ -23,25 +25,44 @@ int kcm_add_mat_mat(struct ihipStream_t *stream, int transA, int transB, int M, 
   }
 }
 
+size_t kcm_add_mat_mat_x3_workspace(int M, int N, int K) {
+  if (M < 0 || N < 0 || K < 0) return 0;
+  return kctc::align_up(kctc::x3p_bytes(M, K), 256) + kctc::align_up(kctc::x3p_bytes(N, K), 256) +
+         sizeof(int) * (size_t)(M + N) + sizeof(unsigned) * (size_t)std::max(M, N) + 256;
+}
+
 int kcm_add_mat_mat_x3(struct ihipStream_t *stream, int transA, int transB, int M, int N, int K,
                        float alpha, const float *A, long lda, const float *B, long ldb, float beta,
-                       float *C, long ldc, unsigned *ws) {
+                       float *C, long ldc, void *ws) {
   if (M < 0 || N < 0 || K < 0 || !C || !ws) return 1;
   try {
-    kctc::GemmArgs g;
-    g.transA = transA != 0; g.transB = transB != 0;
-    g.M = M; g.N = N; g.K = K; g.alpha = alpha; g.beta = beta;
-    g.A = A; g.lda = lda; g.B = B; g.ldb = ldb; g.C = C; g.ldc = ldc;
-    kctc::X3Scales s;
-    s.amaxA = ws;
-    s.amaxB = ws + M;
-    // op(A) rows: rows of A (row-major M x K) or columns of A^T (K x M)
-    if (!transA) kctc::absmax_f32(stream, A, lda, M, K, ws, nullptr);
-    else kctc::absmax_f32(stream, A, lda, K, M, nullptr, ws);
-    // op(B) columns: columns of B (K x N) or rows of B^T (N x K)
-    if (!transB) kctc::absmax_f32(stream, B, ldb, K, N, nullptr, ws + M);
-    else kctc::absmax_f32(stream, B, ldb, N, K, ws + M, nullptr);
-    kctc::gemm_x3(stream, g, s);
+    char *w = static_cast<char *>(ws);
+    _Float16 *Ap = reinterpret_cast<_Float16 *>(w);
+    w += kctc::align_up(kctc::x3p_bytes(M, K), 256);
+    _Float16 *Bp = reinterpret_cast<_Float16 *>(w);
+    w += kctc::align_up(kctc::x3p_bytes(N, K), 256);
+    int *eA = reinterpret_cast<int *>(w);
+    int *eB = eA + M;
+    unsigned *cm = reinterpret_cast<unsigned *>(eB + N);
+    // op(A) rows: rows of A (M x K) or columns of A^T (K x M)
+    if (!transA) {
+      kctc::x3p_pack_rows(stream, A, lda, M, K, Ap, eA, 0.f);
+    } else {
+      kctc::absmax_f32(stream, A, lda, K, M, nullptr, cm);
+      kctc::x3p_pack_cols(stream, A, lda, K, M, 0, Ap, eA, cm, 0.f);
+    }
+    // op(B) columns: rows of B^T (N x K) or columns of B (K x N)
+    if (transB) {
+      kctc::x3p_pack_rows(stream, B, ldb, N, K, Bp, eB, 0.f);
+    } else {
+      kctc::absmax_f32(stream, B, ldb, K, N, nullptr, cm);
+      kctc::x3p_pack_cols(stream, B, ldb, K, N, 0, Bp, eB, cm, 0.f);
+    }
+    kctc::X3PArgs g;
+    g.M = M; g.N = N; g.KB = (K + 31) / 32;
+    g.A = Ap; g.B = Bp; g.eA = eA; g.eB = eB;
+    g.C = C; g.ldc = ldc; g.alpha = alpha; g.beta = beta;
+    kctc::gemm_x3p(stream, g);
     return hipGetLastError() == hipSuccess ? 0 : 3;
   } catch (...) {
     return 3;

@@ -36,20 +36,41 @@ void gemm_f32(hipStream_t stream, const GemmArgs &g);
 // Heuristic split-K so that tiles * split fill the chip; returns 1 if not needed.
 int gemm_pick_split(int M, int N, int K, int batch);
 
-// Split-fp16 ("x3") GEMM, same contract as gemm_f32 (fp32-class results, see
-// gemm.hip).  Operand scaling: per A row (M index) / per B column (N index)
-// max |x| as float bits (absmax_f32), or, when the array is null, a constant
-// bound on |x| (e.g. 1 for an LSTM/GRU output).
-struct X3Scales {
-  const unsigned *amaxA = nullptr, *amaxB = nullptr;
-  long strideA = 0, strideB = 0;  // per batch
-  float boundA = 1.f, boundB = 1.f;
-};
-void gemm_x3(hipStream_t stream, const GemmArgs &g, const X3Scales &s);
-int split_exp_host(float bound);
 // max |X| per row (rmax[b][r]) and per column (cmax[b][c]) as float bits; either may be null
 void absmax_f32(hipStream_t stream, const float *X, long ldx, int rows, int cols, unsigned *rmax, unsigned *cmax,
                 int batch = 1, long strideX = 0, long strideR = 0, long strideC = 0);
+
+// Split-fp16 GEMM on packed operands (gemm_x3p.hip).  Packed operand:
+// [rows][KB][64] fp16 = per 32-k block 32 hi then 32 lo halves of the row
+// scaled by 2^e[row]; e[] int per row.  C[b][m][n] = alpha 2^-(eA[m]+eB[n])
+// sum_k A[m][k] B[n][k] (+ beta C + bias[n] + bias2[n]).
+struct X3PArgs {
+  int M = 0, N = 0, KB = 0;
+  const _Float16 *A = nullptr, *B = nullptr;
+  const int *eA = nullptr, *eB = nullptr;
+  float *C = nullptr;
+  long ldc = 0;
+  float alpha = 1.f, beta = 0.f;
+  const float *bias = nullptr, *bias2 = nullptr;
+  int batch = 1;
+  long sA = 0, sB = 0, sC = 0, sBias = 0, seA = 0, seB = 0;
+  int split_k = 1;
+  float *ws = nullptr;  // split_k * batch * M * N floats
+  int max_blocks = 0;
+  int *tile_counter = nullptr;
+};
+void gemm_x3p(hipStream_t s, const X3PArgs &g);
+// pack rows r < R of X (K values each, row stride ldx) -> out[b][r][KB][64],
+// exponent per row into eout (bound > 0: from the bound, else the row max)
+void x3p_pack_rows(hipStream_t s, const float *X, long ldx, int R, int K, _Float16 *out, int *eout, float bound,
+                   int batch = 1, long sX = 0, long sOut = 0, long sE = 0);
+// pack the transpose: packed row c < Cn = column c of X over its R rows
+// (source row k - shift at k, zero outside), exponents from cmax[c] (float
+// bits of max |x| of the column) or the bound
+void x3p_pack_cols(hipStream_t s, const float *X, long ldx, int R, int Cn, int shift, _Float16 *out, int *eout,
+                   const unsigned *cmax, float bound, int batch = 1, long sX = 0, long sOut = 0, long sE = 0,
+                   long sCm = 0);
+inline size_t x3p_bytes(long rows, long K) { return (size_t)rows * ((K + 31) / 32) * 64 * 2; }
 
 // column sums: out[b][j] (+)= alpha * sum_i X[b][i*ldx + j], i < rows  (accumulate if beta=1)
 void colsum_f32(hipStream_t stream, const float *X, long ldx, int rows, int cols, float alpha,

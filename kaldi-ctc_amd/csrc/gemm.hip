@@ -239,262 +239,6 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(KParams p) {
   for (int id = blockIdx.x; id < total; id += gridDim.x) gemm_tile<TA, TB>(p, lds, id, total, true);
 }
 
-// ---------------------------------------------------------------------------
-// Split-fp16 ("x3") GEMM: the same tiling (128x128, 4 waves of 64x64), both
-// operands converted while they are staged to LDS.  Each A row m / B column n
-// is scaled by a power of two 2^e (e from the row's / column's max |x|, so the
-// largest magnitude lands in [2^13, 2^14)) and split as x = hi + lo,
-// hi = fp16(x), lo = fp16(x - hi); one K-tile of 32 is three
-// v_mfma_f32_16x16x32_f16 per 16x16 output tile (hi*hi + hi*lo + lo*hi, fp32
-// accumulation), the epilogue multiplies by 2^-(eA[m] + eB[n]) (exact).  Each
-// operand keeps 22 significant bits relative to its row / column max and the
-// dropped lo*lo term is 2^-22 of the product: fp32-class results at 48 instead
-// of 128 MFMA issue slots (x 16 vs 32 cycles) per 16x16x32 block.
-// LDS image per operand and stage: [128 rows][36 dwords] = hi k0..31 (16
-// dwords) | lo k0..31 (16 dwords) | pad -- the fp32 kernel's geometry, so the
-// fragment reads (ds_read_b128 at row*36 + fq*4 and +16) are conflict-free.
-// Staging: k-contiguous sources load float4 along k; k-strided sources load 4
-// scalars along k (lanes along rows: 256-B coalesced); either way a thread
-// holds 4 consecutive k of one row and writes 8 B of hi and 8 B of lo.
-typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
-typedef _Float16 halfx4 __attribute__((ext_vector_type(4)));
-constexpr int XLD = 36;
-constexpr int XOPSZ = BM * XLD;
-
-__device__ __forceinline__ int split_exp(float mx) {
-  int e = 0;
-  (void)frexpf(mx, &e);
-  return 14 - e;
-}
-
-struct X3 {
-  const unsigned *amaxA, *amaxB;  // per-row max|A| / per-column max|B| (float bits), or null
-  long samaxA, samaxB;            // batch strides of those arrays
-  int eA0, eB0;                   // exponents used when the array is null
-};
-
-// 4 consecutive k (k0..k0+3) of row r of an operand, zero outside.
-template <bool KC>
-__device__ __forceinline__ floatx4 x3_load4(const float *__restrict__ P, long ld, int rows, int r, int k0, int kend,
-                                            int vec) {
-  floatx4 v = {0.f, 0.f, 0.f, 0.f};
-  if (r >= rows) return v;
-  if (KC) {
-    const float *p = P + (long)r * ld + k0;
-    if (vec && k0 + 3 < kend) return *reinterpret_cast<const floatx4 *>(p);
-#pragma unroll
-    for (int j = 0; j < 4; j++) v[j] = (k0 + j < kend) ? p[j] : 0.f;
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; j++) v[j] = (k0 + j < kend) ? P[(long)(k0 + j) * ld + r] : 0.f;
-  }
-  return v;
-}
-
-// thread t's 4 (row, k-quad) slots of a 128 x 32 tile
-template <bool KC>
-__device__ __forceinline__ void x3_slot(int i, int &r, int &kq) {
-  const int t = threadIdx.x;
-  if (KC) { r = (t >> 3) + 32 * i; kq = t & 7; }
-  else    { r = t & 127; kq = (t >> 7) + 2 * i; }
-}
-
-template <bool KC>
-__device__ __forceinline__ void x3_load(const float *__restrict__ P, long ld, int rows, int k0, int kend, int vec,
-                                        floatx4 (&reg)[4]) {
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    int r, kq;
-    x3_slot<KC>(i, r, kq);
-    reg[i] = x3_load4<KC>(P, ld, rows, r, k0 + kq * 4, kend, vec);
-  }
-}
-
-template <bool KC>
-__device__ __forceinline__ void x3_store(unsigned *__restrict__ S, const floatx4 (&reg)[4], const int (&ex)[4]) {
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    int r, kq;
-    x3_slot<KC>(i, r, kq);
-    halfx4 h, l;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const float x = ldexpf(reg[i][j], ex[i]);
-      h[j] = (_Float16)x;
-      l[j] = (_Float16)(x - (float)h[j]);
-    }
-    *reinterpret_cast<halfx4 *>(S + r * XLD + kq * 2) = h;
-    *reinterpret_cast<halfx4 *>(S + r * XLD + 16 + kq * 2) = l;
-  }
-}
-
-__device__ __forceinline__ int x3_exp(const unsigned *amax, int idx, int e0) {
-  return amax ? split_exp(__uint_as_float(amax[idx])) : e0;
-}
-
-template <bool TA, bool TB>
-__device__ __forceinline__ void gemm_x3_tile(const KParams &p, const X3 &x, unsigned (&lds)[2][2 * XOPSZ], int id,
-                                             int total, bool remap) {
-  const int q = total >> 3, rr = total & 7, xcd = id & 7, loc = id >> 3;
-  const int wl = remap ? (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc : id;
-  const int bz = wl / p.tiles, wg = wl - bz * p.tiles;
-  const int tn = wg % p.gx, tm = wg / p.gx;
-  const int b = bz % p.batch, ks = bz / p.batch;
-  const float *A = p.A + (long)b * p.strideA;
-  const float *B = p.B + (long)b * p.strideB;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = ks * p.kchunk, kend = min(p.K, kbeg + p.kchunk);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
-  const int fr = lane & 15, fq = lane >> 4;
-  const unsigned *amA = x.amaxA ? x.amaxA + (long)b * x.samaxA : nullptr;
-  const unsigned *amB = x.amaxB ? x.amaxB + (long)b * x.samaxB : nullptr;
-
-  // A operand: rows m, k-contiguous iff !TA.  B operand: rows n, k-contiguous iff TB.
-  const float *Ab = TA ? A + m0 : A + (long)m0 * p.lda;
-  const float *Bb = TB ? B + (long)n0 * p.ldb : B + n0;
-  const int arows = p.M - m0, brows = p.N - n0;
-  int exA[4], exB[4];
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    int r, kq;
-    x3_slot<!TA>(i, r, kq);
-    exA[i] = r < arows ? x3_exp(amA, m0 + r, x.eA0) : 0;
-    x3_slot<TB>(i, r, kq);
-    exB[i] = r < brows ? x3_exp(amB, n0 + r, x.eB0) : 0;
-  }
-
-  floatx4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; i++)
-#pragma unroll
-    for (int j = 0; j < 4; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  floatx4 ra[4], rb[4];
-  int nk = (kend - kbeg + BK - 1) / BK;
-  if (nk < 0) nk = 0;
-  if (nk > 0) {
-    x3_load<!TA>(Ab, p.lda, arows, kbeg, kend, p.vecA, ra);
-    x3_load<TB>(Bb, p.ldb, brows, kbeg, kend, p.vecB, rb);
-    x3_store<!TA>(lds[0], ra, exA);
-    x3_store<TB>(lds[0] + XOPSZ, rb, exB);
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nk; kt++) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) {
-      const int k0 = kbeg + (kt + 1) * BK;
-      x3_load<!TA>(Ab, p.lda, arows, k0, kend, p.vecA, ra);
-      x3_load<TB>(Bb, p.ldb, brows, k0, kend, p.vecB, rb);
-    }
-    const unsigned *sA = lds[cur], *sB = lds[cur] + XOPSZ;
-    halfx8 ah[4], al[4], bh[4], bl[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const unsigned *ra_ = sA + (wm + i * 16 + fr) * XLD + fq * 4;
-      ah[i] = *reinterpret_cast<const halfx8 *>(ra_);
-      al[i] = *reinterpret_cast<const halfx8 *>(ra_ + 16);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const unsigned *rb_ = sB + (wn + j * 16 + fr) * XLD + fq * 4;
-      bh[j] = *reinterpret_cast<const halfx8 *>(rb_);
-      bl[j] = *reinterpret_cast<const halfx8 *>(rb_ + 16);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-      for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-      for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-      for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-    if (more) {
-      x3_store<!TA>(lds[cur ^ 1], ra, exA);
-      x3_store<TB>(lds[cur ^ 1] + XOPSZ, rb, exB);
-    }
-    __syncthreads();
-  }
-
-  // epilogue: acc[i][j][r] -> C[m0+wm+16i+4fq+r][n0+wn+16j+fr], unscaled by 2^-(eA + eB)
-  int eb[4], ea[4][4];
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const int col = n0 + wn + j * 16 + fr;
-    eb[j] = col < p.N ? x3_exp(amB, col, x.eB0) : 0;
-  }
-#pragma unroll
-  for (int i = 0; i < 4; i++)
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int row = m0 + wm + i * 16 + fq * 4 + r;
-      ea[i][r] = row < p.M ? x3_exp(amA, row, x.eA0) : 0;
-    }
-  if (p.split > 1) {
-    float *W = p.ws + ((long)ks * p.batch + b) * (long)p.M * p.N;
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const int col = n0 + wn + j * 16 + fr;
-        if (col >= p.N) continue;
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int row = m0 + wm + i * 16 + fq * 4 + r;
-          if (row < p.M) W[(long)row * p.N + col] = ldexpf(acc[i][j][r], -(ea[i][r] + eb[j]));
-        }
-      }
-    return;
-  }
-  float *C = p.C + (long)b * p.strideC;
-  const float *bias = p.bias ? p.bias + (long)b * p.strideBias : nullptr;
-  const float *bias2 = p.bias2 ? p.bias2 + (long)b * p.strideBias : nullptr;
-#pragma unroll
-  for (int i = 0; i < 4; i++)
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const int col = n0 + wn + j * 16 + fr;
-      if (col >= p.N) continue;
-      float badd = 0.f;
-      if (bias) badd += bias[col];
-      if (bias2) badd += bias2[col];
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int row = m0 + wm + i * 16 + fq * 4 + r;
-        if (row < p.M) {
-          float *c = C + (long)row * p.ldc + col;
-          float v = p.alpha * ldexpf(acc[i][j][r], -(ea[i][r] + eb[j])) + badd;
-          if (p.beta != 0.f) v += p.beta * *c;
-          *c = v;
-        }
-      }
-    }
-}
-
-template <bool TA, bool TB>
-__global__ __launch_bounds__(NT, 2) void gemm_x3_kernel(KParams p, X3 x) {
-  __shared__ __attribute__((aligned(16))) unsigned lds[2][2 * XOPSZ];
-  __shared__ int next;
-  const int total = p.tiles * p.batch * p.split;
-  if (p.counter) {
-    while (true) {
-      if (threadIdx.x == 0) next = atomicAdd(p.counter, 1);
-      __syncthreads();
-      const int id = next;
-      __syncthreads();
-      if (id >= total) break;
-      gemm_x3_tile<TA, TB>(p, x, lds, id, total, false);
-    }
-    return;
-  }
-  for (int id = blockIdx.x; id < total; id += gridDim.x) gemm_x3_tile<TA, TB>(p, x, lds, id, total, true);
-}
-
 // max |x| per row (rows < nrows, cols < ncols) into rmax[b][row] (float bits),
 // and per column, atomically max-merged into cmax[b][col] (pre-zeroed); either
 // output may be null.  One wave per (row, 64-column group) pass.
@@ -624,51 +368,6 @@ void gemm_f32(hipStream_t stream, const GemmArgs &g) {
     int blocks = (int)std::min<long>(2048, (total + 255) / 256);
     hipLaunchKernelGGL(splitk_reduce, dim3(blocks), dim3(256), 0, stream, p);
   }
-}
-
-void gemm_x3(hipStream_t stream, const GemmArgs &g, const X3Scales &s) {
-  if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return;
-  KParams p;
-  p.A = g.A; p.B = g.B; p.C = g.C; p.bias = g.bias; p.bias2 = g.bias2;
-  p.lda = g.lda; p.ldb = g.ldb; p.ldc = g.ldc;
-  p.strideA = g.strideA; p.strideB = g.strideB; p.strideC = g.strideC; p.strideBias = g.strideBias;
-  p.M = g.M; p.N = g.N; p.K = g.K; p.alpha = g.alpha; p.beta = g.beta;
-  p.gx = ceil_div(g.N, BN);
-  p.tiles = p.gx * ceil_div(g.M, BM);
-  p.batch = g.batch;
-  p.split = (g.split_k > 1 && g.ws) ? g.split_k : 1;
-  p.kchunk = p.split > 1 ? (int)align_up((size_t)ceil_div(g.K, p.split), BK) : (g.K > 0 ? g.K : 1);
-  if (p.split > 1) p.split = ceil_div(g.K, p.kchunk);
-  p.ws = g.ws;
-  auto aligned = [](const void *ptr, long ld, long stride) {
-    return ((uintptr_t)ptr % 16 == 0) && (ld % 4 == 0) && (stride % 4 == 0);
-  };
-  p.vecA = aligned(g.A, g.lda, g.strideA);
-  p.vecB = aligned(g.B, g.ldb, g.strideB);
-  const int total = p.tiles * p.batch * p.split;
-  int blocks = total;
-  if (g.max_blocks > 0 && total > g.max_blocks) blocks = std::max(8, g.max_blocks / 8 * 8);
-  p.counter = g.tile_counter;
-  if (p.counter) KCTC_HIP_CHECK(hipMemsetAsync(p.counter, 0, sizeof(int), stream));
-  X3 x;
-  x.amaxA = s.amaxA; x.amaxB = s.amaxB; x.samaxA = s.strideA; x.samaxB = s.strideB;
-  x.eA0 = split_exp_host(s.boundA); x.eB0 = split_exp_host(s.boundB);
-  dim3 grid(blocks);
-  if (!g.transA && !g.transB) hipLaunchKernelGGL((gemm_x3_kernel<false, false>), grid, dim3(NT), 0, stream, p, x);
-  else if (!g.transA && g.transB) hipLaunchKernelGGL((gemm_x3_kernel<false, true>), grid, dim3(NT), 0, stream, p, x);
-  else if (g.transA && !g.transB) hipLaunchKernelGGL((gemm_x3_kernel<true, false>), grid, dim3(NT), 0, stream, p, x);
-  else hipLaunchKernelGGL((gemm_x3_kernel<true, true>), grid, dim3(NT), 0, stream, p, x);
-  if (p.split > 1) {
-    long total = (long)p.batch * p.M * p.N;
-    int blocks = (int)std::min<long>(2048, (total + 255) / 256);
-    hipLaunchKernelGGL(splitk_reduce, dim3(blocks), dim3(256), 0, stream, p);
-  }
-}
-
-int split_exp_host(float bound) {
-  int e = 0;
-  (void)std::frexp(bound, &e);
-  return 14 - e;
 }
 
 void absmax_f32(hipStream_t stream, const float *X, long ldx, int rows, int cols, unsigned *rmax, unsigned *cmax,

@@ -110,36 +110,45 @@ static size_t xch_bytes(const RnnDesc &d, int T, int N) {
   const long Npad = (N + 15) / 16 * 16;
   return sizeof(float) * (size_t)T * d.dirs * d.nw() * d.H * Npad;
 }
-// then the split-fp16 GEMM scales (per stacked layer): max |x| of the GEMM
-// operands' rows / columns (float bits), see X3Lay
-struct X3Lay {
-  long rin, wrow, wcol, dxr, dxc, ec, xcol, yc, per_layer;
+// then the packed split-fp16 GEMM operands of one layer at a time (forward,
+// backward-data and the weight GEMMs of a component never overlap):
+//   forward   : input rows [TN][Din], W rows [dirs*G][Din]
+//   bwd data  : dGates rows [dirs*TN][G], W^T rows [dirs*Din][G]
+//   bwd weight: dGates^T [dirs*G][TN] (+ GRU: E^T), input^T [Din][TN],
+//               shifted output^T [dirs*H][TN]
+// plus int exponents and float-bit column maxima (G = nW*H).
+struct PackLay {
+  size_t a, b, c, d, ea, eb, ec, ed, cm, total;
 };
-static X3Lay x3_layout(const RnnDesc &d, int T, int N) {
-  X3Lay x;
-  const long TN = (long)T * N, G = (long)d.dirs * d.nw() * d.H, Dm = std::max(d.D, d.dirs * d.H);
-  long p = 0;
-  x.rin = p;  p += al64(TN);               // rows of the layer input
-  x.wrow = p; p += al64(G);                // rows of W (gate rows), per direction
-  x.wcol = p; p += al64((long)d.dirs * Dm);  // columns of W (input dims), per direction
-  x.dxr = p;  p += al64((long)d.dirs * TN);  // rows of dGates (frames), per direction
-  x.dxc = p;  p += al64(G);                // columns of dGates (input part)
-  x.ec = p;   p += al64(G);                // columns of dGates (recurrent part; GRU)
-  x.xcol = p; p += al64(Dm);               // columns of the layer input
-  x.yc = p;   p += al64((long)d.dirs * d.H);  // columns of the layer output
-  x.per_layer = p;
-  return x;
+static PackLay pack_layout(const RnnDesc &d, int T, int N) {
+  const long TN = (long)T * N, G = (long)d.nw() * d.H, Dm = std::max(d.D, d.dirs * d.H), dirs = d.dirs;
+  const size_t fw_a = x3p_bytes(TN, Dm), fw_b = x3p_bytes(dirs * G, Dm);
+  const size_t bd_a = x3p_bytes(dirs * TN, G), bd_b = x3p_bytes(dirs * Dm, G);
+  const size_t bw_a = x3p_bytes(dirs * G, TN) * (d.mode == kGru ? 2 : 1), bw_b = x3p_bytes(Dm, TN),
+               bw_c = x3p_bytes(dirs * d.H, TN);
+  PackLay p;
+  size_t o = 0;
+  p.a = o; o = align_up(o + std::max({fw_a, bd_a, bw_a}), 256);
+  p.b = o; o = align_up(o + std::max({fw_b, bd_b, bw_b}), 256);
+  p.c = o; o = align_up(o + bw_c, 256);
+  p.d = o;  // unused slot kept for symmetry (0 bytes)
+  const long ne = std::max({TN * dirs, dirs * G * 2, dirs * Dm}) + 64;
+  p.ea = o; o = align_up(o + sizeof(int) * ne, 256);
+  p.eb = o; o = align_up(o + sizeof(int) * ne, 256);
+  p.ec = o; o = align_up(o + sizeof(int) * ne, 256);
+  p.ed = o; o = align_up(o + sizeof(int) * ne, 256);
+  p.cm = o; o = align_up(o + sizeof(unsigned) * ne, 256);
+  p.total = o;
+  return p;
 }
-static size_t x3_offset(const RnnDesc &d, int T, int N) { return align_up(xch_offset(d, T, N) + xch_bytes(d, T, N), 256); }
-size_t rnn_workspace_bytes(const RnnDesc &d, int T, int N) {
-  return x3_offset(d, T, N) + sizeof(unsigned) * (size_t)x3_layout(d, T, N).per_layer * d.layers;
+static size_t pack_offset(const RnnDesc &d, int T, int N) { return align_up(xch_offset(d, T, N) + xch_bytes(d, T, N), 256); }
+size_t rnn_workspace_bytes(const RnnDesc &d, int T, int N) { return pack_offset(d, T, N) + pack_layout(d, T, N).total; }
+template <typename P>
+static P *pk(void *ws, const RnnDesc &d, int T, int N, size_t off) {
+  return reinterpret_cast<P *>(static_cast<char *>(ws) + pack_offset(d, T, N) + off);
 }
-static unsigned *x3_base(void *ws, const RnnDesc &d, int T, int N, int l) {
-  return reinterpret_cast<unsigned *>(static_cast<char *>(ws) + x3_offset(d, T, N)) +
-         (long)x3_layout(d, T, N).per_layer * l;
-}
-// The RNN GEMMs run on the split-fp16 matrix-core path unless KCTC_GEMM=f32
-// (or the contraction is too short to pay for the scale pass).
+// The RNN GEMMs run on the packed split-fp16 matrix-core path (gemm_x3p.hip)
+// unless KCTC_GEMM=f32 (or the contraction is too short to pay for packing).
 static bool use_x3(int K) {
   static int v = -1;
   if (v < 0) {
@@ -148,11 +157,8 @@ static bool use_x3(int K) {
   }
   return v && K >= 128;
 }
-static void absmax_span(hipStream_t s, const float *X, long ldx, int rows, int cols, unsigned *rmax, unsigned *cmax,
-                        int batch = 1, long strideX = 0, long strideR = 0, long strideC = 0) {
-  ProfSpan ps(s, "x3_scales");
-  absmax_f32(s, X, ldx, rows, cols, rmax, cmax, batch, strideX, strideR, strideC);
-}
+// |x| <= 1: an LSTM / GRU / TANH layer output
+static bool bounded_out(const RnnDesc &d) { return d.mode != kRelu; }
 
 namespace {
 
@@ -2162,20 +2168,25 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     g.bias2 = (d.mode == kGru) ? nullptr : wl + bR;
     g.batch = dirs; g.strideA = 0; g.strideB = pls; g.strideC = (long)NW * H; g.strideBias = pls;
     if (use_x3(Din)) {
-      unsigned *x3 = x3_base(workspace, d, T, N, l);
-      const X3Lay xl = x3_layout(d, T, N);
-      X3Scales sc;
-      // the layer input: a lower stacked layer's LSTM/GRU/TANH output is in
-      // [-1, 1]; the component input (layer 0) and RELU outputs get row maxima
-      if (l == 0 || d.mode == kRelu) {
-        absmax_span(s, in, Din, (int)TN, Din, x3 + xl.rin, nullptr);
-        sc.amaxA = x3 + xl.rin;
+      // input rows (a lower stacked layer's output is bounded; the component
+      // input and RELU outputs get per-row exponents) and W rows, packed
+      const PackLay pl = pack_layout(d, T, N);
+      _Float16 *Ap = pk<_Float16>(workspace, d, T, N, pl.a), *Bp = pk<_Float16>(workspace, d, T, N, pl.b);
+      int *eA = pk<int>(workspace, d, T, N, pl.ea), *eB = pk<int>(workspace, d, T, N, pl.eb);
+      const int KB = (Din + 31) / 32;
+      {
+        ProfSpan ps(s, "x3_pack");
+        x3p_pack_rows(s, in, Din, (int)TN, Din, Ap, eA, (l > 0 && bounded_out(d)) ? 1.f : 0.f);
+        x3p_pack_rows(s, wl, Din, NW * H, Din, Bp, eB, 0.f, dirs, pls, (long)NW * H * KB * 64, (long)NW * H);
       }
-      absmax_span(s, wl, Din, NW * H, Din, x3 + xl.wrow, nullptr, dirs, pls, (long)NW * H);
-      sc.amaxB = x3 + xl.wrow;
-      sc.strideB = (long)NW * H;
+      X3PArgs x;
+      x.M = (int)TN; x.N = NW * H; x.KB = KB;
+      x.A = Ap; x.B = Bp; x.eA = eA; x.eB = eB;
+      x.C = g.C; x.ldc = g.ldc; x.bias = g.bias; x.bias2 = g.bias2;
+      x.batch = dirs; x.sA = 0; x.seA = 0; x.sB = (long)NW * H * KB * 64; x.seB = (long)NW * H;
+      x.sC = g.strideC; x.sBias = g.strideBias;
       ProfSpan ps(s, "gemm_fwd_proj");
-      gemm_x3(s, g, sc);
+      gemm_x3p(s, x);
     } else {
       ProfSpan ps(s, "gemm_fwd_proj");
       gemm_f32(s, g);
@@ -2273,36 +2284,41 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     tr.dump("bwd", s, grid.x, p.nwg, T, dirs, ver, ver == 6 ? (p.xpd ? 1 : 0) : p.xpd);
     // dx_l = sum_dir DX_dir W_dir   (lower layer's dy, or the caller's dx)
     float *dxl = (l == 0) ? dx : res + lay.per_layer * (l - 1) + lay.dout;
-    const bool x3 = use_x3(NW * H);
-    unsigned *x3b = x3_base(workspace, d, T, N, l);
-    const X3Lay xl = x3_layout(d, T, N);
-    if (x3) {
-      // scales of dGates for this GEMM (frame rows) and for the weight
-      // GEMMs on the side stream (gate columns; GRU: also the recurrent part E)
-      const long G4 = (long)NW * H;
-      absmax_span(s, DX, (long)dirs * G4, (int)TN, (int)G4, dxl ? x3b + xl.dxr : nullptr, x3b + xl.dxc, dirs, G4,
-                  TN, G4);
-      if (d.mode == kGru) absmax_span(s, E, (long)dirs * G4, (int)TN, (int)G4, nullptr, x3b + xl.ec, dirs, G4, 0, G4);
-    }
     if (dxl) {
-      if (x3)
-        for (int dir = 0; dir < dirs; dir++)
-          absmax_span(s, wl + dir * pls, Din, NW * H, Din, nullptr, x3b + xl.wcol + (long)dir * Din);
+      const bool x3 = use_x3(NW * H);
+      const long G4 = (long)NW * H;
+      const int KB = (int)((G4 + 31) / 32);
+      const PackLay pl = pack_layout(d, T, N);
+      _Float16 *Ap = pk<_Float16>(workspace, d, T, N, pl.a), *Bp = pk<_Float16>(workspace, d, T, N, pl.b);
+      int *eA = pk<int>(workspace, d, T, N, pl.ea), *eB = pk<int>(workspace, d, T, N, pl.eb);
+      unsigned *cm = pk<unsigned>(workspace, d, T, N, pl.cm);
+      if (x3) {
+        // dGates rows (frames, per direction) and W^T rows (input dims), packed over the gates
+        ProfSpan ps(s, "x3_pack");
+        x3p_pack_rows(s, DX, (long)dirs * G4, (int)TN, (int)G4, Ap, eA, 0.f, dirs, G4, TN * KB * 64, TN);
+        for (int dir = 0; dir < dirs; dir++) {
+          absmax_f32(s, wl + dir * pls, Din, (int)G4, Din, nullptr, cm);
+          x3p_pack_cols(s, wl + dir * pls, Din, (int)G4, Din, 0, Bp + (long)dir * Din * KB * 64, eB + dir * Din, cm,
+                        0.f);
+        }
+      }
       for (int dir = 0; dir < dirs; dir++) {
-        GemmArgs g;
-        g.transA = false; g.transB = false;
-        g.M = (int)TN; g.N = Din; g.K = NW * H;
-        g.A = DX + (long)dir * NW * H; g.lda = (long)dirs * NW * H;
-        g.B = wl + dir * pls; g.ldb = Din;
-        g.C = dxl; g.ldc = Din;
-        g.beta = dir == 0 ? 0.f : 1.f;
         ProfSpan ps(s, "gemm_bwd_data");
         if (x3) {
-          X3Scales sc;
-          sc.amaxA = x3b + xl.dxr + (long)dir * TN;
-          sc.amaxB = x3b + xl.wcol + (long)dir * Din;
-          gemm_x3(s, g, sc);
+          X3PArgs x;
+          x.M = (int)TN; x.N = Din; x.KB = KB;
+          x.A = Ap + (long)dir * TN * KB * 64; x.eA = eA + (long)dir * TN;
+          x.B = Bp + (long)dir * Din * KB * 64; x.eB = eB + dir * Din;
+          x.C = dxl; x.ldc = Din; x.beta = dir == 0 ? 0.f : 1.f;
+          gemm_x3p(s, x);
         } else {
+          GemmArgs g;
+          g.transA = false; g.transB = false;
+          g.M = (int)TN; g.N = Din; g.K = NW * H;
+          g.A = DX + (long)dir * NW * H; g.lda = (long)dirs * NW * H;
+          g.B = wl + dir * pls; g.ldb = Din;
+          g.C = dxl; g.ldc = Din;
+          g.beta = dir == 0 ? 0.f : 1.f;
           gemm_f32(s, g);
         }
       }
@@ -2351,18 +2367,44 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     unsigned *fl = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     if (max_blocks > 0) g.tile_counter = reinterpret_cast<int *>(fl + 1008);
     const bool x3 = use_x3((int)TN) && Din >= 64;
-    unsigned *x3b = x3_base(workspace, d, T, N, l);
-    const X3Lay xl = x3_layout(d, T, N);
+    const int KBt = (int)((TN + 31) / 32);
+    const PackLay pl = pack_layout(d, T, N);
+    _Float16 *DXt = pk<_Float16>(workspace, d, T, N, pl.a), *Xt = pk<_Float16>(workspace, d, T, N, pl.b);
+    _Float16 *Yt = pk<_Float16>(workspace, d, T, N, pl.c);
+    _Float16 *Et = d.mode == kGru ? DXt + (long)dirs * G4 * KBt * 64 : DXt;
+    int *eDX = pk<int>(workspace, d, T, N, pl.ea), *eX = pk<int>(workspace, d, T, N, pl.eb);
+    int *eY = pk<int>(workspace, d, T, N, pl.ec), *eE = d.mode == kGru ? pk<int>(workspace, d, T, N, pl.ed) : eDX;
+    unsigned *cm = pk<unsigned>(workspace, d, T, N, pl.cm);
     if (x3) {
-      X3Scales sc;
-      sc.amaxA = x3b + xl.dxc;  // dGates columns (from rnn_backward_data)
-      sc.strideA = G4;
-      if (l == 0 || d.mode == kRelu) {
-        absmax_span(s, in, Din, (int)TN, Din, nullptr, x3b + xl.xcol);
-        sc.amaxB = x3b + xl.xcol;
+      // the transposes, packed over the frames: dGates^T (per-gate exponents),
+      // input^T (per-dim), and for dR the output shifted by one step per direction
+      ProfSpan ps(s, "x3_pack");
+      absmax_f32(s, DX, ldg, (int)TN, (int)(dirs * G4), nullptr, cm);
+      x3p_pack_cols(s, DX, ldg, (int)TN, (int)(dirs * G4), 0, DXt, eDX, cm, 0.f);
+      if (d.mode == kGru) {
+        absmax_f32(s, E, ldg, (int)TN, (int)(dirs * G4), nullptr, cm);
+        x3p_pack_cols(s, E, ldg, (int)TN, (int)(dirs * G4), 0, Et, eE, cm, 0.f);
       }
+      const bool xb = l > 0 && bounded_out(d);
+      if (!xb) absmax_f32(s, in, Din, (int)TN, Din, nullptr, cm);
+      x3p_pack_cols(s, in, Din, (int)TN, Din, 0, Xt, eX, cm, xb ? 1.f : 0.f);
+      if (T > 1) {
+        if (!bounded_out(d)) absmax_f32(s, out, ldy, (int)TN, (int)ldy, nullptr, cm);
+        for (int dir = 0; dir < dirs; dir++)
+          x3p_pack_cols(s, out + (long)dir * H, ldy, (int)TN, H, dir == 0 ? N : -N, Yt + (long)dir * H * KBt * 64,
+                        eY + dir * H, bounded_out(d) ? nullptr : cm + dir * H, bounded_out(d) ? 1.f : 0.f);
+      }
+    }
+    if (x3) {
+      X3PArgs x;
+      x.M = (int)G4; x.N = Din; x.KB = KBt;
+      x.A = DXt; x.eA = eDX; x.sA = G4 * KBt * 64; x.seA = G4;
+      x.B = Xt; x.eB = eX;
+      x.C = dwl; x.ldc = Din; x.beta = 1.f;
+      x.batch = dirs; x.sC = pls;
+      x.split_k = g.split_k; x.ws = ws; x.max_blocks = g.max_blocks; x.tile_counter = g.tile_counter;
       ProfSpan ps(s, "gemm_bwd_w");
-      gemm_x3(s, g, sc);
+      gemm_x3p(s, x);
     } else {
       ProfSpan ps(s, "gemm_bwd_w");
       gemm_f32(s, g);
@@ -2384,19 +2426,18 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       r.ws = ws;
       r.max_blocks = max_blocks;
       if (max_blocks > 0) r.tile_counter = reinterpret_cast<int *>(fl + 1009);
+      ProfSpan ps(s, "gemm_bwd_r");
       if (x3) {
-        X3Scales sc;
-        sc.amaxA = x3b + (d.mode == kGru ? xl.ec : xl.dxc);
-        sc.strideA = G4;
-        if (d.mode == kRelu) {
-          absmax_span(s, out, ldy, (int)TN, (int)ldy, nullptr, x3b + xl.yc);
-          sc.amaxB = x3b + xl.yc;
-          sc.strideB = H;
-        }
-        ProfSpan ps(s, "gemm_bwd_r");
-        gemm_x3(s, r, sc);
+        // all frames: the shifted-out ones are zero in the packed output
+        X3PArgs x;
+        x.M = (int)G4; x.N = H; x.KB = KBt;
+        x.A = Et; x.eA = eE; x.sA = G4 * KBt * 64; x.seA = G4;
+        x.B = Yt; x.eB = eY; x.sB = (long)H * KBt * 64; x.seB = H;
+        x.C = r.C; x.ldc = H; x.beta = 1.f;
+        x.batch = dirs; x.sC = pls;
+        x.split_k = r.split_k; x.ws = ws; x.max_blocks = max_blocks; x.tile_counter = r.tile_counter;
+        gemm_x3p(s, x);
       } else {
-        ProfSpan ps(s, "gemm_bwd_r");
         gemm_f32(s, r);
       }
     }
