@@ -95,6 +95,11 @@ struct kctcEgsReader_;
 int kctc_nnet_train_simple(kctcNnet_t nnet, struct kctcEgsReader_ *reader, long max_minibatches,
                            long *num_egs, double *tot_weight, double *tot_objf, double *tot_accuracy);
 
+/* LevenshteinEditDistance with unit costs (src/util/edit-distance-inl.h), as
+ * ComputeTotAccuracy uses it (src/ctc/ctc-nnet-update.cc:261-317), by Myers'
+ * bit-vector algorithm (ref in ceil(nref/64) 64-bit words; O(nhyp*nref/64)). */
+int kctc_levenshtein(const int *ref, int nref, const int *hyp, int nhyp);
+
 /* FormatNnetInput: pack per-utterance [T_n][dim] host matrices (concatenated
  * in `feats`, row offsets by num_frames) into [T_max*N][dim], row t*N+n,
  * zero padded.  out must hold T_max*N*dim floats (host). */

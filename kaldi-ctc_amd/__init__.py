@@ -409,6 +409,13 @@ def synth_minibatch(seed, T_max, N, dim, A, label_ratio=0.125, want_feats=True):
     return feats, nf, fl[:n].copy(), ll
 
 
+def levenshtein(ref, hyp):
+    """kaldi::LevenshteinEditDistance (unit costs) through kctc_levenshtein (host code)."""
+    r = np.ascontiguousarray(ref, dtype=np.int32)
+    h = np.ascontiguousarray(hyp, dtype=np.int32)
+    return lib().kctc_levenshtein(r.ctypes.data, len(r), h.ctypes.data, len(h))
+
+
 def format_input(utt_feats, T_max=None):
     """FormatNnetInput on a list of [T_n, dim] arrays -> [T_max*N, dim]."""
     N = len(utt_feats)

@@ -56,6 +56,7 @@ SIGS = {
     "kctc_nnet_set_momentum": (ci, [vp, cf]),
     "kctc_nnet_train_simple": (ci, [vp, vp, cl, ctypes.POINTER(cl), ctypes.POINTER(cd), ctypes.POINTER(cd),
                                     ctypes.POINTER(cd)]),
+    "kctc_levenshtein": (ci, [vp, ci, vp, ci]),
     "kctc_format_input": (ci, [vp, vp, ci, ci, ci, vp]),
     "kctc_synth_minibatch": (cl, [ctypes.c_ulonglong, ci, ci, ci, ci, cd, vp, vp, vp, vp]),
     # include/kaldi_ctc_egs.h

@@ -18,6 +18,49 @@
 namespace kctc {
 namespace nnet2 {
 
+// Unit-cost Levenshtein distance (kaldi::LevenshteinEditDistance,
+// src/util/edit-distance-inl.h) by Myers' bit-vector algorithm in its block
+// form (Myers 1999; the per-block step as in edlib): column j of the DP over
+// ref (rows, 64 per word) is kept as vertical +1/-1 delta masks; one pass per
+// hyp symbol costs ceil(m/64) word steps instead of m cell updates.  The
+// horizontal delta at the top boundary is +1 (D[0][j] = j); bits above row
+// m-1 in the last word never reach lower rows (carries and shifts go up).
+int levenshtein(const int *ref, int m, const int *hyp, int n) {
+  if (m <= 0) return n > 0 ? n : 0;
+  if (n <= 0) return m;
+  const int W = (m + 63) / 64;
+  int lo = ref[0], hi = ref[0];
+  for (int i = 1; i < m; i++) { lo = std::min(lo, ref[i]); hi = std::max(hi, ref[i]); }
+  std::vector<uint64_t> peq((size_t)(hi - lo + 2) * W, 0);  // last row: symbols absent from ref
+  for (int i = 0; i < m; i++) peq[(size_t)(ref[i] - lo) * W + i / 64] |= 1ull << (i % 64);
+  std::vector<uint64_t> P(W, ~0ull), M(W, 0ull);
+  const uint64_t last = 1ull << ((m - 1) % 64);
+  int score = m;
+  for (int j = 0; j < n; j++) {
+    const int c = hyp[j];
+    const uint64_t *eq = &peq[(size_t)((c >= lo && c <= hi) ? c - lo : hi - lo + 1) * W];
+    int hin = 1;
+    for (int b = 0; b < W; b++) {
+      const uint64_t Pv = P[b], Mv = M[b], hneg = hin < 0 ? 1ull : 0ull;
+      uint64_t Eq = eq[b];
+      const uint64_t Xv = Eq | Mv;
+      Eq |= hneg;
+      const uint64_t Xh = (((Eq & Pv) + Pv) ^ Pv) | Eq;
+      uint64_t Ph = Mv | ~(Xh | Pv);
+      uint64_t Mh = Pv & Xh;
+      const uint64_t hb = b == W - 1 ? last : (1ull << 63);
+      const int hout = (Ph & hb) ? 1 : ((Mh & hb) ? -1 : 0);
+      Ph = (Ph << 1) | (hin > 0 ? 1ull : 0ull);
+      Mh = (Mh << 1) | hneg;
+      P[b] = Mh | ~(Xv | Ph);
+      M[b] = Ph & Xv;
+      hin = hout;
+    }
+    score += hin;
+  }
+  return score;
+}
+
 // ---------------------------------------------------------------------------
 // plumbing
 // ---------------------------------------------------------------------------
@@ -987,16 +1030,7 @@ MinibatchStats NnetCtcUpdater::ComputeForMinibatch(const float *feats, int T_max
     }
     hyp.resize(F > 0 ? i : 0);
     // LevenshteinEditDistance, unit costs
-    std::vector<int> prev(hyp.size() + 1), cur(hyp.size() + 1);
-    for (size_t q = 0; q <= hyp.size(); q++) prev[q] = (int)q;
-    for (int a = 1; a <= L; a++) {
-      cur[0] = a;
-      for (size_t b = 1; b <= hyp.size(); b++)
-        cur[b] = std::min({prev[b - 1] + (flat_labels[off + a - 1] != hyp[b - 1]), prev[b] + 1,
-                           cur[b - 1] + 1});
-      std::swap(prev, cur);
-    }
-    err += prev[hyp.size()];
+    err += levenshtein(flat_labels + off, L, hyp.data(), (int)hyp.size());
     st.tot_weight += L;
     off += L;
   }

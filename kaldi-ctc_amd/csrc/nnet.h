@@ -341,6 +341,9 @@ struct MinibatchStats {
   double tot_objf = 0, tot_accuracy = 0, tot_weight = 0;
 };
 
+// kaldi::LevenshteinEditDistance (unit costs), bit-parallel (nnet.cpp)
+int levenshtein(const int *ref, int m, const int *hyp, int n);
+
 class NnetCtcUpdater {
  public:
   NnetCtcUpdater(Nnet *nnet, bool update);

@@ -228,6 +228,7 @@ struct RecParams {
   int allow_local;  // v4: hand off through the shared L2 when placement allows it
   int xpd;          // v4: XCD slots per direction (nwg = 32 * xpd workgroups)
   float *xch;       // v4: per-step exchange images [T][dirs][KG][Npad][16] (workspace)
+  int poll_sleep;   // v6: s_sleep between flag polls
 };
 
 // Phase stamps of the first kTraceSteps steps ([steps][grid][16]; thread 0 of every workgroup;
@@ -1333,7 +1334,7 @@ __device__ __forceinline__ unsigned *flag6(const RecParams &p, int d, int g, int
   return p.flags + 1024 + ((long)d * nwg + g) * kFlagStride;
 }
 __device__ __forceinline__ void wait_flags6(const unsigned *f0, int nwg, unsigned epoch, unsigned *err, int &bad,
-                                            int *bad_lds) {
+                                            int *bad_lds, int sleep = 1) {
   if (threadIdx.x < 64) {
     int spins = 0;
     while (true) {
@@ -1347,7 +1348,7 @@ __device__ __forceinline__ void wait_flags6(const unsigned *f0, int nwg, unsigne
         if (threadIdx.x == 0) *bad_lds = 1;
         break;
       }
-      __builtin_amdgcn_s_sleep(1);
+      if (sleep) __builtin_amdgcn_s_sleep(1);
     }
   }
   __syncthreads();
@@ -1504,7 +1505,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
     const int ks = T - 1 - k;  // steps done before this one
     REC_TRACE(ks, 0);
     if (ks > 0) {
-      wait_flags6(flag6(p, d, 0, NWG), NWG, (unsigned)(ks + 1), p.err, bad, &bad_lds);
+      wait_flags6(flag6(p, d, 0, NWG), NWG, (unsigned)(ks + 1), p.err, bad, &bad_lds, p.poll_sleep);
       REC_TRACE(ks, 1);
       const auto rs = rsrc(p.xch + (long)(ks - 1) * xstep, (unsigned)(xstep * 4));
       u32x4 v[PER];
@@ -1600,6 +1601,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ro, off, 0, 16);
       }
     }
+    REC_TRACE(ks, 7);
     signal_epoch(myflag, (unsigned)(ks + 2), local);
     REC_TRACE(ks, 4);
     rotate();
@@ -1748,7 +1750,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec6(RecParams p) {
     for (int ct = 0; ct < CT; ct++) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
     REC_TRACE(k, 0);
     if (k > 0) {
-      wait_flags6(flag6(p, d, 0, NWG), NWG, (unsigned)(k + 1), p.err, bad, &bad_lds);
+      wait_flags6(flag6(p, d, 0, NWG), NWG, (unsigned)(k + 1), p.err, bad, &bad_lds, p.poll_sleep);
       REC_TRACE(k, 1);
       const auto rs = rsrc(xch + (long)tp * XS, (unsigned)(XS * 2));
       u32x4 ah[KBW], al[KBW];
@@ -1823,6 +1825,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec6(RecParams p) {
       const long o = ((((long)d * KB + kb0) * 2 + sp) * 16 + sn) * 32 + koff;
       __builtin_amdgcn_raw_buffer_store_b128(v, rsrc(xch + (long)t * XS, (unsigned)(XS * 2)), (int)(o * 2), 0, 16);
     }
+    REC_TRACE(k, 7);
     signal_epoch(myflag, (unsigned)(k + 2), 0);
     REC_TRACE(k, 4);
 #pragma unroll
@@ -2203,6 +2206,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     const size_t lds = ver == 6 ? fwd6_lds_bytes(d, U) : fwd_lds_bytes(d, N, U);
     p.xpd = ver == 4 ? v4_xpd(d, U) : 1;
     p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
+    p.poll_sleep = env_int("KCTC_POLL_SLEEP", 1);
     const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : dirs * p.nwg);
     RecTrace tr;
     if (tr.arm("fwd", grid.x)) p.trace = tr.dev;
@@ -2267,6 +2271,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
       // fabric port; spread over the XCDs they use four)
       p.xpd = (p.nwg == kCusPerXcd && dirs <= 8 && env_int("KCTC_XCD6", 0)) ? 1 : 0;
       p.allow_local = env_int("KCTC_LOCAL", 1);
+      p.poll_sleep = env_int("KCTC_POLL_SLEEP", 1);
       p.xch = xch_acquire(sizeof(float) * (size_t)T * dirs * p.nwg * (16 * H + 64), s);
     } else {
       p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));

@@ -354,6 +354,11 @@ int kctc_nnet_train_simple(kctcNnet_t n, struct kctcEgsReader_ *r, long max_mini
   });
 }
 
+int kctc_levenshtein(const int *ref, int nref, const int *hyp, int nhyp) {
+  if ((nref > 0 && !ref) || (nhyp > 0 && !hyp)) return -1;
+  return kctc::nnet2::levenshtein(ref, nref, hyp, nhyp);
+}
+
 int kctc_format_input(const float *feats, const int *num_frames, int N, int dim, int T_max,
                       float *out) {
   return guarded([&] {

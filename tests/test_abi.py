@@ -89,6 +89,38 @@ def test_synth_minibatch_contract(kctc):
     np.testing.assert_array_equal(again[0], feats)
 
 
+def _dp_levenshtein(a, b):
+    """kaldi::LevenshteinEditDistance restated as the textbook DP (unit costs)."""
+    prev = list(range(len(b) + 1))
+    for i in range(1, len(a) + 1):
+        cur = [i] + [0] * len(b)
+        for j in range(1, len(b) + 1):
+            cur[j] = min(prev[j - 1] + (a[i - 1] != b[j - 1]), prev[j] + 1, cur[j - 1] + 1)
+        prev = cur
+    return prev[-1]
+
+
+def test_levenshtein_bitparallel_matches_dp(kctc):
+    """ComputeTotAccuracy's edit distance (Myers bit-vector, multi-word refs)
+    against the DP, on the shapes the accuracy sees: refs up to 639 labels
+    (10 words), hyps with and without the kept leading blank, empty sides."""
+    rng = np.random.default_rng(11)
+    cases = [([], []), ([], [3, 4]), ([1, 2], []), ([5], [5]), ([5], [6]), ([1, 2, 3], [1, 3]),
+             ([0, 1, 2], [1, 2])]
+    for m, n, A in ((63, 70, 5), (64, 64, 41), (65, 30, 3), (128, 200, 41), (200, 129, 2), (639, 700, 41)):
+        cases.append((list(rng.integers(0, A, m)), list(rng.integers(0, A, n))))
+    for m in (1, 17, 64, 100):  # near-identical sequences (small distances)
+        a = list(rng.integers(1, 41, m))
+        b = list(a)
+        for _ in range(3):
+            if b:
+                b.pop(int(rng.integers(0, len(b))))
+            b.insert(int(rng.integers(0, len(b) + 1)), int(rng.integers(0, 41)))
+        cases.append((a, b))
+    for a, b in cases:
+        assert kctc.levenshtein(a, b) == _dp_levenshtein(a, b), (len(a), len(b))
+
+
 def test_recipe_config_and_bad_configs(kctc):
     cfg = kctc.recipe_config()
     assert cfg.count("CuDNNRecurrentComponent") == 5 and cfg.count("ClipGradientComponent") == 5

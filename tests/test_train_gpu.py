@@ -57,16 +57,22 @@ def _oracle_spec(oracle, R, mode, H, dirs, D, A, thr, lr, repair_scale=1.0):
     return s
 
 
-@pytest.mark.parametrize("mode,H,thr,steps", [
-    (2, 64, 30.0, 2),     # BLSTM, recipe clip threshold (rarely clips)
-    (2, 64, 0.02, 3),     # every row clipped -> self-repair active on draws <= 0.5
-    (3, 48, 30.0, 2),     # BGRU
+@pytest.mark.parametrize("mode,H,thr,steps,pstd", [
+    (2, 64, 30.0, 2, 0.2),     # BLSTM, recipe clip threshold (rarely clips)
+    (2, 64, 0.02, 3, 0.2),     # every row clipped -> self-repair active on draws <= 0.5
+    (3, 48, 30.0, 2, 0.2),     # BGRU
+    # recipe widths: v6 recurrences + packed split-fp16 GEMMs (layer 2 input 512).
+    # Weights at 0.2 * sqrt(64 / H) so the recurrence is not driven into the
+    # saturated, rounding-amplifying regime (at 0.2 even the all-fp32 path
+    # differs from fp64 by ~1e-4 after two updates)
+    (2, 256, 30.0, 2, 0.1),    # BLSTM-256
+    (3, 256, 30.0, 2, 0.1),    # BGRU-256
 ])
-def test_train_steps_match_oracle(kctc, gpu, oracle, mode, H, thr, steps):
+def test_train_steps_match_oracle(kctc, gpu, oracle, mode, H, thr, steps, pstd):
     import torch
     R, D, A, T, N, lr = 2, 24, 11, 30, 4, 0.02
     cfg = kctc.recipe_config(num_rnn=R, input_dim=D, hidden=H, num_targets=A, rnn_mode=mode,
-                             learning_rate=lr, clipping_threshold=thr, param_stddev=0.2)
+                             learning_rate=lr, clipping_threshold=thr, param_stddev=pstd)
     net = kctc.Nnet(cfg, seed=5)
     net.set_repair_seed(99)
     draws = splitmix_uniforms(99, steps * R)
