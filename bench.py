@@ -170,7 +170,7 @@ def main():
     fam_flops, _ = model_flops(T, N, D, H, A, L)
     prof = {}
     if profile:
-        for fam in list(fam_flops) + ["x3_pack", "ctc_logz", "ctc_alpha_beta", "ctc_grad", "affine",
+        for fam in list(fam_flops) + ["x3_pack", "x3_pack_w", "ctc_logz", "ctc_alpha_beta", "ctc_grad", "affine",
                                       "clip_gradient", "update", "argmax", "scale"]:
             ms, n = net.profile(fam)
             if n:

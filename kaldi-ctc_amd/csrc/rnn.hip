@@ -229,6 +229,7 @@ struct RecParams {
   int xpd;          // v4: XCD slots per direction (nwg = 32 * xpd workgroups)
   float *xch;       // v4: per-step exchange images [T][dirs][KG][Npad][16] (workspace)
   int poll_sleep;   // v6: s_sleep between flag polls
+  int nopf;         // diagnostic (KCTC_DIAG_NOPF): skip the operand prefetch (wrong results)
 };
 
 // Phase stamps of the first kTraceSteps steps ([steps][grid][16]; thread 0 of every workgroup;
@@ -1520,7 +1521,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
     asm volatile("" ::: "memory");
     // behind the hand-off loads: next step's operands, last step's row-major dGates
     if (t_prev >= 0) e_store(t_prev);
-    if (k > 0) prefetch(k - 1);
+    if (k > 0 && !p.nopf) prefetch(k - 1);
     __syncthreads();
     if (has_e) {
       float dhr = 0.f;
@@ -1779,7 +1780,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec6(RecParams p) {
     asm volatile("" ::: "memory");
     // behind the hand-off loads: last step's row-major outputs, next step's input projection
     if (t_prev >= 0) out_store(t_prev);
-    if (k + 1 < T) gin_load(d == 0 ? t + 1 : t - 1, gnx);
+    if (k + 1 < T && !p.nopf) gin_load(d == 0 ? t + 1 : t - 1, gnx);
 #pragma unroll
     for (int ct = 0; ct < CT; ct++)
 #pragma unroll
@@ -2207,6 +2208,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.xpd = ver == 4 ? v4_xpd(d, U) : 1;
     p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
     p.poll_sleep = env_int("KCTC_POLL_SLEEP", 1);
+    p.nopf = env_int("KCTC_DIAG_NOPF", 0);
     const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : dirs * p.nwg);
     RecTrace tr;
     if (tr.arm("fwd", grid.x)) p.trace = tr.dev;
@@ -2272,6 +2274,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
       p.xpd = (p.nwg == kCusPerXcd && dirs <= 8 && env_int("KCTC_XCD6", 0)) ? 1 : 0;
       p.allow_local = env_int("KCTC_LOCAL", 1);
       p.poll_sleep = env_int("KCTC_POLL_SLEEP", 1);
+      p.nopf = env_int("KCTC_DIAG_NOPF", 0);
       p.xch = xch_acquire(sizeof(float) * (size_t)T * dirs * p.nwg * (16 * H + 64), s);
     } else {
       p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
@@ -2383,7 +2386,7 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     if (x3) {
       // the transposes, packed over the frames: dGates^T (per-gate exponents),
       // input^T (per-dim), and for dR the output shifted by one step per direction
-      ProfSpan ps(s, "x3_pack");
+      ProfSpan ps(s, "x3_pack_w");
       absmax_f32(s, DX, ldg, (int)TN, (int)(dirs * G4), nullptr, cm);
       x3p_pack_cols(s, DX, ldg, (int)TN, (int)(dirs * G4), 0, DXt, eDX, cm, 0.f);
       if (d.mode == kGru) {
