@@ -58,6 +58,19 @@ struct X3PArgs {
   float *ws = nullptr;  // split_k * batch * M * N floats
   int max_blocks = 0;
   int *tile_counter = nullptr;
+  int eA0 = 0, eB0 = 0;  // exponents used when eA / eB is null
+  // Streaming mode (stream_flags != null): the A rows are frames (t, n),
+  // row = t * stream_N + n, produced by a concurrently running bidirectional
+  // v6 forward recurrence; a row tile is computed only once direction 0 has
+  // published step t_max of the tile and direction 1 step T-1-t_min (flag
+  // lines of rnn.hip: word 32 * (d * nwg + g) holds the WG's epoch = step + 2).
+  // A is the producer's exchange-image array, read in place with sc1 loads
+  // (eA0 = 14, KB over both directions).  Row tiles are taken in readiness order.
+  // tile_counter is required; the grid must leave >= 64 CUs to the producer.
+  const unsigned *stream_flags = nullptr;
+  int stream_nwg = 0, stream_T = 0, stream_N = 0;
+  long stream_step = 0;              // halves per producer step image (A = image of step 0)
+  unsigned *stream_err = nullptr;    // set (bit 2) if the producer stops publishing
 };
 void gemm_x3p(hipStream_t s, const X3PArgs &g);
 // pack rows r < R of X (K values each, row stride ldx) -> out[b][r][KB][64],

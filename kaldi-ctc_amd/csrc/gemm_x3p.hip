@@ -47,6 +47,12 @@ struct PParams {
   float alpha, beta;
   float *ws;
   int *counter;
+  int eA0, eB0;
+  const unsigned *sflags;  // streaming mode: producer flag lines
+  int snwg, sT, sN;
+  int nrt;                 // row tiles
+  long sxs;                // halves per producer step image
+  unsigned *serr;          // producer's error word (wait timeout)
 };
 
 __device__ __forceinline__ void issue_tile(const _Float16 *__restrict__ P, int rows, int r0, int KB, int kb,
@@ -65,16 +71,108 @@ __device__ __forceinline__ void issue_tile(const _Float16 *__restrict__ P, int r
   }
 }
 
+// streaming A operand: the producer's exchange images, read in place.  Step t
+// of a bidirectional v6 forward recurrence holds h_t * 2^14 as fp16 hi/lo
+// A fragments, [kb = k / 32][hi | lo][16 rows n][32 k] halves (kb over both
+// directions), sxs halves per step; packed row r = t * sN + n.  The tile image
+// is the same swizzled one as issue_tile's, filled by sc1 register loads (the
+// rows were just published by other CUs) + ds_write_b128.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void load_tile_xch(const PParams &p, const _Float16 *__restrict__ X, int r0, int kb,
+                                              u32x4 (&reg)[4]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16 *>(X), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int r = (w * 4 + i) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (r & 7);
+    const int gr = min(r0 + r, p.M - 1);
+    const int t = gr / p.sN, n = gr - t * p.sN;
+    const long off = (long)t * p.sxs + (((long)kb * 2 + (c >> 2)) * 16 + n) * 32 + (c & 3) * 8;
+    reg[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off * 2), 0, 16 /* sc1 */);
+  }
+}
+__device__ __forceinline__ void store_tile_lds(unsigned char *dst, const u32x4 (&reg)[4]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 4; i++) *reinterpret_cast<u32x4 *>(dst + (w * 4 + i) * 1024 + lane * 16) = reg[i];
+}
+
 __device__ __forceinline__ halfx8 frag(const unsigned char *tile, int row, int chunk) {
   return *reinterpret_cast<const halfx8 *>(tile + row * ROWB + ((chunk ^ (row & 7)) << 4));
 }
 
-__device__ void x3p_tile(const PParams &p, unsigned char *lds, int id, int total, bool remap) {
-  const int q = total >> 3, rr = total & 7, xcd = id & 7, loc = id >> 3;
-  const int wl = remap ? (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc : id;
-  const int bz = wl / p.tiles, wg = wl - bz * p.tiles;
-  const int tn = wg % p.gx, tm = wg / p.gx;
-  const int b = bz % p.batch, ks = bz / p.batch;
+// Row tile of the i-th work slot in readiness order of a bidirectional
+// producer: tile rt (frames t0..t1) is complete once direction 0 has reached
+// t1 and direction 1 has reached T-1-t0, i.e. at step max(t1, T-1-t0): the
+// middle of the sequence first, then alternately outwards.
+__device__ __forceinline__ int stream_row_tile(int i, int nrt, int sT, int sN) {
+  // ready step of tile rt: max(t1(rt), T-1-t0(rt)); sort key, ties by rt.
+  // Binary-search-free: walk outwards from the middle tile.
+  const int tmid = (sT - 1) / 2;
+  const int mid = min(nrt - 1, (tmid * sN) / TB);
+  // interleave mid, mid-1, mid+1, mid-2, ... (exact ordering of ready steps
+  // is not required for correctness, only for overlap)
+  const int L = mid, R = nrt - 1 - mid;  // tiles left / right of the middle one
+  if (i > 2 * min(L, R)) return L < R ? mid + (i - L) : mid - (i - R);
+  const int k = (i + 1) / 2;
+  return (i & 1) ? mid - k : mid + k;
+}
+
+__device__ void x3p_wait_rows(const PParams &p, int m0, int *prog) {
+  // prog[0..1]: steps known published by directions 0 / 1 (LDS cache)
+  const int r1 = min(p.M, m0 + TB) - 1;
+  const int t0 = m0 / p.sN, t1 = r1 / p.sN;
+  const int need0 = t1, need1 = p.sT - 1 - t0;
+  if (prog[0] >= need0 && prog[1] >= need1) return;
+  if (threadIdx.x < 64) {
+    for (int spins = 0; spins < (1 << 24); spins++) {
+      unsigned m[2] = {0xffffffffu, 0xffffffffu};
+#pragma unroll
+      for (int d = 0; d < 2; d++)
+        for (int g = threadIdx.x; g < p.snwg; g += 64) {
+          const unsigned v = __hip_atomic_load(p.sflags + 32L * (d * p.snwg + g), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+          m[d] = min(m[d], v);
+        }
+#pragma unroll
+      for (int d = 0; d < 2; d++) {
+        unsigned v = m[d];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, o));
+        m[d] = v;
+      }
+      const int s0 = (int)m[0] - 2, s1 = (int)m[1] - 2;  // epochs: step + 2
+      if (s0 >= need0 && s1 >= need1) {
+        if (threadIdx.x == 0) { prog[0] = s0; prog[1] = s1; }
+        break;
+      }
+      if (spins == (1 << 24) - 1) {  // the producer stopped: flag it, finish on whatever is there
+        if (threadIdx.x == 0) { prog[0] = prog[1] = 1 << 30; if (p.serr) atomicOr(p.serr, 2u); }
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+  }
+  __syncthreads();
+}
+
+template <bool STREAM>
+__device__ void x3p_tile(const PParams &p, unsigned char *lds, int id, int total, bool remap, int *prog) {
+  int tn, tm, b, ks;
+  if (STREAM) {  // id = (row slot * batch + b) * gx + tn; no split-K
+    tn = id % p.gx;
+    const int rest = id / p.gx;
+    b = rest % p.batch;
+    tm = stream_row_tile(rest / p.batch, p.nrt, p.sT, p.sN);
+    ks = 0;
+  } else {
+    const int q = total >> 3, rr = total & 7, xcd = id & 7, loc = id >> 3;
+    const int wl = remap ? (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc : id;
+    const int bz = wl / p.tiles, wg = wl - bz * p.tiles;
+    tn = wg % p.gx; tm = wg / p.gx;
+    b = bz % p.batch; ks = bz / p.batch;
+  }
   const _Float16 *A = p.A + (long)b * p.sA;
   const _Float16 *B = p.B + (long)b * p.sB;
   const int m0 = tm * TB, n0 = tn * TB;
@@ -90,18 +188,26 @@ __device__ void x3p_tile(const PParams &p, unsigned char *lds, int id, int total
 #pragma unroll
     for (int j = 0; j < 4; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+  if (STREAM) x3p_wait_rows(p, m0, prog);
   // LDS: [2 stages][A tile | B tile]
+  u32x4 ra[4];
   if (nk > 0) {
-    issue_tile(A, p.M, m0, p.KB, kb0, lds);
+    if (STREAM) {
+      load_tile_xch(p, A, m0, kb0, ra);
+      store_tile_lds(lds, ra);
+    } else {
+      issue_tile(A, p.M, m0, p.KB, kb0, lds);
+    }
     issue_tile(B, p.N, n0, p.KB, kb0, lds + TILEB);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int it = 0; it < nk; it++) {
     unsigned char *cur = lds + (it & 1) * 2 * TILEB;
+    unsigned char *nxt = lds + ((it + 1) & 1) * 2 * TILEB;
     if (it + 1 < nk) {
-      unsigned char *nxt = lds + ((it + 1) & 1) * 2 * TILEB;
-      issue_tile(A, p.M, m0, p.KB, kb0 + it + 1, nxt);
+      if (STREAM) load_tile_xch(p, A, m0, kb0 + it + 1, ra);
+      else issue_tile(A, p.M, m0, p.KB, kb0 + it + 1, nxt);
       issue_tile(B, p.N, n0, p.KB, kb0 + it + 1, nxt + TILEB);
     }
     halfx8 ah[4], al[4], bh[4], bl[4];
@@ -127,25 +233,26 @@ __device__ void x3p_tile(const PParams &p, unsigned char *lds, int id, int total
     for (int i = 0; i < 4; i++)
 #pragma unroll
       for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+    if (STREAM && it + 1 < nk) store_tile_lds(nxt, ra);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
   // epilogue: acc[i][j][r] -> C[m0+wm+16i+4fq+r][n0+wn+16j+fr], times 2^-(eA + eB)
-  const int *eA = p.eA + (long)b * p.seA;
-  const int *eB = p.eB + (long)b * p.seB;
+  const int *eA = p.eA ? p.eA + (long)b * p.seA : nullptr;
+  const int *eB = p.eB ? p.eB + (long)b * p.seB : nullptr;
   int eb[4], ea[4][4];
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     const int col = n0 + wn + j * 16 + fr;
-    eb[j] = col < p.N ? eB[col] : 0;
+    eb[j] = col < p.N ? (p.eB ? eB[col] : p.eB0) : 0;
   }
 #pragma unroll
   for (int i = 0; i < 4; i++)
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int row = m0 + wm + i * 16 + fq * 4 + r;
-      ea[i][r] = row < p.M ? eA[row] : 0;
+      ea[i][r] = row < p.M ? (p.eA ? eA[row] : p.eA0) : 0;
     }
   if (p.split > 1) {
     float *W = p.ws + ((long)ks * p.batch + b) * (long)p.M * p.N;
@@ -188,12 +295,19 @@ __device__ void x3p_tile(const PParams &p, unsigned char *lds, int id, int total
     }
 }
 
+constexpr size_t kLdsBase = 2 * 2 * TILEB + 16, kLdsStream = 96 * 1024;
+__host__ __device__ inline int stream_total(const PParams &p) { return p.nrt * p.batch * p.gx; }
+
+template <bool STREAM>
 __global__ __launch_bounds__(NTH, 2) void gemm_x3p_kernel(PParams p) {
   // ONE shared array (a second __shared__ object can make hipcc wait vmcnt(0)
-  // before LDS reads while a DMA is in flight)
-  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * 2 * TILEB + 16];
+  // before LDS reads while a DMA is in flight); streaming launches ask for
+  // 96 KB of dynamic LDS on top so no block shares a CU with the producer's
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   int *next = reinterpret_cast<int *>(lds + 2 * 2 * TILEB);
-  const int total = p.tiles * p.batch * p.split;
+  int *prog = next + 1;
+  const int total = STREAM ? stream_total(p) : p.tiles * p.batch * p.split;
+  if (STREAM && threadIdx.x == 0) { prog[0] = -1; prog[1] = -1; }
   if (p.counter) {
     while (true) {
       if (threadIdx.x == 0) *next = atomicAdd(p.counter, 1);
@@ -201,11 +315,11 @@ __global__ __launch_bounds__(NTH, 2) void gemm_x3p_kernel(PParams p) {
       const int id = *next;
       __syncthreads();
       if (id >= total) break;
-      x3p_tile(p, lds, id, total, false);
+      x3p_tile<STREAM>(p, lds, id, total, false, prog);
     }
     return;
   }
-  for (int id = blockIdx.x; id < total; id += gridDim.x) x3p_tile(p, lds, id, total, true);
+  for (int id = blockIdx.x; id < total; id += gridDim.x) x3p_tile<STREAM>(p, lds, id, total, true, prog);
 }
 
 __global__ __launch_bounds__(256) void x3p_splitk_reduce(PParams p) {
@@ -369,8 +483,30 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
   int blocks = total;
   if (g.max_blocks > 0 && total > g.max_blocks) blocks = std::max(8, g.max_blocks / 8 * 8);
   p.counter = g.tile_counter;
+  p.eA0 = g.eA0; p.eB0 = g.eB0;
+  p.sflags = g.stream_flags; p.snwg = g.stream_nwg; p.sT = g.stream_T; p.sN = g.stream_N;
+  p.nrt = ceil_div(g.M, TB);
+  p.sxs = g.stream_step; p.serr = g.stream_err;
   if (p.counter) KCTC_HIP_CHECK(hipMemsetAsync(p.counter, 0, sizeof(int), s));
-  hipLaunchKernelGGL(gemm_x3p_kernel, dim3(blocks), dim3(NTH), 0, s, p);
+  static bool attr = false;  // dynamic LDS above 64 KB
+  if (!attr) {
+    KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_x3p_kernel<false>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBase));
+    KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_x3p_kernel<true>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsStream));
+    attr = true;
+  }
+  if (p.sflags) {
+    if (!p.counter || p.split > 1 || g.stream_N <= 0 || g.stream_step <= 0 ||
+        (long)g.stream_T * g.stream_step * 2 >= (1L << 31))
+      throw std::invalid_argument("gemm_x3p: bad streaming arguments");
+    // persistent blocks, each owning its CU's LDS, so the producer's
+    // workgroups always find free CUs (max_blocks = CUs left to this GEMM)
+    const int sb = std::min(stream_total(p), g.max_blocks > 0 ? g.max_blocks : 176);
+    hipLaunchKernelGGL(gemm_x3p_kernel<true>, dim3(sb), dim3(NTH), kLdsStream, s, p);
+    return;
+  }
+  hipLaunchKernelGGL(gemm_x3p_kernel<false>, dim3(blocks), dim3(NTH), kLdsBase, s, p);
   if (p.split > 1) {
     const long tot = (long)p.batch * p.M * p.N;
     hipLaunchKernelGGL(x3p_splitk_reduce, dim3((int)std::min<long>(2048, (tot + 255) / 256)), dim3(256), 0, s, p);

@@ -419,6 +419,30 @@ std::string CuDNNRecurrentComponent::Info() const {
 
 void CuDNNRecurrentComponent::Propagate(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &in,
                                         CuMatrixBase *out) const {
+  Forward(in, out, nullptr);
+}
+
+void CuDNNRecurrentComponent::PropagateChained(const CuMatrixBase &in, CuMatrixBase *out,
+                                               const CuDNNRecurrentComponent &next) const {
+  auto &dev = CuDevice::Instantiate();
+  const int N = mini_batch_ > 0 ? mini_batch_ : 1;
+  const int T = (int)(in.NumRows() / N);
+  if (!dev.side || next.mini_batch_ != N || next.desc_.D != OutputDim()) {
+    Forward(in, out, nullptr);
+    return;
+  }
+  next.reserve_.ensure(sizeof(float) * rnn_reserve_layout(next.desc_, T, N).total);
+  next.workspace_.ensure(rnn_workspace_bytes(next.desc_, T, N));
+  RnnFwdChain c;
+  c.d = &next.desc_; c.w = next.params_.f();
+  c.workspace = next.workspace_.p; c.ws_bytes = next.workspace_.bytes;
+  c.reserve = next.reserve_.p; c.res_bytes = next.reserve_.bytes;
+  c.side = dev.side;
+  Forward(in, out, &c);
+  next.input_projected_ = c.done;
+}
+
+void CuDNNRecurrentComponent::Forward(const CuMatrixBase &in, CuMatrixBase *out, RnnFwdChain *chain) const {
   // seq_length = rows / mini_batch, no masking (nnet-cudnn-component.cc:521-555)
   const int N = mini_batch_ > 0 ? mini_batch_ : 1;
   const int T = (int)(in.NumRows() / N);
@@ -427,9 +451,11 @@ void CuDNNRecurrentComponent::Propagate(const ChunkInfo &, const ChunkInfo &, co
   seq_length_ = T;
   reserve_.ensure(sizeof(float) * rnn_reserve_layout(desc_, T, N).total);
   workspace_.ensure(rnn_workspace_bytes(desc_, T, N));
+  const bool projected = input_projected_;
+  input_projected_ = false;
   ProfScope ps("layer_rnn_forward");
   int st = rnn_forward_training(desc_, S(), T, N, in.Data(), params_.f(), out->Data(), workspace_.p,
-                                workspace_.bytes, reserve_.p, reserve_.bytes, err_);
+                                workspace_.bytes, reserve_.p, reserve_.bytes, err_, chain, projected);
   if (st) throw std::runtime_error("rnn_forward_training failed: " + std::to_string(st));
 }
 
@@ -1049,7 +1075,17 @@ void NnetCtcUpdater::Propagate(int T, int N) {  // :136-169
       continue;
     }
     out.Resize((long)T * N, comp.OutputDim());
-    comp.Propagate(chunk_info_[c], chunk_info_[c + 1], in, &out);
+    // RNN -> identity-forward components -> RNN: the second one's input
+    // projection streams off the first one's last recurrence
+    const auto *rnn = dynamic_cast<const CuDNNRecurrentComponent *>(&comp);
+    const CuDNNRecurrentComponent *next = nullptr;
+    if (rnn) {
+      int c2 = c + 1;
+      while (c2 < C && nnet_->GetComponent(c2).IsIdentityForward()) c2++;
+      if (c2 < C) next = dynamic_cast<const CuDNNRecurrentComponent *>(&nnet_->GetComponent(c2));
+    }
+    if (next) rnn->PropagateChained(in, &out, *next);
+    else comp.Propagate(chunk_info_[c], chunk_info_[c + 1], in, &out);
   }
 }
 

@@ -222,6 +222,11 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   int side_gemm_blocks() const;
   const RnnDesc &Desc() const { return desc_; }
   void SetMiniBatch(int n) const { mini_batch_ = n; }  // Init(mini_batch) on change
+  // Propagate whose last recurrence also produces `next`'s layer-0 input
+  // projection on the side stream (rnn.h RnnFwdChain), `next` being the
+  // following RNN with only identity-forward components in between; `next`
+  // then skips that projection in its own Propagate.
+  void PropagateChained(const CuMatrixBase &in, CuMatrixBase *out, const CuDNNRecurrentComponent &next) const;
 
  private:
   void Init(Rng &rng);
@@ -232,7 +237,9 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   DevBuf params_, grad_;
   mutable DevBuf reserve_, workspace_;
   mutable int mini_batch_ = 0, seq_length_ = 0;
+  mutable bool input_projected_ = false;  // set by the previous component's PropagateChained
   unsigned *err_ = nullptr;
+  void Forward(const CuMatrixBase &in, CuMatrixBase *out, RnnFwdChain *chain) const;
 };
 
 class ClipGradientComponent : public Component {

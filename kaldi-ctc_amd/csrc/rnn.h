@@ -40,9 +40,28 @@ enum { KRNN_OK = 0, KRNN_BAD_PARAM = 1, KRNN_NOT_SUPPORTED = 2, KRNN_EXEC_FAILED
 
 // All calls are stream-ordered; `err` is a device word (0 = ok) that the
 // persistent kernels set on a bounded-spin timeout.
+// Forward chaining of stacked components: the NEXT RNN component's layer-0
+// input projection (the x3 GEMM of this call's output y) is computed on
+// `side` while this call's last recurrence is still running, reading the
+// recurrence's exchange images in place as their rows get published
+// (gemm_x3p streaming mode).  The fork / join with `s` happens inside; `done`
+// tells the caller whether the chain was taken -- if so it passes
+// input_projected = true to the next component's forward, which then skips
+// its layer-0 projection.
+struct RnnFwdChain {
+  const RnnDesc *d = nullptr;   // the consumer
+  const float *w = nullptr;     // its parameters
+  void *workspace = nullptr;    // its workspace / reserve (rnn_workspace_bytes, rnn_reserve_layout)
+  size_t ws_bytes = 0;
+  void *reserve = nullptr;
+  size_t res_bytes = 0;
+  hipStream_t side = nullptr;
+  bool done = false;
+};
 int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *w, float *y, void *workspace, size_t ws_bytes,
-                         void *reserve, size_t res_bytes, unsigned *err);
+                         void *reserve, size_t res_bytes, unsigned *err, RnnFwdChain *chain = nullptr,
+                         bool input_projected = false);
 int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float *y,
                       const float *dy, const float *w, float *dx, void *workspace,
                       size_t ws_bytes, void *reserve, size_t res_bytes, unsigned *err);

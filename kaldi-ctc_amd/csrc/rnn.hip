@@ -2135,9 +2135,78 @@ static int pick_bwd_u(const RnnDesc &d, int N) {
 // ---------------------------------------------------------------------------
 // host: forward training
 // ---------------------------------------------------------------------------
+namespace {
+// Can `c` consume the exchange images of this component's last forward
+// recurrence (v6, bidirectional) as its layer-0 projection input?
+bool chain_ok(const RnnDesc &d, int ver, int T, int N, const RnnFwdChain *c) {
+  if (!c || !c->d || !c->side || ver != 6 || d.dirs != 2 || !env_int("KCTC_FWD_STREAM", 1)) return false;
+  const RnnDesc &n = *c->d;
+  if (n.D != d.dirs * d.H || !use_x3(n.D) || N > 16) return false;
+  const long xs = 2L * (d.H / 32) * 2 * 16 * 32;  // halves per step image (rnn_fwd_rec6)
+  if ((long)T * xs * 2 >= (1L << 31)) return false;
+  return c->ws_bytes >= rnn_workspace_bytes(n, T, N) &&
+         c->res_bytes >= sizeof(float) * (size_t)rnn_reserve_layout(n, T, N).total;
+}
+
+// Layer-0 projection of the consumer, streamed off the producer's exchange images.
+void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipStream_t s, int T, int N, RnnFwdChain &c,
+                       unsigned *err) {
+  static thread_local hipEvent_t fork_ev = nullptr;
+  if (!fork_ev) KCTC_HIP_CHECK(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
+  KCTC_HIP_CHECK(hipEventRecord(fork_ev, s));  // after the producer's flag reset
+  KCTC_HIP_CHECK(hipStreamWaitEvent(c.side, fork_ev, 0));
+  const RnnDesc &n = *c.d;
+  const int NW = n.nw(), G = NW * n.H, Din = n.D, KB = Din / 32;
+  const long pl0 = n.lin_offset(0, 0, false), pls = n.pl_size(0);
+  const float *wl = c.w + pl0;
+  const PackLay pl = pack_layout(n, T, N);
+  _Float16 *Bp = pk<_Float16>(c.workspace, n, T, N, pl.b);
+  int *eB = pk<int>(c.workspace, n, T, N, pl.eb);
+  {
+    ProfSpan ps(c.side, "x3_pack_chain");
+    x3p_pack_rows(c.side, wl, Din, G, Din, Bp, eB, 0.f, n.dirs, pls, (long)G * KB * 64, (long)G);
+  }
+  const RnnReserveLayout lay = rnn_reserve_layout(n, T, N);
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    KCTC_HIP_CHECK(hipGetDevice(&dev));
+    KCTC_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  X3PArgs x;
+  x.M = T * N; x.N = G; x.KB = KB;
+  x.A = reinterpret_cast<const _Float16 *>(p.xch); x.eA0 = 14;
+  x.B = Bp; x.eB = eB;
+  x.C = static_cast<float *>(c.reserve) + lay.G; x.ldc = (long)n.dirs * G;
+  x.bias = wl + (n.lin_offset(0, 0, true) - pl0);
+  x.bias2 = n.mode == kGru ? nullptr : wl + (n.lin_offset(0, NW, true) - pl0);
+  x.batch = n.dirs; x.sB = (long)G * KB * 64; x.seB = G; x.sC = G; x.sBias = pls;
+  x.tile_counter = reinterpret_cast<int *>(static_cast<char *>(c.workspace) + flags_offset(n, T, N));
+  x.stream_flags = p.flags + 1024; x.stream_nwg = p.nwg; x.stream_T = T; x.stream_N = N;
+  x.stream_step = 2L * (d.H / 32) * 2 * 16 * 32; x.stream_err = err;
+  // every producer workgroup needs a CU of its own (96 KB LDS); the GEMM's
+  // persistent blocks (96 KB each) take the rest minus a margin
+  x.max_blocks = env_int("KCTC_STREAM_BLOCKS", std::max(8, cus - d.dirs * p.nwg - 16));
+  {
+    ProfSpan ps(c.side, "fwd_proj_stream");
+    gemm_x3p(c.side, x);
+  }
+  c.done = true;
+}
+
+void join_chain(hipStream_t s, const RnnFwdChain &c) {
+  static thread_local hipEvent_t join_ev = nullptr;
+  if (!join_ev) KCTC_HIP_CHECK(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
+  KCTC_HIP_CHECK(hipEventRecord(join_ev, c.side));
+  KCTC_HIP_CHECK(hipStreamWaitEvent(s, join_ev, 0));
+}
+}  // namespace
+
 int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *w, float *y, void *workspace, size_t ws_bytes,
-                         void *reserve, size_t res_bytes, unsigned *err) {
+                         void *reserve, size_t res_bytes, unsigned *err, RnnFwdChain *chain,
+                         bool input_projected) {
+  if (chain) chain->done = false;
   if (T <= 0 || N <= 0 || N > 16 * kMaxRT || d.H % 16) return KRNN_NOT_SUPPORTED;
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
   if (res_bytes < sizeof(float) * (size_t)lay.total) return KRNN_BAD_PARAM;
@@ -2165,13 +2234,15 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     GemmArgs g;
     g.transA = false; g.transB = true;
     g.M = (int)TN; g.N = NW * H; g.K = Din;
+    const bool skip_proj = l == 0 && input_projected;  // streamed by the previous component
     g.A = in; g.lda = Din;
     g.B = wl; g.ldb = Din;
     g.C = R0 + lay.G; g.ldc = (long)dirs * NW * H;
     g.bias = wl + bW;
     g.bias2 = (d.mode == kGru) ? nullptr : wl + bR;
     g.batch = dirs; g.strideA = 0; g.strideB = pls; g.strideC = (long)NW * H; g.strideBias = pls;
-    if (use_x3(Din)) {
+    if (skip_proj) {
+    } else if (use_x3(Din)) {
       // input rows (a lower stacked layer's output is bounded; the component
       // input and RELU outputs get per-row exponents) and W rows, packed
       const PackLay pl = pack_layout(d, T, N);
@@ -2212,12 +2283,15 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : dirs * p.nwg);
     RecTrace tr;
     if (tr.arm("fwd", grid.x)) p.trace = tr.dev;
+    const bool chained = l == d.layers - 1 && chain_ok(d, ver, T, N, chain);
+    if (chained) launch_chain_proj(d, p, s, T, N, *chain, err);
     {
       ProfSpan ps(s, "rnn_fwd_rec");
       if (ver == 6) launch_fwd6(d.mode, p, grid, lds, s);
       else launch_rec(true, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
+    if (chained) join_chain(s, *chain);
     tr.dump("fwd", s, grid.x, p.nwg, T, dirs, ver, ver == 6 ? 0 : p.xpd);
     in = out;
   }

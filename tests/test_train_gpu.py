@@ -135,3 +135,32 @@ def test_model_write_read_roundtrip(kctc, gpu, tmp_path):
     feats, nf, fl, ll = kctc.synth_minibatch(3, T, N, D, A, 0.2)
     f = torch.from_numpy(feats).to(gpu)
     assert net.compute_objf(f, T, N, nf, fl, ll) == net2.compute_objf(f, T, N, nf, fl, ll)
+
+
+@pytest.mark.parametrize("mode,H,T,N", [(2, 512, 300, 16), (2, 256, 97, 5), (3, 256, 64, 16)])
+def test_forward_stream_projection_matches_unstreamed(kctc, gpu, monkeypatch, mode, H, T, N):
+    """RNN -> ClipGradient -> RNN: the second RNN's input projection computed
+    while the first one's last recurrence runs (gemm_x3p streaming off the
+    exchange images, KCTC_FWD_STREAM=1, the default) against the projection
+    after it (KCTC_FWD_STREAM=0).  Same split-fp16 products (the images carry
+    h * 2^14, the packed copy h * 2^13): equal up to fp32 rounding of the
+    epilogue; many row tiles, ragged N, LSTM and GRU."""
+    import torch
+    D, A = 40, 41
+    cfg = kctc.recipe_config(num_rnn=3, input_dim=D, hidden=H, num_targets=A, rnn_mode=mode,
+                             learning_rate=1e-3, param_stddev=0.05)
+    feats, nf, fl, ll = kctc.synth_minibatch(17, T, N, D, A, 0.125)
+    f = torch.from_numpy(feats).to(gpu)
+    res = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("KCTC_FWD_STREAM", flag)
+        net = kctc.Nnet(cfg, seed=8)
+        o = net.compute_objf(f, T, N, nf, fl, ll)[0]
+        net.train_step(f, T, N, nf, fl, ll)
+        o2 = net.compute_objf(f, T, N, nf, fl, ll)[0]
+        res[flag] = (o, o2, [net.get_params(c).astype(np.float64) for c in range(net.num_components)
+                             if net.num_params(c) > 0])
+    np.testing.assert_allclose(res["1"][0], res["0"][0], rtol=2e-6)
+    np.testing.assert_allclose(res["1"][1], res["0"][1], rtol=2e-6)
+    for a, b in zip(res["1"][2], res["0"][2]):
+        assert rel_err(a, b) < 1e-6
