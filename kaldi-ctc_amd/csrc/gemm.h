@@ -73,6 +73,34 @@ struct X3PArgs {
   unsigned *stream_err = nullptr;    // set (bit 2) if the producer stops publishing
 };
 void gemm_x3p(hipStream_t s, const X3PArgs &g);
+
+// C = sum over the two directions d of A_d B_d^T, where A_d = columns
+// [d * edoff, d * edoff + 32 KB) of the rows of E, produced step by step by a
+// concurrently running bidirectional v6 backward recurrence (flag lines as
+// X3PArgs streaming; the rows of step s are complete at epoch s + 3, the last
+// step's at T + 2).  One persistent launch packs the rows as they appear
+// (into Ap / eA) and runs the x3 GEMM tiles per direction; the two partials
+// of a tile are added in a fixed order.  B_d packed along K (x3p_pack_cols).
+struct X3PBwdStream {
+  int M = 0, N = 0, KB = 0;            // frames (T * Nf), output columns, kb per direction
+  const float *E = nullptr;
+  long lde = 0, edoff = 0;
+  _Float16 *Ap = nullptr;              // [2][M][KB][64]
+  int *eA = nullptr;                   // [2][M]
+  const _Float16 *B = nullptr;
+  const int *eB = nullptr;
+  long sB = 0, seB = 0;
+  float *C = nullptr;
+  long ldc = 0;
+  float *part = nullptr;               // [M][N] floats
+  int *cnt = nullptr;                  // x3p_bwd_stream_ints(M, N) ints (zeroed here)
+  const unsigned *flags = nullptr;     // producer flag lines
+  int nwg = 0, T = 0, Nf = 0;
+  unsigned *err = nullptr;
+  int blocks = 0;                      // persistent blocks (each takes a CU: 96 KB LDS)
+};
+size_t x3p_bwd_stream_ints(int M, int N);
+void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a);
 // pack rows r < R of X (K values each, row stride ldx) -> out[b][r][KB][64],
 // exponent per row into eout (bound > 0: from the bound, else the row max)
 void x3p_pack_rows(hipStream_t s, const float *X, long ldx, int R, int K, _Float16 *out, int *eout, float bound,

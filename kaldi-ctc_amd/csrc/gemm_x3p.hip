@@ -31,6 +31,7 @@ constexpr int TB = 128;          // tile rows (M) = tile cols (N)
 constexpr int NTH = 256;
 constexpr int ROWB = 128;        // bytes per packed row block (64 halves)
 constexpr int TILEB = TB * ROWB; // 16 KB per operand tile per stage
+constexpr unsigned long long kWaitTicks = 300000000ull;  // streaming waits: 3 s of the 100 MHz clock
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 typedef _Float16 halfx4 __attribute__((ext_vector_type(4)));
@@ -53,8 +54,16 @@ struct PParams {
   int nrt;                 // row tiles
   long sxs;                // halves per producer step image
   unsigned *serr;          // producer's error word (wait timeout)
+  // backward stream (x3p_bwd_stream_kernel)
+  const float *E;          // source rows of direction d: E + row * lde + d * edoff (KB * 32 floats)
+  long lde, edoff;
+  int P;                   // pack jobs per row tile
+  int *done;               // [2][nrt] pack jobs finished
+  int *arrive;             // [nrt][gx] direction partials arrived (+1) / partial published (+2)
+  float *part;             // [M][N] the first direction's partial
 };
 
+template <int AUX = 0>
 __device__ __forceinline__ void issue_tile(const _Float16 *__restrict__ P, int rows, int r0, int KB, int kb,
                                            unsigned char *dst) {
   // wave w fills rows [32 w, 32 w + 32) of the tile: 4 instructions of 8 rows x 128 B
@@ -67,7 +76,7 @@ __device__ __forceinline__ void issue_tile(const _Float16 *__restrict__ P, int r
     int gr = r0 + r;
     gr = gr < rows ? gr : rows - 1;  // rows past the edge: any valid row (results discarded)
     const _Float16 *src = P + ((long)gr * KB + kb) * 64 + c * 8;
-    __builtin_amdgcn_global_load_lds(src, dst + q * 1024, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(src, dst + q * 1024, 16, 0, AUX);
   }
 }
 
@@ -119,60 +128,159 @@ __device__ __forceinline__ int stream_row_tile(int i, int nrt, int sT, int sN) {
   return (i & 1) ? mid - k : mid + k;
 }
 
+// ---- waits on other workgroups ------------------------------------------
+// All polling is done by wave 0 with every lane active and every exit
+// decision made wave-uniform (readfirstlane), and the waves choose between
+// polling and waiting on the barrier by a scalar branch on their wave index.
+// (Thread-0 spin loops followed by a barrier let the compiler structure the
+// barrier into exec-masked control flow: waves 1-3 then ran on without wave
+// 0, observed as a hang on the GPU.)
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+__device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, o));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+// wave-level: true once every flag word f[32 g], g < nwg, holds >= need
+// (false after a timeout or another party's error; then err bit 2 is set)
+__device__ __forceinline__ unsigned wave_flags_min(const unsigned *f, int nwg) {
+  unsigned m = 0xffffffffu;
+  for (int g = threadIdx.x & 63; g < nwg; g += 64)
+    m = min(m, __hip_atomic_load(f + 32L * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  return wave_min_u32(m);
+}
+__device__ __forceinline__ bool wave_timed_out(unsigned *err, int spins, unsigned long long t0) {
+  if ((spins & 255) != 255) return false;
+  const unsigned e = err ? __builtin_amdgcn_readfirstlane(__hip_atomic_load(err, __ATOMIC_RELAXED,
+                                                                            __HIP_MEMORY_SCOPE_AGENT)) : 0u;
+  return e != 0u || __builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks;
+}
+__device__ __forceinline__ void wave_fail(unsigned *err) {
+  if ((threadIdx.x & 63) == 0 && err) atomicOr(err, 2u);
+}
+
+// (Inside the polling loops every branch is wave-uniform; the single-lane
+// stores of the outcome come after the loop: a lane-0 store in front of a
+// `break` let the compiler leave lane 0 of wave 0 switched off, observed as
+// EXEC = ...fffe and a workgroup running on without its thread 0.)
 __device__ void x3p_wait_rows(const PParams &p, int m0, int *prog) {
-  // prog[0..1]: steps known published by directions 0 / 1 (LDS cache)
+  // prog[0..1]: steps known published by directions 0 / 1 (LDS cache; every
+  // wave reads it before the barrier, wave 0 writes it only after)
   const int r1 = min(p.M, m0 + TB) - 1;
   const int t0 = m0 / p.sN, t1 = r1 / p.sN;
   const int need0 = t1, need1 = p.sT - 1 - t0;
-  if (prog[0] >= need0 && prog[1] >= need1) return;
-  if (threadIdx.x < 64) {
-    for (int spins = 0; spins < (1 << 24); spins++) {
-      unsigned m[2] = {0xffffffffu, 0xffffffffu};
-#pragma unroll
-      for (int d = 0; d < 2; d++)
-        for (int g = threadIdx.x; g < p.snwg; g += 64) {
-          const unsigned v = __hip_atomic_load(p.sflags + 32L * (d * p.snwg + g), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-          m[d] = min(m[d], v);
-        }
-#pragma unroll
-      for (int d = 0; d < 2; d++) {
-        unsigned v = m[d];
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, o));
-        m[d] = v;
-      }
-      const int s0 = (int)m[0] - 2, s1 = (int)m[1] - 2;  // epochs: step + 2
-      if (s0 >= need0 && s1 >= need1) {
-        if (threadIdx.x == 0) { prog[0] = s0; prog[1] = s1; }
-        break;
-      }
-      if (spins == (1 << 24) - 1) {  // the producer stopped: flag it, finish on whatever is there
-        if (threadIdx.x == 0) { prog[0] = prog[1] = 1 << 30; if (p.serr) atomicOr(p.serr, 2u); }
-        break;
-      }
+  const bool ok = __builtin_amdgcn_readfirstlane(prog[0] >= need0 && prog[1] >= need1);
+  __syncthreads();
+  if (ok) return;
+  if (wave_id() == 0) {
+    const unsigned long long ts = __builtin_amdgcn_s_memrealtime();
+    int s0 = 0, s1 = 0, spins = 0;
+    bool failed = false;
+    while (true) {
+      s0 = (int)wave_flags_min(p.sflags, p.snwg) - 2;  // epochs: step + 2
+      s1 = (int)wave_flags_min(p.sflags + 32L * p.snwg, p.snwg) - 2;
+      if (s0 >= need0 && s1 >= need1) break;
+      failed = wave_timed_out(p.serr, spins++, ts);
+      if (failed) break;  // the producer stopped: flag it, finish on whatever is there
       __builtin_amdgcn_s_sleep(8);
     }
+    if (failed) s0 = s1 = 1 << 30;
+    if (threadIdx.x == 0) { prog[0] = s0; prog[1] = s1; }
+    if (failed) wave_fail(p.serr);
   }
   __syncthreads();
 }
 
-template <bool STREAM>
-__device__ void x3p_tile(const PParams &p, unsigned char *lds, int id, int total, bool remap, int *prog) {
-  int tn, tm, b, ks;
-  if (STREAM) {  // id = (row slot * batch + b) * gx + tn; no split-K
-    tn = id % p.gx;
-    const int rest = id / p.gx;
-    b = rest % p.batch;
-    tm = stream_row_tile(rest / p.batch, p.nrt, p.sT, p.sN);
-    ks = 0;
-  } else {
-    const int q = total >> 3, rr = total & 7, xcd = id & 7, loc = id >> 3;
-    const int wl = remap ? (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc : id;
-    const int bz = wl / p.tiles, wg = wl - bz * p.tiles;
-    tn = wg % p.gx; tm = wg / p.gx;
-    b = bz % p.batch; ks = bz / p.batch;
+// ---- backward stream helpers -------------------------------------------
+// wave 0 waits for a device counter to reach v, then the workgroup barrier
+__device__ __forceinline__ void wait_count(const int *a, int v, unsigned *err) {
+  if (wave_id() == 0) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool failed = false;
+    int i = 0;
+    while (true) {
+      const int x = __builtin_amdgcn_readfirstlane(__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if (x >= v) break;
+      failed = wave_timed_out(err, i++, t0);
+      if (failed) break;
+      __builtin_amdgcn_s_sleep(4);
+    }
+    if (failed) wave_fail(err);
   }
+  __syncthreads();
+}
+
+// wait until every workgroup of producer direction d has published epoch
+// >= need (seen[d]: the last minimum seen, LDS)
+__device__ void wait_epoch(const PParams &p, int d, int need, int *seen) {
+  const bool ok = __builtin_amdgcn_readfirstlane(seen[d] >= need);
+  __syncthreads();
+  if (ok) return;
+  if (wave_id() == 0) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool failed = false;
+    int m = 0, spins = 0;
+    while (true) {
+      m = (int)wave_flags_min(p.sflags + 32L * d * p.snwg, p.snwg);
+      if (m >= need) break;
+      failed = wave_timed_out(p.serr, spins++, t0);
+      if (failed) break;
+      __builtin_amdgcn_s_sleep(8);
+    }
+    if (threadIdx.x == 0) seen[d] = failed ? 1 << 30 : m;
+    if (failed) wave_fail(p.serr);
+  }
+  __syncthreads();
+}
+
+// the two directions' partial products of output tile (tm, tn) meet here:
+// the first to arrive publishes its partial (sc1), the second adds it and
+// writes C.  dx = part0 + part1 either way (fp addition commutes), so the
+// result does not depend on the order of arrival.
+__device__ __forceinline__ void bwd_combine(const PParams &p, floatx4 (&acc)[4][4], const int (&ea)[4][4], const int (&eb)[4],
+                            int tm, int tn, int m0, int n0, int wm, int wn, int fr, int fq, int *bc) {
+  int *arr = p.arrive + (long)tm * p.gx + tn;
+  if (threadIdx.x == 0) *bc = __hip_atomic_fetch_add(arr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const bool first = __builtin_amdgcn_readfirstlane(*bc) == 0;
+  const auto rp = __builtin_amdgcn_make_buffer_rsrc(p.part, 0, 0x7fffffff, 0x00020000);
+  if (!first) wait_count(arr, 4, p.serr);
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int col = n0 + wn + j * 16 + fr;
+      if (col >= p.N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = m0 + wm + i * 16 + fq * 4 + r;
+        if (row >= p.M) continue;
+        const float v = ldexpf(acc[i][j][r], -(ea[i][r] + eb[j]));
+        const int off = (int)(((long)row * p.N + col) * 4);
+        if (first) {
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rp, off, 0, 16);
+        } else {
+          const float o = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rp, off, 0, 16));
+          p.C[(long)row * p.ldc + col] = v + o;
+        }
+      }
+    }
+  if (first) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(arr, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// SM (source mode): 0 packed A via LDS-DMA; 1 A = a forward producer's
+// exchange images (sc1 register loads); 2 packed A just written by other CUs
+// (LDS-DMA with sc1, exponents read with sc1) and the two-direction combine
+// epilogue of the backward stream.
+template <int SM>
+__device__ __forceinline__ void x3p_tile(const PParams &p, unsigned char *lds, int tm, int tn, int b, int ks, int *prog) {
+  constexpr bool STREAM = SM == 1;
   const _Float16 *A = p.A + (long)b * p.sA;
   const _Float16 *B = p.B + (long)b * p.sB;
   const int m0 = tm * TB, n0 = tn * TB;
@@ -196,7 +304,7 @@ __device__ void x3p_tile(const PParams &p, unsigned char *lds, int id, int total
       load_tile_xch(p, A, m0, kb0, ra);
       store_tile_lds(lds, ra);
     } else {
-      issue_tile(A, p.M, m0, p.KB, kb0, lds);
+      issue_tile<SM == 2 ? 16 : 0>(A, p.M, m0, p.KB, kb0, lds);
     }
     issue_tile(B, p.N, n0, p.KB, kb0, lds + TILEB);
   }
@@ -207,7 +315,7 @@ __device__ void x3p_tile(const PParams &p, unsigned char *lds, int id, int total
     unsigned char *nxt = lds + ((it + 1) & 1) * 2 * TILEB;
     if (it + 1 < nk) {
       if (STREAM) load_tile_xch(p, A, m0, kb0 + it + 1, ra);
-      else issue_tile(A, p.M, m0, p.KB, kb0 + it + 1, nxt);
+      else issue_tile<SM == 2 ? 16 : 0>(A, p.M, m0, p.KB, kb0 + it + 1, nxt);
       issue_tile(B, p.N, n0, p.KB, kb0 + it + 1, nxt + TILEB);
     }
     halfx8 ah[4], al[4], bh[4], bl[4];
@@ -252,8 +360,15 @@ __device__ void x3p_tile(const PParams &p, unsigned char *lds, int id, int total
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int row = m0 + wm + i * 16 + fq * 4 + r;
-      ea[i][r] = row < p.M ? (p.eA ? eA[row] : p.eA0) : 0;
+      ea[i][r] = row >= p.M ? 0
+                 : SM == 2  ? __hip_atomic_load(eA + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                 : p.eA     ? eA[row]
+                            : p.eA0;
     }
+  if (SM == 2) {
+    bwd_combine(p, acc, ea, eb, tm, tn, m0, n0, wm, wn, fr, fq, prog);
+    return;
+  }
   if (p.split > 1) {
     float *W = p.ws + ((long)ks * p.batch + b) * (long)p.M * p.N;
 #pragma unroll
@@ -298,11 +413,20 @@ __device__ void x3p_tile(const PParams &p, unsigned char *lds, int id, int total
 constexpr size_t kLdsBase = 2 * 2 * TILEB + 16, kLdsStream = 96 * 1024;
 __host__ __device__ inline int stream_total(const PParams &p) { return p.nrt * p.batch * p.gx; }
 
+__device__ __forceinline__ void decode_tile(const PParams &p, int id, int total, bool remap, int &tm, int &tn,
+                                            int &b, int &ks) {
+  const int q = total >> 3, rr = total & 7, xcd = id & 7, loc = id >> 3;
+  const int wl = remap ? (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc : id;
+  const int bz = wl / p.tiles, wg = wl - bz * p.tiles;
+  tn = wg % p.gx; tm = wg / p.gx;
+  b = bz % p.batch; ks = bz / p.batch;
+}
+
 template <bool STREAM>
 __global__ __launch_bounds__(NTH, 2) void gemm_x3p_kernel(PParams p) {
   // ONE shared array (a second __shared__ object can make hipcc wait vmcnt(0)
   // before LDS reads while a DMA is in flight); streaming launches ask for
-  // 96 KB of dynamic LDS on top so no block shares a CU with the producer's
+  // 96 KB so that no block shares a CU with a producer workgroup
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   int *next = reinterpret_cast<int *>(lds + 2 * 2 * TILEB);
   int *prog = next + 1;
@@ -312,14 +436,30 @@ __global__ __launch_bounds__(NTH, 2) void gemm_x3p_kernel(PParams p) {
     while (true) {
       if (threadIdx.x == 0) *next = atomicAdd(p.counter, 1);
       __syncthreads();
-      const int id = *next;
+      const int id = __builtin_amdgcn_readfirstlane(*next);
       __syncthreads();
       if (id >= total) break;
-      x3p_tile<STREAM>(p, lds, id, total, false, prog);
+      int tm, tn, b, ks;
+      if (STREAM) {  // id = (row slot * batch + b) * gx + tn; no split-K
+        tn = id % p.gx;
+        const int rest = id / p.gx;
+        b = rest % p.batch;
+        tm = stream_row_tile(rest / p.batch, p.nrt, p.sT, p.sN);
+        x3p_tile<1>(p, lds, tm, tn, b, 0, prog);
+      } else {
+        decode_tile(p, id, total, false, tm, tn, b, ks);
+        x3p_tile<0>(p, lds, tm, tn, b, ks, prog);
+      }
     }
     return;
   }
-  for (int id = blockIdx.x; id < total; id += gridDim.x) x3p_tile<STREAM>(p, lds, id, total, true, prog);
+  if (!STREAM) {
+    for (int id = blockIdx.x; id < total; id += gridDim.x) {
+      int tm, tn, b, ks;
+      decode_tile(p, id, total, true, tm, tn, b, ks);
+      x3p_tile<0>(p, lds, tm, tn, b, ks, prog);
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void x3p_splitk_reduce(PParams p) {
@@ -400,6 +540,92 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(const float *__restrict_
     }
   }
   if (lane == 0 && eout) eout[(long)b * sE + r] = e;
+}
+
+// ---- backward stream: pack jobs + GEMM jobs in one persistent launch ----
+// Rows of direction d of a backward recurrence's dGates (E) become available
+// step by step (direction 0 from t = T-1 down, direction 1 from t = 0 up).
+// Per (row tile, direction) slot: P pack jobs (rows -> packed hi/lo with a
+// per-row exponent, sc1 stores, then done[d][rt] += 1) and gx GEMM jobs
+// (wait done == P, then the tile with sc1 LDS-DMA, combine epilogue).  Slots
+// alternate directions in production order; jobs are taken from one counter,
+// so a GEMM job only ever waits for pack jobs that running blocks own.
+template <int KW>
+__device__ __forceinline__ void bwd_pack_rows(const PParams &p, int d, int r0, int r1) {
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int K = p.KB * 32;
+  for (int r = r0 + w; r < r1; r += 4) {
+    const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p.E + (long)r * p.lde + d * p.edoff), 0,
+                                                      K * 4, 0x00020000);
+    floatx4 v[KW];
+    float mx = 0.f;
+#pragma unroll
+    for (int i = 0; i < KW; i++) {
+      const int k = 4 * lane + 256 * i;
+      v[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (k < K) v[i] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rx, k * 4, 0, 16));
+      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[i][0]), fabsf(v[i][1])), fmaxf(fabsf(v[i][2]), fabsf(v[i][3]))));
+    }
+    mx = wave_max_l63(mx);
+    const int e = split_exp_d(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 63)));
+    const auto ro = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16 *>(p.A) + (long)d * p.sA + (long)r * p.KB * 64, 0, p.KB * 128,
+                                                      0x00020000);
+#pragma unroll
+    for (int i = 0; i < KW; i++) {
+      const int k = 4 * lane + 256 * i;
+      if (k < K) {
+        halfx4 h, l;
+        split4(v[i], e, h, l);
+        const int kb = k >> 5, off = k & 31;
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h), ro, (kb * 64 + off) * 2, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, l), ro, (kb * 64 + 32 + off) * 2, 0, 16);
+      }
+    }
+    if (lane == 0)
+      __hip_atomic_store(const_cast<int *>(p.eA) + (long)d * p.seA + r, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <int KW>
+__global__ __launch_bounds__(NTH, 2) void x3p_bwd_stream_kernel(PParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  int *next = reinterpret_cast<int *>(lds + 2 * 2 * TILEB);
+  int *seen = next + 1;  // [2] producer epochs seen
+  int *bc = next + 3;    // combine broadcast
+  if (threadIdx.x == 0) { seen[0] = 0; seen[1] = 0; }
+  const int J = p.P + p.gx, total = 2 * p.nrt * J, rows_per = TB / p.P;
+  while (true) {
+    if (threadIdx.x == 0) *next = atomicAdd(p.counter, 1);
+    __syncthreads();
+    const int id = __builtin_amdgcn_readfirstlane(*next);
+    __syncthreads();
+    if (id >= total) break;
+    const int slot = id / J, r = id - slot * J, d = slot & 1, rank = slot >> 1;
+    const int rt = d == 0 ? p.nrt - 1 - rank : rank;
+    if (r < p.P) {
+      const int ra = rt * TB + r * rows_per, rb = min(p.M, ra + rows_per);
+      if (ra < rb) {
+        // E rows of step s are stored one step later: complete at epoch s + 3
+        // (s = steps done before it; the last step gets epoch T + 2 at exit)
+        const int ta = ra / p.sN, tb = (rb - 1) / p.sN;
+        wait_epoch(p, d, d == 0 ? p.sT + 2 - ta : tb + 3, seen);
+        bwd_pack_rows<KW>(p, d, ra, rb);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_fetch_add(p.done + d * p.nrt + rt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // a barrier after the lane-0 atomic: with the atomic as the last thing
+      // in the body hipcc structured the job loop as divergent (the loop latch
+      // masks lanes off), which left lane 0 of wave 0 behind with the
+      // barriers inside the loop still completing for the rest
+      __syncthreads();
+    } else {
+      wait_count(p.done + d * p.nrt + rt, p.P, p.serr);
+      x3p_tile<2>(p, lds, rt, r - p.P, d, 0, bc);
+      __syncthreads();
+    }
+  }
 }
 
 // Column packing (transpose): packed row c = column c of X, K = X's rows
@@ -511,6 +737,45 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
     const long tot = (long)p.batch * p.M * p.N;
     hipLaunchKernelGGL(x3p_splitk_reduce, dim3((int)std::min<long>(2048, (tot + 255) / 256)), dim3(256), 0, s, p);
   }
+}
+
+size_t x3p_bwd_stream_ints(int M, int N) {
+  const long nrt = ceil_div(M, TB), gx = ceil_div(N, TB);
+  return (size_t)(1 + 2 * nrt + nrt * gx);
+}
+
+void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a) {
+  if (a.M <= 0 || a.N <= 0) return;
+  const int K = a.KB * 32;
+  if (K > 4096 || a.Nf <= 0 || (long)a.M * a.N * 4 >= (1L << 31) || (a.lde & 3) || (a.edoff & 3))
+    throw std::invalid_argument("gemm_x3p_bwd_stream: unsupported shape");
+  PParams p{};
+  p.A = a.Ap; p.eA = a.eA; p.sA = (long)a.M * a.KB * 64; p.seA = a.M;
+  p.B = a.B; p.eB = a.eB; p.sB = a.sB; p.seB = a.seB;
+  p.C = a.C; p.ldc = a.ldc; p.alpha = 1.f; p.beta = 0.f;
+  p.M = a.M; p.N = a.N; p.KB = a.KB;
+  p.gx = ceil_div(a.N, TB); p.nrt = ceil_div(a.M, TB);
+  p.tiles = p.gx * p.nrt; p.batch = 2; p.split = 1; p.kbchunk = a.KB;
+  p.E = a.E; p.lde = a.lde; p.edoff = a.edoff;
+  p.P = 4;
+  p.counter = a.cnt; p.done = a.cnt + 1; p.arrive = a.cnt + 1 + 2 * p.nrt;
+  p.part = a.part;
+  p.sflags = a.flags; p.snwg = a.nwg; p.sT = a.T; p.sN = a.Nf; p.serr = a.err;
+  KCTC_HIP_CHECK(hipMemsetAsync(a.cnt, 0, sizeof(int) * x3p_bwd_stream_ints(a.M, a.N), s));
+  const int total = 2 * p.nrt * (p.P + p.gx);
+  const dim3 grid(std::min(total, a.blocks > 0 ? a.blocks : 96));
+  auto go = [&](auto kern) {
+    static bool attr = false;
+    if (!attr) {
+      KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsStream));
+      attr = true;
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(NTH), kLdsStream, s, p);
+  };
+  if (K <= 1024) go(x3p_bwd_stream_kernel<4>);
+  else if (K <= 2048) go(x3p_bwd_stream_kernel<8>);
+  else go(x3p_bwd_stream_kernel<16>);
 }
 
 }  // namespace kctc

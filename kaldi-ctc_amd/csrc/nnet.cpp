@@ -468,7 +468,7 @@ void CuDNNRecurrentComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
     ProfScope ps("layer_rnn_backward_data");
     int st = rnn_backward_data(desc_, S(), T, N, out_value.Data(), out_deriv.Data(), params_.f(),
                                in_deriv ? in_deriv->Data() : nullptr, workspace_.p, workspace_.bytes,
-                               reserve_.p, reserve_.bytes, err_);
+                               reserve_.p, reserve_.bytes, err_, CuDevice::Instantiate().stream2);
     if (st) throw std::runtime_error("rnn_backward_data failed: " + std::to_string(st));
   }
   if (to_update_in) {

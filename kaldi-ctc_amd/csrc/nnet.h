@@ -96,6 +96,9 @@ struct CuDevice {
   // Lower-priority stream for the weight-gradient GEMMs, which then overlap
   // the next component's backward recurrence (nullptr: everything on `stream`).
   hipStream_t side = nullptr;
+  // stream of the GEMMs that run concurrently with a recurrence and consume
+  // its rows as they appear (streamed dx; nullptr: off)
+  hipStream_t stream2 = nullptr;
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   void Fork();  // side waits for the work queued so far on stream
   void Join();  // stream waits for the work queued so far on side

@@ -64,7 +64,8 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
                          bool input_projected = false);
 int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float *y,
                       const float *dy, const float *w, float *dx, void *workspace,
-                      size_t ws_bytes, void *reserve, size_t res_bytes, unsigned *err);
+                      size_t ws_bytes, void *reserve, size_t res_bytes, unsigned *err,
+                      hipStream_t overlap = nullptr);  // overlap: stream for the streamed dx GEMM
 int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *y, void *workspace, size_t ws_bytes, float *dw,
                          void *reserve, size_t res_bytes, int max_blocks = 0);

@@ -118,7 +118,7 @@ static size_t xch_bytes(const RnnDesc &d, int T, int N) {
 //               shifted output^T [dirs*H][TN]
 // plus int exponents and float-bit column maxima (G = nW*H).
 struct PackLay {
-  size_t a, b, c, d, ea, eb, ec, ed, cm, total;
+  size_t a, b, c, d, ea, eb, ec, ed, cm, part, cnt, total;
 };
 static PackLay pack_layout(const RnnDesc &d, int T, int N) {
   const long TN = (long)T * N, G = (long)d.nw() * d.H, Dm = std::max(d.D, d.dirs * d.H), dirs = d.dirs;
@@ -138,6 +138,8 @@ static PackLay pack_layout(const RnnDesc &d, int T, int N) {
   p.ec = o; o = align_up(o + sizeof(int) * ne, 256);
   p.ed = o; o = align_up(o + sizeof(int) * ne, 256);
   p.cm = o; o = align_up(o + sizeof(unsigned) * ne, 256);
+  p.part = o; o = align_up(o + sizeof(float) * TN * Dm, 256);            // backward stream partials
+  p.cnt = o; o = align_up(o + sizeof(int) * x3p_bwd_stream_ints((int)TN, (int)Dm), 256);
   p.total = o;
   return p;
 }
@@ -230,6 +232,7 @@ struct RecParams {
   float *xch;       // v4: per-step exchange images [T][dirs][KG][Npad][16] (workspace)
   int poll_sleep;   // v6: s_sleep between flag polls
   int nopf;         // diagnostic (KCTC_DIAG_NOPF): skip the operand prefetch (wrong results)
+  int e_sc1;        // v6 backward: dGates rows written through (sc1) for a streaming consumer
 };
 
 // Phase stamps of the first kTraceSteps steps ([steps][grid][16]; thread 0 of every workgroup;
@@ -1417,6 +1420,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
   _Float16 *Ahi = reinterpret_cast<_Float16 *>(smem);  // [16][AP]
   _Float16 *Alo = Ahi + 16 * AP;
   float *red = reinterpret_cast<float *>(Alo + 16 * AP);  // [NGRP][POS][4]
+  // streamed consumer: this step's dGates tile [16][NW * U] (DX for GRU), then
+  // written through with 16-B stores after the step's signal
+  float *estg = red + (NT * 4 > 2 * 16 * U * NW ? NT * 4 : 2 * 16 * U * NW);
   const float *Wd = p.w + d * p.pl_stride;
   const float *R = Wd + p.r_off;
   if (tid == 0) bad_lds = 0;
@@ -1480,6 +1486,13 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
   auto e_store = [&](int t) {  // row-major dGates of step t (E; GRU also DX)
     if (!live) return;
     const long grow = ((long)t * N + en) * ldg + (long)d * NW * H + u0 + eu;
+    if (p.e_sc1) {  // DX (== E for LSTM) went out through estg already
+      if (MODE == kGru) {
+#pragma unroll
+        for (int q = 0; q < NW; q++) p.E[grow + q * H] = eg[q];
+      }
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < NW; q++) p.E[grow + q * H] = eg[q];
     if (MODE == kGru) {
@@ -1567,6 +1580,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
         Alo[en * AP + q * U + eu] = l;
       }
       if (eu == 0) rowexp[en] = se + sB;
+      if (p.e_sc1) {
+#pragma unroll
+        for (int q = 0; q < NW; q++) estg[en * NW * U + q * U + eu] = MODE == kGru ? dxk[q] : eg[q];
+      }
     }
     __syncthreads();
     REC_TRACE(ks, 3);
@@ -1605,11 +1622,26 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
     REC_TRACE(ks, 7);
     signal_epoch(myflag, (unsigned)(ks + 2), local);
     REC_TRACE(ks, 4);
+    if (p.e_sc1) {
+      // this step's DX rows for a streaming consumer on other XCDs: written
+      // through (sc1) as whole 16-B chunks, 4 lanes per contiguous 64-B run;
+      // issued after the signal, so only the NEXT signal (epoch ks + 3) waits
+      // for them (4-B write-through stores per element cost ~8 us per step)
+      constexpr int CPR = NW * U / 4;  // chunks per row
+      const int n = tid / CPR, c = tid - n * CPR;
+      if (n < N) {
+        const int q = (c * 4) / U, u = (c * 4) % U;
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(estg + n * NW * U + c * 4);
+        const int off = (int)(((long)n * ldg + (long)d * NW * H + q * H + u0 + u) * 4);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc(p.DX + (long)t * N * ldg, (unsigned)(N * ldg * 4)), off, 0, 16);
+      }
+    }
     rotate();
     t_prev = t;
     REC_TRACE(ks, 5);
   }
   if (t_prev >= 0 && !bad) e_store(t_prev);
+  if (!bad) signal_epoch(myflag, (unsigned)(T + 2), 0);  // the last step's rows are out
   // bias partial sums: reduce over n in a fixed order through LDS
   float *bs = red;  // [2][16][U][NW] floats
   __syncthreads();
@@ -2058,9 +2090,10 @@ static size_t bwd6_lds_bytes(const RnnDesc &d, int U) {
   const int K = d.nw() * U, KB = (K + 31) / 32, AP = KB * 32 + 8;
   const size_t img = 2 * 16 * (size_t)AP * 2;
   const size_t red = sizeof(float) * std::max((size_t)NT * 4, (size_t)2 * 16 * U * d.nw());
+  const size_t estg = sizeof(float) * 16 * U * d.nw();  // dGates tile staged for write-through
   // at least 96 KB so that no other workgroup (a side-stream GEMM block)
   // shares the CU with a recurrence workgroup
-  return std::max(img + red, (size_t)96 * 1024);
+  return std::max(img + red + estg, (size_t)96 * 1024);
 }
 static int pick_bwd_u6(const RnnDesc &d, int N) {
   if (env_int("KCTC_BWD_REC", 6) != 6 || rec_version() != 4) return 0;
@@ -2136,6 +2169,24 @@ static int pick_bwd_u(const RnnDesc &d, int N) {
 // host: forward training
 // ---------------------------------------------------------------------------
 namespace {
+// The recurrence and a GEMM streaming off it must run at the same time, so
+// the GEMM's stream forks from the recurrence's stream at an event recorded
+// BEFORE the recurrence launch, and the GEMM is enqueued AFTER it: should the
+// two streams share a hardware queue, the GEMM then merely runs after the
+// recurrence instead of blocking it (its blocks only wait for recurrence flags).
+hipEvent_t fork_event(hipStream_t s) {
+  static thread_local hipEvent_t ev = nullptr;
+  if (!ev) KCTC_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  KCTC_HIP_CHECK(hipEventRecord(ev, s));
+  return ev;
+}
+void join_stream(hipStream_t s, hipStream_t other) {
+  static thread_local hipEvent_t ev = nullptr;
+  if (!ev) KCTC_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  KCTC_HIP_CHECK(hipEventRecord(ev, other));
+  KCTC_HIP_CHECK(hipStreamWaitEvent(s, ev, 0));
+}
+
 // Can `c` consume the exchange images of this component's last forward
 // recurrence (v6, bidirectional) as its layer-0 projection input?
 bool chain_ok(const RnnDesc &d, int ver, int T, int N, const RnnFwdChain *c) {
@@ -2149,12 +2200,9 @@ bool chain_ok(const RnnDesc &d, int ver, int T, int N, const RnnFwdChain *c) {
 }
 
 // Layer-0 projection of the consumer, streamed off the producer's exchange images.
-void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipStream_t s, int T, int N, RnnFwdChain &c,
+void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipEvent_t fork, int T, int N, RnnFwdChain &c,
                        unsigned *err) {
-  static thread_local hipEvent_t fork_ev = nullptr;
-  if (!fork_ev) KCTC_HIP_CHECK(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
-  KCTC_HIP_CHECK(hipEventRecord(fork_ev, s));  // after the producer's flag reset
-  KCTC_HIP_CHECK(hipStreamWaitEvent(c.side, fork_ev, 0));
+  KCTC_HIP_CHECK(hipStreamWaitEvent(c.side, fork, 0));  // after the producer's flag reset
   const RnnDesc &n = *c.d;
   const int NW = n.nw(), G = NW * n.H, Din = n.D, KB = Din / 32;
   const long pl0 = n.lin_offset(0, 0, false), pls = n.pl_size(0);
@@ -2194,12 +2242,6 @@ void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipStream_t s, int 
   c.done = true;
 }
 
-void join_chain(hipStream_t s, const RnnFwdChain &c) {
-  static thread_local hipEvent_t join_ev = nullptr;
-  if (!join_ev) KCTC_HIP_CHECK(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
-  KCTC_HIP_CHECK(hipEventRecord(join_ev, c.side));
-  KCTC_HIP_CHECK(hipStreamWaitEvent(s, join_ev, 0));
-}
 }  // namespace
 
 int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
@@ -2284,26 +2326,68 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     RecTrace tr;
     if (tr.arm("fwd", grid.x)) p.trace = tr.dev;
     const bool chained = l == d.layers - 1 && chain_ok(d, ver, T, N, chain);
-    if (chained) launch_chain_proj(d, p, s, T, N, *chain, err);
+    const hipEvent_t fork = chained ? fork_event(s) : nullptr;
     {
       ProfSpan ps(s, "rnn_fwd_rec");
       if (ver == 6) launch_fwd6(d.mode, p, grid, lds, s);
       else launch_rec(true, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
-    if (chained) join_chain(s, *chain);
+    if (chained) {
+      launch_chain_proj(d, p, fork, T, N, *chain, err);
+      join_stream(s, chain->side);
+    }
     tr.dump("fwd", s, grid.x, p.nwg, T, dirs, ver, ver == 6 ? 0 : p.xpd);
     in = out;
   }
   return KRNN_OK;
 }
 
+namespace {
+// dx of stacked layer l on `ov`, streamed off the backward recurrence about
+// to be launched on `s` (gemm_x3p_bwd_stream): W_d^T packed first, then one
+// persistent launch that packs dGates rows as the recurrence flags them.
+void launch_bwd_stream(const RnnDesc &d, const RecParams &p, int l, const float *w, float *dxl, void *workspace,
+                       int T, int N, hipStream_t ov, hipEvent_t fork, unsigned *err) {
+  KCTC_HIP_CHECK(hipStreamWaitEvent(ov, fork, 0));  // after the flag reset, not after the recurrence
+  const int NW = d.nw(), H = d.H, G4 = NW * H, KB = G4 / 32, Din = d.din(l);
+  const long TN = (long)T * N;
+  const long pl0 = d.lin_offset(l * d.dirs, 0, false), pls = d.pl_size(l);
+  const float *wl = w + pl0;
+  const PackLay pl = pack_layout(d, T, N);
+  _Float16 *Ap = pk<_Float16>(workspace, d, T, N, pl.a), *Bp = pk<_Float16>(workspace, d, T, N, pl.b);
+  int *eA = pk<int>(workspace, d, T, N, pl.ea), *eB = pk<int>(workspace, d, T, N, pl.eb);
+  unsigned *cm = pk<unsigned>(workspace, d, T, N, pl.cm);
+  {
+    ProfSpan ps(ov, "x3_pack_bwd_stream");
+    for (int dir = 0; dir < 2; dir++) {
+      absmax_f32(ov, wl + dir * pls, Din, G4, Din, nullptr, cm + dir * Din);
+      x3p_pack_cols(ov, wl + dir * pls, Din, G4, Din, 0, Bp + (long)dir * Din * KB * 64, eB + dir * Din,
+                    cm + dir * Din, 0.f);
+    }
+  }
+  X3PBwdStream a;
+  a.M = (int)TN; a.N = Din; a.KB = KB;
+  a.E = p.DX; a.lde = 2L * G4; a.edoff = G4;
+  a.Ap = Ap; a.eA = eA;
+  a.B = Bp; a.eB = eB; a.sB = (long)Din * KB * 64; a.seB = Din;
+  a.C = dxl; a.ldc = Din;
+  a.part = pk<float>(workspace, d, T, N, pl.part);
+  a.cnt = pk<int>(workspace, d, T, N, pl.cnt);
+  a.flags = p.flags + 1024; a.nwg = p.nwg; a.T = T; a.Nf = N; a.err = err;
+  a.blocks = env_int("KCTC_BWD_STREAM_BLOCKS", 96);
+  ProfSpan ps(ov, "bwd_data_stream");
+  gemm_x3p_bwd_stream(ov, a);
+}
+}  // namespace
+
 // ---------------------------------------------------------------------------
 // host: backward data (dGates into the reserve, dx)
 // ---------------------------------------------------------------------------
 int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float *y,
                       const float *dy, const float *w, float *dx, void *workspace,
-                      size_t ws_bytes, void *reserve, size_t res_bytes, unsigned *err) {
+                      size_t ws_bytes, void *reserve, size_t res_bytes, unsigned *err,
+                      hipStream_t overlap) {
   if (T <= 0 || N <= 0 || N > 16 * kMaxRT || d.H % 16) return KRNN_NOT_SUPPORTED;
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
   if (res_bytes < sizeof(float) * (size_t)lay.total) return KRNN_BAD_PARAM;
@@ -2356,17 +2440,26 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : ver == 6 && p.xpd ? 8 * p.nwg : dirs * p.nwg);
     RecTrace tr;
     if (tr.arm("bwd", grid.x)) p.trace = tr.dev;
+    // dx_l = sum_dir DX_dir W_dir   (lower layer's dy, or the caller's dx)
+    float *dxl = (l == 0) ? dx : res + lay.per_layer * (l - 1) + lay.dout;
+    // streamed: computed on `overlap` while the recurrence runs, from its rows as they appear
+    const bool streamed = dxl && overlap && ver == 6 && dirs == 2 && !p.xpd && use_x3(NW * H) && NW * H <= 4096 &&
+                          (long)TN * Din * 4 < (1L << 31) && env_int("KCTC_BWD_STREAM", 1);
+    p.e_sc1 = env_int("KCTC_DIAG_ESC1", streamed ? 1 : 0);  // diagnostic override (0 with streaming: wrong dx)
+    const hipEvent_t fork = streamed ? fork_event(s) : nullptr;
     {
       ProfSpan ps(s, "rnn_bwd_rec");
       if (ver == 6) launch_rec6(d.mode, p, grid, lds, s);
       else launch_rec(false, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
+    if (streamed) {
+      launch_bwd_stream(d, p, l, w, dxl, workspace, T, N, overlap, fork, err);
+      join_stream(s, overlap);
+    }
     if (ver == 6) xch_release(s);
     tr.dump("bwd", s, grid.x, p.nwg, T, dirs, ver, ver == 6 ? (p.xpd ? 1 : 0) : p.xpd);
-    // dx_l = sum_dir DX_dir W_dir   (lower layer's dy, or the caller's dx)
-    float *dxl = (l == 0) ? dx : res + lay.per_layer * (l - 1) + lay.dout;
-    if (dxl) {
+    if (dxl && !streamed) {
       const bool x3 = use_x3(NW * H);
       const long G4 = (long)NW * H;
       const int KB = (int)((G4 + 31) / 32);

@@ -76,18 +76,21 @@ struct kctcNnetImpl {
   kctc::nnet2::Nnet nnet;
   kctc::nnet2::NnetCtcUpdater trainer{&nnet, true};
   kctc::nnet2::NnetCtcUpdater evaluator{&nnet, false};
-  hipStream_t side = nullptr;
+  hipStream_t side = nullptr, stream2 = nullptr;
   RcclExchange *dp = nullptr;
   kctc::nnet2::DevBuf egs_feats, egs_scratch;  // TrainNnetSimple staging
   ~kctcNnetImpl() {
     delete dp;
     if (stream) (void)hipStreamSynchronize(stream);
     if (side) (void)hipStreamSynchronize(side);
+    if (stream2) (void)hipStreamSynchronize(stream2);
     auto &d = CuDevice::Instantiate();
     if (d.stream == stream) d.stream = nullptr;
     if (d.side == side) d.side = nullptr;
+    if (d.stream2 == stream2) d.stream2 = nullptr;
     if (stream) (void)hipStreamDestroy(stream);
     if (side) (void)hipStreamDestroy(side);
+    if (stream2) (void)hipStreamDestroy(stream2);
   }
   // compute stream at the highest priority (the latency-bound recurrences),
   // the weight-gradient side stream at the lowest; KCTC_OVERLAP=0 keeps
@@ -97,13 +100,18 @@ struct kctcNnetImpl {
     KCTC_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     KCTC_HIP_CHECK(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, hi));
     const char *e = getenv("KCTC_OVERLAP");
-    if (!(e && *e == '0')) KCTC_HIP_CHECK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, lo));
+    if (!(e && *e == '0')) {
+      KCTC_HIP_CHECK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, lo));
+      // streamed GEMMs (default priority: a queue of its own, neither the recurrences' nor the side stream's)
+      KCTC_HIP_CHECK(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+    }
   }
   void activate() {
     KCTC_HIP_CHECK(hipSetDevice(device));
     CuDevice::Instantiate().device = device;
     CuDevice::Instantiate().stream = stream;
     CuDevice::Instantiate().side = side;
+    CuDevice::Instantiate().stream2 = stream2;
   }
 };
 

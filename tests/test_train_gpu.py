@@ -137,14 +137,17 @@ def test_model_write_read_roundtrip(kctc, gpu, tmp_path):
     assert net.compute_objf(f, T, N, nf, fl, ll) == net2.compute_objf(f, T, N, nf, fl, ll)
 
 
+@pytest.mark.parametrize("knob", ["KCTC_FWD_STREAM", "KCTC_BWD_STREAM"])
 @pytest.mark.parametrize("mode,H,T,N", [(2, 512, 300, 16), (2, 256, 97, 5), (3, 256, 64, 16)])
-def test_forward_stream_projection_matches_unstreamed(kctc, gpu, monkeypatch, mode, H, T, N):
-    """RNN -> ClipGradient -> RNN: the second RNN's input projection computed
-    while the first one's last recurrence runs (gemm_x3p streaming off the
-    exchange images, KCTC_FWD_STREAM=1, the default) against the projection
-    after it (KCTC_FWD_STREAM=0).  Same split-fp16 products (the images carry
-    h * 2^14, the packed copy h * 2^13): equal up to fp32 rounding of the
-    epilogue; many row tiles, ragged N, LSTM and GRU."""
+def test_streamed_gemms_match_unstreamed(kctc, gpu, monkeypatch, knob, mode, H, T, N):
+    """GEMMs that run while the recurrence producing their rows is still going
+    (knob=1, the default) against the same GEMMs after it (knob=0):
+    KCTC_FWD_STREAM -- RNN -> ClipGradient -> RNN, the second RNN's input
+    projection read off the first one's exchange images (h * 2^14 as fp16
+    hi/lo; the packed copy carries h * 2^13); KCTC_BWD_STREAM -- dx of an RNN
+    from its backward recurrence's dGates rows as they are flagged (per-
+    direction partials added in a fixed order instead of beta-accumulated).
+    Equal up to fp32 rounding; many row tiles, ragged N, LSTM and GRU."""
     import torch
     D, A = 40, 41
     cfg = kctc.recipe_config(num_rnn=3, input_dim=D, hidden=H, num_targets=A, rnn_mode=mode,
@@ -153,7 +156,7 @@ def test_forward_stream_projection_matches_unstreamed(kctc, gpu, monkeypatch, mo
     f = torch.from_numpy(feats).to(gpu)
     res = {}
     for flag in ("0", "1"):
-        monkeypatch.setenv("KCTC_FWD_STREAM", flag)
+        monkeypatch.setenv(knob, flag)
         net = kctc.Nnet(cfg, seed=8)
         o = net.compute_objf(f, T, N, nf, fl, ll)[0]
         net.train_step(f, T, N, nf, fl, ll)
