@@ -427,6 +427,8 @@ void CuDNNRecurrentComponent::PropagateChained(const CuMatrixBase &in, CuMatrixB
   auto &dev = CuDevice::Instantiate();
   const int N = mini_batch_ > 0 ? mini_batch_ : 1;
   const int T = (int)(in.NumRows() / N);
+  // |h| <= 1 for LSTM / GRU / TANH outputs: the next RNN's input needs no max pass
+  next.input_bound_ = desc_.mode != kRelu ? 1.f : 0.f;
   if (!dev.side || next.mini_batch_ != N || next.desc_.D != OutputDim()) {
     Forward(in, out, nullptr);
     return;
@@ -486,7 +488,7 @@ void CuDNNRecurrentComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
     ProfScope ps("layer_rnn_backward_weights", ws);
     int st = rnn_backward_weights(desc_, ws, T, N, in_value.Data(), out_value.Data(), workspace_.p,
                                   workspace_.bytes, to_update->grad_.f(), reserve_.p, reserve_.bytes,
-                                  dev.side ? side_gemm_blocks() : 0);
+                                  dev.side ? side_gemm_blocks() : 0, input_bound_);
     if (st) throw std::runtime_error("rnn_backward_weights failed: " + std::to_string(st));
   }
 }

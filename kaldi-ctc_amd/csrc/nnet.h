@@ -241,6 +241,7 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   mutable DevBuf reserve_, workspace_;
   mutable int mini_batch_ = 0, seq_length_ = 0;
   mutable bool input_projected_ = false;  // set by the previous component's PropagateChained
+  mutable float input_bound_ = 0.f;       // ditto: bound on |input| (0: unknown)
   unsigned *err_ = nullptr;
   void Forward(const CuMatrixBase &in, CuMatrixBase *out, RnnFwdChain *chain) const;
 };

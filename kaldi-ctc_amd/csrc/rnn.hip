@@ -118,7 +118,7 @@ static size_t xch_bytes(const RnnDesc &d, int T, int N) {
 //               shifted output^T [dirs*H][TN]
 // plus int exponents and float-bit column maxima (G = nW*H).
 struct PackLay {
-  size_t a, b, c, d, ea, eb, ec, ed, cm, part, cnt, total;
+  size_t a, b, c, d, ea, eb, ec, ed, cm, part, cnt, cme, total;
 };
 static PackLay pack_layout(const RnnDesc &d, int T, int N) {
   const long TN = (long)T * N, G = (long)d.nw() * d.H, Dm = std::max(d.D, d.dirs * d.H), dirs = d.dirs;
@@ -140,6 +140,7 @@ static PackLay pack_layout(const RnnDesc &d, int T, int N) {
   p.cm = o; o = align_up(o + sizeof(unsigned) * ne, 256);
   p.part = o; o = align_up(o + sizeof(float) * TN * Dm, 256);            // backward stream partials
   p.cnt = o; o = align_up(o + sizeof(int) * x3p_bwd_stream_ints((int)TN, (int)Dm), 256);
+  p.cme = o; o = align_up(o + sizeof(unsigned) * 2 * dirs * G, 256);  // dGates column maxima (v6 backward)
   p.total = o;
   return p;
 }
@@ -233,6 +234,7 @@ struct RecParams {
   int poll_sleep;   // v6: s_sleep between flag polls
   int nopf;         // diagnostic (KCTC_DIAG_NOPF): skip the operand prefetch (wrong results)
   int e_sc1;        // v6 backward: dGates rows written through (sc1) for a streaming consumer
+  unsigned *cmax;   // v6 backward: column max |DX| [dirs * nW * H] (GRU: then |E|), as float bits
 };
 
 // Phase stamps of the first kTraceSteps steps ([steps][grid][16]; thread 0 of every workgroup;
@@ -1461,10 +1463,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
   const bool has_e = tid < 16 * U;
   const int en = tid / U, eu = tid - en * U;
   const bool live = has_e && en < N;
-  float carry = 0.f, bsx[NW], bsh[NW], dxk[NW], eg[NW], cg[NW], ng[NW];
+  float carry = 0.f, bsx[NW], bsh[NW], dxk[NW], eg[NW], cg[NW], ng[NW], cmx[NW], cme[NW];
   float cdy = 0.f, ca = 0.f, cap = 0.f, ndy = 0.f, na = 0.f, nap = 0.f;
 #pragma unroll
-  for (int q = 0; q < NW; q++) bsx[q] = bsh[q] = dxk[q] = eg[q] = cg[q] = ng[q] = 0.f;
+  for (int q = 0; q < NW; q++) bsx[q] = bsh[q] = dxk[q] = eg[q] = cg[q] = ng[q] = cmx[q] = cme[q] = 0.f;
   auto prefetch = [&](int k) {  // operands of forward-order step k into n*
     if (!live) return;
     const int t = d == 0 ? k : T - 1 - k, tp = d == 0 ? t - 1 : t + 1;
@@ -1570,6 +1572,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
       for (int q = 0; q < NW; q++) {
         bsx[q] += (MODE == kGru) ? dxk[q] : eg[q];
         m = fmaxf(m, fabsf(eg[q]));
+        if (live) {  // column maxima for the weight GEMMs' packed transposes
+          cmx[q] = fmaxf(cmx[q], fabsf(MODE == kGru ? dxk[q] : eg[q]));
+          if (MODE == kGru) cme[q] = fmaxf(cme[q], fabsf(eg[q]));
+        }
       }
       const int se = split_exp(wave_max16(m, U));
 #pragma unroll
@@ -1659,6 +1665,24 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
     float s2 = 0.f;
     for (int n = 0; n < N; n++) s2 += bs[(long)part * 16 * U * NW + ((long)n * U + u) * NW + gt];
     p.bias[((long)d * 2 + part) * NW * H + gt * H + u0 + u] = s2;
+  }
+  if (p.cmax) {  // column maxima over all frames (rows n of this WG's columns, through LDS)
+    constexpr int NP = MODE == kGru ? 2 : 1;
+    __syncthreads();
+    if (has_e) {
+#pragma unroll
+      for (int q = 0; q < NW; q++) {
+        bs[((long)en * U + eu) * NW + q] = cmx[q];
+        if (MODE == kGru) bs[(long)16 * U * NW + ((long)en * U + eu) * NW + q] = cme[q];
+      }
+    }
+    __syncthreads();
+    for (int q = tid; q < NP * NW * U; q += NT) {
+      const int part = q / (NW * U), rem = q - part * NW * U, gt = rem / U, u = rem - gt * U;
+      float m2 = 0.f;
+      for (int n = 0; n < 16; n++) m2 = fmaxf(m2, bs[(long)part * 16 * U * NW + ((long)n * U + u) * NW + gt]);
+      p.cmax[(long)part * p.dirs * NW * H + (long)d * NW * H + gt * H + u0 + u] = __float_as_uint(m2);
+    }
   }
   if (bad && tid == 0) atomicOr(p.err, 1u);
 }
@@ -2446,6 +2470,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     const bool streamed = dxl && overlap && ver == 6 && dirs == 2 && !p.xpd && use_x3(NW * H) && NW * H <= 4096 &&
                           (long)TN * Din * 4 < (1L << 31) && env_int("KCTC_BWD_STREAM", 1);
     p.e_sc1 = env_int("KCTC_DIAG_ESC1", streamed ? 1 : 0);  // diagnostic override (0 with streaming: wrong dx)
+    if (ver == 6) p.cmax = pk<unsigned>(workspace, d, T, N, pack_layout(d, T, N).cme);
     const hipEvent_t fork = streamed ? fork_event(s) : nullptr;
     {
       ProfSpan ps(s, "rnn_bwd_rec");
@@ -2508,7 +2533,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
 // ---------------------------------------------------------------------------
 int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *y, void *workspace, size_t ws_bytes, float *dw,
-                         void *reserve, size_t res_bytes, int max_blocks) {
+                         void *reserve, size_t res_bytes, int max_blocks, float in_bound) {
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
   if (res_bytes < sizeof(float) * (size_t)lay.total) return KRNN_BAD_PARAM;
   if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
@@ -2554,15 +2579,17 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       // the transposes, packed over the frames: dGates^T (per-gate exponents),
       // input^T (per-dim), and for dR the output shifted by one step per direction
       ProfSpan ps(s, "x3_pack_w");
-      absmax_f32(s, DX, ldg, (int)TN, (int)(dirs * G4), nullptr, cm);
-      x3p_pack_cols(s, DX, ldg, (int)TN, (int)(dirs * G4), 0, DXt, eDX, cm, 0.f);
+      // the v6 backward recurrence leaves the dGates column maxima behind
+      const unsigned *cme = pick_bwd_u6(d, N) ? pk<unsigned>(workspace, d, T, N, pl.cme) : nullptr;
+      if (!cme) absmax_f32(s, DX, ldg, (int)TN, (int)(dirs * G4), nullptr, cm);
+      x3p_pack_cols(s, DX, ldg, (int)TN, (int)(dirs * G4), 0, DXt, eDX, cme ? cme : cm, 0.f);
       if (d.mode == kGru) {
-        absmax_f32(s, E, ldg, (int)TN, (int)(dirs * G4), nullptr, cm);
-        x3p_pack_cols(s, E, ldg, (int)TN, (int)(dirs * G4), 0, Et, eE, cm, 0.f);
+        if (!cme) absmax_f32(s, E, ldg, (int)TN, (int)(dirs * G4), nullptr, cm);
+        x3p_pack_cols(s, E, ldg, (int)TN, (int)(dirs * G4), 0, Et, eE, cme ? cme + dirs * G4 : cm, 0.f);
       }
-      const bool xb = l > 0 && bounded_out(d);
+      const bool xb = (l > 0 && bounded_out(d)) || (l == 0 && in_bound > 0.f);
       if (!xb) absmax_f32(s, in, Din, (int)TN, Din, nullptr, cm);
-      x3p_pack_cols(s, in, Din, (int)TN, Din, 0, Xt, eX, cm, xb ? 1.f : 0.f);
+      x3p_pack_cols(s, in, Din, (int)TN, Din, 0, Xt, eX, cm, xb ? (l > 0 ? 1.f : in_bound) : 0.f);
       if (T > 1) {
         if (!bounded_out(d)) absmax_f32(s, out, ldy, (int)TN, (int)ldy, nullptr, cm);
         for (int dir = 0; dir < dirs; dir++)
