@@ -114,17 +114,20 @@ __global__ __launch_bounds__(256) void ctc_logz(const float *__restrict__ acts, 
 // of the small ones (logf(1 + x) would round x to the ulp of 1).  log1p(x) is
 // evaluated as log(u) * x / (u - 1) with u = fl(1 + x) (the rounding of u
 // cancels to first order), on the hardware v_log_f32 / v_exp_f32.
+// (u in [1, 3]: the raw v_log_f32 / v_rcp_f32 need no range reduction)
 __device__ __forceinline__ float fast_log1p(float x) {
   const float u = 1.f + x;
-  if (u == 1.f) return x;
-  return __logf(u) * __fdividef(x, u - 1.f);
+  const float r = __builtin_amdgcn_logf(u) * 0.693147180559945309f * (x * __builtin_amdgcn_rcpf(u - 1.f));
+  return u == 1.f ? x : r;
 }
+// branch-free: -inf in, -inf out (all three -inf gives m = -inf, and
+// -inf - -inf = NaN is selected away)
 __device__ __forceinline__ float lse3(float a, float b, float c) {
   const float m = fmaxf(a, fmaxf(b, c));
-  if (m == -INFINITY) return -INFINITY;
   const float lo = fminf(a, fminf(b, c));
   const float md = fmaxf(fminf(a, b), fminf(fmaxf(a, b), c));  // median, exact
-  return m + fast_log1p(__expf(md - m) + __expf(lo - m));
+  const float r = m + fast_log1p(__expf(md - m) + __expf(lo - m));
+  return m == -INFINITY ? -INFINITY : r;
 }
 
 // ---------------------------------------------------------------------------
@@ -150,7 +153,7 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <bool SPILL>
+template <bool SPILL, int SPT>
 __global__ __launch_bounds__(kABThreads) void ctc_alpha_beta(
     const float *__restrict__ lp, int N, int A, int blank, UttDesc *__restrict__ descs,
     const int *__restrict__ labels, float *__restrict__ spill, double *__restrict__ offs,
@@ -181,11 +184,11 @@ __global__ __launch_bounds__(kABThreads) void ctc_alpha_beta(
   }
   if (!feasible) return;
 
-  // extended label of each owned state s = tid + 256 i, and its skip permission
-  int ext[kSPT];
-  bool skip[kSPT];
+  // extended label of each owned state s = tid + 512 i, and its skip permission
+  int ext[SPT];
+  bool skip[SPT];
 #pragma unroll
-  for (int i = 0; i < kSPT; i++) {
+  for (int i = 0; i < SPT; i++) {
     int s = tid + i * kABThreads;
     ext[i] = (s < S) ? ((s & 1) ? lab[(s - 1) >> 1] : blank) : blank;
     skip[i] = false;
@@ -210,7 +213,7 @@ __global__ __launch_bounds__(kABThreads) void ctc_alpha_beta(
       if (k >= T) break;
       const float *src = lrow + (long)tframe(k) * tstride;
 #pragma unroll
-      for (int i = 0; i < kSPT; i++) {
+      for (int i = 0; i < SPT; i++) {
         const int sb = wid + kABWaves * i;
         if (sb < nblk) __builtin_amdgcn_global_load_lds(src + ext[i], dst + (size_t)f * SP + sb * 64, 4, 0, 0);
       }
@@ -230,16 +233,16 @@ __global__ __launch_bounds__(kABThreads) void ctc_alpha_beta(
     for (int f = 0; f < fend; f++) {
       const int k = c * F + f;
       const int t = tframe(k);
-      float ly[kSPT];
+      float ly[SPT];
 #pragma unroll
-      for (int i = 0; i < kSPT; i++) ly[i] = (tid + i * kABThreads < S) ? em[(size_t)f * SP + tid + i * kABThreads] : 0.f;
+      for (int i = 0; i < SPT; i++) ly[i] = em[(size_t)f * SP + min(tid + i * kABThreads, SP - 1)];
       float *cc = colb + cur * CP;
       float lmax = -INFINITY;
       if (k == 0) {
         // init: alpha_0(0)=ly(blank), alpha_0(1)=ly(l1); beta_{T-1}(S-1)=beta(S-2)=0,
         // stored as q = beta + ly (the next step's input)
 #pragma unroll
-        for (int i = 0; i < kSPT; i++) {
+        for (int i = 0; i < SPT; i++) {
           int s = tid + i * kABThreads;
           if (s < S) {
             float v;
@@ -252,32 +255,45 @@ __global__ __launch_bounds__(kABThreads) void ctc_alpha_beta(
           }
         }
       } else {
+        // all LDS reads of the frame up front, branch-free (clamped indices,
+        // -inf selected in); the previous column's max mu is only subtracted
+        // at the end: lse3(a, b, c) - mu == lse3(a - mu, b - mu, c - mu)
         const float *wm = wmax + (cur ^ 1) * kABWaves;
+        const float *pv = colb + (cur ^ 1) * CP;
+        float pa[SPT], pb[SPT], pc[SPT];
+#pragma unroll
+        for (int i = 0; i < SPT; i++) {
+          const int s = tid + i * kABThreads;
+          if (!is_beta) {
+            pa[i] = pv[min(s, CP - 1)];
+            pb[i] = pv[max(s - 1, 0)];
+            pc[i] = pv[max(s - 2, 0)];
+            pb[i] = s >= 1 ? pb[i] : -INFINITY;
+            pc[i] = skip[i] ? pc[i] : -INFINITY;
+          } else {
+            pa[i] = pv[min(s, CP - 1)];
+            pb[i] = pv[min(s + 1, CP - 1)];
+            pc[i] = pv[min(s + 2, CP - 1)];
+            pb[i] = s + 1 < S ? pb[i] : -INFINITY;
+            pc[i] = skip[i] ? pc[i] : -INFINITY;
+          }
+        }
         float mu = wm[0];
 #pragma unroll
         for (int w = 1; w < kABWaves; w++) mu = fmaxf(mu, wm[w]);
-        const float *pv = colb + (cur ^ 1) * CP;
 #pragma unroll
-        for (int i = 0; i < kSPT; i++) {
-          int s = tid + i * kABThreads;
+        for (int i = 0; i < SPT; i++) {
+          const int s = tid + i * kABThreads;
+          const float v = lse3(pa[i], pb[i], pc[i]) - mu;
           if (s < S) {
-            float v;
             if (!is_beta) {
-              float a = pv[s];
-              float b = s >= 1 ? pv[s - 1] : -INFINITY;
-              float c2 = skip[i] ? pv[s - 2] : -INFINITY;
-              v = lse3(a - mu, b - mu, c2 - mu);
-              v = (v == -INFINITY) ? v : v + ly[i];
-              if (SPILL) sp[(long)t * S + s] = v;
-              cc[s] = v;
-              lmax = fmaxf(lmax, v);
+              const float va = v + ly[i];
+              if (SPILL) sp[(long)t * S + s] = va;
+              cc[s] = va;
+              lmax = fmaxf(lmax, va);
             } else {
-              float a = pv[s];
-              float b = s + 1 < S ? pv[s + 1] : -INFINITY;
-              float c2 = skip[i] ? pv[s + 2] : -INFINITY;
-              v = lse3(a - mu, b - mu, c2 - mu);
               if (SPILL) sp[(long)t * S + s] = v;
-              float q = (v == -INFINITY) ? v : v + ly[i];
+              const float q = v + ly[i];
               cc[s] = q;
               lmax = fmaxf(lmax, q);
             }
@@ -471,17 +487,21 @@ static ctcStatus_t launch(const float *acts, float *grads, const int *flat_label
     al.F = (int)std::min<size_t>(32, std::max<size_t>(4, (size_t)96 * 1024 / (2 * sizeof(float) * al.SP)));
     const size_t shm = sizeof(float) * al.floats();
     if (shm > 160 * 1024) return CTC_STATUS_INVALID_VALUE;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(ctc_alpha_beta<true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(ctc_alpha_beta<false>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     ProfSpan ps(stream, "ctc_alpha_beta");
-    if (want)
-      hipLaunchKernelGGL(ctc_alpha_beta<true>, dim3(2 * N), dim3(kABThreads), shm, stream, d_lp, N, A, blank,
-                         d_desc, d_lab, d_spill, d_offs, costs_dev, al);
-    else
-      hipLaunchKernelGGL(ctc_alpha_beta<false>, dim3(N), dim3(kABThreads), shm, stream, d_lp, N, A, blank,
-                         d_desc, d_lab, d_spill, d_offs, costs_dev, al);
+    auto go = [&](auto kern, int grid) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)shm);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(kABThreads), shm, stream, d_lp, N, A, blank, d_desc, d_lab,
+                         d_spill, d_offs, costs_dev, al);
+    };
+    // one state per thread up to 512 extended labels (L <= 255), else three
+    if (Smax <= kABThreads) {
+      if (want) go(ctc_alpha_beta<true, 1>, 2 * N);
+      else go(ctc_alpha_beta<false, 1>, N);
+    } else {
+      if (want) go(ctc_alpha_beta<true, kSPT>, 2 * N);
+      else go(ctc_alpha_beta<false, kSPT>, N);
+    }
   }
   if (want && lay.T_max > 0) {
     int Lmax = 0;

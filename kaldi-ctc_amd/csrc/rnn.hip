@@ -2566,7 +2566,7 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     // recurrences of this layer, which use the other flag words, are done)
     unsigned *fl = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     if (max_blocks > 0) g.tile_counter = reinterpret_cast<int *>(fl + 1008);
-    const bool x3 = use_x3((int)TN) && Din >= 64;
+    const bool x3 = use_x3((int)TN);  // K = frames: large (also for a 40-dim input: 0.8 ms/step over fp32)
     const int KBt = (int)((TN + 31) / 32);
     const PackLay pl = pack_layout(d, T, N);
     _Float16 *DXt = pk<_Float16>(workspace, d, T, N, pl.a), *Xt = pk<_Float16>(workspace, d, T, N, pl.b);
