@@ -153,12 +153,13 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <bool SPILL, int SPT>
-__global__ __launch_bounds__(kABThreads) void ctc_alpha_beta(
+// the direction is a template parameter of the body: one code path per
+// direction, so the scheduler is free to hoist each frame's LDS reads
+template <bool SPILL, int SPT, bool is_beta>
+__device__ __forceinline__ void ab_body(
     const float *__restrict__ lp, int N, int A, int blank, UttDesc *__restrict__ descs,
     const int *__restrict__ labels, float *__restrict__ spill, double *__restrict__ offs,
     double *__restrict__ costs, AbLds lay) {
-  const bool is_beta = blockIdx.x >= (unsigned)N;
   const int n = is_beta ? blockIdx.x - N : blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -281,23 +282,18 @@ __global__ __launch_bounds__(kABThreads) void ctc_alpha_beta(
         float mu = wm[0];
 #pragma unroll
         for (int w = 1; w < kABWaves; w++) mu = fmaxf(mu, wm[w]);
+        // every lane computes and writes (cc is padded to SPT * 512 entries;
+        // states >= S only ever feed selects): no load is sunk into a branch,
+        // so the frame's LDS reads share one wait
 #pragma unroll
         for (int i = 0; i < SPT; i++) {
           const int s = tid + i * kABThreads;
           const float v = lse3(pa[i], pb[i], pc[i]) - mu;
-          if (s < S) {
-            if (!is_beta) {
-              const float va = v + ly[i];
-              if (SPILL) sp[(long)t * S + s] = va;
-              cc[s] = va;
-              lmax = fmaxf(lmax, va);
-            } else {
-              if (SPILL) sp[(long)t * S + s] = v;
-              const float q = v + ly[i];
-              cc[s] = q;
-              lmax = fmaxf(lmax, q);
-            }
-          }
+          const float q = v + ly[i];         // alpha: the new alpha~; beta: the next step's input
+          const float spv = is_beta ? v : q;  // spilled: alpha~ / beta~
+          cc[s] = q;
+          lmax = fmaxf(lmax, s < S ? q : -INFINITY);
+          if (SPILL && s < S) sp[(long)t * S + s] = spv;
         }
         off += (double)mu;
       }
@@ -319,6 +315,15 @@ __global__ __launch_bounds__(kABThreads) void ctc_alpha_beta(
     double lpv = off + (double)m + log((double)expf(a - m) + (double)expf(b - m));
     costs[n] = -lpv;
   }
+}
+
+template <bool SPILL, int SPT>
+__global__ __launch_bounds__(kABThreads) void ctc_alpha_beta(
+    const float *__restrict__ lp, int N, int A, int blank, UttDesc *__restrict__ descs,
+    const int *__restrict__ labels, float *__restrict__ spill, double *__restrict__ offs,
+    double *__restrict__ costs, AbLds lay) {
+  if (blockIdx.x >= (unsigned)N) ab_body<SPILL, SPT, true>(lp, N, A, blank, descs, labels, spill, offs, costs, lay);
+  else ab_body<SPILL, SPT, false>(lp, N, A, blank, descs, labels, spill, offs, costs, lay);
 }
 
 // ---------------------------------------------------------------------------
@@ -482,7 +487,7 @@ static ctcStatus_t launch(const float *acts, float *grads, const int *flat_label
     for (int n = 0; n < N; n++) Smax = 2 * label_lengths[n] + 1 > Smax ? 2 * label_lengths[n] + 1 : Smax;
     AbLds al;
     al.SP = (Smax + 63) / 64 * 64;
-    al.CP = (Smax + 4 + 3) / 4 * 4;
+    al.CP = std::max((Smax + 4 + 3) / 4 * 4, (Smax <= kABThreads ? 1 : kSPT) * kABThreads);
     // chunk depth: as many frames as fit 96 KB of double-buffered emissions (4..32)
     al.F = (int)std::min<size_t>(32, std::max<size_t>(4, (size_t)96 * 1024 / (2 * sizeof(float) * al.SP)));
     const size_t shm = sizeof(float) * al.floats();
