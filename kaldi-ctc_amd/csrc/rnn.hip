@@ -152,13 +152,13 @@ static P *pk(void *ws, const RnnDesc &d, int T, int N, size_t off) {
 }
 // The RNN GEMMs run on the packed split-fp16 matrix-core path (gemm_x3p.hip)
 // unless KCTC_GEMM=f32 (or the contraction is too short to pay for packing).
-static bool use_x3(int K) {
+static bool use_x3(int K, int min_k = 128) {
   static int v = -1;
   if (v < 0) {
     const char *e = getenv("KCTC_GEMM");
     v = (e && !strcmp(e, "f32")) ? 0 : 1;
   }
-  return v && K >= 128;
+  return v && K >= min_k;
 }
 // |x| <= 1: an LSTM / GRU / TANH layer output
 static bool bounded_out(const RnnDesc &d) { return d.mode != kRelu; }
@@ -2308,7 +2308,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     g.bias2 = (d.mode == kGru) ? nullptr : wl + bR;
     g.batch = dirs; g.strideA = 0; g.strideB = pls; g.strideC = (long)NW * H; g.strideBias = pls;
     if (skip_proj) {
-    } else if (use_x3(Din)) {
+    } else if (use_x3(Din, 32)) {
       // input rows (a lower stacked layer's output is bounded; the component
       // input and RELU outputs get per-row exponents) and W rows, packed
       const PackLay pl = pack_layout(d, T, N);
