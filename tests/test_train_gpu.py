@@ -167,3 +167,23 @@ def test_streamed_gemms_match_unstreamed(kctc, gpu, monkeypatch, knob, mode, H, 
     np.testing.assert_allclose(res["1"][1], res["0"][1], rtol=2e-6)
     for a, b in zip(res["1"][2], res["0"][2]):
         assert rel_err(a, b) < 1e-6
+
+
+def test_rccl_dp_single_rank_matches_plain(kctc, gpu):
+    """kctc_nnet_enable_dp at world size 1: the per-component RCCL all-reduce
+    (on its own stream, after the side-stream weight GEMMs) runs alongside the
+    streamed GEMMs and recurrences; a sum over one rank is the identity, so the
+    updates equal the plain trainer's bit for bit."""
+    import torch
+    D, A, T, N, H = 40, 41, 64, 16, 256
+    cfg = kctc.recipe_config(num_rnn=3, input_dim=D, hidden=H, num_targets=A, learning_rate=1e-3,
+                             param_stddev=0.05)
+    feats, nf, fl, ll = kctc.synth_minibatch(23, T, N, D, A, 0.125)
+    f = torch.from_numpy(feats).to(gpu)
+    nets = [kctc.Nnet(cfg, seed=4), kctc.Nnet(cfg, seed=4)]
+    nets[1].enable_dp(kctc.dp_unique_id(), 0, 1)
+    outs = [[net.train_step(f, T, N, nf, fl, ll) for _ in range(2)] for net in nets]
+    assert outs[0] == outs[1]
+    for c in range(nets[0].num_components):
+        if nets[0].num_params(c):
+            np.testing.assert_array_equal(nets[0].get_params(c), nets[1].get_params(c))
