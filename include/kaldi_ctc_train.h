@@ -60,6 +60,19 @@ int kctc_nnet_set_repair_seed(kctcNnet_t nnet, unsigned long long seed);
 int kctc_nnet_train_step(kctcNnet_t nnet, const float *feats_dev, int T_max, int N,
                          const int *num_frames, const int *flat_labels, const int *label_lengths,
                          double *tot_objf, double *tot_accuracy, double *tot_weight);
+/* kctc_nnet_train_step split in two for a pipelined host loop: queues the
+ * minibatch's device work (feats_dev must stay valid until its stats come
+ * back) and, once two are queued, waits for the older one and returns ITS
+ * stats with *have_stats = 1 (else *have_stats = 0).  kctc_nnet_train_flush
+ * returns the remaining ones, one per call, until *have_stats = 0.  The
+ * updates are the same as kctc_nnet_train_step's; only the host waits move
+ * (TrainNnetSimple's per-minibatch stats are reported one minibatch late). */
+int kctc_nnet_train_step_async(kctcNnet_t nnet, const float *feats_dev, int T_max, int N,
+                               const int *num_frames, const int *flat_labels, const int *label_lengths,
+                               int *have_stats, double *tot_objf, double *tot_accuracy, double *tot_weight);
+int kctc_nnet_train_flush(kctcNnet_t nnet, int *have_stats, double *tot_objf, double *tot_accuracy,
+                          double *tot_weight);
+
 int kctc_nnet_compute_objf(kctcNnet_t nnet, const float *feats_dev, int T_max, int N,
                            const int *num_frames, const int *flat_labels,
                            const int *label_lengths, double *tot_objf, double *tot_accuracy,

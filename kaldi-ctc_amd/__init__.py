@@ -361,6 +361,32 @@ class Nnet:
         """DoBackprop on one minibatch; feats: device [T*N, D]. -> (objf, accuracy, weight)"""
         return self._step(lib().kctc_nnet_train_step, feats, T, N, num_frames, flat_labels, label_lengths)
 
+    def train_step_async(self, feats, T, N, num_frames, flat_labels, label_lengths):
+        """Queue a training step (feats must stay alive until its stats come
+        back); returns the stats of the minibatch queued before the previous
+        one once two are in flight, else None (kctc_nnet_train_step_async)."""
+        nf = np.ascontiguousarray(num_frames, dtype=np.int32)
+        fl = np.ascontiguousarray(flat_labels, dtype=np.int32)
+        if fl.size == 0:
+            fl = np.zeros(1, np.int32)
+        ll = np.ascontiguousarray(label_lengths, dtype=np.int32)
+        h, o, a, w = ctypes.c_int(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        _tcheck(lib().kctc_nnet_train_step_async(self.h, _ptr(feats), T, N, nf.ctypes.data, fl.ctypes.data,
+                                                 ll.ctypes.data, ctypes.byref(h), ctypes.byref(o),
+                                                 ctypes.byref(a), ctypes.byref(w)), "train_step_async")
+        return (o.value, a.value, w.value) if h.value else None
+
+    def train_flush(self):
+        """Stats of the queued minibatches, oldest first (kctc_nnet_train_flush)."""
+        out = []
+        while True:
+            h, o, a, w = ctypes.c_int(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+            _tcheck(lib().kctc_nnet_train_flush(self.h, ctypes.byref(h), ctypes.byref(o), ctypes.byref(a),
+                                                ctypes.byref(w)), "train_flush")
+            if not h.value:
+                return out
+            out.append((o.value, a.value, w.value))
+
     def compute_objf(self, feats, T, N, num_frames, flat_labels, label_lengths):
         return self._step(lib().kctc_nnet_compute_objf, feats, T, N, num_frames, flat_labels, label_lengths)
 

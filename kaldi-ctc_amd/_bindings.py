@@ -46,6 +46,9 @@ SIGS = {
                                   ctypes.POINTER(cd)]),
     "kctc_nnet_compute_objf": (ci, [vp, vp, ci, ci, vp, vp, vp, ctypes.POINTER(cd), ctypes.POINTER(cd),
                                     ctypes.POINTER(cd)]),
+    "kctc_nnet_train_step_async": (ci, [vp, vp, ci, ci, vp, vp, vp, ip, ctypes.POINTER(cd), ctypes.POINTER(cd),
+                                        ctypes.POINTER(cd)]),
+    "kctc_nnet_train_flush": (ci, [vp, ip, ctypes.POINTER(cd), ctypes.POINTER(cd), ctypes.POINTER(cd)]),
     "kctc_nnet_stream": (vp, [vp]),
     "kctc_nnet_set_profiling": (ci, [vp, ci]),
     "kctc_nnet_profile": (ci, [vp, ctypes.c_char_p, ctypes.POINTER(cd), ctypes.POINTER(ci)]),

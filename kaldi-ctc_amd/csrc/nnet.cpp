@@ -74,6 +74,7 @@ void DevBuf::ensure(size_t b) {
     auto &d = CuDevice::Instantiate();
     KCTC_HIP_CHECK(hipStreamSynchronize(d.stream));
     if (d.side) KCTC_HIP_CHECK(hipStreamSynchronize(d.side));
+    if (d.stream2) KCTC_HIP_CHECK(hipStreamSynchronize(d.stream2));
     KCTC_HIP_CHECK(hipFree(p));
     p = nullptr;
   }
@@ -968,6 +969,14 @@ static void set_minibatch(Nnet *nnet, int N) {  // Nnet::SetMiniBatch (nnet-nnet
 MinibatchStats NnetCtcUpdater::ComputeForMinibatch(const float *feats, int T_max, int N,
                                                    const int *num_frames, const int *flat_labels,
                                                    const int *label_lengths) {
+  if (pending_) throw std::logic_error("ComputeForMinibatch with queued minibatches (Finish them first)");
+  Enqueue(feats, T_max, N, num_frames, flat_labels, label_lengths);
+  return Finish();
+}
+
+void NnetCtcUpdater::Enqueue(const float *feats, int T_max, int N, const int *num_frames,
+                             const int *flat_labels, const int *label_lengths) {
+  if (pending_ == 2) throw std::logic_error("two minibatches already queued");
   const int C = nnet_->NumComponents();
   if (N <= 0 || T_max <= 0) throw std::invalid_argument("empty minibatch");
   const long rows = (long)T_max * N;
@@ -997,6 +1006,14 @@ MinibatchStats NnetCtcUpdater::ComputeForMinibatch(const float *feats, int T_max
     ctcStatus_t st = get_workspace_size(label_lengths, num_frames, A, N, o, &ws);
     if (st != CTC_STATUS_SUCCESS)
       throw std::runtime_error(std::string("get_workspace_size: ") + ctcGetStatusString(st));
+    // size for the longest labels this T_max admits, once: a growing workspace
+    // (label lengths vary per minibatch) would cost a device sync + realloc
+    if (ws > ctc_ws_.bytes) {
+      std::vector<int> worst_l(N, std::min(T_max, 639)), worst_t(N, T_max);
+      size_t w2 = 0;
+      if (get_workspace_size(worst_l.data(), worst_t.data(), A, N, o, &w2) == CTC_STATUS_SUCCESS)
+        ws = std::max(ws, w2);
+    }
   }
   ctc_ws_.ensure(ws);
   costs_dev_.ensure(sizeof(double) * N);
@@ -1018,27 +1035,57 @@ MinibatchStats NnetCtcUpdater::ComputeForMinibatch(const float *feats, int T_max
   }
   if (update_) Backprop(T_max, N);
 
-  // ---- the single end-of-step device->host copy: costs, best-path ids ----
-  const size_t need = sizeof(double) * N + sizeof(int) * rows;
-  if (need > pinned_bytes_) {
-    if (pinned_) (void)hipHostFree(pinned_);
-    KCTC_HIP_CHECK(hipHostMalloc((void **)&pinned_, need, hipHostMallocDefault));
-    pinned_bytes_ = need;
+  // ---- the single end-of-step device->host copy: costs, best-path ids,
+  // the RNN components' device error words (into this slot's pinned buffer)
+  Slot &sl = slots_[next_];
+  const size_t need = sizeof(double) * N + sizeof(int) * rows + sizeof(unsigned) * C;
+  if (need > sl.bytes) {
+    if (sl.pinned) {
+      if (sl.ev) KCTC_HIP_CHECK(hipEventSynchronize(sl.ev));
+      (void)hipHostFree(sl.pinned);
+    }
+    KCTC_HIP_CHECK(hipHostMalloc((void **)&sl.pinned, need, hipHostMallocDefault));
+    sl.bytes = need;
   }
-  double *hcost = reinterpret_cast<double *>(pinned_);
-  int *hids = reinterpret_cast<int *>(reinterpret_cast<char *>(pinned_) + sizeof(double) * N);
+  if (!sl.ev) KCTC_HIP_CHECK(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
+  double *hcost = reinterpret_cast<double *>(sl.pinned);
+  int *hids = reinterpret_cast<int *>(sl.pinned + sizeof(double) * N);
+  unsigned *herr = reinterpret_cast<unsigned *>(hids + rows);
   KCTC_HIP_CHECK(hipMemcpyAsync(hcost, costs_dev_.p, sizeof(double) * N, hipMemcpyDeviceToHost, S()));
   KCTC_HIP_CHECK(hipMemcpyAsync(hids, ids_dev_.p, sizeof(int) * rows, hipMemcpyDeviceToHost, S()));
-  KCTC_HIP_CHECK(hipStreamSynchronize(S()));
-  CuDevice::Instantiate().Collect();
+  sl.nerr = 0;
   for (int c = 0; c < C; c++) {
     auto *r = dynamic_cast<CuDNNRecurrentComponent *>(&nnet_->GetComponent(c));
-    if (r) {
-      unsigned e = 0;
-      KCTC_HIP_CHECK(hipMemcpy(&e, r->DeviceError(), sizeof(e), hipMemcpyDeviceToHost));
-      if (e) throw std::runtime_error("recurrence hand-off timed out (device error word set)");
-    }
+    if (r) KCTC_HIP_CHECK(hipMemcpyAsync(herr + sl.nerr++, r->DeviceError(), sizeof(unsigned),
+                                         hipMemcpyDeviceToHost, S()));
   }
+  KCTC_HIP_CHECK(hipEventRecord(sl.ev, S()));
+  sl.N = N;
+  sl.rows = rows;
+  sl.num_frames.assign(num_frames, num_frames + N);
+  long nlab = 0;
+  for (int n = 0; n < N; n++) nlab += label_lengths[n];
+  sl.labels.assign(flat_labels, flat_labels + nlab);
+  sl.label_lengths.assign(label_lengths, label_lengths + N);
+  next_ ^= 1;
+  pending_++;
+}
+
+MinibatchStats NnetCtcUpdater::Finish() {
+  if (!pending_) throw std::logic_error("no queued minibatch");
+  Slot &sl = slots_[next_ ^ (pending_ == 2 ? 0 : 1)];  // the oldest
+  pending_--;
+  KCTC_HIP_CHECK(hipEventSynchronize(sl.ev));
+  if (!pending_) CuDevice::Instantiate().Collect();  // no span of a later minibatch in flight
+  const int N = sl.N;
+  const long rows = sl.rows;
+  const double *hcost = reinterpret_cast<const double *>(sl.pinned);
+  const int *hids = reinterpret_cast<const int *>(sl.pinned + sizeof(double) * N);
+  const unsigned *herr = reinterpret_cast<const unsigned *>(hids + rows);
+  for (int i = 0; i < sl.nerr; i++)
+    if (herr[i]) throw std::runtime_error("recurrence hand-off timed out (device error word set)");
+  const int *num_frames = sl.num_frames.data(), *flat_labels = sl.labels.data();
+  const int *label_lengths = sl.label_lengths.data();
   MinibatchStats st;
   for (int n = 0; n < N; n++) st.tot_objf += hcost[n];
   if (!(st.tot_objf == st.tot_objf)) throw std::runtime_error("costs sum is nan");  // :254

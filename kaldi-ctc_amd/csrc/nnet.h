@@ -361,6 +361,16 @@ class NnetCtcUpdater {
   // feats: device [T_max*N][input_dim] (FormatNnetInput layout)
   MinibatchStats ComputeForMinibatch(const float *feats, int T_max, int N, const int *num_frames,
                                      const int *flat_labels, const int *label_lengths);
+  // The same split in two: Enqueue queues all device work of a minibatch and
+  // the asynchronous readback of its costs, best paths and device error
+  // words (at most two minibatches in flight); Finish waits for the oldest
+  // one and computes its stats (ComputeTotAccuracy on the host).  With one
+  // minibatch queued ahead the host's per-step work (readback, accuracy,
+  // the caller's loop, the next step's launches) overlaps the device's.
+  void Enqueue(const float *feats, int T_max, int N, const int *num_frames, const int *flat_labels,
+               const int *label_lengths);
+  int Pending() const { return pending_; }
+  MinibatchStats Finish();
   void SetExchange(GradExchange *ex) { exchange_ = ex; }
   void SetRepairRng(uint64_t seed) { repair_rng_ = Rng(seed); }
 
@@ -375,8 +385,16 @@ class NnetCtcUpdater {
   std::vector<ChunkInfo> chunk_info_;
   CuMatrix deriv_a_, deriv_b_;
   DevBuf ctc_ws_, costs_dev_, ids_dev_;
-  float *pinned_ = nullptr;
-  size_t pinned_bytes_ = 0;
+  struct Slot {  // one minibatch in flight: pinned readback + what its stats need
+    char *pinned = nullptr;
+    size_t bytes = 0;
+    hipEvent_t ev = nullptr;
+    int N = 0, nerr = 0;
+    long rows = 0;
+    std::vector<int> num_frames, labels, label_lengths;
+  };
+  Slot slots_[2];
+  int next_ = 0, pending_ = 0;
 };
 
 }  // namespace nnet2

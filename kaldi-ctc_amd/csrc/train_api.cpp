@@ -240,6 +240,38 @@ int kctc_nnet_train_step(kctcNnet_t n, const float *feats_dev, int T_max, int N,
   });
 }
 
+int kctc_nnet_train_step_async(kctcNnet_t n, const float *feats_dev, int T_max, int N,
+                               const int *num_frames, const int *flat_labels, const int *label_lengths,
+                               int *have_stats, double *tot_objf, double *tot_accuracy, double *tot_weight) {
+  return guarded([&] {
+    n->activate();
+    if (have_stats) *have_stats = 0;
+    n->trainer.Enqueue(feats_dev, T_max, N, num_frames, flat_labels, label_lengths);
+    if (n->trainer.Pending() == 2) {
+      auto st = n->trainer.Finish();
+      if (have_stats) *have_stats = 1;
+      if (tot_objf) *tot_objf = st.tot_objf;
+      if (tot_accuracy) *tot_accuracy = st.tot_accuracy;
+      if (tot_weight) *tot_weight = st.tot_weight;
+    }
+  });
+}
+
+int kctc_nnet_train_flush(kctcNnet_t n, int *have_stats, double *tot_objf, double *tot_accuracy,
+                          double *tot_weight) {
+  return guarded([&] {
+    n->activate();
+    if (have_stats) *have_stats = 0;
+    if (n->trainer.Pending()) {
+      auto st = n->trainer.Finish();
+      if (have_stats) *have_stats = 1;
+      if (tot_objf) *tot_objf = st.tot_objf;
+      if (tot_accuracy) *tot_accuracy = st.tot_accuracy;
+      if (tot_weight) *tot_weight = st.tot_weight;
+    }
+  });
+}
+
 int kctc_nnet_compute_objf(kctcNnet_t n, const float *feats_dev, int T_max, int N,
                            const int *num_frames, const int *flat_labels, const int *label_lengths,
                            double *tot_objf, double *tot_accuracy, double *tot_weight) {

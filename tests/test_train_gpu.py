@@ -187,3 +187,30 @@ def test_rccl_dp_single_rank_matches_plain(kctc, gpu):
     for c in range(nets[0].num_components):
         if nets[0].num_params(c):
             np.testing.assert_array_equal(nets[0].get_params(c), nets[1].get_params(c))
+
+
+def test_async_steps_equal_sync_steps(kctc, gpu):
+    """kctc_nnet_train_step_async / train_flush: the same updates and the same
+    per-minibatch stats as kctc_nnet_train_step, reported one step late."""
+    import torch
+    D, A, T, N, H = 40, 41, 50, 4, 256
+    cfg = kctc.recipe_config(num_rnn=2, input_dim=D, hidden=H, num_targets=A, learning_rate=1e-3,
+                             param_stddev=0.05)
+    batches = []
+    for k in range(4):
+        feats, nf, fl, ll = kctc.synth_minibatch(100 + k, T, N, D, A, 0.125)
+        batches.append((torch.from_numpy(feats).to(gpu), nf, fl, ll))
+    a, b = kctc.Nnet(cfg, seed=6), kctc.Nnet(cfg, seed=6)
+    sync = [a.train_step(f, T, N, nf, fl, ll) for f, nf, fl, ll in batches]
+    got = []
+    for f, nf, fl, ll in batches:
+        r = b.train_step_async(f, T, N, nf, fl, ll)
+        if r is not None:
+            got.append(r)
+    assert len(got) == len(batches) - 1  # one queued ahead
+    got += b.train_flush()
+    assert got == sync
+    assert b.train_flush() == []
+    for c in range(a.num_components):
+        if a.num_params(c):
+            np.testing.assert_array_equal(a.get_params(c), b.get_params(c))
