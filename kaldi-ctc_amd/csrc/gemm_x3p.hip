@@ -101,6 +101,21 @@ __device__ __forceinline__ void load_tile_xch(const PParams &p, const _Float16 *
     reg[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off * 2), 0, 16 /* sc1 */);
   }
 }
+// the packed layout [row][KB][64], rows written by other workgroups (sc1 stores):
+// sc1 loads to registers, the tile image as issue_tile's
+__device__ __forceinline__ void load_tile_sc1(const _Float16 *__restrict__ P, int rows, int r0, int KB, int kb,
+                                              u32x4 (&reg)[4]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int r = (w * 4 + i) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (r & 7);
+    const int gr = min(r0 + r, rows - 1);
+    // one (uniform) descriptor: the host keeps rows * KB * 128 B below 2^31
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16 *>(P), 0, 0x7fffffff, 0x00020000);
+    reg[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((long)gr * KB + kb) * 128 + c * 16), 0, 16 /* sc1 */);
+  }
+}
 __device__ __forceinline__ void store_tile_lds(unsigned char *dst, const u32x4 (&reg)[4]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -303,8 +318,11 @@ __device__ __forceinline__ void x3p_tile(const PParams &p, unsigned char *lds, i
     if (STREAM) {
       load_tile_xch(p, A, m0, kb0, ra);
       store_tile_lds(lds, ra);
+    } else if (SM == 2) {  // rows packed by other workgroups: sc1 loads to registers (not LDS-DMA)
+      load_tile_sc1(A, p.M, m0, p.KB, kb0, ra);
+      store_tile_lds(lds, ra);
     } else {
-      issue_tile<SM == 2 ? 16 : 0>(A, p.M, m0, p.KB, kb0, lds);
+      issue_tile(A, p.M, m0, p.KB, kb0, lds);
     }
     issue_tile(B, p.N, n0, p.KB, kb0, lds + TILEB);
   }
@@ -315,7 +333,8 @@ __device__ __forceinline__ void x3p_tile(const PParams &p, unsigned char *lds, i
     unsigned char *nxt = lds + ((it + 1) & 1) * 2 * TILEB;
     if (it + 1 < nk) {
       if (STREAM) load_tile_xch(p, A, m0, kb0 + it + 1, ra);
-      else issue_tile<SM == 2 ? 16 : 0>(A, p.M, m0, p.KB, kb0 + it + 1, nxt);
+      else if (SM == 2) load_tile_sc1(A, p.M, m0, p.KB, kb0 + it + 1, ra);
+      else issue_tile(A, p.M, m0, p.KB, kb0 + it + 1, nxt);
       issue_tile(B, p.N, n0, p.KB, kb0 + it + 1, nxt + TILEB);
     }
     halfx8 ah[4], al[4], bh[4], bl[4];
@@ -341,7 +360,7 @@ __device__ __forceinline__ void x3p_tile(const PParams &p, unsigned char *lds, i
     for (int i = 0; i < 4; i++)
 #pragma unroll
       for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-    if (STREAM && it + 1 < nk) store_tile_lds(nxt, ra);
+    if ((STREAM || SM == 2) && it + 1 < nk) store_tile_lds(nxt, ra);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -747,7 +766,8 @@ size_t x3p_bwd_stream_ints(int M, int N) {
 void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a) {
   if (a.M <= 0 || a.N <= 0) return;
   const int K = a.KB * 32;
-  if (K > 4096 || a.Nf <= 0 || (long)a.M * a.N * 4 >= (1L << 31) || (a.lde & 3) || (a.edoff & 3))
+  if (K > 4096 || a.Nf <= 0 || (long)a.M * a.N * 4 >= (1L << 31) || (long)a.M * a.KB * 128 >= (1L << 31) ||
+      (a.lde & 3) || (a.edoff & 3))
     throw std::invalid_argument("gemm_x3p_bwd_stream: unsupported shape");
   PParams p{};
   p.A = a.Ap; p.eA = a.eA; p.sA = (long)a.M * a.KB * 64; p.seA = a.M;
