@@ -18,6 +18,10 @@
  *                               compressed bytes are uploaded and decoded on the GPU
  *                               (CompressedMatrix::CopyToMat arithmetic, bit-exact)
  *   kctc_cm_compress/decompress <- CompressedMatrix::CopyFromMat / CopyToMat (host)
+ *   kctc_egs_shuffle         <- nnet-ctc-shuffle-egs (src/ctcbin/nnet-ctc-shuffle-egs.cc:25-127)
+ *                               + FrameSubsamplingShiftNnetCtcExampleTimes
+ *                               (src/ctc/ctc-nnet-example.cc:78-106)
+ *   kctc_egs_sort            <- nnet-ctc-sort-egs (src/ctcbin/nnet-ctc-sort-egs.cc:27-133)
  * Archives: binary Kaldi "ark" files ("ark:path" or a plain path).  Return 0 on
  * success, non-zero on error (kctc_last_error() in kaldi_ctc_train.h). */
 #ifndef KALDI_CTC_EGS_H_
@@ -47,6 +51,17 @@ int kctc_egs_write(kctcEgsWriter_t w, const char *key, const float *feats, int n
                    const int *labels, int num_labels, int left_context, const float *spk_info,
                    int spk_dim);
 int kctc_egs_writer_close(kctcEgsWriter_t w);
+
+/* --- egs preparation tools (host) --- */
+/* Copy rspecifier -> wspecifier in the reference tools' order: --srand,
+ * --buffer-size (0 = whole archive in memory), --frame-shift,
+ * --frame-subsampling-factor (shuffle only; > 1 keeps input rows
+ * frame_shift, frame_shift + f, ... and re-compresses).  *num_done = examples
+ * written (the tools exit with status 1 when it is 0). */
+int kctc_egs_shuffle(const char *rspecifier, const char *wspecifier, int srand_seed, int buffer_size,
+                     int frame_shift, int frame_subsampling_factor, long *num_done);
+int kctc_egs_sort(const char *rspecifier, const char *wspecifier, int srand_seed, int buffer_size,
+                  long *num_done);
 
 /* --- background minibatch reader --- */
 /* nnet_left_context / nnet_right_context: the network's context (0 for the

@@ -510,6 +510,22 @@ def cm_decompress(img):
     return out
 
 
+def shuffle_egs(rspecifier, wspecifier, srand=0, buffer_size=0, frame_shift=0, frame_subsampling_factor=0):
+    """nnet-ctc-shuffle-egs (src/ctcbin/nnet-ctc-shuffle-egs.cc:25-127) -> examples written."""
+    n = ctypes.c_long()
+    _tcheck(lib().kctc_egs_shuffle(rspecifier.encode(), wspecifier.encode(), srand, buffer_size, frame_shift,
+                                   frame_subsampling_factor, ctypes.byref(n)), "kctc_egs_shuffle")
+    return n.value
+
+
+def sort_egs(rspecifier, wspecifier, srand=0, buffer_size=0):
+    """nnet-ctc-sort-egs (src/ctcbin/nnet-ctc-sort-egs.cc:27-133) -> examples written."""
+    n = ctypes.c_long()
+    _tcheck(lib().kctc_egs_sort(rspecifier.encode(), wspecifier.encode(), srand, buffer_size, ctypes.byref(n)),
+            "kctc_egs_sort")
+    return n.value
+
+
 class EgsWriter:
     """NnetCtcExampleWriter over a binary Kaldi archive (features compressed)."""
 

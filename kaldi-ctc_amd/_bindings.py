@@ -69,6 +69,8 @@ SIGS = {
     "kctc_egs_writer_open": (ci, [ctypes.POINTER(vp), ctypes.c_char_p]),
     "kctc_egs_write": (ci, [vp, ctypes.c_char_p, vp, ci, ci, vp, ci, ci, vp, ci]),
     "kctc_egs_writer_close": (ci, [vp]),
+    "kctc_egs_shuffle": (ci, [ctypes.c_char_p, ctypes.c_char_p, ci, ci, ci, ci, ctypes.POINTER(cl)]),
+    "kctc_egs_sort": (ci, [ctypes.c_char_p, ctypes.c_char_p, ci, ci, ctypes.POINTER(cl)]),
     "kctc_egs_reader_open": (ci, [ctypes.POINTER(vp), ctypes.c_char_p, ci, ci, ci, ci]),
     "kctc_egs_reader_next": (ci, [vp, ctypes.POINTER(vp)]),
     "kctc_egs_reader_stats": (ci, [vp, ctypes.POINTER(cl), ctypes.POINTER(cl)]),

@@ -138,6 +138,17 @@ class BackgroundReader {
   long skipped_ = 0, read_ = 0;
 };
 
+// Egs preparation tools (egs_tools.cpp): nnet-ctc-shuffle-egs
+// (src/ctcbin/nnet-ctc-shuffle-egs.cc:25-127) and nnet-ctc-sort-egs
+// (src/ctcbin/nnet-ctc-sort-egs.cc:27-133), same example order as the reference
+// binaries (glibc rand stream, libstdc++ shuffle / sort).  Return the number of
+// examples written.
+void FrameSubsamplingShift(int frame_subsampling_factor, int frame_shift, Example *eg);
+long ShuffleEgs(const std::string &rspecifier, const std::string &wspecifier, int srand_seed,
+                int buffer_size, int frame_shift, int frame_subsampling_factor);
+long SortEgs(const std::string &rspecifier, const std::string &wspecifier, int srand_seed,
+             int buffer_size);
+
 // Device side (egs_format.hip).
 size_t format_scratch_bytes(const Minibatch &mb);
 // H2D copy of the blob into `scratch`, then decode + pack into out[T_max*N][dim]

@@ -90,6 +90,25 @@ int kctc_egs_writer_close(kctcEgsWriter_t w) {
   });
 }
 
+int kctc_egs_shuffle(const char *rspecifier, const char *wspecifier, int srand_seed, int buffer_size,
+                     int frame_shift, int frame_subsampling_factor, long *num_done) {
+  return guarded([&] {
+    KCTC_REQUIRE(rspecifier && wspecifier, "kctc_egs_shuffle: null specifier");
+    const long n = ShuffleEgs(rspecifier, wspecifier, srand_seed, buffer_size, frame_shift,
+                              frame_subsampling_factor);
+    if (num_done) *num_done = n;
+  });
+}
+
+int kctc_egs_sort(const char *rspecifier, const char *wspecifier, int srand_seed, int buffer_size,
+                  long *num_done) {
+  return guarded([&] {
+    KCTC_REQUIRE(rspecifier && wspecifier, "kctc_egs_sort: null specifier");
+    const long n = SortEgs(rspecifier, wspecifier, srand_seed, buffer_size);
+    if (num_done) *num_done = n;
+  });
+}
+
 int kctc_egs_reader_open(kctcEgsReader_t *r, const char *spec, int minibatch_size, int max_frames, int l,
                          int rc) {
   return guarded([&] {
