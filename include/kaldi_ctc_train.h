@@ -15,8 +15,10 @@
  *   kctc_nnet_compute_objf  <- ComputeNnetObjf (no backprop; nnet2-ctc-compute-prob,
  *                              src/ctc/ctc-nnet-update.cc:426-431)
  *   kctc_nnet_get/set_params<- UpdatableComponent::Vectorize / UnVectorize
- *   kctc_nnet_write/read    <- Nnet::Write / Read (text form, component tokens of
- *                              nnet-cudnn-component.cc:673-837, nnet-component.cc:1228-1262)
+ *   kctc_nnet_write/read    <- Nnet::Write / Read (nnet-nnet.cc:170-220; component tokens of
+ *                              nnet-cudnn-component.cc:673-837, nnet-component.cc:1228-1274,
+ *                              2797-2831), Kaldi text or binary mode
+ *   kctc_am_nnet_*          <- CtcTransitionModel + AmNnet model files (am-nnet.cc:31-55)
  *   kctc_format_input       <- FormatNnetInput (src/ctc/ctc-nnet-update.cc:351-424)
  *   kctc_nnet_enable_dp     <- (new) data parallelism: RCCL all-reduce of the
  *                              weight gradients over xGMI; replaces the recipe's
@@ -84,8 +86,24 @@ struct ihipStream_t *kctc_nnet_stream(kctcNnet_t nnet);
 int kctc_nnet_set_profiling(kctcNnet_t nnet, int on);
 int kctc_nnet_profile(kctcNnet_t nnet, const char *family, double *ms_total, int *launches);
 
-int kctc_nnet_write(kctcNnet_t nnet, const char *path);
+int kctc_nnet_write(kctcNnet_t nnet, const char *path);  /* text mode */
+/* Nnet::Write in Kaldi text (binary = 0) or binary ("\0B" header) mode */
+int kctc_nnet_write_kaldi(kctcNnet_t nnet, const char *path, int binary);
+/* either mode (detected from the "\0B" header) */
 int kctc_nnet_read(kctcNnet_t *nnet, const char *path, int device);
+
+/* nnet2-ctc model files, the <model-in> / <model-out> of nnet2-ctc-train-simple
+ * (src/ctcbin/nnet2-ctc-train-simple.cc:58-77): CtcTransitionModel
+ * (src/ctc/ctc-transition-model.h:83-90, kept as the opaque bytes it was read
+ * as and written back unchanged) then AmNnet::Write = Nnet + priors
+ * (src/nnet2/am-nnet.cc:31-42).  Read detects the mode; a model whose
+ * transition model was read in one mode must be written in that mode. */
+int kctc_am_nnet_read(kctcNnet_t *nnet, const char *path, int device);
+int kctc_am_nnet_write(kctcNnet_t nnet, const char *path, int binary);
+int kctc_am_nnet_num_priors(kctcNnet_t nnet);
+int kctc_am_nnet_get_priors(kctcNnet_t nnet, float *priors, int dim);
+/* AmNnet::SetPriors (am-nnet.cc:44-55): dim <= output dim, zero-extended */
+int kctc_am_nnet_set_priors(kctcNnet_t nnet, const float *priors, int dim);
 
 /* Data parallelism over RCCL (one process per GPU).  uid: 128-byte
  * ncclUniqueId from kctc_dp_unique_id on rank 0, broadcast by the launcher. */

@@ -300,8 +300,30 @@ class Nnet:
         _tcheck(lib().kctc_nnet_read(ctypes.byref(h), str(path).encode(), device), "kctc_nnet_read")
         return cls(_handle=h)
 
-    def write(self, path):
-        _tcheck(lib().kctc_nnet_write(self.h, str(path).encode()), "kctc_nnet_write")
+    def write(self, path, binary=False):
+        """Nnet::Write (nnet-nnet.cc:170-183), Kaldi text or binary mode."""
+        _tcheck(lib().kctc_nnet_write_kaldi(self.h, str(path).encode(), int(binary)), "kctc_nnet_write_kaldi")
+
+    @classmethod
+    def read_am(cls, path, device=0):
+        """nnet2-ctc model file: CtcTransitionModel (kept opaque) + AmNnet (Nnet + priors)."""
+        h = ctypes.c_void_p()
+        _tcheck(lib().kctc_am_nnet_read(ctypes.byref(h), str(path).encode(), device), "kctc_am_nnet_read")
+        return cls(_handle=h)
+
+    def write_am(self, path, binary=True):
+        _tcheck(lib().kctc_am_nnet_write(self.h, str(path).encode(), int(binary)), "kctc_am_nnet_write")
+
+    @property
+    def priors(self):
+        n = lib().kctc_am_nnet_num_priors(self.h)
+        out = np.zeros(n, dtype=np.float32)
+        _tcheck(lib().kctc_am_nnet_get_priors(self.h, out.ctypes.data, n), "kctc_am_nnet_get_priors")
+        return out
+
+    def set_priors(self, priors):
+        p = np.ascontiguousarray(priors, dtype=np.float32)
+        _tcheck(lib().kctc_am_nnet_set_priors(self.h, p.ctypes.data, p.size), "kctc_am_nnet_set_priors")
 
     def close(self):
         if getattr(self, "h", None):

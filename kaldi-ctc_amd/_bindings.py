@@ -54,6 +54,12 @@ SIGS = {
     "kctc_nnet_profile": (ci, [vp, ctypes.c_char_p, ctypes.POINTER(cd), ctypes.POINTER(ci)]),
     "kctc_nnet_write": (ci, [vp, ctypes.c_char_p]),
     "kctc_nnet_read": (ci, [ctypes.POINTER(vp), ctypes.c_char_p, ci]),
+    "kctc_nnet_write_kaldi": (ci, [vp, ctypes.c_char_p, ci]),
+    "kctc_am_nnet_read": (ci, [ctypes.POINTER(vp), ctypes.c_char_p, ci]),
+    "kctc_am_nnet_write": (ci, [vp, ctypes.c_char_p, ci]),
+    "kctc_am_nnet_num_priors": (ci, [vp]),
+    "kctc_am_nnet_get_priors": (ci, [vp, vp, ci]),
+    "kctc_am_nnet_set_priors": (ci, [vp, vp, ci]),
     "kctc_dp_unique_id": (ci, [vp]),
     "kctc_nnet_enable_dp": (ci, [vp, vp, ci, ci]),
     "kctc_nnet_set_momentum": (ci, [vp, cf]),

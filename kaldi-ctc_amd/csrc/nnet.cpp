@@ -1,6 +1,7 @@
 // nnet.cpp -- nnet2 CTC training path on MI355X (see nnet.h for the mapping to
 // the reference's classes).
 #include "nnet.h"
+#include "kaldi_io.h"
 
 #include <algorithm>
 #include <cmath>
@@ -241,26 +242,11 @@ static bool ParseFromString(const std::string &name, std::string *args, std::vec
   return true;
 }
 
-// ---- text I/O helpers (Kaldi text-mode token stream) ----
-static void WriteToken(std::ostream &os, const char *t) { os << t << ' '; }
-static void ExpectToken(std::istream &is, const char *t) {
-  std::string s;
-  is >> s;
-  if (s != t) throw std::runtime_error(std::string("Expected token ") + t + ", got " + s);
-}
-static void WriteVec(std::ostream &os, const std::vector<float> &v) {
-  os << " [ ";
-  for (float x : v) os << std::setprecision(9) << x << ' ';
-  os << "]\n";
-}
-static std::vector<float> ReadVec(std::istream &is) {
-  std::string s;
-  is >> s;
-  if (s != "[") throw std::runtime_error("Expected [ , got " + s);
-  std::vector<float> v;
-  while (is >> s && s != "]") v.push_back(std::stof(s));
-  return v;
-}
+// ---- Kaldi token stream, both modes (kaldi_io.h) ----
+using kio::ExpectToken;
+using kio::WriteToken;
+// counters are int32 in the reference's files (nnet-cudnn-component.h:263-266)
+static int32_t as_i32(double v) { return (int32_t)(uint32_t)(uint64_t)(int64_t)v; }
 static std::vector<float> d2h(const float *d, long n) {
   std::vector<float> h((size_t)n);
   if (n) {
@@ -324,32 +310,36 @@ void SpliceComponent::Backprop(const ChunkInfo &, const ChunkInfo &, const CuMat
                                   sizeof(float) * out_deriv.NumRows() * out_deriv.NumCols(),
                                   hipMemcpyDeviceToDevice, S()));
 }
-void SpliceComponent::Write(std::ostream &os) const {
-  WriteToken(os, "<SpliceComponent>");
-  WriteToken(os, "<InputDim>");
-  os << input_dim_ << ' ';
-  WriteToken(os, "<Context>");
-  os << "[ ";
-  for (int c : context_) os << c << ' ';
-  os << "] ";
-  WriteToken(os, "<ConstComponentDim>");
-  os << 0 << ' ';
-  WriteToken(os, "</SpliceComponent>");
-}
-void SpliceComponent::Read(std::istream &is) {
-  ExpectToken(is, "<InputDim>");
-  is >> input_dim_;
-  ExpectToken(is, "<Context>");
-  std::string s;
-  is >> s;
+void SpliceComponent::Write(std::ostream &os, bool binary) const {
+  WriteToken(os, binary, "<SpliceComponent>");
+  WriteToken(os, binary, "<InputDim>");
+  kio::WriteInt(os, binary, input_dim_);
+  WriteToken(os, binary, "<Context>");
+  kio::WriteIntVector(os, binary, std::vector<int32_t>(context_.begin(), context_.end()));
+  WriteToken(os, binary, "<ConstComponentDim>");
+  kio::WriteInt(os, binary, 0);
+  WriteToken(os, binary, "</SpliceComponent>");
+}// SpliceComponent::Read (nnet-component.cc:2797-2820), incl. the old
+// <LeftContext>/<RightContext> form
+void SpliceComponent::Read(std::istream &is, bool binary) {
+  ExpectToken(is, binary, "<InputDim>");
+  input_dim_ = kio::ReadInt(is, binary);
+  const std::string t = kio::ReadToken(is, binary);
   context_.clear();
-  while (is >> s && s != "]") context_.push_back(std::stoi(s));
-  ExpectToken(is, "<ConstComponentDim>");
-  int c;
-  is >> c;
-  ExpectToken(is, "</SpliceComponent>");
+  if (t == "<LeftContext>") {
+    const int l = kio::ReadInt(is, binary);
+    ExpectToken(is, binary, "<RightContext>");
+    const int r = kio::ReadInt(is, binary);
+    for (int i = -l; i <= r; i++) context_.push_back(i);
+  } else if (t == "<Context>") {
+    for (int32_t c : kio::ReadIntVector(is, binary)) context_.push_back(c);
+  } else {
+    throw std::runtime_error("SpliceComponent: unknown token " + t);
+  }
+  ExpectToken(is, binary, "<ConstComponentDim>");
+  if (kio::ReadInt(is, binary) != 0) throw std::runtime_error("SpliceComponent: const_component_dim != 0 is not supported");
+  ExpectToken(is, binary, "</SpliceComponent>");
 }
-
 // ---------------------------------------------------------------------------
 // CuDNNRecurrentComponent (nnet-cudnn-component.cc:56-772)
 // ---------------------------------------------------------------------------
@@ -529,42 +519,60 @@ void CuDNNRecurrentComponent::Vectorize(float *host) const {
 }
 void CuDNNRecurrentComponent::UnVectorize(const float *host) { h2d(params_.f(), host, NumParameters()); }
 
-void CuDNNRecurrentComponent::Write(std::ostream &os) const {
-  WriteToken(os, "<CuDNNRecurrentComponent>");
-  WriteToken(os, "<LearningRate>"); os << learning_rate_ << ' ';
-  WriteToken(os, "<IsGradient>"); os << (is_gradient_ ? "T" : "F") << ' ';
-  WriteToken(os, "<ClipGradient>"); os << clip_gradient_ << ' ';
-  WriteToken(os, "<InputDim>"); os << desc_.D << ' ';
-  WriteToken(os, "<HiddenDim>"); os << desc_.H << ' ';
-  WriteToken(os, "<NumLayers>"); os << desc_.layers << ' ';
-  WriteToken(os, "<Bidirectional>"); os << (desc_.dirs == 2 ? "T" : "F") << ' ';
-  WriteToken(os, "<RNNMode>"); os << desc_.mode << ' ';
-  WriteToken(os, "<MaxSeqLength>"); os << max_seq_length_ << ' ';
-  WriteToken(os, "<FilterParams>");
-  WriteVec(os, d2h(params_.f(), NumParameters()));
-  WriteToken(os, "</CuDNNRecurrentComponent>");
-}
-void CuDNNRecurrentComponent::Read(std::istream &is) {
-  std::string b;
-  ExpectToken(is, "<LearningRate>"); is >> learning_rate_;
-  ExpectToken(is, "<IsGradient>"); is >> b; is_gradient_ = (b == "T" || b == "1");
-  ExpectToken(is, "<ClipGradient>"); is >> clip_gradient_;
-  ExpectToken(is, "<InputDim>"); is >> desc_.D;
-  ExpectToken(is, "<HiddenDim>"); is >> desc_.H;
-  ExpectToken(is, "<NumLayers>"); is >> desc_.layers;
-  ExpectToken(is, "<Bidirectional>"); is >> b; desc_.dirs = (b == "T" || b == "1") ? 2 : 1;
-  ExpectToken(is, "<RNNMode>"); is >> desc_.mode;
-  ExpectToken(is, "<MaxSeqLength>"); is >> max_seq_length_;
-  ExpectToken(is, "<FilterParams>");
-  auto v = ReadVec(is);
+// nnet-cudnn-component.cc:698-721
+void CuDNNRecurrentComponent::Write(std::ostream &os, bool binary) const {
+  WriteToken(os, binary, "<CuDNNRecurrentComponent>");
+  WriteToken(os, binary, "<LearningRate>");
+  kio::WriteFloat(os, binary, learning_rate_);
+  WriteToken(os, binary, "<IsGradient>");
+  kio::WriteBool(os, binary, is_gradient_);
+  WriteToken(os, binary, "<ClipGradient>");
+  kio::WriteFloat(os, binary, clip_gradient_);
+  WriteToken(os, binary, "<InputDim>");
+  kio::WriteInt(os, binary, desc_.D);
+  WriteToken(os, binary, "<HiddenDim>");
+  kio::WriteInt(os, binary, desc_.H);
+  WriteToken(os, binary, "<NumLayers>");
+  kio::WriteInt(os, binary, desc_.layers);
+  WriteToken(os, binary, "<Bidirectional>");
+  kio::WriteBool(os, binary, desc_.dirs == 2);
+  WriteToken(os, binary, "<RNNMode>");
+  kio::WriteInt(os, binary, desc_.mode);
+  WriteToken(os, binary, "<MaxSeqLength>");
+  kio::WriteInt(os, binary, max_seq_length_);
+  WriteToken(os, binary, "<FilterParams>");
+  auto v = d2h(params_.f(), NumParameters());
+  kio::WriteFloatVector(os, binary, v.data(), (long)v.size());
+  WriteToken(os, binary, "</CuDNNRecurrentComponent>");
+}// nnet-cudnn-component.cc:673-696
+void CuDNNRecurrentComponent::Read(std::istream &is, bool binary) {
+  ExpectToken(is, binary, "<LearningRate>");
+  learning_rate_ = kio::ReadFloat(is, binary);
+  ExpectToken(is, binary, "<IsGradient>");
+  is_gradient_ = kio::ReadBool(is, binary);
+  ExpectToken(is, binary, "<ClipGradient>");
+  clip_gradient_ = kio::ReadFloat(is, binary);
+  ExpectToken(is, binary, "<InputDim>");
+  desc_.D = kio::ReadInt(is, binary);
+  ExpectToken(is, binary, "<HiddenDim>");
+  desc_.H = kio::ReadInt(is, binary);
+  ExpectToken(is, binary, "<NumLayers>");
+  desc_.layers = kio::ReadInt(is, binary);
+  ExpectToken(is, binary, "<Bidirectional>");
+  desc_.dirs = kio::ReadBool(is, binary) ? 2 : 1;
+  ExpectToken(is, binary, "<RNNMode>");
+  desc_.mode = kio::ReadInt(is, binary);
+  ExpectToken(is, binary, "<MaxSeqLength>");
+  max_seq_length_ = kio::ReadInt(is, binary);
+  ExpectToken(is, binary, "<FilterParams>");
+  auto v = kio::ReadFloatVector(is, binary);
   if ((long)v.size() != desc_.params_size())
     throw std::runtime_error("CuDNNRecurrentComponent: FilterParams size mismatch");
   params_.ensure(sizeof(float) * v.size());
   grad_.ensure(sizeof(float) * v.size());
   h2d(params_.f(), v.data(), (long)v.size());
-  ExpectToken(is, "</CuDNNRecurrentComponent>");
+  ExpectToken(is, binary, "</CuDNNRecurrentComponent>");
 }
-
 // ---------------------------------------------------------------------------
 // ClipGradientComponent (nnet-cudnn-component.cc:775-1075)
 // ---------------------------------------------------------------------------
@@ -685,48 +693,65 @@ void ClipGradientComponent::ZeroStats() {
   num_clipped_ = count_ = num_self_repaired_ = num_backpropped_ = 0;
 }
 
-void ClipGradientComponent::Write(std::ostream &os) const {
+// nnet-cudnn-component.cc:814-837
+void ClipGradientComponent::Write(std::ostream &os, bool binary) const {
   SyncStats();
-  WriteToken(os, "<ClipGradientComponent>");
-  WriteToken(os, "<Dim>"); os << dim_ << ' ';
-  WriteToken(os, "<ClippingThreshold>"); os << clipping_threshold_ << ' ';
-  WriteToken(os, "<NormBasedClipping>"); os << (norm_based_clipping_ ? "T" : "F") << ' ';
-  WriteToken(os, "<SelfRepairClippedProportionThreshold>");
-  os << self_repair_clipped_proportion_threshold_ << ' ';
-  WriteToken(os, "<SelfRepairTarget>"); os << self_repair_target_ << ' ';
-  WriteToken(os, "<SelfRepairScale>"); os << self_repair_scale_ << ' ';
-  WriteToken(os, "<NumElementsClipped>"); os << num_clipped_ << ' ';
-  WriteToken(os, "<NumElementsProcessed>"); os << count_ << ' ';
-  WriteToken(os, "<NumSelfRepaired>"); os << num_self_repaired_ << ' ';
-  WriteToken(os, "<NumBackpropped>"); os << num_backpropped_ << ' ';
-  WriteToken(os, "</ClipGradientComponent>");
-}
-void ClipGradientComponent::Read(std::istream &is) {
-  std::string b;
-  ExpectToken(is, "<Dim>"); is >> dim_;
-  ExpectToken(is, "<ClippingThreshold>"); is >> clipping_threshold_;
-  ExpectToken(is, "<NormBasedClipping>"); is >> b; norm_based_clipping_ = (b == "T" || b == "1");
-  is >> b;
-  if (b == "<SelfRepairClippedProportionThreshold>") {
-    is >> self_repair_clipped_proportion_threshold_;
-    ExpectToken(is, "<SelfRepairTarget>"); is >> self_repair_target_;
-    ExpectToken(is, "<SelfRepairScale>"); is >> self_repair_scale_;
-    ExpectToken(is, "<NumElementsClipped>");
+  WriteToken(os, binary, "<ClipGradientComponent>");
+  WriteToken(os, binary, "<Dim>");
+  kio::WriteInt(os, binary, dim_);
+  WriteToken(os, binary, "<ClippingThreshold>");
+  kio::WriteFloat(os, binary, clipping_threshold_);
+  WriteToken(os, binary, "<NormBasedClipping>");
+  kio::WriteBool(os, binary, norm_based_clipping_);
+  WriteToken(os, binary, "<SelfRepairClippedProportionThreshold>");
+  kio::WriteFloat(os, binary, self_repair_clipped_proportion_threshold_);
+  WriteToken(os, binary, "<SelfRepairTarget>");
+  kio::WriteFloat(os, binary, self_repair_target_);
+  WriteToken(os, binary, "<SelfRepairScale>");
+  kio::WriteFloat(os, binary, self_repair_scale_);
+  WriteToken(os, binary, "<NumElementsClipped>");
+  kio::WriteInt(os, binary, as_i32(num_clipped_));
+  WriteToken(os, binary, "<NumElementsProcessed>");
+  kio::WriteInt(os, binary, as_i32(count_));
+  WriteToken(os, binary, "<NumSelfRepaired>");
+  kio::WriteInt(os, binary, as_i32(num_self_repaired_));
+  WriteToken(os, binary, "<NumBackpropped>");
+  kio::WriteInt(os, binary, as_i32(num_backpropped_));
+  WriteToken(os, binary, "</ClipGradientComponent>");
+}// nnet-cudnn-component.cc:775-812 (older files without the self-repair fields)
+void ClipGradientComponent::Read(std::istream &is, bool binary) {
+  ExpectToken(is, binary, "<Dim>");
+  dim_ = kio::ReadInt(is, binary);
+  ExpectToken(is, binary, "<ClippingThreshold>");
+  clipping_threshold_ = kio::ReadFloat(is, binary);
+  ExpectToken(is, binary, "<NormBasedClipping>");
+  norm_based_clipping_ = kio::ReadBool(is, binary);
+  std::string t = kio::ReadToken(is, binary);
+  if (t == "<SelfRepairClippedProportionThreshold>") {
+    self_repair_clipped_proportion_threshold_ = kio::ReadFloat(is, binary);
+    ExpectToken(is, binary, "<SelfRepairTarget>");
+    self_repair_target_ = kio::ReadFloat(is, binary);
+    ExpectToken(is, binary, "<SelfRepairScale>");
+    self_repair_scale_ = kio::ReadFloat(is, binary);
+    ExpectToken(is, binary, "<NumElementsClipped>");
   } else {
     self_repair_clipped_proportion_threshold_ = 1.0f;
     self_repair_target_ = 0.0f;
     self_repair_scale_ = 0.0f;
-    if (b != "<NumElementsClipped>") throw std::runtime_error("ClipGradientComponent: bad token " + b);
+    if (t != "<NumElementsClipped>") throw std::runtime_error("ClipGradientComponent: bad token " + t);
   }
-  is >> num_clipped_;
-  ExpectToken(is, "<NumElementsProcessed>"); is >> count_;
-  is >> b;
-  if (b == "<NumSelfRepaired>") {
-    is >> num_self_repaired_;
-    ExpectToken(is, "<NumBackpropped>"); is >> num_backpropped_;
-    ExpectToken(is, "</ClipGradientComponent>");
+  num_clipped_ = kio::ReadInt(is, binary);
+  ExpectToken(is, binary, "<NumElementsProcessed>");
+  count_ = kio::ReadInt(is, binary);
+  t = kio::ReadToken(is, binary);
+  if (t == "<NumSelfRepaired>") {
+    num_self_repaired_ = kio::ReadInt(is, binary);
+    ExpectToken(is, binary, "<NumBackpropped>");
+    num_backpropped_ = kio::ReadInt(is, binary);
+    ExpectToken(is, binary, "</ClipGradientComponent>");
   } else {
     num_self_repaired_ = num_backpropped_ = 0;
+    if (t != "</ClipGradientComponent>") throw std::runtime_error("ClipGradientComponent: bad token " + t);
   }
   ClipState h{};
   h.num_clipped = num_clipped_;
@@ -734,7 +759,6 @@ void ClipGradientComponent::Read(std::istream &is) {
   h.num_self_repaired = num_self_repaired_;
   KCTC_HIP_CHECK(hipMemcpy(dev_, &h, sizeof(h), hipMemcpyHostToDevice));
 }
-
 // ---------------------------------------------------------------------------
 // AffineComponent (nnet-component.cc:1125-1274)
 // ---------------------------------------------------------------------------
@@ -820,59 +844,49 @@ void AffineComponent::Vectorize(float *host) const {
 }
 void AffineComponent::UnVectorize(const float *host) { h2d(params_.f(), host, NumParameters()); }
 
-void AffineComponent::Write(std::ostream &os) const {
+// nnet-component.cc:1260-1274
+void AffineComponent::Write(std::ostream &os, bool binary) const {
   auto v = d2h(params_.f(), NumParameters());
-  WriteToken(os, "<AffineComponent>");
-  WriteToken(os, "<LearningRate>"); os << learning_rate_ << ' ';
-  WriteToken(os, "<LinearParams>");
-  os << " [\n";
-  for (int r = 0; r < out_dim_; r++) {
-    os << "  ";
-    for (int c = 0; c < in_dim_; c++) os << std::setprecision(9) << v[(size_t)r * in_dim_ + c] << ' ';
-    os << (r + 1 == out_dim_ ? "]\n" : "\n");
-  }
-  WriteToken(os, "<BiasParams>");
-  WriteVec(os, std::vector<float>(v.begin() + (long)in_dim_ * out_dim_, v.end()));
-  WriteToken(os, "<IsGradient>"); os << "F ";
-  WriteToken(os, "</AffineComponent>");
-}
-void AffineComponent::Read(std::istream &is) {
-  ExpectToken(is, "<LearningRate>"); is >> learning_rate_;
-  ExpectToken(is, "<LinearParams>");
-  std::string s;
-  is >> s;
-  if (s != "[") throw std::runtime_error("AffineComponent: expected [");
-  std::vector<float> lin;
-  std::vector<int> row_len;
-  // rows are newline separated; count columns from the first line
-  std::string line;
-  std::getline(is, line);
-  while (std::getline(is, line)) {
-    std::istringstream ls(line);
-    int n = 0;
-    bool end = false;
-    while (ls >> s) {
-      if (s == "]") { end = true; break; }
-      lin.push_back(std::stof(s));
-      n++;
-    }
-    if (n) row_len.push_back(n);
-    if (end) break;
-  }
-  if (row_len.empty()) throw std::runtime_error("AffineComponent: empty LinearParams");
-  out_dim_ = (int)row_len.size();
-  in_dim_ = row_len[0];
-  ExpectToken(is, "<BiasParams>");
-  auto b = ReadVec(is);
+  WriteToken(os, binary, "<AffineComponent>");
+  WriteToken(os, binary, "<LearningRate>");
+  kio::WriteFloat(os, binary, learning_rate_);
+  WriteToken(os, binary, "<LinearParams>");
+  kio::WriteFloatMatrix(os, binary, v.data(), out_dim_, in_dim_);
+  WriteToken(os, binary, "<BiasParams>");
+  kio::WriteFloatVector(os, binary, v.data() + (long)in_dim_ * out_dim_, out_dim_);
+  WriteToken(os, binary, "<IsGradient>");
+  kio::WriteBool(os, binary, false);
+  WriteToken(os, binary, "</AffineComponent>");
+}// nnet-component.cc:1228-1258 (incl. the <AvgInput> back-compatibility fields)
+void AffineComponent::Read(std::istream &is, bool binary) {
+  ExpectToken(is, binary, "<LearningRate>");
+  learning_rate_ = kio::ReadFloat(is, binary);
+  ExpectToken(is, binary, "<LinearParams>");
+  int rows = 0, cols = 0;
+  auto lin = kio::ReadFloatMatrix(is, binary, &rows, &cols);
+  if (rows == 0 || cols == 0) throw std::runtime_error("AffineComponent: empty LinearParams");
+  out_dim_ = rows;
+  in_dim_ = cols;
+  ExpectToken(is, binary, "<BiasParams>");
+  auto b = kio::ReadFloatVector(is, binary);
   if ((int)b.size() != out_dim_) throw std::runtime_error("AffineComponent: bias size mismatch");
-  is >> s;
-  if (s == "<IsGradient>") { is >> s; ExpectToken(is, "</AffineComponent>"); }
+  std::string t = kio::ReadToken(is, binary);
+  if (t == "<AvgInput>") {  // discarded
+    kio::ReadFloatVector(is, binary);
+    ExpectToken(is, binary, "<AvgInputCount>");
+    kio::ReadFloat(is, binary);
+    t = kio::ReadToken(is, binary);
+  }
+  if (t == "<IsGradient>") {
+    kio::ReadBool(is, binary);
+    t = kio::ReadToken(is, binary);
+  }
+  if (t != "</AffineComponent>") throw std::runtime_error("AffineComponent: bad token " + t);
   lin.insert(lin.end(), b.begin(), b.end());
   params_.ensure(sizeof(float) * lin.size());
   grad_.ensure(sizeof(float) * lin.size());
   h2d(params_.f(), lin.data(), (long)lin.size());
 }
-
 // ---------------------------------------------------------------------------
 // Nnet
 // ---------------------------------------------------------------------------
@@ -926,34 +940,36 @@ void Nnet::SetLearningRate(float lr) {
     if (c->IsUpdatable()) static_cast<UpdatableComponent *>(c)->SetLearningRate(lr);
 }
 
-void Nnet::Write(std::ostream &os) const {
-  os << "<Nnet> <NumComponents> " << components_.size() << "\n<Components> ";
+// nnet-nnet.cc:170-183
+void Nnet::Write(std::ostream &os, bool binary) const {
+  WriteToken(os, binary, "<Nnet>");
+  WriteToken(os, binary, "<NumComponents>");
+  kio::WriteInt(os, binary, (int32_t)components_.size());
+  WriteToken(os, binary, "<Components>");
   for (auto *c : components_) {
-    c->Write(os);
-    os << "\n";
+    c->Write(os, binary);
+    if (!binary) os << "\n";
   }
-  os << "</Components> </Nnet>\n";
+  WriteToken(os, binary, "</Components>");
+  WriteToken(os, binary, "</Nnet>");
 }
-
-void Nnet::Read(std::istream &is) {
-  ExpectToken(is, "<Nnet>");
-  ExpectToken(is, "<NumComponents>");
-  int n;
-  is >> n;
-  ExpectToken(is, "<Components>");
+// nnet-nnet.cc:185-220 (Component::ReadNew: "<Type>" token, then the body)
+void Nnet::Read(std::istream &is, bool binary) {
+  ExpectToken(is, binary, "<Nnet>");
+  ExpectToken(is, binary, "<NumComponents>");
+  const int n = kio::ReadInt(is, binary);
+  ExpectToken(is, binary, "<Components>");
   for (int i = 0; i < n; i++) {
-    std::string t;
-    is >> t;
+    const std::string t = kio::ReadToken(is, binary);
     if (t.size() < 3) throw std::runtime_error("bad component token " + t);
     Component *c = Component::NewComponentOfType(t.substr(1, t.size() - 2));
     if (!c) throw std::runtime_error("Unknown component " + t);
-    c->Read(is);
     components_.push_back(c);
+    c->Read(is, binary);
   }
-  ExpectToken(is, "</Components>");
-  ExpectToken(is, "</Nnet>");
+  ExpectToken(is, binary, "</Components>");
+  ExpectToken(is, binary, "</Nnet>");
 }
-
 // ---------------------------------------------------------------------------
 // NnetCtcUpdater (src/ctc/ctc-nnet-update.cc:76-348)
 // ---------------------------------------------------------------------------

@@ -143,8 +143,8 @@ class Component {
                         const CuMatrixBase &in_value, const CuMatrixBase &out_value,
                         const CuMatrixBase &out_deriv, Component *to_update,
                         CuMatrixBase *in_deriv) const = 0;
-  virtual void Write(std::ostream &os) const = 0;
-  virtual void Read(std::istream &is) = 0;
+  virtual void Write(std::ostream &os, bool binary) const = 0;
+  virtual void Read(std::istream &is, bool binary) = 0;
   virtual void ZeroStats() {}
   static Component *NewComponentOfType(const std::string &type);
 };
@@ -189,8 +189,8 @@ class SpliceComponent : public Component {
                  CuMatrixBase *out) const override;
   void Backprop(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &, const CuMatrixBase &,
                 const CuMatrixBase &, Component *, CuMatrixBase *) const override;
-  void Write(std::ostream &os) const override;
-  void Read(std::istream &is) override;
+  void Write(std::ostream &os, bool binary) const override;
+  void Read(std::istream &is, bool binary) override;
 
  private:
   int input_dim_ = 0;
@@ -212,8 +212,8 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
                 const CuMatrixBase &in_value, const CuMatrixBase &out_value,
                 const CuMatrixBase &out_deriv, Component *to_update,
                 CuMatrixBase *in_deriv) const override;
-  void Write(std::ostream &os) const override;
-  void Read(std::istream &is) override;
+  void Write(std::ostream &os, bool binary) const override;
+  void Read(std::istream &is, bool binary) override;
   long NumParameters() const override { return desc_.params_size(); }
   void Vectorize(float *host) const override;
   void UnVectorize(const float *host) override;
@@ -262,8 +262,8 @@ class ClipGradientComponent : public Component {
   void Backprop(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &in_value,
                 const CuMatrixBase &, const CuMatrixBase &out_deriv, Component *to_update,
                 CuMatrixBase *in_deriv) const override;
-  void Write(std::ostream &os) const override;
-  void Read(std::istream &is) override;
+  void Write(std::ostream &os, bool binary) const override;
+  void Read(std::istream &is, bool binary) override;
   void ZeroStats() override;
   // host view of the device counters (valid after a stream sync)
   void SyncStats() const;
@@ -302,8 +302,8 @@ class AffineComponent : public UpdatableComponent {
   void Backprop(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &in_value,
                 const CuMatrixBase &, const CuMatrixBase &out_deriv, Component *to_update,
                 CuMatrixBase *in_deriv) const override;
-  void Write(std::ostream &os) const override;
-  void Read(std::istream &is) override;
+  void Write(std::ostream &os, bool binary) const override;
+  void Read(std::istream &is, bool binary) override;
   long NumParameters() const override { return (long)(in_dim_ + 1) * out_dim_; }
   void Vectorize(float *host) const override;  // linear (row-major) then bias
   void UnVectorize(const float *host) override;
@@ -331,8 +331,8 @@ class Nnet {
   void SetLearningRate(float lr);
   void SetMomentum(float m);
   float Momentum() const { return momentum_; }
-  void Write(std::ostream &os) const;
-  void Read(std::istream &is);
+  void Write(std::ostream &os, bool binary) const;
+  void Read(std::istream &is, bool binary);
 
  private:
   std::vector<Component *> components_;

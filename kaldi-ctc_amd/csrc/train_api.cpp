@@ -13,6 +13,7 @@
 
 #include "common.h"
 #include "egs.h"
+#include "kaldi_io.h"
 #include "nnet.h"
 
 using kctc::nnet2::CuDevice;
@@ -79,6 +80,11 @@ struct kctcNnetImpl {
   hipStream_t side = nullptr, stream2 = nullptr;
   RcclExchange *dp = nullptr;
   kctc::nnet2::DevBuf egs_feats, egs_scratch;  // TrainNnetSimple staging
+  // nnet2-ctc model file extras: the CtcTransitionModel exactly as read (opaque
+  // bytes, in the mode of the file it came from) and AmNnet's priors
+  std::string trans_model;
+  bool trans_model_binary = false;
+  std::vector<float> priors;
   ~kctcNnetImpl() {
     delete dp;
     if (stream) (void)hipStreamSynchronize(stream);
@@ -305,31 +311,122 @@ int kctc_nnet_profile(kctcNnet_t n, const char *family, double *ms_total, int *l
   });
 }
 
-int kctc_nnet_write(kctcNnet_t n, const char *path) {
+int kctc_nnet_write(kctcNnet_t n, const char *path) { return kctc_nnet_write_kaldi(n, path, 0); }
+
+int kctc_nnet_write_kaldi(kctcNnet_t n, const char *path, int binary) {
   return guarded([&] {
     n->activate();
-    std::ofstream os(path);
+    std::ofstream os(path, std::ios::binary | std::ios::trunc);
     if (!os) throw std::runtime_error(std::string("cannot open ") + path);
-    n->nnet.Write(os);
+    kctc::kio::InitOutput(os, binary != 0);
+    n->nnet.Write(os, binary != 0);
+    if (!os) throw std::runtime_error(std::string("write failed: ") + path);
   });
+}
+
+static std::string slurp(const char *path) {
+  std::ifstream is(path, std::ios::binary);
+  if (!is) throw std::runtime_error(std::string("cannot open ") + path);
+  std::ostringstream ss;
+  ss << is.rdbuf();
+  return ss.str();
+}
+
+static kctcNnetImpl *new_on_device(int device) {
+  auto *n = new kctcNnetImpl;
+  try {
+    n->device = device;
+    KCTC_HIP_CHECK(hipSetDevice(device));
+    n->create_streams();
+    n->activate();
+  } catch (...) {
+    delete n;
+    throw;
+  }
+  return n;
+}
+
+// whole file in memory (models are ~0.1 GB); `am`: the nnet2-ctc model form
+// (CtcTransitionModel + Nnet + priors, nnet2-ctc-train-simple.cc:58-64)
+static void read_model(kctcNnetImpl *n, const char *path, bool am) {
+  std::istringstream is(slurp(path));
+  const bool binary = kctc::kio::InitInput(is);
+  if (am && kctc::kio::PeekToken(is, binary) == "<TransitionModel>") {
+    // kept opaque: everything up to and including the "</TransitionModel> " token
+    const std::string &buf = is.str();
+    const std::string end_tok = "</TransitionModel> ";
+    const auto start = (size_t)is.tellg();
+    const auto e = buf.find(end_tok, start);
+    if (e == std::string::npos) throw std::runtime_error("unterminated <TransitionModel>");
+    n->trans_model = buf.substr(start, e + end_tok.size() - start);
+    n->trans_model_binary = binary;
+    is.seekg((std::streamoff)(e + end_tok.size()));
+  }
+  n->nnet.Read(is, binary);
+  if (am) {
+    n->priors = kctc::kio::ReadFloatVector(is, binary);
+    if (!n->priors.empty() && (int)n->priors.size() != n->nnet.OutputDim())
+      throw std::runtime_error("AmNnet priors dimension != network output dimension");
+  }
 }
 
 int kctc_nnet_read(kctcNnet_t *out, const char *path, int device) {
   return guarded([&] {
-    auto *n = new kctcNnetImpl;
+    auto *n = new_on_device(device);
     try {
-      n->device = device;
-      KCTC_HIP_CHECK(hipSetDevice(device));
-      n->create_streams();
-      n->activate();
-      std::ifstream is(path);
-      if (!is) throw std::runtime_error(std::string("cannot open ") + path);
-      n->nnet.Read(is);
+      read_model(n, path, false);
     } catch (...) {
       delete n;
       throw;
     }
     *out = n;
+  });
+}
+
+int kctc_am_nnet_read(kctcNnet_t *out, const char *path, int device) {
+  return guarded([&] {
+    auto *n = new_on_device(device);
+    try {
+      read_model(n, path, true);
+    } catch (...) {
+      delete n;
+      throw;
+    }
+    *out = n;
+  });
+}
+
+int kctc_am_nnet_write(kctcNnet_t n, const char *path, int binary) {
+  return guarded([&] {
+    n->activate();
+    if (!n->trans_model.empty() && n->trans_model_binary != (binary != 0))
+      throw std::runtime_error("the transition model was read in the other mode; write the model in that mode");
+    std::ofstream os(path, std::ios::binary | std::ios::trunc);
+    if (!os) throw std::runtime_error(std::string("cannot open ") + path);
+    kctc::kio::InitOutput(os, binary != 0);
+    os.write(n->trans_model.data(), (std::streamsize)n->trans_model.size());
+    n->nnet.Write(os, binary != 0);
+    kctc::kio::WriteFloatVector(os, binary != 0, n->priors.data(), (long)n->priors.size());
+    if (!os) throw std::runtime_error(std::string("write failed: ") + path);
+  });
+}
+
+int kctc_am_nnet_num_priors(kctcNnet_t n) { return n ? (int)n->priors.size() : -1; }
+
+int kctc_am_nnet_get_priors(kctcNnet_t n, float *priors, int dim) {
+  return guarded([&] {
+    KCTC_REQUIRE(dim == (int)n->priors.size() && (dim == 0 || priors), "kctc_am_nnet_get_priors: bad size");
+    std::copy(n->priors.begin(), n->priors.end(), priors);
+  });
+}
+
+int kctc_am_nnet_set_priors(kctcNnet_t n, const float *priors, int dim) {
+  return guarded([&] {  // AmNnet::SetPriors (am-nnet.cc:44-55)
+    const int pdfs = n->nnet.OutputDim();
+    KCTC_REQUIRE(dim >= 0 && dim <= pdfs, "Dimension of priors cannot exceed number of pdfs.");
+    KCTC_REQUIRE(dim == 0 || priors, "kctc_am_nnet_set_priors: null priors");
+    n->priors.assign(priors, priors + dim);
+    if (dim > 0 && dim < pdfs) n->priors.resize(pdfs, 0.f);
   });
 }
 
