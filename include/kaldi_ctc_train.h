@@ -54,8 +54,22 @@ int kctc_nnet_set_params(kctcNnet_t nnet, int c, const float *host, long n);
 int kctc_nnet_set_learning_rate(kctcNnet_t nnet, float lr);
 /* ClipGradientComponent counters of component c: num_clipped, count */
 int kctc_nnet_clip_stats(kctcNnet_t nnet, int c, double *num_clipped, double *count);
-/* RNG stream for the self-repair draws (glibc rand() in the reference) */
-int kctc_nnet_set_repair_seed(kctcNnet_t nnet, unsigned long long seed);
+/* srand(seed) of the trainer's rand() stream (nnet2-ctc-train-simple --srand,
+ * src/ctcbin/nnet2-ctc-train-simple.cc:47,69; 0 when never called).  The only
+ * consumer on this path is ClipGradientComponent self-repair: one RandUniform()
+ * = (rand() + 1.0) / (RAND_MAX + 2.0) per ClipGradient Backprop, top component
+ * first, drawn only when the reference's short-circuit conditions reach it
+ * (src/nnet2/nnet-cudnn-component.cc:987-991) -- the same glibc generator, so
+ * the repair decisions equal the reference's for the same --srand.
+ * kctc_nnet_rand_calls: rand() calls made so far. */
+int kctc_nnet_srand(kctcNnet_t nnet, unsigned seed);
+int kctc_nnet_rand_calls(kctcNnet_t nnet, long *calls);
+/* The last finished minibatch's best path (FindRowMaxId of the network
+ * output, [T_max*N] int32, row t*N+n; the ids ComputeTotAccuracy collapsed)
+ * and its network output ([T_max*N][A] fp32; valid until the next step is
+ * queued).  len must equal T_max*N (ids) / T_max*N*A (output). */
+int kctc_nnet_last_best_path(kctcNnet_t nnet, int *ids, long len);
+int kctc_nnet_last_output(kctcNnet_t nnet, float *host, long len);
 
 /* One SGD minibatch.  feats_dev [T_max*N][input_dim] (device, zero padded).
  * Outputs: sum of CTC costs, accuracy numerator (sum L - edits), weight (sum L). */
@@ -108,7 +122,16 @@ int kctc_am_nnet_set_priors(kctcNnet_t nnet, const float *priors, int dim);
 /* Data parallelism over RCCL (one process per GPU).  uid: 128-byte
  * ncclUniqueId from kctc_dp_unique_id on rank 0, broadcast by the launcher. */
 int kctc_dp_unique_id(void *uid128);
+/* world_size >= 1 (a one-rank communicator is valid and runs the same
+ * all-reduce path); world_size 0 switches data parallelism off. */
 int kctc_nnet_enable_dp(kctcNnet_t nnet, const void *uid128, int rank, int world_size);
+/* The same exchange over a host transport: each component's gradient bucket
+ * is copied to pinned host memory on the comm stream, `allreduce(buf, n,
+ * user)` sums it in place across the ranks (e.g. gloo), and it is copied back;
+ * the updates then run exactly as with RCCL.  For hosts without RCCL peers
+ * (several processes sharing one GPU, CPU-side rendezvous). */
+typedef void (*kctc_host_allreduce_fn)(float *buf, long n, void *user);
+int kctc_nnet_enable_dp_host(kctcNnet_t nnet, kctc_host_allreduce_fn allreduce, void *user, int world_size);
 
 /* TrainNnetSimple momentum (src/ctc/ctc-nnet-train.cc:194-245, config
  * ctc-nnet-train.h:33-66): with m != 0 every update goes to a delta copy

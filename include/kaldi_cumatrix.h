@@ -30,8 +30,12 @@ size_t kcm_add_mat_mat_x3_workspace(int M, int N, int K);
 int kcm_add_mat_mat_x3(struct ihipStream_t *stream, int transA, int transB, int M, int N, int K,
                        float alpha, const float *A, long lda, const float *B, long ldb, float beta,
                        float *C, long ldc, void *ws);
-/* ids[r] = argmax_c m[r][c], first maximum wins.  Replaces CuMatrix::FindRowMaxId
- * (src/cudamatrix/cu-matrix.cc:1612-1645). */
+/* ids[r] = argmax_c m[r][c].  Replaces CuMatrix::FindRowMaxId on the device
+ * (src/cudamatrix/cu-matrix.cc:1612-1628 -> _find_row_max_id,
+ * src/cudamatrix/cu-kernels.cu:2454-2500) with the same result bit for bit:
+ * only values > -1e20 count (else -1), and ties resolve as that kernel's
+ * 256-thread strict-greater reduction tree does (not always to the lowest
+ * column; equal maxima at columns 1 and 2 give 2). */
 int kcm_find_row_max_id(struct ihipStream_t *stream, const float *m, long rows, int cols, int *ids);
 /* ClipGradientComponent norm-based backprop (src/nnet2/nnet-cudnn-component.cc:936-957):
  * rows with |row|_2 >= threshold rescaled to norm threshold; *num_clipped_dev

@@ -96,6 +96,7 @@ def exported_symbols():
         if fn.endswith(".h"):
             txt = open(os.path.join(inc, fn)).read()
             txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+            txt = re.sub(r"^\s*typedef[^;]*;", "", txt, flags=re.M)  # function-pointer types are not symbols
             names += re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b([a-zA-Z_]\w*)\s*\([^;{]*\)\s*;",
                                 txt, flags=re.M)
     return sorted(set(n for n in names if n not in ("if", "while", "for", "return")))
@@ -253,6 +254,18 @@ def add_mat_mat_x3(C, A, B, transA=False, transB=False, alpha=1.0, beta=0.0, str
         raise KctcError(f"kcm_add_mat_mat_x3 failed ({st})")
 
 
+def find_row_max_id(m, stream=None):
+    """CuMatrix::FindRowMaxId of a 2-D torch CUDA float32 tensor -> int32
+    CUDA tensor (kcm_find_row_max_id: the _find_row_max_id tie rule)."""
+    import torch
+    assert m.is_cuda and m.dtype == torch.float32 and m.is_contiguous() and m.dim() == 2
+    ids = torch.empty(m.shape[0], dtype=torch.int32, device=m.device)
+    st = lib().kcm_find_row_max_id(_stream_handle(stream), _ptr(m), m.shape[0], m.shape[1], _ptr(ids))
+    if st != 0:
+        raise KctcError(f"kcm_find_row_max_id failed ({st})")
+    return ids
+
+
 # ---------------------------------------------------------------------------
 # nnet2 trainer (include/kaldi_ctc_train.h)
 # ---------------------------------------------------------------------------
@@ -365,8 +378,27 @@ class Nnet:
         _tcheck(lib().kctc_nnet_clip_stats(self.h, c, ctypes.byref(a), ctypes.byref(b)), "clip_stats")
         return a.value, b.value
 
-    def set_repair_seed(self, seed):
-        _tcheck(lib().kctc_nnet_set_repair_seed(self.h, seed), "set_repair_seed")
+    def srand(self, seed):
+        """srand(seed) of the trainer's rand() stream (nnet2-ctc-train-simple --srand)."""
+        _tcheck(lib().kctc_nnet_srand(self.h, int(seed)), "srand")
+
+    @property
+    def rand_calls(self):
+        n = ctypes.c_long()
+        _tcheck(lib().kctc_nnet_rand_calls(self.h, ctypes.byref(n)), "rand_calls")
+        return n.value
+
+    def last_best_path(self, T, N):
+        """FindRowMaxId ids [T*N] of the last finished minibatch."""
+        out = np.empty(T * N, np.int32)
+        _tcheck(lib().kctc_nnet_last_best_path(self.h, out.ctypes.data, out.size), "last_best_path")
+        return out
+
+    def last_output(self, T, N, A):
+        """Network output [T*N, A] of the last minibatch (host copy)."""
+        out = np.empty((T * N, A), np.float32)
+        _tcheck(lib().kctc_nnet_last_output(self.h, out.ctypes.data, out.size), "last_output")
+        return out
 
     def _step(self, fn, feats, T, N, num_frames, flat_labels, label_lengths):
         nf = np.ascontiguousarray(num_frames, dtype=np.int32)
@@ -437,6 +469,18 @@ class Nnet:
     def enable_dp(self, uid, rank, world):
         buf = ctypes.create_string_buffer(bytes(uid), 128)
         _tcheck(lib().kctc_nnet_enable_dp(self.h, buf, rank, world), "enable_dp")
+
+    def enable_dp_host(self, allreduce, world):
+        """Gradient exchange over a host transport: allreduce(np.float32 array)
+        must sum it in place across the ranks (e.g. gloo)."""
+        def cb(buf, n, user):
+            allreduce(np.ctypeslib.as_array(buf, shape=(n,)))
+        self._dp_cb = _HOST_ALLREDUCE(cb)  # keep the thunk alive
+        _tcheck(lib().kctc_nnet_enable_dp_host(self.h, ctypes.cast(self._dp_cb, ctypes.c_void_p), None, world),
+                "enable_dp_host")
+
+
+_HOST_ALLREDUCE = ctypes.CFUNCTYPE(None, ctypes.POINTER(ctypes.c_float), ctypes.c_long, ctypes.c_void_p)
 
 
 def dp_unique_id():

@@ -41,7 +41,10 @@ SIGS = {
     "kctc_nnet_set_params": (ci, [vp, ci, vp, cl]),
     "kctc_nnet_set_learning_rate": (ci, [vp, cf]),
     "kctc_nnet_clip_stats": (ci, [vp, ci, ctypes.POINTER(cd), ctypes.POINTER(cd)]),
-    "kctc_nnet_set_repair_seed": (ci, [vp, ctypes.c_ulonglong]),
+    "kctc_nnet_srand": (ci, [vp, ctypes.c_uint]),
+    "kctc_nnet_rand_calls": (ci, [vp, ctypes.POINTER(cl)]),
+    "kctc_nnet_last_best_path": (ci, [vp, vp, cl]),
+    "kctc_nnet_last_output": (ci, [vp, vp, cl]),
     "kctc_nnet_train_step": (ci, [vp, vp, ci, ci, vp, vp, vp, ctypes.POINTER(cd), ctypes.POINTER(cd),
                                   ctypes.POINTER(cd)]),
     "kctc_nnet_compute_objf": (ci, [vp, vp, ci, ci, vp, vp, vp, ctypes.POINTER(cd), ctypes.POINTER(cd),
@@ -62,6 +65,7 @@ SIGS = {
     "kctc_am_nnet_set_priors": (ci, [vp, vp, ci]),
     "kctc_dp_unique_id": (ci, [vp]),
     "kctc_nnet_enable_dp": (ci, [vp, vp, ci, ci]),
+    "kctc_nnet_enable_dp_host": (ci, [vp, vp, vp, ci]),
     "kctc_nnet_set_momentum": (ci, [vp, cf]),
     "kctc_nnet_train_simple": (ci, [vp, vp, cl, ctypes.POINTER(cl), ctypes.POINTER(cd), ctypes.POINTER(cd),
                                     ctypes.POINTER(cd)]),

@@ -23,37 +23,11 @@
 #include <vector>
 
 #include "egs.h"
+#include "glibc_rand.h"
 
 namespace kctc {
 namespace egs {
 
-namespace {
-
-// glibc srand(seed) / rand() on a private TYPE_3 state (128-byte state
-// buffer = the default generator behind rand()).
-class GlibcRand {
- public:
-  explicit GlibcRand(unsigned seed) {
-    memset(&rd_, 0, sizeof(rd_));
-    if (initstate_r(seed, state_, sizeof(state_), &rd_) != 0) throw std::runtime_error("initstate_r failed");
-  }
-  int operator()() {
-    int32_t r = 0;
-    random_r(&rd_, &r);
-    return (int)r;
-  }
-  // RandInt(min, max): no draw when max == min (kaldi-math.cc:103)
-  int RandInt(int lo, int hi) {
-    if (hi == lo) return lo;
-    return lo + ((*this)() % (hi + 1 - lo));
-  }
-
- private:
-  char state_[128];
-  struct random_data rd_;
-};
-
-}  // namespace
 
 void FrameSubsamplingShift(int frame_subsampling_factor, int frame_shift, Example *eg) {
   if (frame_subsampling_factor <= 1) return;

@@ -6,16 +6,18 @@
 
 namespace kctc {
 
-// w += lr * clamp(dw, -clip, clip)   (clip <= 0: no clamp)
-void clip_sgd_update(hipStream_t s, float *w, const float *dw, long n, float lr, float clip);
+// w += lr * clamp(dw, -clip, clip)   (clip <= 0: no clamp).  skip (device,
+// nullable): when *skip != 0 the update is not applied (a failed step).
+void clip_sgd_update(hipStream_t s, float *w, const float *dw, long n, float lr, float clip,
+                     const unsigned *skip = nullptr);
 // momentum form (TrainNnetSimple with a delta nnet, ctc-nnet-train.cc:194-245):
 // delta += lr * clamp(dw); w += delta; delta *= m
 void momentum_update(hipStream_t s, float *w, float *delta, const float *dw, long n, float lr, float clip,
-                     float m);
+                     float m, const unsigned *skip = nullptr);
 // ClipGradientComponent norm-based backprop: rows with |row| >= thr scaled to
 // norm thr; *nclipped (device int) += number of such rows.
 void rownorm_clip(hipStream_t s, float *d, long rows, int dim, float thr, int *nclipped);
-// best-path ids: first maximum per row
+// best-path ids: _find_row_max_id tie rule (-1 when nothing > -1e20)
 void row_argmax(hipStream_t s, const float *m, long rows, int cols, int *ids);
 // out[j] = alpha * sum_rows X[:, j] + beta * out[j]; ws >= sum_rows_ws_floats
 size_t sum_rows_ws_floats(long rows, int cols);

@@ -14,7 +14,8 @@ namespace {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(256) void k_clip_sgd(float *__restrict__ w, const float *__restrict__ dw,
-                                                  long n, float lr, float clip) {
+                                                  long n, float lr, float clip, const unsigned *skip) {
+  if (skip && *skip) return;
   const long n4 = n / 4;
   const long stride = (long)gridDim.x * 256;
   const bool vec = ((uintptr_t)w % 16 == 0) && ((uintptr_t)dw % 16 == 0);
@@ -82,27 +83,43 @@ __global__ __launch_bounds__(256) void k_rownorm_clip(float *__restrict__ d, lon
   }
 }
 
-// One wave per row, first maximum wins (CPU FindRowMaxId tie order,
-// cu-matrix.cc:1635-1644).
+// FindRowMaxId with the tie rule of the kernel the reference's CTC path runs,
+// _find_row_max_id (cu-kernels.cu:2454-2500): 256 virtual threads t keep the
+// first strict maximum above -1e20f of columns t, t+256, ...; a tree then lets
+// position p take p+w (w = 128 .. 1) only when strictly greater, so ties
+// resolve by the tree position, and a row with nothing above -1e20 gives -1.
+// Here one wave per row: lane l holds virtual threads l, l+64, l+128, l+192;
+// levels 128 and 64 combine in registers, 32 .. 1 by shuffles (a lane reads its
+// source's value from before the level, as the tree does).
 __global__ __launch_bounds__(256) void k_row_argmax(const float *__restrict__ m, long rows, int cols,
                                                     int *__restrict__ ids) {
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
   const float *r = m + row * cols;
-  float best = -INFINITY;
-  int bi = 0x7fffffff;
-  for (int j = lane; j < cols; j += 64) {
-    float v = r[j];
-    if (v > best || (v == best && j < bi)) { best = v; bi = j; }
-  }
+  float v[4];
+  int vi[4];
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    float ob = __shfl_xor(best, o, 64);
-    int oi = __shfl_xor(bi, o, 64);
-    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  for (int k = 0; k < 4; k++) {
+    v[k] = -1e20f;
+    vi[k] = -1;
+    for (int j = lane + 64 * k; j < cols; j += 256) {
+      const float x = r[j];
+      if (x > v[k]) { v[k] = x; vi[k] = j; }
+    }
   }
-  if (lane == 0) ids[row] = bi == 0x7fffffff ? 0 : bi;
+  if (v[2] > v[0]) { v[0] = v[2]; vi[0] = vi[2]; }  // w = 128
+  if (v[3] > v[1]) { v[1] = v[3]; vi[1] = vi[3]; }
+  if (v[1] > v[0]) { v[0] = v[1]; vi[0] = vi[1]; }  // w = 64
+  float b = v[0];
+  int bi = vi[0];
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const float ob = __shfl_down(b, w, 64);
+    const int oi = __shfl_down(bi, w, 64);
+    if (ob > b) { b = ob; bi = oi; }
+  }
+  if (lane == 0) ids[row] = bi;
 }
 
 // out[j] = alpha * sum_i X[i][j] + beta * out[j]; one workgroup per 64 cols,
@@ -149,7 +166,8 @@ static int grid_for(long n, int per = 256) {
 
 __global__ __launch_bounds__(256) void k_momentum(float *__restrict__ w, float *__restrict__ delta,
                                                   const float *__restrict__ dw, long n, float lr, float clip,
-                                                  float m) {
+                                                  float m, const unsigned *skip) {
+  if (skip && *skip) return;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
     float g = dw[i];
     if (clip > 0.f) g = fminf(fmaxf(g, -clip), clip);
@@ -160,14 +178,15 @@ __global__ __launch_bounds__(256) void k_momentum(float *__restrict__ w, float *
 }
 
 void momentum_update(hipStream_t s, float *w, float *delta, const float *dw, long n, float lr, float clip,
-                     float m) {
+                     float m, const unsigned *skip) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_momentum, dim3(grid_for(n)), dim3(256), 0, s, w, delta, dw, n, lr, clip, m);
+  hipLaunchKernelGGL(k_momentum, dim3(grid_for(n)), dim3(256), 0, s, w, delta, dw, n, lr, clip, m, skip);
 }
 
-void clip_sgd_update(hipStream_t s, float *w, const float *dw, long n, float lr, float clip) {
+void clip_sgd_update(hipStream_t s, float *w, const float *dw, long n, float lr, float clip,
+                     const unsigned *skip) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_clip_sgd, dim3(grid_for((n + 3) / 4)), dim3(256), 0, s, w, dw, n, lr, clip);
+  hipLaunchKernelGGL(k_clip_sgd, dim3(grid_for((n + 3) / 4)), dim3(256), 0, s, w, dw, n, lr, clip, skip);
 }
 
 void rownorm_clip(hipStream_t s, float *d, long rows, int dim, float thr, int *nclipped) {

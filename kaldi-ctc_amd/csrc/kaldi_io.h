@@ -95,7 +95,7 @@ inline void WriteFloat(std::ostream &os, bool binary, float v) {
     os.put((char)sizeof(v));
     os.write(reinterpret_cast<const char *>(&v), sizeof(v));
   } else {
-    os << std::setprecision(9) << v << ' ';
+    os << std::setprecision(7) << v << ' ';
   }
 }
 inline float ReadFloat(std::istream &is, bool binary) {
@@ -173,7 +173,7 @@ inline void WriteFloatVector(std::ostream &os, bool binary, const float *v, long
     if (n) os.write(reinterpret_cast<const char *>(v), 4 * (size_t)n);
   } else {
     os << " [ ";
-    for (long i = 0; i < n; i++) os << std::setprecision(9) << v[i] << ' ';
+    for (long i = 0; i < n; i++) os << std::setprecision(7) << v[i] << ' ';
     os << "]\n";
   }
 }
@@ -219,7 +219,7 @@ inline void WriteFloatMatrix(std::ostream &os, bool binary, const float *m, int 
   os << " [";
   for (int r = 0; r < rows; r++) {
     os << "\n  ";
-    for (int c = 0; c < cols; c++) os << std::setprecision(9) << m[(size_t)r * cols + c] << ' ';
+    for (int c = 0; c < cols; c++) os << std::setprecision(7) << m[(size_t)r * cols + c] << ' ';
   }
   os << "]\n";
 }

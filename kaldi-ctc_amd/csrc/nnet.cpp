@@ -339,6 +339,11 @@ void SpliceComponent::Read(std::istream &is, bool binary) {
   ExpectToken(is, binary, "<ConstComponentDim>");
   if (kio::ReadInt(is, binary) != 0) throw std::runtime_error("SpliceComponent: const_component_dim != 0 is not supported");
   ExpectToken(is, binary, "</SpliceComponent>");
+  // as InitFromString: this path aliases the input (context {0}, the CTC
+  // recipe's splice); a spliced model would make OutputDim != InputDim
+  if (input_dim_ <= 0) throw std::runtime_error("SpliceComponent: bad <InputDim>");
+  if (context_ != std::vector<int>{0})
+    throw std::runtime_error("SpliceComponent: only context {0} (the CTC recipe's splice) is supported on this path");
 }
 // ---------------------------------------------------------------------------
 // CuDNNRecurrentComponent (nnet-cudnn-component.cc:56-772)
@@ -448,7 +453,7 @@ void CuDNNRecurrentComponent::Forward(const CuMatrixBase &in, CuMatrixBase *out,
   input_projected_ = false;
   ProfScope ps("layer_rnn_forward");
   int st = rnn_forward_training(desc_, S(), T, N, in.Data(), params_.f(), out->Data(), workspace_.p,
-                                workspace_.bytes, reserve_.p, reserve_.bytes, err_, chain, projected);
+                                workspace_.bytes, reserve_.p, reserve_.bytes, DeviceError(), chain, projected);
   if (st) throw std::runtime_error("rnn_forward_training failed: " + std::to_string(st));
 }
 
@@ -461,7 +466,7 @@ void CuDNNRecurrentComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
     ProfScope ps("layer_rnn_backward_data");
     int st = rnn_backward_data(desc_, S(), T, N, out_value.Data(), out_deriv.Data(), params_.f(),
                                in_deriv ? in_deriv->Data() : nullptr, workspace_.p, workspace_.bytes,
-                               reserve_.p, reserve_.bytes, err_, CuDevice::Instantiate().stream2);
+                               reserve_.p, reserve_.bytes, DeviceError(), CuDevice::Instantiate().stream2);
     if (st) throw std::runtime_error("rnn_backward_data failed: " + std::to_string(st));
   }
   if (to_update_in) {
@@ -495,11 +500,11 @@ void UpdatableComponent::SetMomentum(float m) {
   }
 }
 
-void UpdatableComponent::UpdateWith(float *params, const float *grad, float clip) {
+void UpdatableComponent::UpdateWith(float *params, const float *grad, float clip, const unsigned *skip) {
   if (momentum_ == 0.f)
-    clip_sgd_update(S(), params, grad, NumParameters(), learning_rate_, clip);
+    clip_sgd_update(S(), params, grad, NumParameters(), learning_rate_, clip, skip);
   else
-    momentum_update(S(), params, delta_.f(), grad, NumParameters(), learning_rate_, clip, momentum_);
+    momentum_update(S(), params, delta_.f(), grad, NumParameters(), learning_rate_, clip, momentum_, skip);
 }
 
 int CuDNNRecurrentComponent::side_gemm_blocks() const {
@@ -508,9 +513,9 @@ int CuDNNRecurrentComponent::side_gemm_blocks() const {
   return 512;  // dynamic tile scheduling: two per CU, late starters exit
 }
 
-void CuDNNRecurrentComponent::ApplyUpdate() {
+void CuDNNRecurrentComponent::ApplyUpdate(const unsigned *skip) {
   // ApplyFloor(-clip) / ApplyCeiling(clip) then filter_params_ += lr * grad
-  UpdateWith(params_.f(), grad_.f(), clip_gradient_);
+  UpdateWith(params_.f(), grad_.f(), clip_gradient_, skip);
 }
 
 void CuDNNRecurrentComponent::Vectorize(float *host) const {
@@ -564,6 +569,12 @@ void CuDNNRecurrentComponent::Read(std::istream &is, bool binary) {
   desc_.mode = kio::ReadInt(is, binary);
   ExpectToken(is, binary, "<MaxSeqLength>");
   max_seq_length_ = kio::ReadInt(is, binary);
+  // InitFromString's checks (nnet-cudnn-component.cc:72-98), before any size is trusted
+  if (desc_.mode < 0 || desc_.mode > 3)
+    throw std::runtime_error("CuDNNRecurrentComponent: rnn_mode_ = " + std::to_string(desc_.mode) +
+                             ", should in [0, 1, 2, 3].");
+  if (desc_.D <= 0 || desc_.H <= 0 || desc_.layers <= 0 || max_seq_length_ <= 0)
+    throw std::runtime_error("CuDNNRecurrentComponent: bad dimensions in model file");
   ExpectToken(is, binary, "<FilterParams>");
   auto v = kio::ReadFloatVector(is, binary);
   if ((long)v.size() != desc_.params_size())
@@ -667,8 +678,10 @@ void ClipGradientComponent::Backprop(const ChunkInfo &, const ChunkInfo &, const
     to_update->num_backpropped_ += 1;
     const double count_after = count_ + ((norm_based_clipping_ && to_update == this) ? rows : 0);
     if (!(self_repair_clipped_proportion_threshold_ >= 1.0f || self_repair_scale_ == 0.0f ||
-          count_after == 0))
-      try_repair = !(next_draw_ > 0.5f);
+          count_after == 0)) {
+      if (!rng_) throw std::logic_error("ClipGradientComponent: no random stream for self-repair");
+      try_repair = !(rng_->RandUniform() > 0.5f);  // RandUniform() > repair_probability
+    }
     if (norm_based_clipping_) to_update->count_ += rows;
   }
   ProfScope ps("clip_gradient");
@@ -835,8 +848,8 @@ void AffineComponent::Backprop(const ChunkInfo &, const ChunkInfo &, const CuMat
   }
 }
 
-void AffineComponent::ApplyUpdate() {
-  UpdateWith(params_.f(), grad_.f(), 0.f);
+void AffineComponent::ApplyUpdate(const unsigned *skip) {
+  UpdateWith(params_.f(), grad_.f(), 0.f, skip);
 }
 void AffineComponent::Vectorize(float *host) const {
   auto v = d2h(params_.f(), NumParameters());
@@ -855,7 +868,7 @@ void AffineComponent::Write(std::ostream &os, bool binary) const {
   WriteToken(os, binary, "<BiasParams>");
   kio::WriteFloatVector(os, binary, v.data() + (long)in_dim_ * out_dim_, out_dim_);
   WriteToken(os, binary, "<IsGradient>");
-  kio::WriteBool(os, binary, false);
+  kio::WriteBool(os, binary, is_gradient_);
   WriteToken(os, binary, "</AffineComponent>");
 }// nnet-component.cc:1228-1258 (incl. the <AvgInput> back-compatibility fields)
 void AffineComponent::Read(std::istream &is, bool binary) {
@@ -877,8 +890,9 @@ void AffineComponent::Read(std::istream &is, bool binary) {
     kio::ReadFloat(is, binary);
     t = kio::ReadToken(is, binary);
   }
+  is_gradient_ = false;
   if (t == "<IsGradient>") {
-    kio::ReadBool(is, binary);
+    is_gradient_ = kio::ReadBool(is, binary);
     t = kio::ReadToken(is, binary);
   }
   if (t != "</AffineComponent>") throw std::runtime_error("AffineComponent: bad token " + t);
@@ -958,6 +972,7 @@ void Nnet::Read(std::istream &is, bool binary) {
   ExpectToken(is, binary, "<Nnet>");
   ExpectToken(is, binary, "<NumComponents>");
   const int n = kio::ReadInt(is, binary);
+  if (n <= 0) throw std::runtime_error("Nnet::Read: <NumComponents> " + std::to_string(n));
   ExpectToken(is, binary, "<Components>");
   for (int i = 0; i < n; i++) {
     const std::string t = kio::ReadToken(is, binary);
@@ -969,6 +984,16 @@ void Nnet::Read(std::istream &is, bool binary) {
   }
   ExpectToken(is, binary, "</Components>");
   ExpectToken(is, binary, "</Nnet>");
+  // Nnet::Read -> Check (nnet-nnet.cc:197-198, 281-289): every component's output feeds the next
+  for (int i = 0; i < n; i++) {
+    if (components_[i]->InputDim() <= 0 || components_[i]->OutputDim() <= 0)
+      throw std::runtime_error("Nnet::Read: component " + std::to_string(i) + " has a non-positive dimension");
+    if (i + 1 < n && components_[i]->OutputDim() != components_[i + 1]->InputDim())
+      throw std::runtime_error("Nnet::Read: dimension mismatch between components " + std::to_string(i) + " (" +
+                               components_[i]->Type() + ", output " + std::to_string(components_[i]->OutputDim()) +
+                               ") and " + std::to_string(i + 1) + " (" + components_[i + 1]->Type() + ", input " +
+                               std::to_string(components_[i + 1]->InputDim()) + ")");
+  }
 }
 // ---------------------------------------------------------------------------
 // NnetCtcUpdater (src/ctc/ctc-nnet-update.cc:76-348)
@@ -997,6 +1022,14 @@ void NnetCtcUpdater::Enqueue(const float *feats, int T_max, int N, const int *nu
   if (N <= 0 || T_max <= 0) throw std::invalid_argument("empty minibatch");
   const long rows = (long)T_max * N;
   set_minibatch(nnet_, N);
+  // one error word per step for every recurrence: cleared here (stream order:
+  // after the previous step's readback), read back at the end, and the
+  // updates of a step that set it are skipped on the device
+  err_word_.ensure(256);
+  KCTC_HIP_CHECK(hipMemsetAsync(err_word_.p, 0, sizeof(unsigned), S()));
+  for (int c = 0; c < C; c++)
+    if (auto *r = dynamic_cast<CuDNNRecurrentComponent *>(&nnet_->GetComponent(c)))
+      r->SetErrorWord(static_cast<unsigned *>(err_word_.p));
   forward_data_.resize(C + 1);
   chunk_info_.resize(C + 1);
   for (int c = 0; c <= C; c++) {
@@ -1069,12 +1102,8 @@ void NnetCtcUpdater::Enqueue(const float *feats, int T_max, int N, const int *nu
   unsigned *herr = reinterpret_cast<unsigned *>(hids + rows);
   KCTC_HIP_CHECK(hipMemcpyAsync(hcost, costs_dev_.p, sizeof(double) * N, hipMemcpyDeviceToHost, S()));
   KCTC_HIP_CHECK(hipMemcpyAsync(hids, ids_dev_.p, sizeof(int) * rows, hipMemcpyDeviceToHost, S()));
-  sl.nerr = 0;
-  for (int c = 0; c < C; c++) {
-    auto *r = dynamic_cast<CuDNNRecurrentComponent *>(&nnet_->GetComponent(c));
-    if (r) KCTC_HIP_CHECK(hipMemcpyAsync(herr + sl.nerr++, r->DeviceError(), sizeof(unsigned),
-                                         hipMemcpyDeviceToHost, S()));
-  }
+  sl.nerr = 1;
+  KCTC_HIP_CHECK(hipMemcpyAsync(herr, err_word_.p, sizeof(unsigned), hipMemcpyDeviceToHost, S()));
   KCTC_HIP_CHECK(hipEventRecord(sl.ev, S()));
   sl.N = N;
   sl.rows = rows;
@@ -1098,8 +1127,11 @@ MinibatchStats NnetCtcUpdater::Finish() {
   const double *hcost = reinterpret_cast<const double *>(sl.pinned);
   const int *hids = reinterpret_cast<const int *>(sl.pinned + sizeof(double) * N);
   const unsigned *herr = reinterpret_cast<const unsigned *>(hids + rows);
+  last_ids_.assign(hids, hids + rows);
   for (int i = 0; i < sl.nerr; i++)
-    if (herr[i]) throw std::runtime_error("recurrence hand-off timed out (device error word set)");
+    if (herr[i])
+      throw std::runtime_error("recurrence hand-off timed out (device error word set); this minibatch's "
+                               "updates were skipped, the parameters are those before it");
   const int *num_frames = sl.num_frames.data(), *flat_labels = sl.labels.data();
   const int *label_lengths = sl.label_lengths.data();
   MinibatchStats st;
@@ -1186,8 +1218,7 @@ void NnetCtcUpdater::Backprop(int T, int N) {  // :320-348
       }
     }
     if (auto *cg = dynamic_cast<ClipGradientComponent *>(&comp)) {
-      // RandUniform() for RepairGradients, one stream per updater
-      cg->next_draw_ = (float)repair_rng_.uniform();
+      cg->rng_ = &repair_rng_;  // RepairGradients draws RandUniform() from the process stream
       if (cg->Shadow()) to_update = cg->Shadow();  // momentum: delta_nnet's copy
     }
     const CuMatrixBase od(cur->Data(), rows, comp.OutputDim());
@@ -1203,7 +1234,7 @@ void NnetCtcUpdater::Backprop(int T, int N) {  // :320-348
   if (exchange_) exchange_->Finish();
   for (int c : updated) {
     ProfScope ps("update");
-    static_cast<UpdatableComponent *>(&nnet_->GetComponent(c))->ApplyUpdate();
+    static_cast<UpdatableComponent *>(&nnet_->GetComponent(c))->ApplyUpdate(err_word_.p ? static_cast<const unsigned *>(err_word_.p) : nullptr);
   }
 }
 

@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "clipgrad.h"
+#include "glibc_rand.h"
 #include "rnn.h"
 
 namespace kctc {
@@ -161,7 +162,9 @@ class UpdatableComponent : public Component {
   virtual float *GradData() = 0;
   // stream on which GradData() was produced (the exchange waits on it)
   hipStream_t GradStream() const;
-  virtual void ApplyUpdate() = 0;  // params += lr * (clipped) grad
+  // params += lr * (clipped) grad; skipped on device when *skip != 0 (the
+  // step's recurrence hand-off failed: its gradients are not trusted)
+  virtual void ApplyUpdate(const unsigned *skip = nullptr) = 0;
   // TrainNnetSimple momentum (ctc-nnet-train.cc:194-245): the update goes to
   // a delta copy (delta += lr * clip(grad)), then params += delta and
   // delta *= momentum.  0 = plain SGD (the recipe's default).
@@ -169,7 +172,7 @@ class UpdatableComponent : public Component {
   float Momentum() const { return momentum_; }
 
  protected:
-  void UpdateWith(float *params, const float *grad, float clip);
+  void UpdateWith(float *params, const float *grad, float clip, const unsigned *skip);
   float learning_rate_ = 0.001f;
   hipStream_t grad_stream_ = nullptr;  // nullptr: the device's compute stream
   float momentum_ = 0.f;
@@ -218,8 +221,11 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   void Vectorize(float *host) const override;
   void UnVectorize(const float *host) override;
   float *GradData() override { return grad_.f(); }
-  void ApplyUpdate() override;
-  unsigned *DeviceError() const { return err_; }
+  void ApplyUpdate(const unsigned *skip = nullptr) override;
+  // device error word of the recurrences (hand-off timeout); the updater
+  // points every RNN at its own per-step word (SetErrorWord)
+  unsigned *DeviceError() const { return err_ext_ ? err_ext_ : err_; }
+  void SetErrorWord(unsigned *e) const { err_ext_ = e; }
   // workgroup cap of the side-stream weight GEMMs: the CUs left over by the
   // backward recurrence (KCTC_SIDE_BLOCKS overrides)
   int side_gemm_blocks() const;
@@ -243,6 +249,7 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   mutable bool input_projected_ = false;  // set by the previous component's PropagateChained
   mutable float input_bound_ = 0.f;       // ditto: bound on |input| (0: unknown)
   unsigned *err_ = nullptr;
+  mutable unsigned *err_ext_ = nullptr;
   void Forward(const CuMatrixBase &in, CuMatrixBase *out, RnnFwdChain *chain) const;
 };
 
@@ -269,8 +276,10 @@ class ClipGradientComponent : public Component {
   void SyncStats() const;
   double NumClipped() const { return num_clipped_; }
   double Count() const { return count_; }
-  // one RandUniform() per Backprop, drawn by the updater (glibc rand() in the reference)
-  mutable float next_draw_ = 1.0f;
+  // the process's rand() stream (NnetCtcUpdater's, seeded by --srand): the
+  // RandUniform() of RepairGradients is drawn from it during Backprop, only
+  // when the reference's short-circuit conditions get that far (:988-991)
+  mutable GlibcRand *rng_ = nullptr;
   // momentum training passes delta_nnet's copy as to_update: counters go to
   // the copy, the repair decision reads this component's own counters
   void EnableShadow(bool on);
@@ -308,10 +317,11 @@ class AffineComponent : public UpdatableComponent {
   void Vectorize(float *host) const override;  // linear (row-major) then bias
   void UnVectorize(const float *host) override;
   float *GradData() override { return grad_.f(); }
-  void ApplyUpdate() override;
+  void ApplyUpdate(const unsigned *skip = nullptr) override;
 
  private:
   int in_dim_ = 0, out_dim_ = 0;
+  bool is_gradient_ = false;  // <IsGradient>, read and written back
   DevBuf params_, grad_;  // [out][in] followed by [out]
   mutable DevBuf ws_;
 };
@@ -372,7 +382,14 @@ class NnetCtcUpdater {
   int Pending() const { return pending_; }
   MinibatchStats Finish();
   void SetExchange(GradExchange *ex) { exchange_ = ex; }
-  void SetRepairRng(uint64_t seed) { repair_rng_ = Rng(seed); }
+  // best-path ids ([T_max*N], FindRowMaxId) of the last minibatch Finish()ed
+  const std::vector<int> &LastBestPath() const { return last_ids_; }
+  // network output of the last minibatch queued (device, [T_max*N][A])
+  const CuMatrixBase &Output() const { return forward_data_.empty() ? empty_ : forward_data_.back(); }
+  // srand(seed) of the process stream (nnet2-ctc-train-simple.cc:47,69;
+  // default 0) that ClipGradient self-repair draws from
+  void Srand(unsigned seed) { repair_rng_.Seed(seed); }
+  long RandCalls() const { return repair_rng_.Calls(); }
 
  private:
   void Propagate(int T, int N);
@@ -380,11 +397,14 @@ class NnetCtcUpdater {
   Nnet *nnet_;
   bool update_;
   GradExchange *exchange_ = nullptr;
-  Rng repair_rng_{12345};
+  GlibcRand repair_rng_{0};
   std::vector<CuMatrix> forward_data_;
+  std::vector<int> last_ids_;
+  CuMatrixBase empty_;
   std::vector<ChunkInfo> chunk_info_;
   CuMatrix deriv_a_, deriv_b_;
   DevBuf ctc_ws_, costs_dev_, ids_dev_;
+  DevBuf err_word_;  // this step's recurrence error word (all RNNs), cleared per step
   struct Slot {  // one minibatch in flight: pinned readback + what its stats need
     char *pinned = nullptr;
     size_t bytes = 0;

@@ -5,11 +5,13 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <fstream>
 #include <sstream>
 #include <string>
+#include <vector>
 
 #include "common.h"
 #include "egs.h"
@@ -67,6 +69,59 @@ class RcclExchange : public kctc::nnet2::GradExchange {
   hipEvent_t ready_ = nullptr, done_ = nullptr;
 };
 
+// The same exchange over a host transport (kctc_nnet_enable_dp_host): the
+// buckets are registered in backprop order as with RCCL; Finish() sums each
+// one through the caller's all-reduce (device -> pinned host -> all-reduce ->
+// device) before the updates.  Host-synchronous: a transport for ranks that
+// share a GPU or have no RCCL peer, not the fast path.
+class HostExchange : public kctc::nnet2::GradExchange {
+ public:
+  HostExchange(kctc_host_allreduce_fn fn, void *user, int world, hipStream_t compute)
+      : fn_(fn), user_(user), world_(world), compute_(compute) {
+    KCTC_HIP_CHECK(hipEventCreateWithFlags(&ev_, hipEventDisableTiming));
+  }
+  ~HostExchange() override {
+    if (host_) (void)hipHostFree(host_);
+    (void)hipEventDestroy(ev_);
+  }
+  void GradReady(int, float *grad, long n, hipStream_t producer) override {
+    buckets_.push_back({grad, n, producer});
+  }
+  void Finish() override {
+    for (const auto &b : buckets_) {
+      if ((size_t)b.n > cap_) {
+        if (host_) KCTC_HIP_CHECK(hipHostFree(host_));
+        KCTC_HIP_CHECK(hipHostMalloc((void **)&host_, sizeof(float) * b.n, hipHostMallocDefault));
+        cap_ = (size_t)b.n;
+      }
+      KCTC_HIP_CHECK(hipEventRecord(ev_, b.producer));
+      KCTC_HIP_CHECK(hipStreamWaitEvent(compute_, ev_, 0));
+      KCTC_HIP_CHECK(hipMemcpyAsync(host_, b.grad, sizeof(float) * b.n, hipMemcpyDeviceToHost, compute_));
+      KCTC_HIP_CHECK(hipStreamSynchronize(compute_));
+      fn_(host_, b.n, user_);
+      KCTC_HIP_CHECK(hipMemcpyAsync(b.grad, host_, sizeof(float) * b.n, hipMemcpyHostToDevice, compute_));
+      KCTC_HIP_CHECK(hipStreamSynchronize(compute_));
+    }
+    buckets_.clear();
+  }
+  int WorldSize() const override { return world_; }
+
+ private:
+  struct Bucket {
+    float *grad;
+    long n;
+    hipStream_t producer;
+  };
+  kctc_host_allreduce_fn fn_;
+  void *user_;
+  int world_;
+  hipStream_t compute_;
+  hipEvent_t ev_ = nullptr;
+  float *host_ = nullptr;
+  size_t cap_ = 0;
+  std::vector<Bucket> buckets_;
+};
+
 }  // namespace
 
 void kctc_set_error(const char *msg) { g_err = msg ? msg : ""; }
@@ -78,7 +133,7 @@ struct kctcNnetImpl {
   kctc::nnet2::NnetCtcUpdater trainer{&nnet, true};
   kctc::nnet2::NnetCtcUpdater evaluator{&nnet, false};
   hipStream_t side = nullptr, stream2 = nullptr;
-  RcclExchange *dp = nullptr;
+  kctc::nnet2::GradExchange *dp = nullptr;
   kctc::nnet2::DevBuf egs_feats, egs_scratch;  // TrainNnetSimple staging
   // nnet2-ctc model file extras: the CtcTransitionModel exactly as read (opaque
   // bytes, in the mode of the file it came from) and AmNnet's priors
@@ -159,7 +214,6 @@ int kctc_nnet_create(kctcNnet_t *out, const char *config, unsigned long long see
       n->activate();
       kctc::nnet2::Rng rng(seed);
       n->nnet.Init(config ? config : "", rng);
-      n->trainer.SetRepairRng(seed ^ 0x5DEECE66DULL);
     } catch (...) {
       delete n;
       throw;
@@ -229,8 +283,39 @@ int kctc_nnet_clip_stats(kctcNnet_t n, int c, double *num_clipped, double *count
   });
 }
 
-int kctc_nnet_set_repair_seed(kctcNnet_t n, unsigned long long seed) {
-  return guarded([&] { n->trainer.SetRepairRng(seed); });
+int kctc_nnet_srand(kctcNnet_t n, unsigned seed) {
+  return guarded([&] {
+    KCTC_REQUIRE(n, "null nnet");
+    n->trainer.Srand(seed);
+  });
+}
+
+int kctc_nnet_rand_calls(kctcNnet_t n, long *calls) {
+  return guarded([&] {
+    KCTC_REQUIRE(n && calls, "null argument");
+    *calls = n->trainer.RandCalls();
+  });
+}
+
+int kctc_nnet_last_best_path(kctcNnet_t n, int *ids, long len) {
+  return guarded([&] {
+    KCTC_REQUIRE(n && ids, "null argument");
+    const auto &v = n->trainer.LastBestPath();
+    KCTC_REQUIRE(len == (long)v.size(), "kctc_nnet_last_best_path: len != T_max*N of the last minibatch");
+    std::copy(v.begin(), v.end(), ids);
+  });
+}
+
+int kctc_nnet_last_output(kctcNnet_t n, float *host, long len) {
+  return guarded([&] {
+    KCTC_REQUIRE(n && host, "null argument");
+    n->activate();
+    const auto &o = n->trainer.Output();
+    KCTC_REQUIRE(o.Data() && len == o.NumRows() * (long)o.NumCols(),
+                 "kctc_nnet_last_output: len != T_max*N*A of the last minibatch");
+    KCTC_HIP_CHECK(hipStreamSynchronize(n->stream));
+    KCTC_HIP_CHECK(hipMemcpy(host, o.Data(), sizeof(float) * len, hipMemcpyDeviceToHost));
+  });
 }
 
 int kctc_nnet_train_step(kctcNnet_t n, const float *feats_dev, int T_max, int N,
@@ -358,9 +443,13 @@ static void read_model(kctcNnetImpl *n, const char *path, bool am) {
     const auto start = (size_t)is.tellg();
     const auto e = buf.find(end_tok, start);
     if (e == std::string::npos) throw std::runtime_error("unterminated <TransitionModel>");
-    n->trans_model = buf.substr(start, e + end_tok.size() - start);
+    // text mode: TransitionModel::Write ends the token with a newline
+    // (src/hmm/transition-model.cc:316-317); keep it, so write-back is byte-identical
+    size_t stop = e + end_tok.size();
+    if (!binary && stop < buf.size() && buf[stop] == '\n') stop++;
+    n->trans_model = buf.substr(start, stop - start);
     n->trans_model_binary = binary;
-    is.seekg((std::streamoff)(e + end_tok.size()));
+    is.seekg((std::streamoff)stop);
   }
   n->nnet.Read(is, binary);
   if (am) {
@@ -442,13 +531,27 @@ int kctc_dp_unique_id(void *uid128) {
 int kctc_nnet_enable_dp(kctcNnet_t n, const void *uid128, int rank, int world_size) {
   return guarded([&] {
     n->activate();
+    KCTC_REQUIRE(world_size >= 0 && (world_size == 0 || (rank >= 0 && rank < world_size && uid128)),
+                 "kctc_nnet_enable_dp: bad rank / world size");
+    KCTC_REQUIRE(n->trainer.Pending() == 0, "kctc_nnet_enable_dp with minibatches in flight");
     delete n->dp;
     n->dp = nullptr;
     n->trainer.SetExchange(nullptr);
-    if (world_size > 1) {
+    if (world_size >= 1) {  // one rank included: the same communicator and all-reduce path
       n->dp = new RcclExchange(uid128, rank, world_size, n->stream);
       n->trainer.SetExchange(n->dp);
     }
+  });
+}
+
+int kctc_nnet_enable_dp_host(kctcNnet_t n, kctc_host_allreduce_fn fn, void *user, int world_size) {
+  return guarded([&] {
+    KCTC_REQUIRE(n && fn && world_size >= 1, "kctc_nnet_enable_dp_host: bad argument");
+    KCTC_REQUIRE(n->trainer.Pending() == 0, "kctc_nnet_enable_dp_host with minibatches in flight");
+    n->activate();
+    delete n->dp;
+    n->dp = new HostExchange(fn, user, world_size, n->stream);
+    n->trainer.SetExchange(n->dp);
   });
 }
 

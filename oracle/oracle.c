@@ -77,12 +77,48 @@ int oracle_levenshtein(const int *a, int na, const int *b, int nb) {
   return r;
 }
 
-void oracle_find_row_max_id_f32(const float *m, int rows, int cols, int *ids) {
+/* CPU CuMatrixBase::FindRowMaxId (src/cudamatrix/cu-matrix.cc:1630-1644):
+ * first strict maximum above -1e21, -1 when there is none. */
+void oracle_find_row_max_id_cpu_f32(const float *m, int rows, int cols, int *ids) {
   for (int r = 0; r < rows; r++) {
     const float *row = m + (size_t)r * cols;
-    int b = 0;
-    for (int c = 1; c < cols; c++) if (row[c] > row[b]) b = c;
+    float mx = -1e21f;
+    int b = -1;
+    for (int c = 0; c < cols; c++)
+      if (mx < row[c]) { mx = row[c]; b = c; }
     ids[r] = b;
+  }
+}
+
+/* GPU _find_row_max_id (src/cudamatrix/cu-kernels.cu:2454-2500), the kernel
+ * the reference's CTC path runs (CTC_GPU is hard-wired, ComputeTotAccuracy ->
+ * FindRowMaxId on a device matrix, src/ctc/ctc-nnet-update.cc:270-273):
+ * block of CU1DBLOCK = 256 threads per row; thread t keeps the first strict
+ * maximum above -1e20f of columns t, t+256, ... (index -1 if none), then a
+ * shared-memory tree halves the active threads (128, 64, 32 with barriers,
+ * then 16 .. 1 inside one warp) and position p takes position p+w only when
+ * strictly greater.  Ties between threads therefore resolve by the tree, not
+ * to the lowest column: equal maxima at columns 1 and 2 give 2.  Rows whose
+ * values are all <= -1e20 (or NaN) give -1. */
+void oracle_find_row_max_id_f32(const float *m, int rows, int cols, int *ids) {
+  enum { B = 256 };
+  float smax[B];
+  int sidx[B];
+  for (int r = 0; r < rows; r++) {
+    const float *row = m + (size_t)r * cols;
+    for (int t = 0; t < B; t++) {
+      float tmax = -1e20f;
+      int tidx = -1;
+      for (int j = t; j < cols; j += B)
+        if (row[j] > tmax) { tmax = row[j]; tidx = j; }
+      smax[t] = tmax;
+      sidx[t] = tidx;
+    }
+    /* within one level reads (p + w >= w) and writes (p < w) are disjoint */
+    for (int w = B / 2; w >= 1; w >>= 1)
+      for (int p = 0; p < w; p++)
+        if (smax[p + w] > smax[p]) { smax[p] = smax[p + w]; sidx[p] = sidx[p + w]; }
+    ids[r] = sidx[0];
   }
 }
 

@@ -82,9 +82,14 @@ void oracle_gemm_f64(int transA, int transB, int M, int N, int K, double alpha,
 void oracle_gemm_f32(int transA, int transB, int M, int N, int K, float alpha,
                      const float *A, int lda, const float *B, int ldb,
                      float beta, float *C, int ldc);
-/* Row argmax, ties to the lowest index (CPU CuMatrix::FindRowMaxId,
- * src/cudamatrix/cu-matrix.cc:1635-1644). */
+/* Row argmax of the reference's CTC path: the GPU _find_row_max_id
+ * (src/cudamatrix/cu-kernels.cu:2454-2500) -- 256-thread strided scan, then
+ * a strict-greater shared-memory tree, so ties resolve by the tree (columns 1
+ * and 2 equal -> 2); -1 when every value is <= -1e20 or NaN. */
 void oracle_find_row_max_id_f32(const float *m, int rows, int cols, int *ids);
+/* The CPU-only FindRowMaxId (src/cudamatrix/cu-matrix.cc:1630-1644): first
+ * maximum above -1e21, else -1.  Not on the CTC path (kept for comparison). */
+void oracle_find_row_max_id_cpu_f32(const float *m, int rows, int cols, int *ids);
 /* ComputeTotAccuracy (src/ctc/ctc-nnet-update.cc:261-317): returns sum_n L_n -
  * sum_n Levenshtein(ref_n, collapse(best ids)); *tot_weight = sum_n L_n. */
 double oracle_ctc_accuracy(const int *best_ids, int T_max, int N,
@@ -130,6 +135,23 @@ double oracle_train_step_f64(const oracle_nnet_spec *spec, double **rnn_params,
                              const int *label_lengths, const float *repair_draws,
                              double *clip_num_clipped, double *clip_count,
                              double *tot_accuracy, double *tot_weight);
+
+/* The same step, also returning the per-utterance costs [N], the network
+ * output [T*N][A] and its best path [T*N] (each nullable). */
+double oracle_train_step_ex_f32(const oracle_nnet_spec *spec, float **rnn_params,
+                                float *affine_W, float *affine_b, const float *feats,
+                                int T, int N, const int *num_frames, const int *flat_labels,
+                                const int *label_lengths, const float *repair_draws,
+                                double *clip_num_clipped, double *clip_count,
+                                double *tot_accuracy, double *tot_weight,
+                                double *costs_out, float *logits_out, int *ids_out);
+double oracle_train_step_ex_f64(const oracle_nnet_spec *spec, double **rnn_params,
+                                double *affine_W, double *affine_b, const double *feats,
+                                int T, int N, const int *num_frames, const int *flat_labels,
+                                const int *label_lengths, const float *repair_draws,
+                                double *clip_num_clipped, double *clip_count,
+                                double *tot_accuracy, double *tot_weight,
+                                double *costs_out, double *logits_out, int *ids_out);
 
 int oracle_num_threads(void);
 

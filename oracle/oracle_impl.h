@@ -424,6 +424,18 @@ double FN(oracle_train_step)(const oracle_nnet_spec *sp, REAL **rnn_params,
                              const int *label_lengths, const float *repair_draws,
                              double *clip_num_clipped, double *clip_count,
                              double *tot_accuracy, double *tot_weight) {
+  return FN(oracle_train_step_ex)(sp, rnn_params, affine_W, affine_b, feats, T, N, num_frames, flat_labels,
+                                  label_lengths, repair_draws, clip_num_clipped, clip_count, tot_accuracy,
+                                  tot_weight, NULL, NULL, NULL);
+}
+
+double FN(oracle_train_step_ex)(const oracle_nnet_spec *sp, REAL **rnn_params,
+                                REAL *affine_W, REAL *affine_b, const REAL *feats,
+                                int T, int N, const int *num_frames, const int *flat_labels,
+                                const int *label_lengths, const float *repair_draws,
+                                double *clip_num_clipped, double *clip_count,
+                                double *tot_accuracy, double *tot_weight,
+                                double *costs_out, REAL *logits_out, int *ids_out) {
   const int C = sp->num_rnn, H = sp->hidden, dirs = sp->dirs, Lr = sp->layers_per_rnn;
   const int A = sp->num_targets, Dout = dirs * H, mode = sp->mode;
   const long rows = (long)T * N;
@@ -446,15 +458,31 @@ double FN(oracle_train_step)(const oracle_nnet_spec *sp, REAL **rnn_params,
   FN(oracle_ctc)(logits, grad, flat_labels, label_lengths, num_frames, A, N, T, costs, 0);
   double tot = 0;
   for (int n = 0; n < N; n++) tot += costs[n];
-  /* accuracy on the forward logits */
+  if (costs_out)
+    for (int n = 0; n < N; n++) costs_out[n] = (double)costs[n];
+  if (logits_out) memcpy(logits_out, logits, sizeof(REAL) * rows * A);
+  /* accuracy on the forward logits, best path by the GPU _find_row_max_id
+   * rule (oracle_find_row_max_id_f32; cu-kernels.cu:2454-2500) in REAL */
   {
     int *ids = (int *)malloc(sizeof(int) * rows);
+    REAL smax[256];
+    int sidx[256];
     for (long r = 0; r < rows; r++) {
-      int b = 0;
-      for (int a = 1; a < A; a++) if (logits[r * A + a] > logits[r * A + b]) b = a;
-      ids[r] = b;
+      for (int t = 0; t < 256; t++) {
+        REAL tmax = (REAL)-1e20f;
+        int tidx = -1;
+        for (int a = t; a < A; a += 256)
+          if (logits[r * A + a] > tmax) { tmax = logits[r * A + a]; tidx = a; }
+        smax[t] = tmax;
+        sidx[t] = tidx;
+      }
+      for (int w = 128; w >= 1; w >>= 1)
+        for (int p = 0; p < w; p++)
+          if (smax[p + w] > smax[p]) { smax[p] = smax[p + w]; sidx[p] = sidx[p + w]; }
+      ids[r] = sidx[0];
     }
     *tot_accuracy = oracle_ctc_accuracy(ids, T, N, num_frames, flat_labels, label_lengths, tot_weight);
+    if (ids_out) memcpy(ids_out, ids, sizeof(int) * rows);
     free(ids);
   }
   /* Backprop: deriv *= -1 (ctc-nnet-update.cc:323) */

@@ -57,6 +57,12 @@ def lib():
                            f64p, f64p, ctypes.POINTER(ctypes.c_double),
                            ctypes.POINTER(ctypes.c_double)]
             fn.restype = ctypes.c_double
+            fn = getattr(L, "oracle_train_step_ex" + sfx)
+            fn.argtypes = [ctypes.POINTER(NnetSpec), ctypes.c_void_p, rp, rp, rp,
+                           ctypes.c_int, ctypes.c_int, i32p, i32p, i32p, ctypes.c_void_p,
+                           f64p, f64p, ctypes.POINTER(ctypes.c_double),
+                           ctypes.POINTER(ctypes.c_double), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+            fn.restype = ctypes.c_double
         for name in ("oracle_rnn_params_size", "oracle_rnn_reserve_size"):
             getattr(L, name).restype = ctypes.c_long
         L.oracle_rnn_params_size.argtypes = [ctypes.c_int] * 5
@@ -69,6 +75,7 @@ def lib():
         L.oracle_levenshtein.argtypes = [i32p, ctypes.c_int, i32p, ctypes.c_int]
         L.oracle_levenshtein.restype = ctypes.c_int
         L.oracle_find_row_max_id_f32.argtypes = [f32p, ctypes.c_int, ctypes.c_int, i32p]
+        L.oracle_find_row_max_id_cpu_f32.argtypes = [f32p, ctypes.c_int, ctypes.c_int, i32p]
         L.oracle_num_threads.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -125,6 +132,17 @@ def rnn_backward(mode, x, w, y, dy, res, H, layers, dirs):
     return dx, dw
 
 
+def find_row_max_id(m, cpu_rule=False):
+    """Best path ids of a [rows, cols] fp32 matrix: the reference CTC path's GPU
+    _find_row_max_id tie rule (default) or the CPU FindRowMaxId rule."""
+    m = np.ascontiguousarray(m, dtype=np.float32)
+    rows, cols = m.shape
+    ids = np.empty(rows, np.int32)
+    fn = lib().oracle_find_row_max_id_cpu_f32 if cpu_rule else lib().oracle_find_row_max_id_f32
+    fn(m, rows, cols, ids)
+    return ids
+
+
 def accuracy(best_ids, T, N, num_frames, flat_labels, label_lengths):
     w = ctypes.c_double()
     acc = lib().oracle_ctc_accuracy(np.ascontiguousarray(best_ids, dtype=np.int32), T, N,
@@ -137,9 +155,10 @@ def accuracy(best_ids, T, N, num_frames, flat_labels, label_lengths):
 
 
 def train_step(spec, rnn_params, affine_W, affine_b, feats, num_frames, flat_labels,
-               label_lengths, repair_draws=None, clip_num_clipped=None, clip_count=None):
+               label_lengths, repair_draws=None, clip_num_clipped=None, clip_count=None, extras=None):
     """One NnetCtcUpdater step on the CPU; parameters are updated in place.
-    Returns (tot_objf, tot_accuracy, tot_weight)."""
+    Returns (tot_objf, tot_accuracy, tot_weight).  extras (a dict, optional)
+    receives "costs" [N], "logits" [T*N, A] and "ids" [T*N] of the step."""
     sfx, dt = _dt(feats.dtype)
     T, N, D = feats.shape
     C = spec.num_rnn
@@ -150,13 +169,19 @@ def train_step(spec, rnn_params, affine_W, affine_b, feats, num_frames, flat_lab
     if repair_draws is not None:
         draws = np.ascontiguousarray(repair_draws, dtype=np.float32)
     acc, wt = ctypes.c_double(), ctypes.c_double()
-    tot = getattr(lib(), "oracle_train_step" + sfx)(
+    ex = [None, None, None]
+    if extras is not None:
+        extras["costs"] = np.zeros(N)
+        extras["logits"] = np.zeros((T * N, spec.num_targets), dtype=dt)
+        extras["ids"] = np.zeros(T * N, np.int32)
+        ex = [extras["costs"].ctypes.data, extras["logits"].ctypes.data, extras["ids"].ctypes.data]
+    tot = getattr(lib(), "oracle_train_step_ex" + sfx)(
         ctypes.byref(spec), arr, affine_W, affine_b, np.ascontiguousarray(feats, dtype=dt), T, N,
         np.ascontiguousarray(num_frames, dtype=np.int32),
         np.ascontiguousarray(flat_labels, dtype=np.int32),
         np.ascontiguousarray(label_lengths, dtype=np.int32),
         draws.ctypes.data if draws is not None else None, cnc, cc,
-        ctypes.byref(acc), ctypes.byref(wt))
+        ctypes.byref(acc), ctypes.byref(wt), *ex)
     return tot, acc.value, wt.value
 
 

@@ -124,7 +124,9 @@ def test_am_model_binary_loads_and_writes_back_byte_identical(kctc, gpu, tmp_pat
 
 def test_nnet_binary_matches_restatement_and_text_round_trip(kctc, gpu, tmp_path):
     """Nnet::Write binary of a created network == the restatement built from its
-    own parameters; text <-> binary round trips are exact."""
+    own parameters; binary round trips are exact, text ones keep the 7
+    significant digits of Kaldi's text streams (InitKaldiOutputStream,
+    base/io-funcs-inl.h:296-302) and are a fixed point after one pass."""
     D, H, A = 16, 32, 9
     net = kctc.Nnet(kctc.recipe_config(num_rnn=2, input_dim=D, hidden=H, num_targets=A, learning_rate=5e-4), seed=7)
     pb, pt = tmp_path / "n.bin", tmp_path / "n.txt"
@@ -143,15 +145,22 @@ def test_nnet_binary_matches_restatement_and_text_round_trip(kctc, gpu, tmp_path
             else:
                 i = data.index(tok("FV") + i32(len(raw) // 4) + raw, pos)
             pos = i + 1
-    for p in (pb, pt):
-        n2 = kctc.Nnet.read(p)
-        for c in range(net.num_components):
-            if net.num_params(c):
-                np.testing.assert_array_equal(n2.get_params(c), net.get_params(c))
-        p2 = tmp_path / "again.bin"
-        n2.write(p2, binary=True)
-        assert p2.read_bytes() == data
-        n2.close()
+    n2 = kctc.Nnet.read(pb)
+    for c in range(net.num_components):
+        if net.num_params(c):
+            np.testing.assert_array_equal(n2.get_params(c), net.get_params(c))
+    p2 = tmp_path / "again.bin"
+    n2.write(p2, binary=True)
+    assert p2.read_bytes() == data
+    n2.close()
+    n3 = kctc.Nnet.read(pt)
+    for c in range(net.num_components):
+        if net.num_params(c):
+            np.testing.assert_allclose(n3.get_params(c), net.get_params(c), rtol=6e-7, atol=1e-30)
+    p3 = tmp_path / "again.txt"
+    n3.write(p3, binary=False)
+    assert p3.read_bytes() == pt.read_bytes()
+    n3.close()
 
 
 def test_am_model_text_mode_and_priors(kctc, gpu, tmp_path):
@@ -171,13 +180,24 @@ def test_am_model_text_mode_and_priors(kctc, gpu, tmp_path):
     assert t.startswith("<Nnet> <NumComponents> 6") and "<CuDNNRecurrentComponent>" in t
     net2 = kctc.Nnet.read_am(txt)
     for c, p in enumerate(params):
-        if p is not None:
-            np.testing.assert_array_equal(net2.get_params(c), p)
+        if p is not None:  # text: 7 significant digits
+            np.testing.assert_allclose(net2.get_params(c), p, rtol=6e-7, atol=1e-30)
     np.testing.assert_array_equal(net2.priors, net.priors)
-    back = tmp_path / "back.mdl"
-    net2.write_am(back, binary=True)
+    back = tmp_path / "back.txt"
+    net2.write_am(back, binary=False)
+    assert back.read_bytes() == txt.read_bytes()
     pri = np.array([0.5, 0.25] + [0] * 7, np.float32)
-    assert back.read_bytes() == b"\0B" + nnet(comps) + fvec(pri)
+    # a text transition model is kept with its trailing newline
+    # (transition-model.cc:316-317): text write-back is byte-identical
+    ttrans = (b"<TransitionModel> \n<Topology> \n<TopologyEntry> \n</TopologyEntry> \n</Topology> \n"
+              b"<Triples> 0 \n</Triples> \n<LogProbs> \n [ ]\n</LogProbs> \n</TransitionModel> \n")
+    src3 = tmp_path / "tt.mdl"
+    src3.write_bytes(ttrans + txt.read_bytes())
+    n4 = kctc.Nnet.read_am(src3)
+    out4 = tmp_path / "tt_out.mdl"
+    n4.write_am(out4, binary=False)
+    assert out4.read_bytes() == src3.read_bytes()
+    n4.close()
     # a binary transition model cannot be re-emitted in text mode
     src2 = tmp_path / "t.mdl"
     src2.write_bytes(b"\0B" + TRANS + nnet(comps) + fvec(pri))
@@ -209,4 +229,45 @@ def test_old_component_forms_are_read(kctc, gpu, tmp_path):
     np.testing.assert_array_equal(net.get_params(5), params[5])
     info = net.info(2)
     assert "ClipGradient" in info
+    net.close()
+
+
+def test_bad_models_are_refused(kctc, gpu, tmp_path):
+    """Reader checks (nnet-component.cc SpliceComponent / nnet-cudnn-component.cc
+    InitFromString, nnet-nnet.cc Check): a spliced model (context != {0}: this
+    path aliases the input), an out-of-range <RNNMode>, a dimension mismatch
+    between components -- clean errors, not out-of-bounds device accesses."""
+    rng = np.random.default_rng(8)
+    comps, params = build_model(rng)
+    bad = []
+    c = list(comps)
+    c[0] = (tok("<SpliceComponent>") + tok("<InputDim>") + i32(16) + tok("<LeftContext>") + i32(1) +
+            tok("<RightContext>") + i32(1) + tok("<ConstComponentDim>") + i32(0) + tok("</SpliceComponent>"))
+    bad.append(c)
+    c = list(comps)
+    c[1] = rnn(5e-4, 16, 32, 5, True, params[1])
+    bad.append(c)
+    c = list(comps)
+    c[2] = clipgrad(48)  # RNN output 64 -> ClipGradient 48
+    bad.append(c)
+    for i, cs in enumerate(bad):
+        p = tmp_path / f"bad{i}.mdl"
+        p.write_bytes(b"\0B" + nnet(cs))
+        with pytest.raises(RuntimeError):
+            kctc.Nnet.read(p)
+
+
+def test_affine_is_gradient_round_trips(kctc, gpu, tmp_path):
+    rng = np.random.default_rng(9)
+    comps, params = build_model(rng)
+    W, b = params[5][:9 * 64].reshape(9, 64), params[5][9 * 64:]
+    comps[5] = (tok("<AffineComponent>") + tok("<LearningRate>") + f32(1e-3) + tok("<LinearParams>") + fmat(W) +
+                tok("<BiasParams>") + fvec(b) + tok("<IsGradient>") + bl(True) + tok("</AffineComponent>"))
+    blob = b"\0B" + nnet(comps)
+    p = tmp_path / "g.mdl"
+    p.write_bytes(blob)
+    net = kctc.Nnet.read(p)
+    out = tmp_path / "g_out.mdl"
+    net.write(out, binary=True)
+    assert out.read_bytes() == blob
     net.close()

@@ -126,11 +126,62 @@ def test_train_step_cfg0_matches_golden(oracle, dtype):
     assert rel_err(w - g["w0"].astype(dtype), g["w_delta"]) < (1e-6 if dtype == np.float64 else 1e-3)
     assert rel_err(Wa - g["Wa0"].astype(dtype), g["Wa_delta"]) < (1e-6 if dtype == np.float64 else 1e-3)
     assert rel_err(ba - g["ba0"].astype(dtype), g["ba_delta"]) < (1e-6 if dtype == np.float64 else 1e-3)
-    # accuracy matches argmax of the golden logits through the reference collapse rule
-    ids = g["logits"].reshape(-1, int(g["A"])).argmax(-1).astype(np.int32)
+    # accuracy matches the best path of the golden logits through the reference collapse rule
+    ids = oracle.find_row_max_id(g["logits"].reshape(-1, int(g["A"])))
     acc_ref, _ = oracle.accuracy(ids, int(g["T"]), int(g["N"]), g["num_frames"], g["flat_labels"],
                                  g["label_lengths"])
     assert acc == acc_ref
+
+
+def _find_row_max_id_lockstep(row):
+    """Literal transcription of _find_row_max_id (src/cudamatrix/cu-kernels.cu:
+    2454-2500) for one row: 256 threads (CU1DBLOCK, cu-matrixdim.h:63), the
+    strided scan, the __syncthreads() levels 128/64/32 and the warp levels
+    16..1 (warpSize 32), every thread of a level reading before any writes."""
+    B = 256
+    smax = [np.float32(-1e20)] * B
+    sidx = [-1] * B
+    for t in range(B):
+        for j in range(t, len(row), B):
+            if row[j] > smax[t]:
+                smax[t], sidx[t] = row[j], j
+    w = B // 2
+    while w >= 1:
+        active = range(w) if w >= 32 else range(16)  # warp part: tid < warpSize / 2
+        take = [(p, smax[p + w], sidx[p + w]) for p in active if smax[p + w] > smax[p]]
+        for p, v, i in take:
+            smax[p], sidx[p] = v, i
+        w //= 2
+    return sidx[0]
+
+
+def test_find_row_max_id_gpu_tie_rule(oracle):
+    """The reference's CTC path runs the GPU _find_row_max_id: ties resolve by
+    its reduction tree, not to the first column (the CPU rule)."""
+    m = np.full((4, 41), -3.0, np.float32)
+    m[0, [1, 2]] = 7.0         # tree: 2 (CPU rule: 1)
+    m[1, [0, 1]] = 7.0         # 0
+    m[2, :] = -1e20            # nothing above -1e20: -1
+    m[3, [5, 37]] = 2.0        # 37 sits in thread 37's slot; 5 wins through the tree
+    got = oracle.find_row_max_id(m)
+    assert got.tolist() == [_find_row_max_id_lockstep(r) for r in m]
+    assert got[:3].tolist() == [2, 0, -1]
+    assert oracle.find_row_max_id(m, cpu_rule=True)[:3].tolist() == [1, 0, 0]  # CPU floor is -1e21
+
+
+@pytest.mark.parametrize("cols", [1, 5, 41, 64, 256, 257, 300, 700])
+def test_find_row_max_id_matches_lockstep_kernel(oracle, cols):
+    rng = np.random.default_rng(cols)
+    m = rng.integers(-3, 3, size=(40, cols)).astype(np.float32)  # many ties
+    m[0] = -1e20
+    m[1] = np.nan
+    m[2, ::2] = -np.inf
+    m[3, :] = -2e20
+    m[3, -1] = -9.9e19
+    got = oracle.find_row_max_id(m)
+    want = [_find_row_max_id_lockstep(r) for r in m]
+    assert got.tolist() == want
+    assert got[0] == -1 and got[1] == -1 and got[3] == cols - 1
 
 
 def test_accuracy_collapse_keeps_first_frame(oracle):

@@ -37,8 +37,8 @@ def test_train_simple_equals_stepwise(kctc, gpu, tmp_path):
                              max_seq_length=100)
     a = kctc.Nnet(cfg, seed=4)
     b = kctc.Nnet(cfg, seed=4)
-    a.set_repair_seed(5)
-    b.set_repair_seed(5)
+    a.srand(5)
+    b.srand(5)
     r = kctc.EgsReader(path, minibatch_size=4, max_frames=1000)
     st = a.train_simple(r)
     assert st["num_egs"] == 11

@@ -4,6 +4,8 @@ with the in-place SGD of the reference) and the torch-fp64 cfg0 golden.
 
 Tolerances: objective 1e-5 relative; parameter updates (lr * clipped grad)
 1e-4 relative norm-wise per component (north_star: grads within 1e-4)."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -11,20 +13,13 @@ from conftest import golden, rel_err
 
 pytestmark = pytest.mark.gpu
 
-M64 = (1 << 64) - 1
-
-
-def splitmix_uniforms(seed, n):
-    """The trainer's RandUniform() stream (nnet.cpp Rng): splitmix64."""
-    s, out = seed & M64, []
-    for _ in range(n):
-        s = (s + 0x9E3779B97F4A7C15) & M64
-        z = s
-        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
-        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
-        z ^= z >> 31
-        out.append(((z >> 11) + 0.5) / 9007199254740992.0)
-    return out
+def glibc_rand_uniforms(seed, n):
+    """RandUniform() = (float)((rand() + 1.0) / (RAND_MAX + 2.0))
+    (src/base/kaldi-math.h:151-153) after srand(seed), drawn from the host's
+    own glibc -- the generator the reference process calls."""
+    libc = ctypes.CDLL("libc.so.6")
+    libc.srand(ctypes.c_uint(seed))
+    return [float(np.float32((libc.rand() + 1.0) / (2147483647 + 2.0))) for _ in range(n)]
 
 
 def test_train_step_cfg0_golden(kctc, gpu):
@@ -74,8 +69,8 @@ def test_train_steps_match_oracle(kctc, gpu, oracle, mode, H, thr, steps, pstd):
     cfg = kctc.recipe_config(num_rnn=R, input_dim=D, hidden=H, num_targets=A, rnn_mode=mode,
                              learning_rate=lr, clipping_threshold=thr, param_stddev=pstd)
     net = kctc.Nnet(cfg, seed=5)
-    net.set_repair_seed(99)
-    draws = splitmix_uniforms(99, steps * R)
+    net.srand(99)
+    draws = glibc_rand_uniforms(99, steps * R)
     upd = [c for c in range(net.num_components) if net.num_params(c) > 0]
     params = [net.get_params(c).astype(np.float64) for c in upd]
     spec = _oracle_spec(oracle, R, mode, H, 2, D, A, thr, lr)
@@ -95,7 +90,14 @@ def test_train_steps_match_oracle(kctc, gpu, oracle, mode, H, thr, steps, pstd):
         params[-1] = np.concatenate([Wa.ravel(), ba])
         np.testing.assert_allclose(objf, robjf, rtol=1e-5)
         assert wt == rwt
-        assert abs(acc - racc) <= 1  # argmax ties on nearly-equal logits may differ by one edit
+        # best path: the trainer's ids are _find_row_max_id of its own output
+        # (bit-exact), and ComputeTotAccuracy on them is the oracle's exactly
+        logits = net.last_output(T, N, A)
+        ids = net.last_best_path(T, N)
+        np.testing.assert_array_equal(ids, oracle.find_row_max_id(logits))
+        assert acc == oracle.accuracy(ids, T, N, nf, fl, ll)[0]
+        assert abs(acc - racc) <= 1  # vs fp64 logits: a near-tie may flip one frame
+    assert net.rand_calls == steps * R  # one RandUniform() per ClipGradient Backprop
     for c, p in zip(upd, params):
         got = net.get_params(c).astype(np.float64)
         init = None
@@ -125,8 +127,8 @@ def test_model_write_read_roundtrip(kctc, gpu, tmp_path):
     import torch
     D, A, T, N = 16, 9, 20, 3
     net = kctc.Nnet(kctc.recipe_config(num_rnn=2, input_dim=D, hidden=32, num_targets=A), seed=2)
-    p = tmp_path / "m.txt"
-    net.write(p)
+    p = tmp_path / "m.bin"
+    net.write(p, binary=True)
     net2 = kctc.Nnet.read(p)
     assert net2.num_components == net.num_components
     for c in range(net.num_components):
@@ -170,10 +172,12 @@ def test_streamed_gemms_match_unstreamed(kctc, gpu, monkeypatch, knob, mode, H, 
 
 
 def test_rccl_dp_single_rank_matches_plain(kctc, gpu):
-    """kctc_nnet_enable_dp at world size 1: the per-component RCCL all-reduce
-    (on its own stream, after the side-stream weight GEMMs) runs alongside the
-    streamed GEMMs and recurrences; a sum over one rank is the identity, so the
-    updates equal the plain trainer's bit for bit."""
+    """kctc_nnet_enable_dp at world size 1 builds the RCCL exchange
+    (ncclCommInitRank on a one-rank communicator): every component's bucket is
+    ncclAllReduce'd on the comm stream (forked after the side-stream weight
+    GEMMs, joined before the updates) beside the streamed GEMMs and
+    recurrences; a sum over one rank is the identity, so the updates equal
+    the plain trainer's bit for bit."""
     import torch
     D, A, T, N, H = 40, 41, 64, 16, 256
     cfg = kctc.recipe_config(num_rnn=3, input_dim=D, hidden=H, num_targets=A, learning_rate=1e-3,
