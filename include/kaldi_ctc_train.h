@@ -51,6 +51,9 @@ int kctc_nnet_component_info(kctcNnet_t nnet, int c, char *buf, size_t buflen);
 long kctc_nnet_num_params(kctcNnet_t nnet, int c);
 int kctc_nnet_get_params(kctcNnet_t nnet, int c, float *host, long n);
 int kctc_nnet_set_params(kctcNnet_t nnet, int c, const float *host, long n);
+/* the gradient component c's last update used, before its clip (the
+ * summed one under data parallelism), in Vectorize order */
+int kctc_nnet_get_grad(kctcNnet_t nnet, int c, float *host, long n);
 int kctc_nnet_set_learning_rate(kctcNnet_t nnet, float lr);
 /* ClipGradientComponent counters of component c: num_clipped, count */
 int kctc_nnet_clip_stats(kctcNnet_t nnet, int c, double *num_clipped, double *count);
@@ -69,6 +72,8 @@ int kctc_nnet_rand_calls(kctcNnet_t nnet, long *calls);
  * and its network output ([T_max*N][A] fp32; valid until the next step is
  * queued).  len must equal T_max*N (ids) / T_max*N*A (output). */
 int kctc_nnet_last_best_path(kctcNnet_t nnet, int *ids, long len);
+/* per-utterance costs (-log p(l_n | x_n), warp-ctc `costs`) of that minibatch */
+int kctc_nnet_last_costs(kctcNnet_t nnet, double *costs, int N);
 int kctc_nnet_last_output(kctcNnet_t nnet, float *host, long len);
 
 /* One SGD minibatch.  feats_dev [T_max*N][input_dim] (device, zero padded).

@@ -366,6 +366,12 @@ class Nnet:
         _tcheck(lib().kctc_nnet_get_params(self.h, c, out.ctypes.data, out.size), "get_params")
         return out
 
+    def get_grad(self, c):
+        """The gradient component c's last update used (before its clip)."""
+        out = np.zeros(self.num_params(c), np.float32)
+        _tcheck(lib().kctc_nnet_get_grad(self.h, c, out.ctypes.data, out.size), "get_grad")
+        return out
+
     def set_params(self, c, arr):
         a = np.ascontiguousarray(arr, dtype=np.float32)
         _tcheck(lib().kctc_nnet_set_params(self.h, c, a.ctypes.data, a.size), "set_params")
@@ -392,6 +398,12 @@ class Nnet:
         """FindRowMaxId ids [T*N] of the last finished minibatch."""
         out = np.empty(T * N, np.int32)
         _tcheck(lib().kctc_nnet_last_best_path(self.h, out.ctypes.data, out.size), "last_best_path")
+        return out
+
+    def last_costs(self, N):
+        """Per-utterance CTC costs [N] of the last finished minibatch."""
+        out = np.empty(N, np.float64)
+        _tcheck(lib().kctc_nnet_last_costs(self.h, out.ctypes.data, N), "last_costs")
         return out
 
     def last_output(self, T, N, A):

@@ -39,12 +39,14 @@ SIGS = {
     "kctc_nnet_num_params": (cl, [vp, ci]),
     "kctc_nnet_get_params": (ci, [vp, ci, vp, cl]),
     "kctc_nnet_set_params": (ci, [vp, ci, vp, cl]),
+    "kctc_nnet_get_grad": (ci, [vp, ci, vp, cl]),
     "kctc_nnet_set_learning_rate": (ci, [vp, cf]),
     "kctc_nnet_clip_stats": (ci, [vp, ci, ctypes.POINTER(cd), ctypes.POINTER(cd)]),
     "kctc_nnet_srand": (ci, [vp, ctypes.c_uint]),
     "kctc_nnet_rand_calls": (ci, [vp, ctypes.POINTER(cl)]),
     "kctc_nnet_last_best_path": (ci, [vp, vp, cl]),
     "kctc_nnet_last_output": (ci, [vp, vp, cl]),
+    "kctc_nnet_last_costs": (ci, [vp, vp, ci]),
     "kctc_nnet_train_step": (ci, [vp, vp, ci, ci, vp, vp, vp, ctypes.POINTER(cd), ctypes.POINTER(cd),
                                   ctypes.POINTER(cd)]),
     "kctc_nnet_compute_objf": (ci, [vp, vp, ci, ci, vp, vp, vp, ctypes.POINTER(cd), ctypes.POINTER(cd),

@@ -1128,6 +1128,7 @@ MinibatchStats NnetCtcUpdater::Finish() {
   const int *hids = reinterpret_cast<const int *>(sl.pinned + sizeof(double) * N);
   const unsigned *herr = reinterpret_cast<const unsigned *>(hids + rows);
   last_ids_.assign(hids, hids + rows);
+  last_costs_.assign(hcost, hcost + N);
   for (int i = 0; i < sl.nerr; i++)
     if (herr[i])
       throw std::runtime_error("recurrence hand-off timed out (device error word set); this minibatch's "

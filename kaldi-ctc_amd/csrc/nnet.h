@@ -384,6 +384,8 @@ class NnetCtcUpdater {
   void SetExchange(GradExchange *ex) { exchange_ = ex; }
   // best-path ids ([T_max*N], FindRowMaxId) of the last minibatch Finish()ed
   const std::vector<int> &LastBestPath() const { return last_ids_; }
+  // per-utterance CTC costs (-log p, warp-ctc `costs`) of that minibatch
+  const std::vector<double> &LastCosts() const { return last_costs_; }
   // network output of the last minibatch queued (device, [T_max*N][A])
   const CuMatrixBase &Output() const { return forward_data_.empty() ? empty_ : forward_data_.back(); }
   // srand(seed) of the process stream (nnet2-ctc-train-simple.cc:47,69;
@@ -400,6 +402,7 @@ class NnetCtcUpdater {
   GlibcRand repair_rng_{0};
   std::vector<CuMatrix> forward_data_;
   std::vector<int> last_ids_;
+  std::vector<double> last_costs_;
   CuMatrixBase empty_;
   std::vector<ChunkInfo> chunk_info_;
   CuMatrix deriv_a_, deriv_b_;

@@ -14,6 +14,9 @@ inline int rnn_nw(int mode) { return mode == kLstm ? 4 : mode == kGru ? 3 : 1; }
 
 struct RnnDesc {
   int mode = kLstm, D = 0, H = 0, layers = 1, dirs = 2;
+  // products of the recurrences and gate GEMMs: 0 fp32-class (split-fp16
+  // pairs, fp32 accumulation), 1 bf16 (fp32 accumulation, fp32 master weights)
+  int prec = 0;
   int nw() const { return rnn_nw(mode); }
   int din(int layer) const { return layer == 0 ? D : dirs * H; }
   // floats of one pseudo-layer block [W | R | bW | bR] of stacked layer `layer`

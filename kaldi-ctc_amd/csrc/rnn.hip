@@ -37,6 +37,7 @@
 #include <cstdlib>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "common.h"
@@ -75,7 +76,7 @@ RnnReserveLayout rnn_reserve_layout(const RnnDesc &d, int T, int N) {
   r.aux = p;  p += al64(TN * dirs * H);
   r.E = p;    p += al64(TN * dirs * nw * H);
   r.DX = p;   p += (d.mode == kGru) ? al64(TN * dirs * nw * H) : 0;
-  r.bias = p; p += al64(dirs * 2 * nw * H);
+  r.bias = p; p += al64(dirs * 2 * nw * H * (long)((N + 15) / 16));  // v6: per row group
   r.out = p;  p += (d.layers > 1) ? al64(TN * dirs * H) : 0;
   r.dout = p; p += (d.layers > 1) ? al64(TN * dirs * H) : 0;
   r.per_layer = p;
@@ -104,7 +105,7 @@ static size_t flags_offset(const RnnDesc &d, int T, int N) {
 // layer never overlap): T * dirs * max(H, nW*H) * Npad floats
 // flag region: words 0..1023 (v3/v4 flags, placement ids, GEMM tile counters
 // at 1008/1009), then one 128-B line per (direction, workgroup) for v6
-constexpr size_t kFlagBytes = 4096 + 2 * 64 * 128;
+constexpr size_t kFlagBytes = 4096 + 512 * 128;  // v6: up to 4 row groups x 2 dirs x 64 workgroups
 static size_t xch_offset(const RnnDesc &d, int T, int N) { return flags_offset(d, T, N) + kFlagBytes; }
 static size_t xch_bytes(const RnnDesc &d, int T, int N) {
   const long Npad = (N + 15) / 16 * 16;
@@ -213,6 +214,7 @@ __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); 
 
 struct RecParams {
   int T, N, H, dirs, U, nwg, ncol, Npad;
+  int rg;           // v6: row groups of 16 sequences (independent recurrences)
   const float *w;   // params base of this stacked layer's pseudo-layer 0
   long pl_stride;   // floats between the two directions' blocks
   long r_off;       // R within a pseudo-layer block
@@ -1326,18 +1328,23 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
 // Hand-off as v4 (sc1 payload stores, vmcnt(0), barrier, sc1 epoch flag;
 // sc1 loads) into a per-step image that is never rewritten within a launch.
 typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
-
-__device__ __forceinline__ float wave_max16(float v, int width) {
-  // max over groups of `width` (8 or 16) consecutive lanes
-  return width > 8 ? group_max16(v) : group_max8(v);
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+// products of the v6 recurrences: split-fp16 (fp32-class) or bf16
+enum { kPrecX3 = 0, kPrecBf16 = 1 };
+// max over each aligned group of U (8, 16, 32) lanes, all lanes active
+__device__ __forceinline__ float group_maxU(float v, int U) {
+  v = U > 8 ? group_max16(v) : group_max8(v);
+  if (U > 16) v = fmaxf(v, __shfl_xor(v, 16));
+  return v;
 }
+
 
 // v6 flag words: one 128-B line per (direction, workgroup), so that the
 // producers' flag stores and the consumers' polls spread over L2 / memory
 // channels instead of hammering one line.
 constexpr int kFlagStride = 32;  // words
-__device__ __forceinline__ unsigned *flag6(const RecParams &p, int d, int g, int nwg) {
-  return p.flags + 1024 + ((long)d * nwg + g) * kFlagStride;
+__device__ __forceinline__ unsigned *flag6(const RecParams &p, int grp, int d, int g, int nwg) {
+  return p.flags + 1024 + (((long)grp * p.dirs + d) * nwg + g) * kFlagStride;
 }
 __device__ __forceinline__ void wait_flags6(const unsigned *f0, int nwg, unsigned epoch, unsigned *err, int &bad,
                                             int *bad_lds, int sleep = 1) {
@@ -1367,8 +1374,8 @@ __device__ int probe6(const RecParams &p, int d, int g, int nwg, int &bad, int *
   unsigned *ids = p.flags + 512 + d * nwg;
   const unsigned me = xcc_id() + 1u;
   if (threadIdx.x == 0) __hip_atomic_store(ids + g, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  signal_epoch(flag6(p, d, g, nwg), 1u, 0);
-  wait_flags6(flag6(p, d, 0, nwg), nwg, 1u, p.err, bad, bad_lds);
+  signal_epoch(flag6(p, 0, d, g, nwg), 1u, 0);
+  wait_flags6(flag6(p, 0, d, 0, nwg), nwg, 1u, p.err, bad, bad_lds);
   if (threadIdx.x < 64) {
     bool ok = true;
     for (int i = threadIdx.x; i < nwg; i += 64)
@@ -1392,77 +1399,107 @@ __device__ __forceinline__ void split16(float x, _Float16 &hi, _Float16 &lo) {
   lo = (_Float16)(x - (float)hi);
 }
 
-template <int MODE, int U, int CTW>
-__global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
+// Generalisation (row groups, wide workgroups, bf16): the N sequences are
+// split into RG = ceil(N / 16) groups of 16 rows, each an independent
+// recurrence on its own dirs x NWG workgroups, flag lines and exchange images
+// (block b -> direction b % dirs, workgroup (b / dirs) % NWG, group
+// b / (dirs NWG)); a workgroup of NTH = 256 or 512 threads owns U = 8, 16 or
+// 32 units (one (row, unit) element per thread, NTH / 64 waves each owning
+// H / (16 NTH / 64) output column tiles).  P = kPrecBf16 multiplies bf16
+// dGates by a bf16 R slice instead of the split-fp16 pair (one MFMA per
+// block, no scaling; partial dh stay fp32).
+template <int MODE, int U, int H, int NTH, int P>
+__global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   constexpr int NW = MODE == kLstm ? 4 : 3;
+  constexpr int NWV = NTH / 64;
   constexpr int K = NW * U, KB = (K + 31) / 32, AP = KB * 32 + 8;  // A image row pitch (halves)
-  constexpr int H = CTW * 64, CTT = H / 16, NWG = H / U;
-  constexpr int POS = 4 * U;       // 16-B chunks of the own column tile per producer
-  constexpr int NGRP = NT / POS;   // producer groups
+  constexpr int CTW = H / (16 * NWV), CTT = H / 16, NWG = H / U;
+  static_assert(CTW * 16 * NWV == H, "output column tiles per wave");
+  static_assert(16 * U <= NTH, "one (row, unit) element per thread");
+  constexpr int POS = 4 * U;       // 16-B chunks of the own column tiles per producer
+  constexpr int NGRP = NTH / POS;  // producer groups
   constexpr int PER = NWG / NGRP;  // producers summed per group
   static_assert(NWG % NGRP == 0, "producer groups");
+  constexpr bool BF = P == kPrecBf16;
+  using AT = typename std::conditional<BF, __bf16, _Float16>::type;
+  using AV = typename std::conditional<BF, bf16x8, halfx8>::type;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int bad_lds, loc_lds;
   __shared__ int rowexp[16];
-  __shared__ float wmax[4];
+  __shared__ float wmax[NWV];
   // xpd = 1: XCD-slot mapping (block b -> direction b & 7, so a direction's 32
-  // workgroups share one XCD under round-robin dispatch; checked by probe6);
-  // else block b -> direction b % dirs
-  const int d = p.xpd ? (blockIdx.x & 7) : blockIdx.x % p.dirs;
-  const int g = p.xpd ? (blockIdx.x >> 3) : blockIdx.x / p.dirs;
-  if (d >= p.dirs || g >= NWG) return;
-  const int N = p.N, T = p.T;
+  // workgroups share one XCD under round-robin dispatch; checked by probe6;
+  // one row group only); else block b -> (group, workgroup, direction)
+  const int dirs = p.dirs;
+  const int d = p.xpd ? (blockIdx.x & 7) : blockIdx.x % dirs;
+  const int g = p.xpd ? (blockIdx.x >> 3) : (blockIdx.x / dirs) % NWG;
+  const int grp = p.xpd ? 0 : blockIdx.x / (dirs * NWG);
+  if (d >= dirs || g >= NWG || grp >= p.rg) return;
+  const int N = p.N, T = p.T, n0 = grp * 16;
   const int u0 = g * U, ct_own = u0 >> 4, fr0 = u0 & 15;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
-  const long ldy = (long)p.dirs * H, ldg = (long)p.dirs * NW * H;
+  const long ldy = (long)dirs * H, ldg = (long)dirs * NW * H;
   // floats per producer block (16 x H) + 256 B, so that the 1-KB chunks a
   // consumer reads from consecutive producers fall in different L2 channels
   constexpr long PSTR = (long)CTT * 64 * 4 + 64;
-  const long xstep = (long)p.dirs * NWG * PSTR;
-  _Float16 *Ahi = reinterpret_cast<_Float16 *>(smem);  // [16][AP]
-  _Float16 *Alo = Ahi + 16 * AP;
-  float *red = reinterpret_cast<float *>(Alo + 16 * AP);  // [NGRP][POS][4]
+  const long xgrp = (long)dirs * NWG * PSTR;  // one row group's images of a step
+  const long xstep = xgrp * p.rg;
+  AT *Ahi = reinterpret_cast<AT *>(smem);  // [16][AP]
+  AT *Alo = Ahi + 16 * AP;                 // x3 only
+  float *red = reinterpret_cast<float *>(Alo + (BF ? 0 : 16 * AP));  // [NGRP][POS][4]
   // streamed consumer: this step's dGates tile [16][NW * U] (DX for GRU), then
   // written through with 16-B stores after the step's signal
-  float *estg = red + (NT * 4 > 2 * 16 * U * NW ? NT * 4 : 2 * 16 * U * NW);
+  float *estg = red + (NTH * 4 > 2 * 16 * U * NW ? NTH * 4 : 2 * 16 * U * NW);
   const float *Wd = p.w + d * p.pl_stride;
   const float *R = Wd + p.r_off;
   if (tid == 0) bad_lds = 0;
-  for (int i = tid; i < 32 * AP; i += NT) Ahi[i] = (_Float16)0.f;  // Ahi and Alo, padding included
-  // ---- R slice -> scaled hi/lo B fragments in registers ----
+  for (int i = tid; i < (BF ? 16 : 32) * AP; i += NTH) Ahi[i] = (AT)0.f;  // the image(s), padding included
+  // ---- R slice -> B fragments in registers (x3: scaled hi/lo; bf16: as is) ----
   auto rval = [&](int kk, int col) -> float {
     if (kk >= K) return 0.f;
     const int q = kk / U, u = kk - q * U;
     return R[(long)(q * H + u0 + u) * H + col];
   };
-  float mx = 0.f;
+  int sB = 0;
+  if constexpr (!BF) {
+    float mx = 0.f;
 #pragma unroll
-  for (int c = 0; c < CTW; c++)
+    for (int c = 0; c < CTW; c++)
 #pragma unroll
-    for (int kb = 0; kb < KB; kb++)
+      for (int kb = 0; kb < KB; kb++)
 #pragma unroll
-      for (int j = 0; j < 8; j++) mx = fmaxf(mx, fabsf(rval(kb * 32 + fq * 8 + j, (w * CTW + c) * 16 + fr)));
+        for (int j = 0; j < 8; j++) mx = fmaxf(mx, fabsf(rval(kb * 32 + fq * 8 + j, (w * CTW + c) * 16 + fr)));
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-  if (lane == 0) wmax[w] = mx;
-  __syncthreads();
-  const int sB = split_exp(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3])));
-  halfx8 bhi[CTW][KB], blo[CTW][KB];
+    for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    if (lane == 0) wmax[w] = mx;
+    __syncthreads();
+    float m4 = wmax[0];
+#pragma unroll
+    for (int i = 1; i < NWV; i++) m4 = fmaxf(m4, wmax[i]);
+    sB = split_exp(m4);
+  }
+  AV bhi[CTW][KB], blo[BF ? 1 : CTW][BF ? 1 : KB];
 #pragma unroll
   for (int c = 0; c < CTW; c++)
 #pragma unroll
     for (int kb = 0; kb < KB; kb++)
 #pragma unroll
       for (int j = 0; j < 8; j++) {
-        _Float16 h, l;
-        split16(ldexpf(rval(kb * 32 + fq * 8 + j, (w * CTW + c) * 16 + fr), sB), h, l);
-        bhi[c][kb][j] = h;
-        blo[c][kb][j] = l;
+        const float v = rval(kb * 32 + fq * 8 + j, (w * CTW + c) * 16 + fr);
+        if constexpr (BF) {
+          bhi[c][kb][j] = (__bf16)v;
+        } else {
+          _Float16 h, l;
+          split16(ldexpf(v, sB), h, l);
+          bhi[c][kb][j] = h;
+          blo[c][kb][j] = l;
+        }
       }
-  // ---- per-element state: thread tid <-> (n = tid / U, u = tid % U) ----
+  // ---- per-element state: thread tid <-> (row n0 + en, unit u0 + eu) ----
   const bool has_e = tid < 16 * U;
   const int en = tid / U, eu = tid - en * U;
-  const bool live = has_e && en < N;
+  const int n = n0 + en;
+  const bool live = has_e && n < N;
   float carry = 0.f, bsx[NW], bsh[NW], dxk[NW], eg[NW], cg[NW], ng[NW], cmx[NW], cme[NW];
   float cdy = 0.f, ca = 0.f, cap = 0.f, ndy = 0.f, na = 0.f, nap = 0.f;
 #pragma unroll
@@ -1470,9 +1507,9 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
   auto prefetch = [&](int k) {  // operands of forward-order step k into n*
     if (!live) return;
     const int t = d == 0 ? k : T - 1 - k, tp = d == 0 ? t - 1 : t + 1;
-    const long yrow = ((long)t * N + en) * ldy + (long)d * H + u0 + eu;
-    const long grow = ((long)t * N + en) * ldg + (long)d * NW * H + u0 + eu;
-    const long prow = ((long)tp * N + en) * ldy + (long)d * H + u0 + eu;
+    const long yrow = ((long)t * N + n) * ldy + (long)d * H + u0 + eu;
+    const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + eu;
+    const long prow = ((long)tp * N + n) * ldy + (long)d * H + u0 + eu;
     ndy = p.dy[yrow];
 #pragma unroll
     for (int q = 0; q < NW; q++) ng[q] = p.G[grow + q * H];
@@ -1487,7 +1524,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
   };
   auto e_store = [&](int t) {  // row-major dGates of step t (E; GRU also DX)
     if (!live) return;
-    const long grow = ((long)t * N + en) * ldg + (long)d * NW * H + u0 + eu;
+    const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + eu;
     if (p.e_sc1) {  // DX (== E for LSTM) went out through estg already
       if (MODE == kGru) {
 #pragma unroll
@@ -1502,17 +1539,18 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
       for (int q = 0; q < NW; q++) p.DX[grow + q * H] = dxk[q];
     }
   };
-  // consumer chunk of this thread: position pos (lane of the own column tile)
-  // of producers grp, grp + NGRP, ...
-  const int pos = tid % POS, grp = tid / POS;
-  const int pln = U == 16 ? pos : (pos >> 3) * 16 + fr0 + (pos & 7);
-  const long coff = (long)d * NWG * PSTR + ((long)ct_own * 64 + pln) * 4 + (long)grp * PSTR;
-  // where element (en, eu) finds its sum: chunk of lane (en/4)*16 + fr0 + eu, register en % 4
-  const int epos = U == 16 ? (en >> 2) * 16 + eu : (en >> 2) * 8 + eu;
+  // consumer chunk of this thread: position pos (of the own column tiles'
+  // C-fragment chunks) of producers pg, pg + NGRP, ...
+  const int pos = tid % POS, pg = tid / POS;
+  const int pln = U >= 16 ? pos : (pos >> 3) * 16 + fr0 + (pos & 7);
+  const long coff = (long)grp * xgrp + (long)d * NWG * PSTR + ((long)ct_own * 64 + pln) * 4 + (long)pg * PSTR;
+  // where element (en, eu) finds its sum: own tile eu / 16, lane (en / 4) * 16
+  // + (eu % 16) (U = 8: compacted to 8 per row quad), register en % 4
+  const int epos = (eu >> 4) * 64 + (en >> 2) * (U < 16 ? U : 16) + (eu & 15);
   prefetch(T - 1);
   rotate();
   int bad = 0;
-  unsigned *myflag = flag6(p, d, g, NWG);
+  unsigned *myflag = flag6(p, grp, d, g, NWG);
   if (tid == 0) loc_lds = 0;
   const int local = (p.xpd && p.allow_local) ? probe6(p, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
   int t_prev = -1;
@@ -1521,16 +1559,16 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
     const int ks = T - 1 - k;  // steps done before this one
     REC_TRACE(ks, 0);
     if (ks > 0) {
-      wait_flags6(flag6(p, d, 0, NWG), NWG, (unsigned)(ks + 1), p.err, bad, &bad_lds, p.poll_sleep);
+      wait_flags6(flag6(p, grp, d, 0, NWG), NWG, (unsigned)(ks + 1), p.err, bad, &bad_lds, p.poll_sleep);
       REC_TRACE(ks, 1);
       const auto rs = rsrc(p.xch + (long)(ks - 1) * xstep, (unsigned)(xstep * 4));
       u32x4 v[PER];
 #pragma unroll
       for (int i = 0; i < PER; i++) v[i] = ld_sc1(rs, (unsigned)((coff + (long)i * NGRP * PSTR) * 4));
-      floatx4 s = __builtin_bit_cast(floatx4, v[0]);
+      floatx4 sm = __builtin_bit_cast(floatx4, v[0]);
 #pragma unroll
-      for (int i = 1; i < PER; i++) s += __builtin_bit_cast(floatx4, v[i]);
-      st4(red + (long)(grp * POS + pos) * 4, s);
+      for (int i = 1; i < PER; i++) sm += __builtin_bit_cast(floatx4, v[i]);
+      st4(red + (long)(pg * POS + pos) * 4, sm);
       REC_TRACE(ks, 2);
     }
     asm volatile("" ::: "memory");
@@ -1577,15 +1615,20 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
           if (MODE == kGru) cme[q] = fmaxf(cme[q], fabsf(eg[q]));
         }
       }
-      const int se = split_exp(wave_max16(m, U));
+      if constexpr (BF) {
 #pragma unroll
-      for (int q = 0; q < NW; q++) {
-        _Float16 h, l;
-        split16(ldexpf(eg[q], se), h, l);
-        Ahi[en * AP + q * U + eu] = h;
-        Alo[en * AP + q * U + eu] = l;
+        for (int q = 0; q < NW; q++) Ahi[en * AP + q * U + eu] = (__bf16)eg[q];
+      } else {
+        const int se = split_exp(group_maxU(m, U));
+#pragma unroll
+        for (int q = 0; q < NW; q++) {
+          _Float16 h, l;
+          split16(ldexpf(eg[q], se), h, l);
+          Ahi[en * AP + q * U + eu] = h;
+          Alo[en * AP + q * U + eu] = l;
+        }
+        if (eu == 0) rowexp[en] = se + sB;
       }
-      if (eu == 0) rowexp[en] = se + sB;
       if (p.e_sc1) {
 #pragma unroll
         for (int q = 0; q < NW; q++) estg[en * NW * U + q * U + eu] = MODE == kGru ? dxk[q] : eg[q];
@@ -1599,25 +1642,32 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
       for (int c = 0; c < CTW; c++) acc[c] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kb = 0; kb < KB; kb++) {
-        const halfx8 ah = *reinterpret_cast<const halfx8 *>(Ahi + fr * AP + kb * 32 + fq * 8);
-        const halfx8 al = *reinterpret_cast<const halfx8 *>(Alo + fr * AP + kb * 32 + fq * 8);
+        const AV ah = *reinterpret_cast<const AV *>(Ahi + fr * AP + kb * 32 + fq * 8);
+        if constexpr (BF) {
 #pragma unroll
-        for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bhi[c][kb], acc[c], 0, 0, 0);
+          for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bhi[c][kb], acc[c], 0, 0, 0);
+        } else {
+          const AV al = *reinterpret_cast<const AV *>(Alo + fr * AP + kb * 32 + fq * 8);
 #pragma unroll
-        for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, blo[c][kb], acc[c], 0, 0, 0);
+          for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bhi[c][kb], acc[c], 0, 0, 0);
 #pragma unroll
-        for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bhi[c][kb], acc[c], 0, 0, 0);
+          for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, blo[c][kb], acc[c], 0, 0, 0);
+#pragma unroll
+          for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bhi[c][kb], acc[c], 0, 0, 0);
+        }
       }
-      int ex[4];
+      int ex[4] = {0, 0, 0, 0};
+      if constexpr (!BF) {
 #pragma unroll
-      for (int i = 0; i < 4; i++) ex[i] = -rowexp[fq * 4 + i];
+        for (int i = 0; i < 4; i++) ex[i] = -rowexp[fq * 4 + i];
+      }
       const auto ro = rsrc(p.xch + (long)ks * xstep, (unsigned)(xstep * 4));
-      const long obase = (long)(d * NWG + g) * PSTR;
+      const long obase = (long)grp * xgrp + (long)(d * NWG + g) * PSTR;
 #pragma unroll
       for (int c = 0; c < CTW; c++) {
         floatx4 o;
 #pragma unroll
-        for (int i = 0; i < 4; i++) o[i] = ldexpf(acc[c][i], ex[i]);
+        for (int i = 0; i < 4; i++) o[i] = BF ? acc[c][i] : ldexpf(acc[c][i], ex[i]);
         const int off = (int)((obase + ((long)(w * CTW + c) * 64 + lane) * 4) * 4);
         // write-through (sc1) payload in either mode: the stored lines leave
         // the XCD's L2, so the consumers' sc1 loads read them from the
@@ -1634,11 +1684,11 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
       // issued after the signal, so only the NEXT signal (epoch ks + 3) waits
       // for them (4-B write-through stores per element cost ~8 us per step)
       constexpr int CPR = NW * U / 4;  // chunks per row
-      const int n = tid / CPR, c = tid - n * CPR;
-      if (n < N) {
+      const int rn = tid / CPR, c = tid - rn * CPR;
+      if (rn < 16 && n0 + rn < N) {
         const int q = (c * 4) / U, u = (c * 4) % U;
-        const u32x4 v = *reinterpret_cast<const u32x4 *>(estg + n * NW * U + c * 4);
-        const int off = (int)(((long)n * ldg + (long)d * NW * H + q * H + u0 + u) * 4);
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(estg + rn * NW * U + c * 4);
+        const int off = (int)(((long)(n0 + rn) * ldg + (long)d * NW * H + q * H + u0 + u) * 4);
         __builtin_amdgcn_raw_buffer_store_b128(v, rsrc(p.DX + (long)t * N * ldg, (unsigned)(N * ldg * 4)), off, 0, 16);
       }
     }
@@ -1648,7 +1698,8 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
   }
   if (t_prev >= 0 && !bad) e_store(t_prev);
   if (!bad) signal_epoch(myflag, (unsigned)(T + 2), 0);  // the last step's rows are out
-  // bias partial sums: reduce over n in a fixed order through LDS
+  // bias partial sums of this row group: reduce over its rows in a fixed
+  // order through LDS; the host adds the groups in order
   float *bs = red;  // [2][16][U][NW] floats
   __syncthreads();
   if (has_e) {
@@ -1660,13 +1711,13 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
     }
   }
   __syncthreads();
-  for (int q = tid; q < 2 * NW * U; q += NT) {
+  for (int q = tid; q < 2 * NW * U; q += NTH) {
     const int part = q / (NW * U), rem = q - part * NW * U, gt = rem / U, u = rem - gt * U;
     float s2 = 0.f;
-    for (int n = 0; n < N; n++) s2 += bs[(long)part * 16 * U * NW + ((long)n * U + u) * NW + gt];
-    p.bias[((long)d * 2 + part) * NW * H + gt * H + u0 + u] = s2;
+    for (int r = 0; r < 16; r++) s2 += bs[(long)part * 16 * U * NW + ((long)r * U + u) * NW + gt];
+    p.bias[(((long)grp * dirs + d) * 2 + part) * NW * H + gt * H + u0 + u] = s2;
   }
-  if (p.cmax) {  // column maxima over all frames (rows n of this WG's columns, through LDS)
+  if (p.cmax) {  // column maxima over all frames (this group's rows, through LDS; max over groups)
     constexpr int NP = MODE == kGru ? 2 : 1;
     __syncthreads();
     if (has_e) {
@@ -1677,11 +1728,13 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
       }
     }
     __syncthreads();
-    for (int q = tid; q < NP * NW * U; q += NT) {
+    for (int q = tid; q < NP * NW * U; q += NTH) {
       const int part = q / (NW * U), rem = q - part * NW * U, gt = rem / U, u = rem - gt * U;
       float m2 = 0.f;
-      for (int n = 0; n < 16; n++) m2 = fmaxf(m2, bs[(long)part * 16 * U * NW + ((long)n * U + u) * NW + gt]);
-      p.cmax[(long)part * p.dirs * NW * H + (long)d * NW * H + gt * H + u0 + u] = __float_as_uint(m2);
+      for (int r = 0; r < 16; r++) m2 = fmaxf(m2, bs[(long)part * 16 * U * NW + ((long)r * U + u) * NW + gt]);
+      unsigned *dst = p.cmax + (long)part * dirs * NW * H + (long)d * NW * H + gt * H + u0 + u;
+      if (p.rg > 1) atomicMax(dst, __float_as_uint(m2));  // non-negative floats order as their bits
+      else *dst = __float_as_uint(m2);
     }
   }
   if (bad && tid == 0) atomicOr(p.err, 1u);
@@ -1702,77 +1755,101 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec6(RecParams p) {
 // and 16 B of lo per 32-k block.  The R slice lives in registers (B
 // fragments) for the whole launch.  Hand-off as v4 (sc1 stores, vmcnt(0),
 // barrier, sc1 epoch flag; sc1 loads).
-template <int MODE, int U, int H>
-__global__ __launch_bounds__(NT, 1) void rnn_fwd_rec6(RecParams p) {
+// Generalised like rnn_bwd_rec6: row groups of 16 sequences (block b ->
+// direction b % dirs, workgroup (b / dirs) % NWG, group b / (dirs NWG); each
+// group has its own flag lines and step images), NTH = 256 or 512 threads (K
+// split over NTH / 64 waves), U up to 32; P = kPrecBf16 exchanges h as bf16
+// and multiplies by a bf16 R slice (one MFMA per block, no scaling).
+template <int MODE, int U, int H, int NTH, int P>
+__global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   constexpr int NW = MODE == kLstm ? 4 : 3;
+  constexpr int NWV = NTH / 64;
   constexpr int NC = NW * U, CT = (NC + 15) / 16, RP = CT * 16 + 1;  // red row pitch (floats)
-  constexpr int KB = H / 32, KBW = (KB + 3) / 4, NWG = H / U;
-  constexpr int CH = U / 8;  // 16-B chunks of a published row
+  constexpr int KB = H / 32, KBW = (KB + NWV - 1) / NWV, NWG = H / U;
+  constexpr int CH = U / 8;  // 16-B chunks of a published row part
+  constexpr bool BF = P == kPrecBf16;
+  constexpr int NP = BF ? 1 : 2;  // parts of an exchanged h: hi (+ lo)
+  static_assert(16 * U <= NTH, "one (row, unit) element per thread");
+  using AT = typename std::conditional<BF, __bf16, _Float16>::type;
+  using AV = typename std::conditional<BF, bf16x8, halfx8>::type;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int bad_lds;
-  __shared__ float wmax[4];
-  const int d = blockIdx.x % p.dirs, g = blockIdx.x / p.dirs;
-  if (g >= NWG) return;
-  const int N = p.N, T = p.T;
+  __shared__ float wmax[NWV];
+  const int dirs = p.dirs;
+  const int d = blockIdx.x % dirs, g = (blockIdx.x / dirs) % NWG, grp = blockIdx.x / (dirs * NWG);
+  if (grp >= p.rg) return;
+  const int N = p.N, T = p.T, n0 = grp * 16;
   const int u0 = g * U;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
-  const long ldy = (long)p.dirs * H, ldg = (long)p.dirs * NW * H;
-  constexpr long XS = 2L * KB * 2 * 16 * 32;  // halves per step image (dirs <= 2)
-  float *red = smem;                                                     // [4][16][RP]
-  _Float16 *stg = reinterpret_cast<_Float16 *>(smem + 4 * 16 * RP + 3);  // [2][16][U], 16-B aligned below
-  stg = reinterpret_cast<_Float16 *>((reinterpret_cast<uintptr_t>(stg) + 15) & ~uintptr_t(15));
+  const long ldy = (long)dirs * H, ldg = (long)dirs * NW * H;
+  constexpr long XG = 2L * KB * NP * 16 * 32;  // halves per row group's image of a step (dirs <= 2)
+  const long XS = XG * p.rg;                    // halves per step image
+  float *red = smem;                                                       // [NWV][16][RP]
+  AT *stg = reinterpret_cast<AT *>(smem + NWV * 16 * RP + 3);              // [NP][16][U], 16-B aligned below
+  stg = reinterpret_cast<AT *>((reinterpret_cast<uintptr_t>(stg) + 15) & ~uintptr_t(15));
   const float *Wd = p.w + d * p.pl_stride;
   const float *R = Wd + p.r_off;
-  _Float16 *xch = reinterpret_cast<_Float16 *>(p.xch);
+  AT *xch = reinterpret_cast<AT *>(p.xch);
   if (tid == 0) bad_lds = 0;
-  // ---- R slice -> scaled hi/lo B fragments: B[k][c] = R[q*H + u0 + u][k], c = q*U + u ----
+  // ---- R slice -> B fragments: B[k][c] = R[q*H + u0 + u][k], c = q*U + u ----
   auto rrow = [&](int c) -> const float * {
     const int q = c / U, u = c - q * U;
     return R + (long)(q * H + u0 + u) * H;
   };
-  float mx = 0.f;
+  int sB = 0, sOut = 0;
+  if constexpr (!BF) {
+    float mx = 0.f;
 #pragma unroll
-  for (int ct = 0; ct < CT; ct++) {
-    const int c = ct * 16 + fr;
-    if (c < NC) {
-      const float *rr = rrow(c);
+    for (int ct = 0; ct < CT; ct++) {
+      const int c = ct * 16 + fr;
+      if (c < NC) {
+        const float *rr = rrow(c);
 #pragma unroll
-      for (int i = 0; i < KBW; i++) {
-        const int kb = w + 4 * i;
-        if (kb < KB) {
+        for (int i = 0; i < KBW; i++) {
+          const int kb = w + NWV * i;
+          if (kb < KB) {
 #pragma unroll
-          for (int j = 0; j < 8; j++) mx = fmaxf(mx, fabsf(rr[kb * 32 + fq * 8 + j]));
+            for (int j = 0; j < 8; j++) mx = fmaxf(mx, fabsf(rr[kb * 32 + fq * 8 + j]));
+          }
         }
       }
     }
-  }
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-  if (lane == 0) wmax[w] = mx;
-  __syncthreads();
-  const int sB = split_exp(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3])));
-  const int sOut = -(sB + 14);
-  halfx8 bhi[CT][KBW], blo[CT][KBW];
+    for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    if (lane == 0) wmax[w] = mx;
+    __syncthreads();
+    float m4 = wmax[0];
+#pragma unroll
+    for (int i = 1; i < NWV; i++) m4 = fmaxf(m4, wmax[i]);
+    sB = split_exp(m4);
+    sOut = -(sB + 14);
+  }
+  AV bhi[CT][KBW], blo[BF ? 1 : CT][BF ? 1 : KBW];
 #pragma unroll
   for (int ct = 0; ct < CT; ct++) {
     const int c = ct * 16 + fr;
 #pragma unroll
     for (int i = 0; i < KBW; i++) {
-      const int kb = w + 4 * i;
+      const int kb = w + NWV * i;
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         const float v = (c < NC && kb < KB) ? rrow(c)[kb * 32 + fq * 8 + j] : 0.f;
-        _Float16 h, l;
-        split16(ldexpf(v, sB), h, l);
-        bhi[ct][i][j] = h;
-        blo[ct][i][j] = l;
+        if constexpr (BF) {
+          bhi[ct][i][j] = (__bf16)v;
+        } else {
+          _Float16 h, l;
+          split16(ldexpf(v, sB), h, l);
+          bhi[ct][i][j] = h;
+          blo[ct][i][j] = l;
+        }
       }
     }
   }
-  // ---- per-element state: thread tid <-> (n = tid / U, u = tid % U) ----
+  // ---- per-element state: thread tid <-> (row n0 + en, unit u0 + eu) ----
   const bool has_e = tid < 16 * U;
   const int en = tid / U, eu = tid - en * U;
-  const bool live = has_e && en < N;
+  const int n = n0 + en;
+  const bool live = has_e && n < N;
   float cst = 0.f, hpv = 0.f, cnew = 0.f, hval = 0.f;
   float gin[NW], gnx[NW], bR[NW], act[NW];
 #pragma unroll
@@ -1783,22 +1860,23 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec6(RecParams p) {
   auto gin_load = [&](int t, float (&dst)[NW]) {
     if (!live) return;
 #pragma unroll
-    for (int q = 0; q < NW; q++) dst[q] = p.G[((long)t * N + en) * ldg + (long)d * NW * H + q * H + u0 + eu];
+    for (int q = 0; q < NW; q++) dst[q] = p.G[((long)t * N + n) * ldg + (long)d * NW * H + q * H + u0 + eu];
   };
   auto out_store = [&](int t) {  // row-major y, activations (in place of G), aux of step t
     if (!live) return;
-    p.y[((long)t * N + en) * ldy + (long)d * H + u0 + eu] = hval;
-    const long grow = ((long)t * N + en) * ldg + (long)d * NW * H + u0 + eu;
+    p.y[((long)t * N + n) * ldy + (long)d * H + u0 + eu] = hval;
+    const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + eu;
 #pragma unroll
     for (int q = 0; q < NW; q++) p.G[grow + q * H] = act[q];
-    p.aux[((long)t * N + en) * ldy + (long)d * H + u0 + eu] = cnew;
+    p.aux[((long)t * N + n) * ldy + (long)d * H + u0 + eu] = cnew;
   };
   gin_load(d == 0 ? 0 : T - 1, gin);
   int bad = 0;
-  unsigned *myflag = flag6(p, d, g, NWG);
-  // publish geometry: store thread s < 32 * CH: part = s / (16 CH), row, chunk
+  unsigned *myflag = flag6(p, grp, d, g, NWG);
+  // publish geometry: store thread s < NP * 16 * CH: part = s / (16 CH), row, chunk
   const int sp = tid / (16 * CH), sn = (tid / CH) % 16, sch = tid % CH;
   const int kb0 = u0 >> 5, koff = (u0 & 31) + sch * 8;
+  const long gimg = (long)grp * XG;
   int t_prev = -1;
   for (int k = 0; k < T && !bad; k++) {
     const int t = d == 0 ? k : T - 1 - k, tp = d == 0 ? t - 1 : t + 1;
@@ -1807,29 +1885,35 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec6(RecParams p) {
     for (int ct = 0; ct < CT; ct++) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
     REC_TRACE(k, 0);
     if (k > 0) {
-      wait_flags6(flag6(p, d, 0, NWG), NWG, (unsigned)(k + 1), p.err, bad, &bad_lds, p.poll_sleep);
+      wait_flags6(flag6(p, grp, d, 0, NWG), NWG, (unsigned)(k + 1), p.err, bad, &bad_lds, p.poll_sleep);
       REC_TRACE(k, 1);
-      const auto rs = rsrc(xch + (long)tp * XS, (unsigned)(XS * 2));
+      const auto rs = rsrc(xch + (long)tp * XS, (unsigned)(XS * sizeof(AT)));
       u32x4 ah[KBW], al[KBW];
 #pragma unroll
       for (int i = 0; i < KBW; i++) {
-        const int kb = w + 4 * i;
+        const int kb = w + NWV * i;
         if (kb < KB) {
-          const long o = ((((long)d * KB + kb) * 2) * 16 + fr) * 32 + fq * 8;
-          ah[i] = ld_sc1(rs, (unsigned)(o * 2));
-          al[i] = ld_sc1(rs, (unsigned)((o + 16 * 32) * 2));
+          const long o = gimg + ((((long)d * KB + kb) * NP) * 16 + fr) * 32 + fq * 8;
+          ah[i] = ld_sc1(rs, (unsigned)(o * sizeof(AT)));
+          if constexpr (!BF) al[i] = ld_sc1(rs, (unsigned)((o + 16 * 32) * sizeof(AT)));
         }
       }
 #pragma unroll
       for (int i = 0; i < KBW; i++) {
-        if (w + 4 * i < KB) {
-          const halfx8 a0 = __builtin_bit_cast(halfx8, ah[i]), a1 = __builtin_bit_cast(halfx8, al[i]);
+        if (w + NWV * i < KB) {
+          const AV a0 = __builtin_bit_cast(AV, ah[i]);
+          if constexpr (BF) {
 #pragma unroll
-          for (int ct = 0; ct < CT; ct++) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bhi[ct][i], acc[ct], 0, 0, 0);
+            for (int ct = 0; ct < CT; ct++) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bhi[ct][i], acc[ct], 0, 0, 0);
+          } else {
+            const AV a1 = __builtin_bit_cast(AV, al[i]);
 #pragma unroll
-          for (int ct = 0; ct < CT; ct++) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, blo[ct][i], acc[ct], 0, 0, 0);
+            for (int ct = 0; ct < CT; ct++) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bhi[ct][i], acc[ct], 0, 0, 0);
 #pragma unroll
-          for (int ct = 0; ct < CT; ct++) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bhi[ct][i], acc[ct], 0, 0, 0);
+            for (int ct = 0; ct < CT; ct++) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, blo[ct][i], acc[ct], 0, 0, 0);
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bhi[ct][i], acc[ct], 0, 0, 0);
+          }
         }
       }
     }
@@ -1848,9 +1932,10 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec6(RecParams p) {
 #pragma unroll
       for (int q = 0; q < NW; q++) {
         const int c = q * U + eu;
-        rh[q] = ldexpf(((red[(0 * 16 + en) * RP + c] + red[(1 * 16 + en) * RP + c]) + red[(2 * 16 + en) * RP + c]) +
-                           red[(3 * 16 + en) * RP + c],
-                       sOut);
+        float sm = red[(0 * 16 + en) * RP + c];  // the waves' K partials in a fixed order
+#pragma unroll
+        for (int v = 1; v < NWV; v++) sm += red[(v * 16 + en) * RP + c];
+        rh[q] = BF ? sm : ldexpf(sm, sOut);
       }
       float h;
       if (MODE == kLstm) {
@@ -1871,16 +1956,21 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec6(RecParams p) {
       }
       if (!live) h = 0.f;
       hval = h;
-      _Float16 hh, hl;
-      split16(h * 16384.f, hh, hl);
-      stg[en * U + eu] = hh;
-      stg[(16 + en) * U + eu] = hl;
+      if constexpr (BF) {
+        stg[en * U + eu] = (__bf16)h;
+      } else {
+        _Float16 hh, hl;
+        split16(h * 16384.f, hh, hl);
+        stg[en * U + eu] = hh;
+        stg[(16 + en) * U + eu] = hl;
+      }
     }
     __syncthreads();
-    if (tid < 32 * CH) {
+    if (tid < NP * 16 * CH) {
       const u32x4 v = *reinterpret_cast<const u32x4 *>(stg + (sp * 16 + sn) * U + sch * 8);
-      const long o = ((((long)d * KB + kb0) * 2 + sp) * 16 + sn) * 32 + koff;
-      __builtin_amdgcn_raw_buffer_store_b128(v, rsrc(xch + (long)t * XS, (unsigned)(XS * 2)), (int)(o * 2), 0, 16);
+      const long o = gimg + ((((long)d * KB + kb0) * NP + sp) * 16 + sn) * 32 + koff;
+      __builtin_amdgcn_raw_buffer_store_b128(v, rsrc(xch + (long)t * XS, (unsigned)(XS * sizeof(AT))),
+                                             (int)(o * sizeof(AT)), 0, 16);
     }
     REC_TRACE(k, 7);
     signal_epoch(myflag, (unsigned)(k + 2), 0);
@@ -1931,46 +2021,52 @@ static void launch_mode(bool fwd, const RecParams &p, dim3 grid, size_t lds, hip
     default: launch_one<MODE, 4>(fwd, p, grid, lds, s, ver); break;
   }
 }
-template <int MODE, int U, int CTW>
-static void launch6_one(const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
-  set_lds(rnn_bwd_rec6<MODE, U, CTW>, lds);
-  hipLaunchKernelGGL((rnn_bwd_rec6<MODE, U, CTW>), grid, dim3(NT), lds, s, p);
+// v6 shapes that compile: H in {256, 320, 512, 1024}; U in {8, 16} at 256
+// threads, U = 32 at 512 threads (H / (16 * waves) output tiles per wave and
+// H / U producers in groups of 512 / (4 U) for the backward)
+template <int U, int H, int NTH>
+constexpr bool v6_shape_ok() {
+  return NTH == (U == 32 ? 512 : 256) && H % (16 * (NTH / 64)) == 0 && (H / U) % (NTH / (4 * U)) == 0;
 }
-template <int MODE, int U>
-static void launch6_u(const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
-  switch (p.H / 64) {
-    case 4: launch6_one<MODE, U, 4>(p, grid, lds, s); break;
-    case 5: launch6_one<MODE, U, 5>(p, grid, lds, s); break;
-    default: launch6_one<MODE, U, 8>(p, grid, lds, s); break;
-  }
-}
-static void launch_rec6(int mode, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
-  if (mode == kLstm) {
-    if (p.U == 16) launch6_u<kLstm, 16>(p, grid, lds, s);
-    else launch6_u<kLstm, 8>(p, grid, lds, s);
+template <int MODE, int U, int H, int NTH, int P>
+static void launch6_shape(bool fwd, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
+  if constexpr (v6_shape_ok<U, H, NTH>()) {
+    if (fwd) {
+      set_lds(rnn_fwd_rec6<MODE, U, H, NTH, P>, lds);
+      hipLaunchKernelGGL((rnn_fwd_rec6<MODE, U, H, NTH, P>), grid, dim3(NTH), lds, s, p);
+    } else {
+      set_lds(rnn_bwd_rec6<MODE, U, H, NTH, P>, lds);
+      hipLaunchKernelGGL((rnn_bwd_rec6<MODE, U, H, NTH, P>), grid, dim3(NTH), lds, s, p);
+    }
   } else {
-    if (p.U == 16) launch6_u<kGru, 16>(p, grid, lds, s);
-    else launch6_u<kGru, 8>(p, grid, lds, s);
+    throw std::logic_error("v6 recurrence: shape not compiled");
   }
 }
-template <int MODE, int U>
-static void launchf6_u(const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
+template <int MODE, int U, int NTH, int P>
+static void launch6_h(bool fwd, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
   switch (p.H) {
-    case 256: set_lds(rnn_fwd_rec6<MODE, U, 256>, lds);
-      hipLaunchKernelGGL((rnn_fwd_rec6<MODE, U, 256>), grid, dim3(NT), lds, s, p); break;
-    case 320: set_lds(rnn_fwd_rec6<MODE, U, 320>, lds);
-      hipLaunchKernelGGL((rnn_fwd_rec6<MODE, U, 320>), grid, dim3(NT), lds, s, p); break;
-    default: set_lds(rnn_fwd_rec6<MODE, U, 512>, lds);
-      hipLaunchKernelGGL((rnn_fwd_rec6<MODE, U, 512>), grid, dim3(NT), lds, s, p); break;
+    case 256: launch6_shape<MODE, U, 256, NTH, P>(fwd, p, grid, lds, s); break;
+    case 320: launch6_shape<MODE, U, 320, NTH, P>(fwd, p, grid, lds, s); break;
+    case 512: launch6_shape<MODE, U, 512, NTH, P>(fwd, p, grid, lds, s); break;
+    case 1024: launch6_shape<MODE, U, 1024, NTH, P>(fwd, p, grid, lds, s); break;
+    default: throw std::logic_error("v6 recurrence: H not compiled");
   }
 }
-static void launch_fwd6(int mode, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
+template <int MODE, int P>
+static void launch6_u(bool fwd, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
+  switch (p.U) {
+    case 8: launch6_h<MODE, 8, 256, P>(fwd, p, grid, lds, s); break;
+    case 16: launch6_h<MODE, 16, 256, P>(fwd, p, grid, lds, s); break;
+    default: launch6_h<MODE, 32, 512, P>(fwd, p, grid, lds, s); break;
+  }
+}
+static void launch6(bool fwd, int mode, int prec, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
   if (mode == kLstm) {
-    if (p.U == 16) launchf6_u<kLstm, 16>(p, grid, lds, s);
-    else launchf6_u<kLstm, 8>(p, grid, lds, s);
+    if (prec == kPrecBf16) launch6_u<kLstm, kPrecBf16>(fwd, p, grid, lds, s);
+    else launch6_u<kLstm, kPrecX3>(fwd, p, grid, lds, s);
   } else {
-    if (p.U == 16) launchf6_u<kGru, 16>(p, grid, lds, s);
-    else launchf6_u<kGru, 8>(p, grid, lds, s);
+    if (prec == kPrecBf16) launch6_u<kGru, kPrecBf16>(fwd, p, grid, lds, s);
+    else launch6_u<kGru, kPrecX3>(fwd, p, grid, lds, s);
   }
 }
 static void launch_rec(bool fwd, int mode, const RecParams &p, dim3 grid, size_t lds, hipStream_t s,
@@ -2089,45 +2185,61 @@ static int pick_bwd_u4(const RnnDesc &d, int N) {
   return 0;
 }
 
-// v6 forward (split-fp16 MFMA, fp16 hi/lo h all-gather): LSTM/GRU, N <= 16,
-// H in {256, 320, 512}, U in {8, 16}
-static size_t fwd6_lds_bytes(const RnnDesc &d, int U) {
-  const int CT = (d.nw() * U + 15) / 16;
-  const size_t b = sizeof(float) * (4 * 16 * (size_t)(CT * 16 + 1) + 8) + 2 * 16 * (size_t)U * 2;
+// v6 recurrences (LSTM / GRU): one configuration for a (shape, N):
+//   rg   row groups of 16 sequences, each an independent recurrence
+//   U    units per workgroup (8, 16 at 256 threads; 32 at 512 threads)
+// chosen so that dirs * (H / U) * rg workgroups (one per CU, >= 96 KB LDS
+// each) stay within KCTC_REC_MAX_WG (default 128: half the chip, the rest
+// for the GEMMs that overlap the recurrences).  Preference U = 16, then 32,
+// then 8 (measured on BLSTM-512 N=16: U=16 34.2 ms/step of forward
+// recurrence, U=8 37.1).  KCTC_FWD_U / KCTC_BWD_U force U.
+struct V6Cfg {
+  int U = 0, nth = 0, rg = 0;
+  explicit operator bool() const { return U > 0; }
+};
+static V6Cfg pick6(const RnnDesc &d, int N, bool fwd) {
+  V6Cfg c;
+  if (env_int(fwd ? "KCTC_FWD_REC" : "KCTC_BWD_REC", 6) != 6 || rec_version() != 4) return c;
+  if ((d.mode != kLstm && d.mode != kGru) || N <= 0 || N > 64 || d.dirs > 2) return c;
+  if (d.H != 256 && d.H != 320 && d.H != 512 && d.H != 1024) return c;
+  const int rg = (N + 15) / 16;
+  const int max_wg = env_int("KCTC_REC_MAX_WG", 128);
+  auto ok = [&](int U) {
+    const int nth = U == 32 ? 512 : 256, nwv = nth / 64;
+    if (d.H % U || d.H % (16 * nwv) || (d.H / U) % (nth / (4 * U))) return false;
+    return (long)d.dirs * (d.H / U) * rg <= std::max(max_wg, d.dirs * (d.H / U));  // rg = 1 always fits
+  };
+  auto take = [&](int U) {
+    c.U = U;
+    c.nth = U == 32 ? 512 : 256;
+    c.rg = rg;
+    return c;
+  };
+  const int want = env_int(fwd ? "KCTC_FWD_U" : "KCTC_BWD_U", 0);
+  if (want) return ok(want) ? take(want) : c;
+  for (int U : {16, 32, 8})
+    if (ok(U)) {
+      // rg = 1 keeps the measured N <= 16 choice even above the budget
+      if (rg == 1 || (long)d.dirs * (d.H / U) * rg <= max_wg) return take(U);
+    }
+  return c;
+}
+static int pick_fwd_u6(const RnnDesc &d, int N) { return pick6(d, N, true).U; }
+static int pick_bwd_u6(const RnnDesc &d, int N) { return pick6(d, N, false).U; }
+
+static size_t fwd6_lds_bytes(const RnnDesc &d, const V6Cfg &c) {
+  const int CT = (d.nw() * c.U + 15) / 16, nwv = c.nth / 64, np = d.prec == kPrecBf16 ? 1 : 2;
+  const size_t b = sizeof(float) * (nwv * 16 * (size_t)(CT * 16 + 1) + 8) + np * 16 * (size_t)c.U * 2 + 16;
   return std::max(b, (size_t)96 * 1024);  // one recurrence workgroup per CU
 }
-static int pick_fwd_u6(const RnnDesc &d, int N) {
-  if (env_int("KCTC_FWD_REC", 6) != 6 || rec_version() != 4) return 0;
-  if ((d.mode != kLstm && d.mode != kGru) || N > 16 || (d.H != 256 && d.H != 320 && d.H != 512)) return 0;
-  auto ok = [&](int U) { return d.H % U == 0 && (long)d.dirs * (d.H / U) <= 256; };
-  const int want = env_int("KCTC_FWD_U", 0);
-  if (want) return ok(want) ? want : 0;
-  // measured on BLSTM-512 N=16: U=16 34.2 ms/step of forward recurrence, U=8 37.1
-  for (int U : {16, 8})
-    if (ok(U)) return U;
-  return 0;
-}
-
-// v6 backward (reduce-scatter, split-fp16 MFMA): LSTM/GRU, N <= 16,
-// H in {256, 320, 512}, U in {16, 8}
-static size_t bwd6_lds_bytes(const RnnDesc &d, int U) {
-  const int K = d.nw() * U, KB = (K + 31) / 32, AP = KB * 32 + 8;
-  const size_t img = 2 * 16 * (size_t)AP * 2;
-  const size_t red = sizeof(float) * std::max((size_t)NT * 4, (size_t)2 * 16 * U * d.nw());
-  const size_t estg = sizeof(float) * 16 * U * d.nw();  // dGates tile staged for write-through
+static size_t bwd6_lds_bytes(const RnnDesc &d, const V6Cfg &c) {
+  const int K = d.nw() * c.U, KB = (K + 31) / 32, AP = KB * 32 + 8;
+  const size_t img = (d.prec == kPrecBf16 ? 1 : 2) * 16 * (size_t)AP * 2;
+  const size_t red = sizeof(float) * std::max((size_t)c.nth * 4, (size_t)2 * 16 * c.U * d.nw());
+  const size_t estg = sizeof(float) * 16 * c.U * d.nw();  // dGates tile staged for write-through
   // at least 96 KB so that no other workgroup (a side-stream GEMM block)
   // shares the CU with a recurrence workgroup
   return std::max(img + red + estg, (size_t)96 * 1024);
-}
-static int pick_bwd_u6(const RnnDesc &d, int N) {
-  if (env_int("KCTC_BWD_REC", 6) != 6 || rec_version() != 4) return 0;
-  if ((d.mode != kLstm && d.mode != kGru) || N > 16 || (d.H != 256 && d.H != 320 && d.H != 512)) return 0;
-  auto ok = [&](int U) { return d.H % U == 0 && (long)d.dirs * (d.H / U) <= 256 && (d.H / U) % (NT / (4 * U)) == 0; };
-  const int want = env_int("KCTC_BWD_U", 0);
-  if (want) return ok(want) ? want : 0;
-  for (int U : {16, 8})
-    if (ok(U)) return U;
-  return 0;
 }
 
 // Per-device exchange pool of the v6 backward: one step image per time step,
@@ -2216,7 +2328,7 @@ void join_stream(hipStream_t s, hipStream_t other) {
 bool chain_ok(const RnnDesc &d, int ver, int T, int N, const RnnFwdChain *c) {
   if (!c || !c->d || !c->side || ver != 6 || d.dirs != 2 || !env_int("KCTC_FWD_STREAM", 1)) return false;
   const RnnDesc &n = *c->d;
-  if (n.D != d.dirs * d.H || !use_x3(n.D) || N > 16) return false;
+  if (n.D != d.dirs * d.H || !use_x3(n.D) || N > 16 || d.prec != kPrecX3 || n.prec != kPrecX3) return false;
   const long xs = 2L * (d.H / 32) * 2 * 16 * 32;  // halves per step image (rnn_fwd_rec6)
   if ((long)T * xs * 2 >= (1L << 31)) return false;
   return c->ws_bytes >= rnn_workspace_bytes(n, T, N) &&
@@ -2277,10 +2389,12 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
   if (res_bytes < sizeof(float) * (size_t)lay.total) return KRNN_BAD_PARAM;
   if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
-  const int U6 = pick_fwd_u6(d, N);
+  const V6Cfg c6 = pick6(d, N, true);
+  const int U6 = c6.U;
   const int U4 = U6 ? 0 : pick_fwd_u4(d, N);
   const int ver = U6 ? 6 : U4 ? 4 : 3;
   const int U = U6 ? U6 : U4 ? U4 : pick_fwd_u(d, N);
+  if (d.prec == kPrecBf16 && ver != 6) return KRNN_NOT_SUPPORTED;  // bf16 exists on v6 only
   if (!U) return KRNN_NOT_SUPPORTED;
   const int NW = d.nw(), H = d.H, dirs = d.dirs;
   const long TN = (long)T * N;
@@ -2341,19 +2455,20 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.allow_local = env_int("KCTC_LOCAL", 0);
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, kFlagBytes, s));
-    const size_t lds = ver == 6 ? fwd6_lds_bytes(d, U) : fwd_lds_bytes(d, N, U);
+    const size_t lds = ver == 6 ? fwd6_lds_bytes(d, c6) : fwd_lds_bytes(d, N, U);
     p.xpd = ver == 4 ? v4_xpd(d, U) : 1;
+    p.rg = ver == 6 ? c6.rg : 1;
     p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
     p.poll_sleep = env_int("KCTC_POLL_SLEEP", 1);
     p.nopf = env_int("KCTC_DIAG_NOPF", 0);
-    const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : dirs * p.nwg);
+    const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : dirs * p.nwg * p.rg);
     RecTrace tr;
     if (tr.arm("fwd", grid.x)) p.trace = tr.dev;
     const bool chained = l == d.layers - 1 && chain_ok(d, ver, T, N, chain);
     const hipEvent_t fork = chained ? fork_event(s) : nullptr;
     {
       ProfSpan ps(s, "rnn_fwd_rec");
-      if (ver == 6) launch_fwd6(d.mode, p, grid, lds, s);
+      if (ver == 6) launch6(true, d.mode, d.prec, p, grid, lds, s);
       else launch_rec(true, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
@@ -2415,10 +2530,12 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
   if (T <= 0 || N <= 0 || N > 16 * kMaxRT || d.H % 16) return KRNN_NOT_SUPPORTED;
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
   if (res_bytes < sizeof(float) * (size_t)lay.total) return KRNN_BAD_PARAM;
-  const int U6 = pick_bwd_u6(d, N);
+  const V6Cfg c6 = pick6(d, N, false);
+  const int U6 = c6.U;
   const int U4 = U6 ? 0 : pick_bwd_u4(d, N);
   const int ver = U6 ? 6 : U4 ? 4 : 3;
   const int U = U6 ? U6 : U4 ? U4 : pick_bwd_u(d, N);
+  if (d.prec == kPrecBf16 && ver != 6) return KRNN_NOT_SUPPORTED;
   if (!U) return KRNN_NOT_SUPPORTED;
   const int NW = d.nw(), H = d.H, dirs = d.dirs;
   const long TN = (long)T * N;
@@ -2446,35 +2563,41 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, kFlagBytes, s));
-    const size_t lds = ver == 6 ? bwd6_lds_bytes(d, U) : bwd_lds_bytes(d, N, U, ver);
+    const size_t lds = ver == 6 ? bwd6_lds_bytes(d, c6) : bwd_lds_bytes(d, N, U, ver);
     p.xpd = ver == 4 ? v4_xpd(d, U) : 1;
+    p.rg = ver == 6 ? c6.rg : 1;
     if (ver == 6) {
       // XCD-slot mapping when a direction's workgroups fit one XCD
       // (measured slower, 37.2 vs 33.6 ms/step of backward recurrence: the 32
       // workgroups of a direction then load 1 MB per step through ONE XCD's
       // fabric port; spread over the XCDs they use four)
-      p.xpd = (p.nwg == kCusPerXcd && dirs <= 8 && env_int("KCTC_XCD6", 0)) ? 1 : 0;
+      p.xpd = (p.nwg == kCusPerXcd && dirs <= 8 && p.rg == 1 && env_int("KCTC_XCD6", 0)) ? 1 : 0;
       p.allow_local = env_int("KCTC_LOCAL", 1);
       p.poll_sleep = env_int("KCTC_POLL_SLEEP", 1);
       p.nopf = env_int("KCTC_DIAG_NOPF", 0);
-      p.xch = xch_acquire(sizeof(float) * (size_t)T * dirs * p.nwg * (16 * H + 64), s);
+      p.xch = xch_acquire(sizeof(float) * (size_t)T * dirs * p.nwg * (16 * H + 64) * p.rg, s);
     } else {
       p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
     }
-    const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : ver == 6 && p.xpd ? 8 * p.nwg : dirs * p.nwg);
+    const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : ver == 6 && p.xpd ? 8 * p.nwg : dirs * p.nwg * p.rg);
     RecTrace tr;
     if (tr.arm("bwd", grid.x)) p.trace = tr.dev;
     // dx_l = sum_dir DX_dir W_dir   (lower layer's dy, or the caller's dx)
     float *dxl = (l == 0) ? dx : res + lay.per_layer * (l - 1) + lay.dout;
     // streamed: computed on `overlap` while the recurrence runs, from its rows as they appear
-    const bool streamed = dxl && overlap && ver == 6 && dirs == 2 && !p.xpd && use_x3(NW * H) && NW * H <= 4096 &&
-                          (long)TN * Din * 4 < (1L << 31) && env_int("KCTC_BWD_STREAM", 1);
+    const bool streamed = dxl && overlap && ver == 6 && dirs == 2 && !p.xpd && p.rg == 1 && d.prec == kPrecX3 &&
+                          use_x3(NW * H) && NW * H <= 4096 && (long)TN * Din * 4 < (1L << 31) &&
+                          env_int("KCTC_BWD_STREAM", 1);
     p.e_sc1 = env_int("KCTC_DIAG_ESC1", streamed ? 1 : 0);  // diagnostic override (0 with streaming: wrong dx)
-    if (ver == 6) p.cmax = pk<unsigned>(workspace, d, T, N, pack_layout(d, T, N).cme);
+    if (ver == 6) {
+      p.cmax = pk<unsigned>(workspace, d, T, N, pack_layout(d, T, N).cme);
+      if (p.rg > 1)  // max over the row groups by atomicMax on the float bits
+        KCTC_HIP_CHECK(hipMemsetAsync(p.cmax, 0, sizeof(unsigned) * 2 * dirs * NW * H, s));
+    }
     const hipEvent_t fork = streamed ? fork_event(s) : nullptr;
     {
       ProfSpan ps(s, "rnn_bwd_rec");
-      if (ver == 6) launch_rec6(d.mode, p, grid, lds, s);
+      if (ver == 6) launch6(false, d.mode, d.prec, p, grid, lds, s);
       else launch_rec(false, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
@@ -2646,11 +2769,14 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     // biases: dbW += sum dGx, dbR += sum dGh (partials from the recurrence)
     const long bW = d.lin_offset(l * dirs, 0, true) - pl0;
     const long bR = d.lin_offset(l * dirs, NW, true) - pl0;
-    for (int dir = 0; dir < dirs; dir++) {
-      const float *part = R0 + lay.bias + (long)dir * 2 * G4;
-      clip_sgd_update(s, dwl + dir * pls + bW, part, G4, 1.f, 0.f);
-      clip_sgd_update(s, dwl + dir * pls + bR, part + G4, G4, 1.f, 0.f);
-    }
+    // (v6: one partial per row group, [group][dir][2][G], added in group order)
+    const int rg = pick_bwd_u6(d, N) ? (N + 15) / 16 : 1;
+    for (int gi = 0; gi < rg; gi++)
+      for (int dir = 0; dir < dirs; dir++) {
+        const float *part = R0 + lay.bias + ((long)gi * dirs + dir) * 2 * G4;
+        clip_sgd_update(s, dwl + dir * pls + bW, part, G4, 1.f, 0.f);
+        clip_sgd_update(s, dwl + dir * pls + bR, part + G4, G4, 1.f, 0.f);
+      }
   }
   return KRNN_OK;
 }

@@ -268,6 +268,17 @@ int kctc_nnet_set_params(kctcNnet_t n, int c, const float *host, long len) {
   });
 }
 
+int kctc_nnet_get_grad(kctcNnet_t n, int c, float *host, long len) {
+  return guarded([&] {
+    n->activate();
+    auto &u = ucomp(n, c);
+    if (len != u.NumParameters()) throw std::invalid_argument("size mismatch");
+    KCTC_HIP_CHECK(hipStreamSynchronize(n->stream));
+    KCTC_HIP_CHECK(hipStreamSynchronize(u.GradStream()));
+    KCTC_HIP_CHECK(hipMemcpy(host, u.GradData(), sizeof(float) * len, hipMemcpyDeviceToHost));
+  });
+}
+
 int kctc_nnet_set_learning_rate(kctcNnet_t n, float lr) {
   return guarded([&] { n->nnet.SetLearningRate(lr); });
 }
@@ -303,6 +314,15 @@ int kctc_nnet_last_best_path(kctcNnet_t n, int *ids, long len) {
     const auto &v = n->trainer.LastBestPath();
     KCTC_REQUIRE(len == (long)v.size(), "kctc_nnet_last_best_path: len != T_max*N of the last minibatch");
     std::copy(v.begin(), v.end(), ids);
+  });
+}
+
+int kctc_nnet_last_costs(kctcNnet_t n, double *costs, int N) {
+  return guarded([&] {
+    KCTC_REQUIRE(n && costs, "null argument");
+    const auto &v = n->trainer.LastCosts();
+    KCTC_REQUIRE(N == (int)v.size(), "kctc_nnet_last_costs: N != minibatch of the last minibatch");
+    std::copy(v.begin(), v.end(), costs);
   });
 }
 

@@ -1,0 +1,117 @@
+"""Full-size parity by sketches (TEST INFRASTRUCTURE).
+
+The fp64 oracle needs minutes for a configs[1]-sized layer or train step, so
+it runs once, here in the build container (tests/golden/make_sketch.py), and
+only a SKETCH of each output tensor is committed (tests/golden/sketch_*.npz):
+its norm, 4 projections onto fixed Gaussian vectors and 256 sampled entries.
+The GPU tests regenerate the identical inputs (numpy PCG64 streams and the
+library's host-side synthetic generator are deterministic across machines),
+run the HIP path and compare sketches.
+
+Why projections: for r ~ N(0, I), E[(r.a - r.b)^2] = |a - b|^2, so
+|r.(y_gpu - y_ref)| / |y_ref| estimates the norm-wise relative error that
+north_star bounds (1e-4), while a localised fault (one wrong row of 2H
+entries among T*N) moves a projection by ~sqrt(2H / (T*N)) >> 1e-4.
+"""
+import numpy as np
+
+NPROJ = 4
+NSAMP = 256
+
+
+def proj_vectors(n, seed):
+    """The k-th projection vector of a tensor of n entries (float32 N(0,1))."""
+    return [np.random.default_rng([seed, k, n]).standard_normal(n, dtype=np.float32) for k in range(NPROJ)]
+
+
+def sample_index(n, seed):
+    return np.random.default_rng([seed, 99, n]).integers(0, n, NSAMP)
+
+
+def sketch(a, seed):
+    """dict(norm, proj[NPROJ], idx[NSAMP], val[NSAMP]) of a flattened tensor."""
+    a = np.ascontiguousarray(a).ravel()
+    a64 = a.astype(np.float64)
+    idx = sample_index(a.size, seed)
+    return {"norm": float(np.linalg.norm(a64)),
+            "proj": np.array([float(np.dot(r.astype(np.float64), a64)) for r in proj_vectors(a.size, seed)]),
+            "idx": idx, "val": a64[idx]}
+
+
+def save(prefix, sk, out):
+    for k, v in sk.items():
+        out[f"{prefix}.{k}"] = np.asarray(v)
+
+
+def load(g, prefix):
+    return {k: g[f"{prefix}.{k}"] for k in ("norm", "proj", "idx", "val")}
+
+
+def compare(a, ref, seed, tol):
+    """Max relative sketch error of tensor a vs the committed sketch ref:
+    max(|norm diff|, max_k |proj diff|) / |ref|, and the sampled entries'
+    max |diff| / rms(ref)."""
+    s = sketch(a, seed)
+    n = np.asarray(a).size
+    den = float(ref["norm"]) or 1.0
+    e_norm = abs(s["norm"] - float(ref["norm"])) / den
+    e_proj = float(np.max(np.abs(s["proj"] - ref["proj"]))) / den
+    rms = den / np.sqrt(n)
+    e_samp = float(np.max(np.abs(s["val"] - ref["val"]))) / rms
+    return {"norm": e_norm, "proj": e_proj, "samp": e_samp, "ok": e_norm < tol and e_proj < tol}
+
+
+# ---- the two workloads --------------------------------------------------------
+# (i) one BLSTM-512 layer at the configs[1] shape, D = 40 (first layer) and
+#     D = 1024 (layers 2-5): recipe init (matrices N(0, 0.02^2), biases 0.2,
+#     nnet-cudnn-component.cc:336-407), x = the synthetic features (D = 40) or
+#     tanh(N(0,1)) (D = 1024, a bounded LSTM output), dy ~ N(0, 1e-2^2).
+LAYER_CASES = {"lstm512_d40": dict(mode=2, T=2000, N=16, D=40, H=512, seed=11),
+               "lstm512_d1024": dict(mode=2, T=2000, N=16, D=1024, H=512, seed=12),
+               # configs[2]: frame_subsampling_factor 3 -> T_max 667, minibatch 64
+               "lstm512_d1024_n64": dict(mode=2, T=667, N=64, D=1024, H=512, seed=13)}
+
+
+def recipe_rnn_params(oracle, mode, D, H, seed, stddev=0.02, bias=0.2):
+    P = oracle.params_size(mode, D, H, 1, 2)
+    w = (np.random.default_rng([seed, 1]).standard_normal(P) * stddev).astype(np.float32)
+    nlin = 2 * (4 if mode == 2 else 3 if mode == 3 else 1)
+    for pl in range(2):
+        for lin in range(nlin):
+            off = oracle.lin_offset(mode, D, H, 1, 2, pl, lin, 1)
+            w[off:off + H] = bias
+    return w
+
+
+def layer_inputs(kctc, oracle, case):
+    c = LAYER_CASES[case]
+    T, N, D, H = c["T"], c["N"], c["D"], c["H"]
+    w = recipe_rnn_params(oracle, c["mode"], D, H, c["seed"])
+    if D == 40:
+        feats, _, _, _ = kctc.synth_minibatch(c["seed"], T, N, D, 41, 0.125)
+        x = feats.reshape(T, N, D)
+    else:
+        x = np.tanh(np.random.default_rng([c["seed"], 2]).standard_normal((T, N, D))).astype(np.float32)
+    dy = (np.random.default_rng([c["seed"], 3]).standard_normal((T, N, 2 * H)) * 1e-2).astype(np.float32)
+    return w, x, dy
+
+
+# (ii) one configs[1] train step (bench.py's first minibatch, seed 20161015):
+#      5 x BLSTM-512, N=16, T_max=2000, lr 5e-4; recipe init, affine
+#      N(0, 1/1024) / N(0, 1) (nnet-component.cc:1169-1174).
+STEP = dict(T=2000, N=16, D=40, H=512, A=41, R=5, lr=5e-4, seed=20161015, pseed=77)
+
+
+def step_params(oracle):
+    s = STEP
+    rnn = [recipe_rnn_params(oracle, 2, s["D"] if c == 0 else 2 * s["H"], s["H"], s["pseed"] + c)
+           for c in range(s["R"])]
+    rng = np.random.default_rng([s["pseed"], 9])
+    Wa = (rng.standard_normal((s["A"], 2 * s["H"])) / np.sqrt(2 * s["H"])).astype(np.float32)
+    ba = rng.standard_normal(s["A"]).astype(np.float32)
+    return rnn, Wa, ba
+
+
+def step_inputs(kctc):
+    s = STEP
+    return kctc.synth_minibatch(s["seed"], s["T"], s["N"], s["D"], s["A"], 0.125)

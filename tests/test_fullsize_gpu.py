@@ -1,0 +1,109 @@
+"""configs[1] at full length on the GPU vs the fp64 oracle, by sketches
+(tests/sketch_common.py; fixtures from tests/golden/make_sketch.py).
+
+(i)  one BLSTM-512 layer, T=2000, N=16, D=40 and D=1024: y, dx, dW
+(ii) one 5 x BLSTM-512 train step of bench.py's first minibatch: per-utterance
+     costs, network output, every component's applied gradient (+-5 clipped
+     for the RNNs), and the best path bit for bit against _find_row_max_id of
+     the GPU's own output.
+
+Tolerance: norm-wise relative 1e-4 (north_star: "loss/grads within 1e-4 rel
+of reference"), estimated by the projections (sketch_common.compare); the
+recurrences run on the split-fp16 path, so this is what pins
+its drift over 2000 serial steps."""
+import numpy as np
+import pytest
+
+import sketch_common as S
+from conftest import golden
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
+TOL = 1e-4
+
+
+@pytest.mark.parametrize("case", sorted(S.LAYER_CASES))
+def test_layer_full_length_matches_oracle(kctc, gpu, oracle, case):
+    import torch
+    g = golden("sketch_layers")
+    c = S.LAYER_CASES[case]
+    T, N, D, H = c["T"], c["N"], c["D"], c["H"]
+    w, x, dy = S.layer_inputs(kctc, oracle, case)
+    r = kctc.Rnn(c["mode"], D, H, 1, True)
+    ws_b, res_b = r.sizes(T, N)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+    wd, xd, dyd = t(w), t(x), t(dy)
+    y = torch.empty((T, N, 2 * H), device=gpu)
+    dx = torch.empty((T, N, D), device=gpu)
+    dw = torch.zeros(r.num_params, device=gpu)
+    ws = torch.empty(ws_b, dtype=torch.uint8, device=gpu)
+    res = torch.empty(res_b, dtype=torch.uint8, device=gpu)
+    r.forward_training(xd, wd, y, ws, res)
+    r.backward_data(y, dyd, wd, dx, ws, res)
+    r.backward_weights(xd, y, dw, ws, res)
+    torch.cuda.synchronize()
+    assert r.device_status() == 0
+    y, dx, dw = y.cpu().numpy(), dx.cpu().numpy(), dw.cpu().numpy()
+    seed = c["seed"]
+    errs = {"y": S.compare(y, S.load(g, f"{case}.y"), seed, TOL),
+            "dx": S.compare(dx, S.load(g, f"{case}.dx"), seed + 1, TOL),
+            "dw": S.compare(dw, S.load(g, f"{case}.dw"), seed + 2, TOL)}
+    print(case, {k: {kk: f"{vv:.2e}" for kk, vv in v.items() if kk != "ok"} for k, v in errs.items()})
+    for k, e in errs.items():
+        assert e["ok"], (k, e)
+    # every dW region (W, R, bW, bR of both directions) keeps its norm
+    regs = []
+    for pl in range(2):
+        for lin in range(8):
+            for isb in (0, 1):
+                off, (h, cc) = r.lin_offset(pl, lin, isb)
+                regs.append(np.linalg.norm(dw[off:off + h * cc].astype(np.float64)))
+    ref = g[f"{case}.dw_region_norms"]
+    np.testing.assert_allclose(regs, ref, rtol=TOL)
+    np.testing.assert_allclose(y[0, :, :H], g[f"{case}.y_t0_fwd"], rtol=1e-5, atol=1e-6)
+
+
+def test_train_step_full_size_matches_oracle(kctc, gpu, oracle):
+    import torch
+    g = golden("sketch_step")
+    s = S.STEP
+    T, N, D, H, A, R = s["T"], s["N"], s["D"], s["H"], s["A"], s["R"]
+    rnn, Wa, ba = S.step_params(oracle)
+    feats, nf, fl, ll = S.step_inputs(kctc)
+    net = kctc.Nnet(kctc.recipe_config(num_rnn=R, input_dim=D, hidden=H, num_targets=A, learning_rate=s["lr"],
+                                       max_seq_length=T), seed=1)
+    rnn_idx = [1 + 2 * c for c in range(R)]
+    aff_idx = 2 * R + 1
+    for c, i in enumerate(rnn_idx):
+        net.set_params(i, rnn[c])
+    net.set_params(aff_idx, np.concatenate([Wa.ravel(), ba]))
+    net.srand(0)
+    objf, acc, wt = net.train_step(torch.from_numpy(feats).to(gpu), T, N, nf, fl, ll)
+    costs = net.last_costs(N)
+    np.testing.assert_allclose(costs, g["costs"], rtol=TOL)
+    np.testing.assert_allclose(objf, float(g["tot_objf"]), rtol=TOL)
+    assert wt == float(g["tot_weight"])
+    logits = net.last_output(T, N, A)
+    e = S.compare(logits, S.load(g, "logits"), 500, TOL)
+    assert e["ok"], ("logits", e)
+    # best path: bit-exact on the GPU's own output; vs the fp64 output only
+    # near-ties may flip
+    ids = net.last_best_path(T, N)
+    np.testing.assert_array_equal(ids, oracle.find_row_max_id(logits))
+    assert acc == oracle.accuracy(ids, T, N, nf, fl, ll)[0]
+    flips = int(np.sum(ids != g["ids"]))
+    assert flips <= 1e-3 * ids.size, flips
+    # the applied gradients (the fp32 parameters cannot carry an lr-scaled
+    # update exactly: compare the gradient the update used, +-5 clipped for
+    # the RNNs, against the oracle's fp64 (W_after - W_before) / lr)
+    report = {}
+    for c, i in enumerate(rnn_idx):
+        gc = np.clip(net.get_grad(i).astype(np.float64), -5.0, 5.0)
+        report[f"rnn{c}"] = S.compare(gc, S.load(g, f"g{c}"), 600 + c, TOL)
+    report["affine"] = S.compare(net.get_grad(aff_idx).astype(np.float64), S.load(g, "gaff"), 700, TOL)
+    print({k: {kk: f"{vv:.2e}" for kk, vv in v.items() if kk != "ok"} for k, v in report.items()},
+          "flips", flips)
+    for k, e in report.items():
+        assert e["ok"], (k, e)
+    for i, (ncl, cnt) in enumerate(net.clip_stats(1 + 2 * c + 1) for c in range(R)):
+        assert cnt == g["clip_count"][i] and ncl == g["clip_num_clipped"][i]
+    net.close()

@@ -54,6 +54,15 @@ CASES = [
     (2, 16, 5, 48, 320, 1, False),   # uni LSTM H=320 (the recipe's cell dim)
     (3, 12, 16, 40, 512, 2, True),   # stacked BGRU-512
     (2, 30, 1, 40, 256, 1, True),    # a single utterance
+    # v6 row groups (N > 16: independent recurrences per 16 sequences)
+    (2, 24, 64, 40, 512, 1, True),   # configs[2] width: 4 groups, U=32 on 512-thread workgroups
+    (2, 18, 32, 64, 512, 1, True),   # 2 groups, U=16
+    (3, 20, 33, 48, 256, 1, True),   # 3 groups, ragged last group (1 row)
+    (3, 15, 45, 24, 512, 2, True),   # stacked, 3 groups
+    (2, 14, 20, 16, 256, 1, False),  # uni, 2 groups
+    # H = 1024 (configs[4] width)
+    (3, 12, 8, 40, 1024, 1, True),   # one group, U=16
+    (3, 10, 32, 40, 1024, 1, True),  # 2 groups, U=32 on 512-thread workgroups
 ]
 
 

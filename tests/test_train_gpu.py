@@ -107,6 +107,34 @@ def test_train_steps_match_oracle(kctc, gpu, oracle, mode, H, thr, steps, pstd):
         assert cnt == cc[i] and ncl == cnc[i]
 
 
+@pytest.mark.parametrize("mode,H,T,N", [(2, 256, 24, 40), (3, 512, 16, 64), (2, 512, 20, 33)])
+def test_train_step_row_groups_match_oracle(kctc, gpu, oracle, mode, H, T, N):
+    """N > 16: the v6 recurrences run one independent recurrence per group of
+    16 sequences (bias partial sums per group added in order, dGates column
+    maxima combined by atomicMax); the GEMMs are not streamed."""
+    import torch
+    R, D, A, lr = 2, 24, 11, 0.02
+    cfg = kctc.recipe_config(num_rnn=R, input_dim=D, hidden=H, num_targets=A, rnn_mode=mode,
+                             learning_rate=lr, param_stddev=0.1 * np.sqrt(64 / H))
+    net = kctc.Nnet(cfg, seed=15)
+    upd = [c for c in range(net.num_components) if net.num_params(c) > 0]
+    params = [net.get_params(c).astype(np.float64) for c in upd]
+    spec = _oracle_spec(oracle, R, mode, H, 2, D, A, 30.0, lr)
+    feats, nf, fl, ll = kctc.synth_minibatch(77, T, N, D, A, 0.2)
+    objf, acc, wt = net.train_step(torch.from_numpy(feats).to(gpu), T, N, nf, fl, ll)
+    Wa = params[-1][:-A].reshape(A, -1).copy()
+    ba = params[-1][-A:].copy()
+    robjf, racc, rwt = oracle.train_step(spec, params[:-1], Wa, ba, feats.reshape(T, N, D).astype(np.float64),
+                                         nf, fl, ll, repair_draws=np.ones(R, np.float32))
+    params[-1] = np.concatenate([Wa.ravel(), ba])
+    np.testing.assert_allclose(objf, robjf, rtol=1e-5)
+    assert wt == rwt
+    ids = net.last_best_path(T, N)
+    np.testing.assert_array_equal(ids, oracle.find_row_max_id(net.last_output(T, N, A)))
+    for c, p in zip(upd, params):
+        assert rel_err(net.get_params(c).astype(np.float64), p) < 1e-5, c
+
+
 def test_train_loss_decreases_and_objf_only(kctc, gpu):
     import torch
     D, A, T, N = 40, 41, 120, 8
