@@ -45,6 +45,9 @@ CONFIGS = {
     2: dict(T=667, N=64, H=512, mode=2, ratio=0.375, fs=3,
             name="configs[2]: librispeech CTC-monophone 5xBLSTM-512, fs=3 (google config), minibatch=64/GPU, "
                  "T_max=667, fp32"),
+    4: dict(T=2000, N=32, H=1024, mode=3, ratio=0.125, fs=1, prec="bf16",
+            name="configs[4]: 5xBGRU-1024, bf16 recurrences and MFMA gate GEMMs (fp32 accumulation, fp32 "
+                 "master weights), minibatch=32/GPU, T_max=2000"),
 }
 
 
@@ -89,7 +92,7 @@ def pmc_traffic(kernel):
     return None, None
 
 
-def cpu_baseline(T, D, H, A, L, steps_seed, ratio=0.125):
+def cpu_baseline(T, D, H, A, L, steps_seed, ratio=0.125, mode=2, Ns=4):
     """The oracle's fp32 restatement (warp-ctc-CPU-style CTC + blocked-GEMM
     LSTM/affine, OpenMP) on a bounded sample: 4 utterances of the same shape
     (about 7 s of CPU work, so it does not dominate the bench's lease)."""
@@ -97,14 +100,13 @@ def cpu_baseline(T, D, H, A, L, steps_seed, ratio=0.125):
     import oracle_lib as O
     import __graft_entry__ as ge
     k = ge.load_package()
-    Ns = 4
     s = O.NnetSpec()
-    s.num_rnn, s.mode, s.hidden, s.dirs, s.layers_per_rnn = L, 2, H, 2, 1
+    s.num_rnn, s.mode, s.hidden, s.dirs, s.layers_per_rnn = L, mode, H, 2, 1
     s.input_dim, s.num_targets = D, A
     s.clip_threshold, s.repair_threshold, s.repair_scale, s.repair_target = 30.0, 0.01, 1.0, 0.0
     s.rnn_clip_gradient, s.lr_rnn, s.lr_affine = 5.0, 5e-4, 5e-4
     rng = np.random.default_rng(0)
-    ps = [(rng.standard_normal(O.params_size(2, D if i == 0 else 2 * H, H, 1, 2)) * 0.02).astype(np.float32)
+    ps = [(rng.standard_normal(O.params_size(mode, D if i == 0 else 2 * H, H, 1, 2)) * 0.02).astype(np.float32)
           for i in range(L)]
     Wa = (rng.standard_normal((A, 2 * H)) / np.sqrt(2 * H)).astype(np.float32)
     ba = rng.standard_normal(A).astype(np.float32)
@@ -114,7 +116,7 @@ def cpu_baseline(T, D, H, A, L, steps_seed, ratio=0.125):
     dt = time.time() - t0
     return {"value": float(nf.sum() / dt), "unit": "frames/s", "cores": int(O.lib().oracle_num_threads()),
             "kind": "port",
-            "sample": f"one full train step (5xBLSTM-512 fwd+CTC+bwd+SGD, fp32) on {Ns} utterances "
+            "sample": f"one full train step ({L}x{'BLSTM' if mode == 2 else 'BGRU'}-{H} fwd+CTC+bwd+SGD, fp32) on {Ns} utterances "
                       f"x T_max={T} ({int(nf.sum())} frames) in {dt:.1f}s"}
 
 
@@ -153,6 +155,10 @@ def main():
     cfg = k.recipe_config(num_rnn=L, input_dim=D, hidden=H, num_targets=A, learning_rate=5e-4,
                           max_seq_length=T, rnn_mode=mode)
     net = k.Nnet(cfg, seed=20161015, device=local)  # same init on every rank
+    bf16 = cf.get("prec") == "bf16"
+    if bf16:
+        net.set_precision("bf16")
+    peak_mfma = PEAK_F16_TFLOPS if bf16 else PEAK_FP32_TFLOPS
     if world > 1:
         uid = k.dp_unique_id() if rank == 0 else bytes(128)
         obj = [uid]
@@ -215,6 +221,9 @@ def main():
     acc = sum(a for _, a, _ in stats)
     wt = sum(w for _, _, w in stats)
     fam_flops, _ = model_flops(T, N, D, H, A, L, nw=nw)
+    if args.config != 1:
+        # the committed PMC traffic was measured on configs[1]
+        globals()["pmc_traffic"] = lambda kernel: (None, None)
     prof = {}
     if profile:
         # *_stream / x3_pack_chain / x3_pack_bwd_stream: GEMMs and packs on the
@@ -254,19 +263,25 @@ def main():
         # the recurrences multiply on the split-fp16 (x3) path: priced against
         # the fp32 MFMA peak (the precision class they deliver) and, as
         # issue_frac, against what the f16 engine they run on could do
-        roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic, "traffic_source": tsrc,
+        roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak_mfma, "unit": "TFLOP/s",
+                "frac": round(achieved / peak_mfma, 4), "traffic": traffic, "traffic_source": tsrc,
                 "kernel": dom,
                 "avg_launch_ms": round(ms / n, 4),
                 "flops_per_launch": flops_per_launch,
-                "issue_frac_x3_on_f16": round(achieved / PEAK_X3_TFLOPS, 4),
+                "issue_frac_x3_on_f16": None if bf16 else round(achieved / PEAK_X3_TFLOPS, 4),
                 "families_ms_per_step": {f: round(prof[f][0] / args.steps, 3) for f in prof}}
         aux = {}
         # the input projections and dx GEMMs of layers 2..L stream off the
         # recurrences (no kernel time of their own to price); the weight-gradient
         # GEMM dW = dGates^T [x | 1] is the same packed split-fp16 kernel, timed
         # on its own (side stream); its ceiling is the f16 engine / 3
-        if "gemm_bwd_w" in prof:
+        if "gemm_bwd_w" in prof and bf16:
+            ms_g, n_g = prof["gemm_bwd_w"]
+            tf = fam_flops["gemm_bwd_w"] * args.steps / (ms_g / 1e3) / 1e12
+            aux["gate_gemm"] = {"bound": "mfma", "kernel": "gemm_bwd_w (gemm_x3p, bf16 operands)",
+                                "achieved": round(tf, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
+                                "frac": round(tf / PEAK_F16_TFLOPS, 4)}
+        elif "gemm_bwd_w" in prof:
             ms_g, n_g = prof["gemm_bwd_w"]
             tf = fam_flops["gemm_bwd_w"] * args.steps / (ms_g / 1e3) / 1e12
             aux["gate_gemm"] = {"bound": "mfma", "kernel": "gemm_bwd_w (gemm_x3p, split-fp16)", "achieved": round(tf, 2),
@@ -290,14 +305,14 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(T, D, H, A, L, 20161015, ratio)
+        cpu = cpu_baseline(T, D, H, A, L, 20161015, ratio, mode=mode, Ns=2 if H > 512 else 4)
 
     if rank == 0:
         value = frames / dt
         fpf = step_flops_per_frame(D, H, A, L, nw=nw)
         out = {"metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2),
-               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if bf16 else "f32",
                "data": f"synthetic (BASELINE.md generator: N(0,1) 40-dim features, T_n=T_max-floor(u*0.1*T_max), "
                        f"L_n=floor(T_n*{ratio}) labels in [1,40]); random-init weights (recipe init)",
                "config": {"workload": cf["name"] if (T, N, H) == (cf["T"], cf["N"], cf["H"]) else
@@ -311,7 +326,7 @@ def main():
                # whole train step against the fp32 MFMA peak (algorithmic
                # FLOPs/frame x frames/s; BASELINE.md's whole-step fraction)
                "step_roofline": {"flops_per_frame": fpf, "achieved_tflops": round(value * fpf / 1e12, 2),
-                                 "peak": PEAK_FP32_TFLOPS, "frac": round(value * fpf / 1e12 / PEAK_FP32_TFLOPS, 4)},
+                                 "peak": peak_mfma, "frac": round(value * fpf / 1e12 / peak_mfma, 4)},
                "loss": {"objf_per_label": round(objf / max(wt, 1), 4), "accuracy": round(acc / max(wt, 1), 4)},
                "roofline": roof, "cpu_baseline": cpu}
         if h2d:

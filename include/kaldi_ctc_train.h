@@ -138,6 +138,12 @@ int kctc_nnet_enable_dp(kctcNnet_t nnet, const void *uid128, int rank, int world
 typedef void (*kctc_host_allreduce_fn)(float *buf, long n, void *user);
 int kctc_nnet_enable_dp_host(kctcNnet_t nnet, kctc_host_allreduce_fn allreduce, void *user, int world_size);
 
+/* Arithmetic of every CuDNNRecurrentComponent's recurrences and gate GEMMs:
+ * 0 fp32-class (default), 1 bf16 operands with fp32 accumulation and fp32
+ * master weights (BASELINE configs[4]).  Affine, CTC and the updates stay
+ * fp32; model files are unaffected. */
+int kctc_nnet_set_precision(kctcNnet_t nnet, int precision);
+
 /* TrainNnetSimple momentum (src/ctc/ctc-nnet-train.cc:194-245, config
  * ctc-nnet-train.h:33-66): with m != 0 every update goes to a delta copy
  * (delta += lr * clip(grad); params += delta; delta *= m) and ClipGradient

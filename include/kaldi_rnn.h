@@ -59,6 +59,12 @@ typedef struct krnnContext *krnnDescriptor_t;
 int krnnCreate(krnnDescriptor_t *desc, int mode, int input_dim, int hidden_dim, int num_layers,
                int bidirectional);
 int krnnDestroy(krnnDescriptor_t desc);
+/* Arithmetic of the recurrences and gate GEMMs (an extension; cuDNN 5 has
+ * no such switch): KRNN_PREC_FP32 (default) -- fp32-class products (split-fp16
+ * pairs, fp32 accumulation); KRNN_PREC_BF16 -- bf16 operands, fp32
+ * accumulation and master weights (LSTM / GRU only, BASELINE configs[4]). */
+enum { KRNN_PREC_FP32 = 0, KRNN_PREC_BF16 = 1 };
+int krnnSetPrecision(krnnDescriptor_t desc, int precision);
 const char *krnnGetStatusString(int status);
 
 /* bytes of the opaque weight buffer (cudnnGetRNNParamsSize) */

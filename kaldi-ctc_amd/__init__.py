@@ -182,6 +182,10 @@ class Rnn:
                                      1 if bidirectional else 0), "krnnCreate")
         self.h = h
 
+    def set_precision(self, prec):
+        """krnnSetPrecision: 0 fp32-class, 1 (or "bf16") bf16 operands."""
+        _krnn_check(lib().krnnSetPrecision(self.h, 1 if prec in (1, "bf16") else 0), "krnnSetPrecision")
+
     def __del__(self):
         try:
             if self.h:
@@ -467,6 +471,12 @@ class Nnet:
         ms, n = ctypes.c_double(), ctypes.c_int()
         _tcheck(lib().kctc_nnet_profile(self.h, family.encode(), ctypes.byref(ms), ctypes.byref(n)), "profile")
         return ms.value, n.value
+
+    def set_precision(self, prec):
+        """0: fp32-class recurrences / gate GEMMs (default); 1 or "bf16": bf16
+        operands, fp32 accumulation (kctc_nnet_set_precision)."""
+        prec = 1 if prec in (1, "bf16") else 0
+        _tcheck(lib().kctc_nnet_set_precision(self.h, prec), "set_precision")
 
     def set_momentum(self, m):
         _tcheck(lib().kctc_nnet_set_momentum(self.h, float(m)), "set_momentum")

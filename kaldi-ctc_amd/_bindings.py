@@ -69,6 +69,8 @@ SIGS = {
     "kctc_nnet_enable_dp": (ci, [vp, vp, ci, ci]),
     "kctc_nnet_enable_dp_host": (ci, [vp, vp, vp, ci]),
     "kctc_nnet_set_momentum": (ci, [vp, cf]),
+    "kctc_nnet_set_precision": (ci, [vp, ci]),
+    "krnnSetPrecision": (ci, [vp, ci]),
     "kctc_nnet_train_simple": (ci, [vp, vp, cl, ctypes.POINTER(cl), ctypes.POINTER(cd), ctypes.POINTER(cd),
                                     ctypes.POINTER(cd)]),
     "kctc_levenshtein": (ci, [vp, ci, vp, ci]),

@@ -71,8 +71,18 @@ struct X3PArgs {
   int stream_nwg = 0, stream_T = 0, stream_N = 0;
   long stream_step = 0;              // halves per producer step image (A = image of step 0)
   unsigned *stream_err = nullptr;    // set (bit 2) if the producer stops publishing
+  // bf16 operands (bf16_pack_rows / _cols: [rows][KB][64] bf16, KB = 64-k
+  // blocks, no exponents): two v_mfma_f32_16x16x32_bf16 per stage, fp32
+  // accumulation; not with streaming
+  bool bf16 = false;
 };
 void gemm_x3p(hipStream_t s, const X3PArgs &g);
+// bf16-packed operands for gemm_x3p(bf16): rows (out[b][r][KB][64], KB =
+// ceil(K / 64)) and columns (the transpose, source row k - shift), zero pad
+void bf16_pack_rows(hipStream_t s, const float *X, long ldx, int R, int K, __bf16 *out, int batch = 1, long sX = 0,
+                    long sOut = 0);
+void bf16_pack_cols(hipStream_t s, const float *X, long ldx, int R, int Cn, int shift, __bf16 *out, int batch = 1,
+                    long sX = 0, long sOut = 0);
 
 // C = sum over the two directions d of A_d B_d^T, where A_d = columns
 // [d * edoff, d * edoff + 32 KB) of the rows of E, produced step by step by a

@@ -35,6 +35,8 @@ constexpr unsigned long long kWaitTicks = 300000000ull;  // streaming waits: 3 s
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 typedef _Float16 halfx4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 struct PParams {
   const _Float16 *A, *B;
@@ -293,7 +295,10 @@ __device__ __forceinline__ void bwd_combine(const PParams &p, floatx4 (&acc)[4][
 // exchange images (sc1 register loads); 2 packed A just written by other CUs
 // (LDS-DMA with sc1, exponents read with sc1) and the two-direction combine
 // epilogue of the backward stream.
-template <int SM>
+// BFM: the operands are bf16-packed ([row][KB][64] bf16, 64 consecutive k per
+// 128-B block): a stage is two v_mfma_f32_16x16x32_bf16 (chunks fq and 4 + fq)
+// instead of the three split-fp16 products, no exponents.
+template <int SM, bool BFM = false>
 __device__ __forceinline__ void x3p_tile(const PParams &p, unsigned char *lds, int tm, int tn, int b, int ks, int *prog) {
   constexpr bool STREAM = SM == 1;
   const _Float16 *A = p.A + (long)b * p.sA;
@@ -348,18 +353,33 @@ __device__ __forceinline__ void x3p_tile(const PParams &p, unsigned char *lds, i
       bh[j] = frag(cur + TILEB, wn + j * 16 + fr, fq);
       bl[j] = frag(cur + TILEB, wn + j * 16 + fr, 4 + fq);
     }
+    if constexpr (BFM) {
 #pragma unroll
-    for (int i = 0; i < 4; i++)
+      for (int i = 0; i < 4; i++)
 #pragma unroll
-      for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; j++)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ah[i]),
+                                                              __builtin_bit_cast(bf16x8, bh[j]), acc[i][j], 0, 0, 0);
 #pragma unroll
-    for (int i = 0; i < 4; i++)
+      for (int i = 0; i < 4; i++)
 #pragma unroll
-      for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; j++)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al[i]),
+                                                              __builtin_bit_cast(bf16x8, bl[j]), acc[i][j], 0, 0, 0);
+    } else {
 #pragma unroll
-    for (int i = 0; i < 4; i++)
+      for (int i = 0; i < 4; i++)
 #pragma unroll
-      for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+    }
     if ((STREAM || SM == 2) && it + 1 < nk) store_tile_lds(nxt, ra);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -441,7 +461,7 @@ __device__ __forceinline__ void decode_tile(const PParams &p, int id, int total,
   b = bz % p.batch; ks = bz / p.batch;
 }
 
-template <bool STREAM>
+template <bool STREAM, bool BFM = false>
 __global__ __launch_bounds__(NTH, 2) void gemm_x3p_kernel(PParams p) {
   // ONE shared array (a second __shared__ object can make hipcc wait vmcnt(0)
   // before LDS reads while a DMA is in flight); streaming launches ask for
@@ -467,7 +487,7 @@ __global__ __launch_bounds__(NTH, 2) void gemm_x3p_kernel(PParams p) {
         x3p_tile<1>(p, lds, tm, tn, b, 0, prog);
       } else {
         decode_tile(p, id, total, false, tm, tn, b, ks);
-        x3p_tile<0>(p, lds, tm, tn, b, ks, prog);
+        x3p_tile<0, BFM>(p, lds, tm, tn, b, ks, prog);
       }
     }
     return;
@@ -476,7 +496,7 @@ __global__ __launch_bounds__(NTH, 2) void gemm_x3p_kernel(PParams p) {
     for (int id = blockIdx.x; id < total; id += gridDim.x) {
       int tm, tn, b, ks;
       decode_tile(p, id, total, true, tm, tn, b, ks);
-      x3p_tile<0>(p, lds, tm, tn, b, ks, prog);
+      x3p_tile<0, BFM>(p, lds, tm, tn, b, ks, prog);
     }
   }
 }
@@ -685,7 +705,89 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
   if (kb == 0 && part == 0 && eout) eout[(long)b * sE + c0 + c] = e;
 }
 
+// bf16 packing: out[b][r][kb][64] = bf16(x[r][64 kb + j]), zero past K.
+// Rows: one wave per row, lane l holds k = 4 l + 256 i.
+template <int KW>
+__global__ __launch_bounds__(256) void bf16_pack_rows_kernel(const float *__restrict__ X, long ldx, int R, int K,
+                                                             int KB, long sX, __bf16 *__restrict__ out, long sOut,
+                                                             int vec) {
+  const int b = blockIdx.y;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= R) return;
+  const float *x = X + (long)b * sX + (long)r * ldx;
+  __bf16 *o = out + (long)b * sOut + (long)r * KB * 64;
+#pragma unroll
+  for (int i = 0; i < KW; i++) {
+    const int k = 4 * lane + 256 * i;
+    if (k >= KB * 64) continue;
+    floatx4 t = {0.f, 0.f, 0.f, 0.f};
+    if (vec && k + 3 < K) {
+      t = *reinterpret_cast<const floatx4 *>(x + k);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; j++) t[j] = k + j < K ? x[k + j] : 0.f;
+    }
+    bf16x4 h;
+#pragma unroll
+    for (int j = 0; j < 4; j++) h[j] = (__bf16)t[j];
+    *reinterpret_cast<bf16x4 *>(o + k) = h;
+  }
+}
+// Columns (transpose): packed row c = column c of X over its R rows (row
+// k - shift, zero outside).  Block: 64 columns x one 64-k block.
+__global__ __launch_bounds__(256) void bf16_pack_cols_kernel(const float *__restrict__ X, long ldx, int R, int Cn,
+                                                             int KB, int shift, long sX, __bf16 *__restrict__ out,
+                                                             long sOut) {
+  __shared__ float tile[64][65];
+  const int b = blockIdx.z, c0 = blockIdx.x * 64, kb = blockIdx.y;
+  const float *x = X + (long)b * sX;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const int kr = (t >> 6) + 4 * i, cc = t & 63;
+    const int src = kb * 64 + kr - shift;
+    float v = 0.f;
+    if (kb * 64 + kr < R && src >= 0 && src < R && c0 + cc < Cn) v = x[(long)src * ldx + c0 + cc];
+    tile[kr][cc] = v;
+  }
+  __syncthreads();
+  const int c = t >> 2, part = t & 3;
+  if (c0 + c >= Cn) return;
+  __bf16 *o = out + (long)b * sOut + ((long)(c0 + c) * KB + kb) * 64 + part * 16;
+  bf16x8 h0, h1;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    h0[j] = (__bf16)tile[part * 16 + j][c];
+    h1[j] = (__bf16)tile[part * 16 + 8 + j][c];
+  }
+  *reinterpret_cast<bf16x8 *>(o) = h0;
+  *reinterpret_cast<bf16x8 *>(o + 8) = h1;
+}
+
 }  // namespace
+
+void bf16_pack_rows(hipStream_t s, const float *X, long ldx, int R, int K, __bf16 *out, int batch, long sX,
+                    long sOut) {
+  if (R <= 0 || K <= 0 || batch <= 0) return;
+  const int KB = (K + 63) / 64;
+  const int vec = ((uintptr_t)X % 16 == 0) && (ldx % 4 == 0) && (sX % 4 == 0);
+  const dim3 grid(ceil_div(R, 4), batch);
+  const int need = KB * 64;
+  if (need <= 256) hipLaunchKernelGGL(bf16_pack_rows_kernel<1>, grid, dim3(256), 0, s, X, ldx, R, K, KB, sX, out, sOut, vec);
+  else if (need <= 512) hipLaunchKernelGGL(bf16_pack_rows_kernel<2>, grid, dim3(256), 0, s, X, ldx, R, K, KB, sX, out, sOut, vec);
+  else if (need <= 1024) hipLaunchKernelGGL(bf16_pack_rows_kernel<4>, grid, dim3(256), 0, s, X, ldx, R, K, KB, sX, out, sOut, vec);
+  else if (need <= 2048) hipLaunchKernelGGL(bf16_pack_rows_kernel<8>, grid, dim3(256), 0, s, X, ldx, R, K, KB, sX, out, sOut, vec);
+  else if (need <= 4096) hipLaunchKernelGGL(bf16_pack_rows_kernel<16>, grid, dim3(256), 0, s, X, ldx, R, K, KB, sX, out, sOut, vec);
+  else throw std::invalid_argument("bf16_pack_rows: K > 4096");
+}
+
+void bf16_pack_cols(hipStream_t s, const float *X, long ldx, int R, int Cn, int shift, __bf16 *out, int batch, long sX,
+                    long sOut) {
+  if (R <= 0 || Cn <= 0 || batch <= 0) return;
+  const int KB = (R + 63) / 64;
+  hipLaunchKernelGGL(bf16_pack_cols_kernel, dim3(ceil_div(Cn, 64), KB, batch), dim3(256), 0, s, X, ldx, R, Cn, KB,
+                     shift, sX, out, sOut);
+}
 
 void x3p_pack_rows(hipStream_t s, const float *X, long ldx, int R, int K, _Float16 *out, int *eout, float bound,
                    int batch, long sX, long sOut, long sE) {
@@ -737,11 +839,16 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
   if (!attr) {
     KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_x3p_kernel<false>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBase));
+    KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_x3p_kernel<false, true>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBase));
     KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_x3p_kernel<true>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsStream));
     attr = true;
   }
-  if (p.sflags) {
+  if (g.bf16) {
+    if (p.sflags || p.eA || p.eB) throw std::invalid_argument("gemm_x3p: bf16 operands take no exponents / streaming");
+    hipLaunchKernelGGL((gemm_x3p_kernel<false, true>), dim3(blocks), dim3(NTH), kLdsBase, s, p);
+  } else if (p.sflags) {
     if (!p.counter || p.split > 1 || g.stream_N <= 0 || g.stream_step <= 0 ||
         (long)g.stream_T * g.stream_step * 2 >= (1L << 31))
       throw std::invalid_argument("gemm_x3p: bad streaming arguments");
@@ -750,8 +857,9 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
     const int sb = std::min(stream_total(p), g.max_blocks > 0 ? g.max_blocks : 176);
     hipLaunchKernelGGL(gemm_x3p_kernel<true>, dim3(sb), dim3(NTH), kLdsStream, s, p);
     return;
+  } else {
+    hipLaunchKernelGGL(gemm_x3p_kernel<false>, dim3(blocks), dim3(NTH), kLdsBase, s, p);
   }
-  hipLaunchKernelGGL(gemm_x3p_kernel<false>, dim3(blocks), dim3(NTH), kLdsBase, s, p);
   if (p.split > 1) {
     const long tot = (long)p.batch * p.M * p.N;
     hipLaunchKernelGGL(x3p_splitk_reduce, dim3((int)std::min<long>(2048, (tot + 255) / 256)), dim3(256), 0, s, p);

@@ -230,6 +230,13 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   // backward recurrence (KCTC_SIDE_BLOCKS overrides)
   int side_gemm_blocks() const;
   const RnnDesc &Desc() const { return desc_; }
+  // arithmetic of the recurrences and gate GEMMs (rnn.h RnnDesc::prec); the
+  // parameters and the model file stay fp32
+  void SetPrecision(int prec) {
+    if (prec == 1 && desc_.mode != kLstm && desc_.mode != kGru)
+      throw std::invalid_argument("bf16 products exist for LSTM / GRU only");
+    desc_.prec = prec;
+  }
   void SetMiniBatch(int n) const { mini_batch_ = n; }  // Init(mini_batch) on change
   // Propagate whose last recurrence also produces `next`'s layer-0 input
   // projection on the side stream (rnn.h RnnFwdChain), `next` being the

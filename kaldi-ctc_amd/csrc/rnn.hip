@@ -2422,6 +2422,25 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     g.bias2 = (d.mode == kGru) ? nullptr : wl + bR;
     g.batch = dirs; g.strideA = 0; g.strideB = pls; g.strideC = (long)NW * H; g.strideBias = pls;
     if (skip_proj) {
+    } else if (d.prec == kPrecBf16 && use_x3(Din, 32)) {
+      // bf16 gate GEMM: input rows and W rows packed as bf16, fp32 accumulation
+      const PackLay pl = pack_layout(d, T, N);
+      __bf16 *Ap = pk<__bf16>(workspace, d, T, N, pl.a), *Bp = pk<__bf16>(workspace, d, T, N, pl.b);
+      const int KB = (Din + 63) / 64;
+      {
+        ProfSpan ps(s, "x3_pack");
+        bf16_pack_rows(s, in, Din, (int)TN, Din, Ap);
+        bf16_pack_rows(s, wl, Din, NW * H, Din, Bp, dirs, pls, (long)NW * H * KB * 64);
+      }
+      X3PArgs x;
+      x.bf16 = true;
+      x.M = (int)TN; x.N = NW * H; x.KB = KB;
+      x.A = reinterpret_cast<const _Float16 *>(Ap); x.B = reinterpret_cast<const _Float16 *>(Bp);
+      x.C = g.C; x.ldc = g.ldc; x.bias = g.bias; x.bias2 = g.bias2;
+      x.batch = dirs; x.sA = 0; x.sB = (long)NW * H * KB * 64;
+      x.sC = g.strideC; x.sBias = g.strideBias;
+      ProfSpan ps(s, "gemm_fwd_proj");
+      gemm_x3p(s, x);
     } else if (use_x3(Din, 32)) {
       // input rows (a lower stacked layer's output is bounded; the component
       // input and RELU outputs get per-row exponents) and W rows, packed
@@ -2607,7 +2626,29 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     }
     if (ver == 6) xch_release(s);
     tr.dump("bwd", s, grid.x, p.nwg, T, dirs, ver, ver == 6 ? (p.xpd ? 1 : 0) : p.xpd);
-    if (dxl && !streamed) {
+    if (dxl && !streamed && d.prec == kPrecBf16 && use_x3(NW * H)) {
+      // bf16: dGates rows and W^T rows (columns of W) packed as bf16
+      const long G4 = (long)NW * H;
+      const int KB = (int)((G4 + 63) / 64);
+      const PackLay pl = pack_layout(d, T, N);
+      __bf16 *Ap = pk<__bf16>(workspace, d, T, N, pl.a), *Bp = pk<__bf16>(workspace, d, T, N, pl.b);
+      {
+        ProfSpan ps(s, "x3_pack");
+        bf16_pack_rows(s, DX, (long)dirs * G4, (int)TN, (int)G4, Ap, dirs, G4, TN * KB * 64);
+        for (int dir = 0; dir < dirs; dir++)
+          bf16_pack_cols(s, wl + dir * pls, Din, (int)G4, Din, 0, Bp + (long)dir * Din * KB * 64);
+      }
+      for (int dir = 0; dir < dirs; dir++) {
+        ProfSpan ps(s, "gemm_bwd_data");
+        X3PArgs x;
+        x.bf16 = true;
+        x.M = (int)TN; x.N = Din; x.KB = KB;
+        x.A = reinterpret_cast<const _Float16 *>(Ap + (long)dir * TN * KB * 64);
+        x.B = reinterpret_cast<const _Float16 *>(Bp + (long)dir * Din * KB * 64);
+        x.C = dxl; x.ldc = Din; x.beta = dir == 0 ? 0.f : 1.f;
+        gemm_x3p(s, x);
+      }
+    } else if (dxl && !streamed) {
       const bool x3 = use_x3(NW * H);
       const long G4 = (long)NW * H;
       const int KB = (int)((G4 + 31) / 32);
@@ -2690,6 +2731,51 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     unsigned *fl = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     if (max_blocks > 0) g.tile_counter = reinterpret_cast<int *>(fl + 1008);
     const bool x3 = use_x3((int)TN);  // K = frames: large (also for a 40-dim input: 0.8 ms/step over fp32)
+    if (x3 && d.prec == kPrecBf16) {
+      // bf16 weight GEMMs: the transposes packed along the frames as bf16
+      const int KB = (int)((TN + 63) / 64);
+      const PackLay pl = pack_layout(d, T, N);
+      __bf16 *DXt = pk<__bf16>(workspace, d, T, N, pl.a), *Xt = pk<__bf16>(workspace, d, T, N, pl.b);
+      __bf16 *Yt = pk<__bf16>(workspace, d, T, N, pl.c);
+      __bf16 *Et = d.mode == kGru ? DXt + (long)dirs * G4 * KB * 64 : DXt;
+      {
+        ProfSpan ps(s, "x3_pack_w");
+        bf16_pack_cols(s, DX, ldg, (int)TN, (int)(dirs * G4), 0, DXt);
+        if (d.mode == kGru) bf16_pack_cols(s, E, ldg, (int)TN, (int)(dirs * G4), 0, Et);
+        bf16_pack_cols(s, in, Din, (int)TN, Din, 0, Xt);
+        if (T > 1)
+          for (int dir = 0; dir < dirs; dir++)
+            bf16_pack_cols(s, out + (long)dir * H, ldy, (int)TN, H, dir == 0 ? N : -N, Yt + (long)dir * H * KB * 64);
+      }
+      {
+        X3PArgs x;
+        x.bf16 = true;
+        x.M = (int)G4; x.N = Din; x.KB = KB;
+        x.A = reinterpret_cast<const _Float16 *>(DXt); x.sA = G4 * KB * 64;
+        x.B = reinterpret_cast<const _Float16 *>(Xt);
+        x.C = dwl; x.ldc = Din; x.beta = 1.f;
+        x.batch = dirs; x.sC = pls;
+        x.split_k = g.split_k; x.ws = ws; x.max_blocks = g.max_blocks; x.tile_counter = g.tile_counter;
+        ProfSpan ps(s, "gemm_bwd_w");
+        gemm_x3p(s, x);
+      }
+      if (T > 1) {
+        X3PArgs x;
+        x.bf16 = true;
+        x.M = (int)G4; x.N = H; x.KB = KB;
+        x.A = reinterpret_cast<const _Float16 *>(Et); x.sA = G4 * KB * 64;
+        x.B = reinterpret_cast<const _Float16 *>(Yt); x.sB = (long)H * KB * 64;
+        x.C = dwl + (d.lin_offset(l * dirs, NW, false) - pl0); x.ldc = H; x.beta = 1.f;
+        x.batch = dirs; x.sC = pls;
+        x.split_k = gemm_pick_split((int)G4, H, (int)((long)(T - 1) * N), dirs); x.ws = ws;
+        x.max_blocks = max_blocks;
+        if (max_blocks > 0) x.tile_counter = reinterpret_cast<int *>(fl + 1009);
+        ProfSpan ps(s, "gemm_bwd_r");
+        gemm_x3p(s, x);
+      }
+    }
+    if (x3 && d.prec == kPrecBf16) {
+    } else {
     const int KBt = (int)((TN + 31) / 32);
     const PackLay pl = pack_layout(d, T, N);
     _Float16 *DXt = pk<_Float16>(workspace, d, T, N, pl.a), *Xt = pk<_Float16>(workspace, d, T, N, pl.b);
@@ -2766,6 +2852,7 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
         gemm_f32(s, r);
       }
     }
+    }  // x3 / fp32 weight GEMMs
     // biases: dbW += sum dGx, dbR += sum dGh (partials from the recurrence)
     const long bW = d.lin_offset(l * dirs, 0, true) - pl0;
     const long bR = d.lin_offset(l * dirs, NW, true) - pl0;

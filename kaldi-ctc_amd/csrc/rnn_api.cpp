@@ -39,6 +39,14 @@ int krnnCreate(krnnDescriptor_t *desc, int mode, int input_dim, int hidden_dim, 
   return KRNN_STATUS_SUCCESS;
 }
 
+int krnnSetPrecision(krnnDescriptor_t desc, int precision) {
+  if (!desc || (precision != KRNN_PREC_FP32 && precision != KRNN_PREC_BF16)) return KRNN_STATUS_BAD_PARAM;
+  if (precision == KRNN_PREC_BF16 && desc->desc.mode != kctc::kLstm && desc->desc.mode != kctc::kGru)
+    return KRNN_STATUS_NOT_SUPPORTED;
+  desc->desc.prec = precision;
+  return KRNN_STATUS_SUCCESS;
+}
+
 int krnnDestroy(krnnDescriptor_t desc) {
   if (!desc) return KRNN_STATUS_BAD_PARAM;
   if (desc->err) (void)hipFree(desc->err);

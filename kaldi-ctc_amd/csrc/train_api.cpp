@@ -575,6 +575,16 @@ int kctc_nnet_enable_dp_host(kctcNnet_t n, kctc_host_allreduce_fn fn, void *user
   });
 }
 
+int kctc_nnet_set_precision(kctcNnet_t n, int precision) {
+  return guarded([&] {
+    KCTC_REQUIRE(n && (precision == 0 || precision == 1), "kctc_nnet_set_precision: precision must be 0 or 1");
+    KCTC_REQUIRE(n->trainer.Pending() == 0, "kctc_nnet_set_precision with minibatches in flight");
+    for (int c = 0; c < n->nnet.NumComponents(); c++)
+      if (auto *r = dynamic_cast<kctc::nnet2::CuDNNRecurrentComponent *>(&n->nnet.GetComponent(c)))
+        r->SetPrecision(precision);
+  });
+}
+
 int kctc_nnet_set_momentum(kctcNnet_t n, float momentum) {
   return guarded([&] {
     KCTC_REQUIRE(n, "null nnet");

@@ -89,6 +89,38 @@ def test_rnn_matches_oracle(kctc, gpu, oracle, case):
                 assert rel_err(dw[sl], rdw[sl]) < 2e-4, (pl, lin, isb)
 
 
+BF16_CASES = [
+    # (mode, T, N, D, H, layers, bidir): configs[4] shapes in miniature
+    (3, 20, 32, 64, 1024, 1, True),   # BGRU-1024, 2 row groups, U=32
+    (3, 16, 8, 40, 1024, 1, True),    # one group, U=16
+    (2, 18, 20, 48, 512, 1, True),    # BLSTM-512 in bf16
+    (3, 12, 5, 32, 256, 2, False),    # stacked uni GRU
+]
+# bf16 operands (8 significant bits, relative rounding 2^-9) with fp32
+# accumulation, against the fp64 oracle: norm-wise relative error bounds
+BF16_TOL = {"y": 1e-2, "dx": 2e-2, "dw": 2e-2}
+
+
+@pytest.mark.parametrize("case", BF16_CASES, ids=[f"m{c[0]}_T{c[1]}_N{c[2]}_D{c[3]}_H{c[4]}_L{c[5]}" for c in BF16_CASES])
+def test_rnn_bf16_matches_oracle(kctc, gpu, oracle, case):
+    """krnnSetPrecision(KRNN_PREC_BF16): bf16 recurrences and gate GEMMs."""
+    mode, T, N, D, H, layers, bidir = case
+    r, (w, x, dy), b = _mk(kctc, gpu, mode, T, N, D, H, layers, bidir, seed=sum(case) + 1, wscale=0.05)
+    r.set_precision("bf16")
+    y, dx, dw = _run_gpu(r, b)
+    ry, res = oracle.rnn_forward(mode, x.astype(np.float64), w.astype(np.float64), H, layers, r.dirs)
+    rdx, rdw = oracle.rnn_backward(mode, x.astype(np.float64), w.astype(np.float64), ry,
+                                   dy.astype(np.float64), res, H, layers, r.dirs)
+    errs = {"y": rel_err(y, ry), "dx": rel_err(dx, rdx), "dw": rel_err(dw, rdw)}
+    print(case, {k: f"{v:.2e}" for k, v in errs.items()})
+    for k, e in errs.items():
+        assert e < BF16_TOL[k], (k, e)
+    # and it is the bf16 path: the fp32-class result is far closer
+    r2, _, b2 = _mk(kctc, gpu, mode, T, N, D, H, layers, bidir, seed=sum(case) + 1, wscale=0.05)
+    y2, _, _ = _run_gpu(r2, b2)
+    assert rel_err(y2, ry) < 1e-5 < errs["y"]
+
+
 def test_rnn_golden_layout(kctc, gpu):
     """The torch-fp64 golden fixture through the HIP path (cuDNN layout)."""
     import torch

@@ -135,6 +135,38 @@ def test_train_step_row_groups_match_oracle(kctc, gpu, oracle, mode, H, T, N):
         assert rel_err(net.get_params(c).astype(np.float64), p) < 1e-5, c
 
 
+@pytest.mark.parametrize("mode,H,T,N", [(3, 1024, 16, 32), (2, 512, 12, 16)])
+def test_train_step_bf16_matches_oracle(kctc, gpu, oracle, mode, H, T, N):
+    """kctc_nnet_set_precision(1): bf16 recurrences and gate GEMMs, fp32
+    master weights, affine / CTC / updates in fp32 (configs[4]).  Tolerance
+    for bf16 operands: objective 1e-3 relative, updates 5e-2 norm-wise."""
+    import torch
+    R, D, A, lr = 2, 40, 41, 0.02
+    cfg = kctc.recipe_config(num_rnn=R, input_dim=D, hidden=H, num_targets=A, rnn_mode=mode,
+                             learning_rate=lr, param_stddev=0.05)
+    net = kctc.Nnet(cfg, seed=16)
+    net.set_precision("bf16")
+    upd = [c for c in range(net.num_components) if net.num_params(c) > 0]
+    params = [net.get_params(c).astype(np.float64) for c in upd]
+    p0 = [p.copy() for p in params]
+    spec = _oracle_spec(oracle, R, mode, H, 2, D, A, 30.0, lr)
+    feats, nf, fl, ll = kctc.synth_minibatch(78, T, N, D, A, 0.2)
+    objf, acc, wt = net.train_step(torch.from_numpy(feats).to(gpu), T, N, nf, fl, ll)
+    Wa = params[-1][:-A].reshape(A, -1).copy()
+    ba = params[-1][-A:].copy()
+    robjf, racc, rwt = oracle.train_step(spec, params[:-1], Wa, ba, feats.reshape(T, N, D).astype(np.float64),
+                                         nf, fl, ll, repair_draws=np.ones(R, np.float32))
+    params[-1] = np.concatenate([Wa.ravel(), ba])
+    np.testing.assert_allclose(objf, robjf, rtol=1e-3)
+    assert wt == rwt
+    ids = net.last_best_path(T, N)
+    np.testing.assert_array_equal(ids, oracle.find_row_max_id(net.last_output(T, N, A)))
+    for c, p, q in zip(upd, params, p0):
+        e = rel_err(net.get_params(c).astype(np.float64) - q, p - q)
+        print(c, f"{e:.2e}")
+        assert e < 5e-2, (c, e)
+
+
 def test_train_loss_decreases_and_objf_only(kctc, gpu):
     import torch
     D, A, T, N = 40, 41, 120, 8
