@@ -472,6 +472,31 @@ class Nnet:
         _tcheck(lib().kctc_nnet_profile(self.h, family.encode(), ctypes.byref(ms), ctypes.byref(n)), "profile")
         return ms.value, n.value
 
+    def propagate(self, feats, T, N, out=None):
+        """NnetComputation: network output [T*N, output_dim] (torch CUDA tensor)."""
+        import torch
+        A = int(self.info(self.num_components - 1).split("output-dim=")[1].split(",")[0])
+        if out is None:
+            out = torch.empty((T * N, A), dtype=torch.float32, device=feats.device)
+        _tcheck(lib().kctc_nnet_propagate(self.h, _ptr(feats), T, N, _ptr(out), out.numel()), "propagate")
+        return out
+
+    def decodable(self, feats, T, prob_scale=1.0, blank_threshold=1.0):
+        """CtcDecodableAmNnet of one utterance -> np [kept, A] log-likelihoods."""
+        A = int(self.info(self.num_components - 1).split("output-dim=")[1].split(",")[0])
+        out = np.empty((T, A), np.float32)
+        k = ctypes.c_int()
+        _tcheck(lib().kctc_am_nnet_decodable(self.h, _ptr(feats), T, prob_scale, blank_threshold, out.ctypes.data,
+                                             ctypes.byref(k)), "am_nnet_decodable")
+        return out[:k.value].copy()
+
+    def compute_prob(self, rspecifier):
+        """nnet2-ctc-compute-prob -> dict(num_examples, tot_like, tot_accuracy, tot_weight)."""
+        ne, l, a, w = ctypes.c_long(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        _tcheck(lib().kctc_nnet_compute_prob(self.h, str(rspecifier).encode(), ctypes.byref(ne), ctypes.byref(l),
+                                             ctypes.byref(a), ctypes.byref(w)), "compute_prob")
+        return {"num_examples": ne.value, "tot_like": l.value, "tot_accuracy": a.value, "tot_weight": w.value}
+
     def set_precision(self, prec):
         """0: fp32-class recurrences / gate GEMMs (default); 1 or "bf16": bf16
         operands, fp32 accumulation (kctc_nnet_set_precision)."""
@@ -503,6 +528,28 @@ class Nnet:
 
 
 _HOST_ALLREDUCE = ctypes.CFUNCTYPE(None, ctypes.POINTER(ctypes.c_float), ctypes.c_long, ctypes.c_void_p)
+
+
+def softmax_rows(x, stream=None):
+    """SoftmaxComponent forward of a 2-D torch CUDA tensor (kctc_softmax_rows)."""
+    import torch
+    out = torch.empty_like(x)
+    _tcheck(lib().kctc_softmax_rows(_stream_handle(stream), _ptr(x), x.shape[0], x.shape[1], _ptr(out)),
+            "kctc_softmax_rows")
+    return out
+
+
+def ctc_decodable(probs, priors=None, prob_scale=1.0, blank_threshold=1.0, floor=1e-10, stream=None):
+    """CtcDecodableAmNnet's matrix from device probs [T, A] -> torch CUDA [kept, A]."""
+    import torch
+    T, A = probs.shape
+    out = torch.empty_like(probs)
+    scratch = torch.empty(lib().kctc_ctc_decodable_scratch_bytes(T), dtype=torch.uint8, device=probs.device)
+    k = ctypes.c_int()
+    _tcheck(lib().kctc_ctc_decodable(_stream_handle(stream), _ptr(probs), T, A, _ptr(priors), prob_scale,
+                                     blank_threshold, floor, _ptr(out), _ptr(scratch), ctypes.byref(k)),
+            "kctc_ctc_decodable")
+    return out[:k.value]
 
 
 def dp_unique_id():

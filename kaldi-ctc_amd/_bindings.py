@@ -76,6 +76,14 @@ SIGS = {
     "kctc_levenshtein": (ci, [vp, ci, vp, ci]),
     "kctc_format_input": (ci, [vp, vp, ci, ci, ci, vp]),
     "kctc_synth_minibatch": (cl, [ctypes.c_ulonglong, ci, ci, ci, ci, cd, vp, vp, vp, vp]),
+    # include/kaldi_ctc_decode.h
+    "kctc_softmax_rows": (ci, [vp, vp, cl, ci, vp]),
+    "kctc_ctc_decodable_scratch_bytes": (sz, [ci]),
+    "kctc_ctc_decodable": (ci, [vp, vp, ci, ci, vp, cf, cf, cf, vp, vp, ip]),
+    "kctc_nnet_propagate": (ci, [vp, vp, ci, ci, vp, cl]),
+    "kctc_am_nnet_decodable": (ci, [vp, vp, ci, cf, cf, vp, ip]),
+    "kctc_nnet_compute_prob": (ci, [vp, ctypes.c_char_p, ctypes.POINTER(cl), ctypes.POINTER(cd), ctypes.POINTER(cd),
+                                    ctypes.POINTER(cd)]),
     # include/kaldi_ctc_egs.h
     "kctc_cm_compressed_bytes": (cl, [ci, ci]),
     "kctc_cm_compress": (ci, [vp, ci, ci, vp]),

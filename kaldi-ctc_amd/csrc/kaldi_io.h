@@ -120,6 +120,36 @@ inline float ReadFloat(std::istream &is, bool binary) {
   if (is.fail()) Fail("ReadBasicType<float>: not a number");
   return (float)v;
 }
+inline void WriteDouble(std::ostream &os, bool binary, double v) {
+  if (binary) {
+    os.put((char)sizeof(v));
+    os.write(reinterpret_cast<const char *>(&v), sizeof(v));
+  } else {
+    os << std::setprecision(7) << v << ' ';
+  }
+}
+inline double ReadDouble(std::istream &is, bool binary) {
+  if (binary) {
+    const int c = is.get();
+    if (c == 8) {
+      double v;
+      is.read(reinterpret_cast<char *>(&v), 8);
+      if (!is) Fail("ReadBasicType<double>: truncated");
+      return v;
+    }
+    if (c == 4) {
+      float v;
+      is.read(reinterpret_cast<char *>(&v), 4);
+      if (!is) Fail("ReadBasicType<double>: truncated");
+      return v;
+    }
+    Fail("ReadBasicType<double>: size byte " + std::to_string(c));
+  }
+  double v;
+  is >> v;
+  if (is.fail()) Fail("ReadBasicType<double>: not a number");
+  return v;
+}
 inline void WriteBool(std::ostream &os, bool binary, bool b) {
   os << (b ? "T" : "F");
   if (!binary) os << ' ';
@@ -200,6 +230,45 @@ inline std::vector<float> ReadFloatVector(std::istream &is, bool binary) {
   is >> s;
   if (s != "[") Fail("Vector::Read: expected [, got " + s);
   while (is >> s && s != "]") v.push_back(std::stof(s));
+  if (s != "]") Fail("Vector::Read: expected ]");
+  return v;
+}
+
+// Vector<double>::Write / Read ("DV" n raw | " [ a b ]"); a float vector is accepted
+inline void WriteDoubleVector(std::ostream &os, bool binary, const std::vector<double> &v) {
+  if (binary) {
+    WriteToken(os, binary, "DV");
+    WriteInt(os, binary, (int32_t)v.size());
+    if (!v.empty()) os.write(reinterpret_cast<const char *>(v.data()), 8 * v.size());
+  } else {
+    os << " [ ";
+    for (double x : v) os << std::setprecision(7) << x << ' ';
+    os << "]\n";
+  }
+}
+inline std::vector<double> ReadDoubleVector(std::istream &is, bool binary) {
+  std::vector<double> v;
+  if (binary) {
+    const std::string t = ReadToken(is, binary);
+    const int32_t n = ReadInt(is, binary);
+    if (n < 0) Fail("Vector::Read: negative size");
+    v.resize(n);
+    if (t == "DV") {
+      if (n) is.read(reinterpret_cast<char *>(v.data()), 8 * (size_t)n);
+    } else if (t == "FV") {
+      std::vector<float> f(n);
+      if (n) is.read(reinterpret_cast<char *>(f.data()), 4 * (size_t)n);
+      for (int32_t i = 0; i < n; i++) v[i] = f[i];
+    } else {
+      Fail("Vector::Read: expected DV or FV, got " + t);
+    }
+    if (!is) Fail("Vector::Read: truncated");
+    return v;
+  }
+  std::string s;
+  is >> s;
+  if (s != "[") Fail("Vector::Read: expected [, got " + s);
+  while (is >> s && s != "]") v.push_back(std::stod(s));
   if (s != "]") Fail("Vector::Read: expected ]");
   return v;
 }

@@ -12,6 +12,7 @@
 
 #include "common.h"
 #include "ctc.h"
+#include "decodable.h"
 #include "elementwise.h"
 #include "gemm.h"
 #include "prof.h"
@@ -272,6 +273,7 @@ Component *Component::NewComponentOfType(const std::string &type) {
   if (type == "CuDNNRecurrentComponent") return new CuDNNRecurrentComponent;
   if (type == "ClipGradientComponent") return new ClipGradientComponent;
   if (type == "AffineComponent") return new AffineComponent;
+  if (type == "SoftmaxComponent") return new SoftmaxComponent;
   return nullptr;
 }
 
@@ -773,6 +775,53 @@ void ClipGradientComponent::Read(std::istream &is, bool binary) {
   KCTC_HIP_CHECK(hipMemcpy(dev_, &h, sizeof(h), hipMemcpyHostToDevice));
 }
 // ---------------------------------------------------------------------------
+// SoftmaxComponent (NonlinearComponent I/O, nnet-component.cc:383-426)
+// ---------------------------------------------------------------------------
+void SoftmaxComponent::InitFromString(std::string args, Rng &) {
+  const std::string orig = args;
+  const bool ok = ParseFromString("dim", &args, &dim_);
+  if (!ok || !args.empty() || dim_ <= 0)
+    throw std::invalid_argument("Invalid initializer for layer of type SoftmaxComponent: \"" + orig + "\"");
+  value_sum_.clear();
+  deriv_sum_.clear();
+  count_ = 0;
+}
+void SoftmaxComponent::Propagate(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &in,
+                                 CuMatrixBase *out) const {
+  ProfScope ps("softmax");
+  softmax_rows(S(), in.Data(), in.NumRows(), dim_, out->Data());  // ApplySoftMaxPerRow + ApplyFloor(1e-20)
+}
+void SoftmaxComponent::Backprop(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &, const CuMatrixBase &,
+                                const CuMatrixBase &, Component *, CuMatrixBase *) const {
+  throw std::logic_error("SoftmaxComponent::Backprop: not on the CTC training path (CTC trains on the "
+                         "un-normalised affine output; the softmax is appended for decoding)");
+}
+void SoftmaxComponent::Write(std::ostream &os, bool binary) const {
+  WriteToken(os, binary, "<SoftmaxComponent>");
+  WriteToken(os, binary, "<Dim>");
+  kio::WriteInt(os, binary, dim_);
+  WriteToken(os, binary, "<ValueSum>");
+  kio::WriteDoubleVector(os, binary, value_sum_);
+  WriteToken(os, binary, "<DerivSum>");
+  kio::WriteDoubleVector(os, binary, deriv_sum_);
+  WriteToken(os, binary, "<Count>");
+  kio::WriteDouble(os, binary, count_);
+  WriteToken(os, binary, "</SoftmaxComponent>");
+}
+void SoftmaxComponent::Read(std::istream &is, bool binary) {
+  // ExpectOneOrTwoTokens(<SoftmaxComponent>, <Dim>): the type token was consumed by Nnet::Read
+  ExpectToken(is, binary, "<Dim>");
+  dim_ = kio::ReadInt(is, binary);
+  if (dim_ <= 0) throw std::runtime_error("SoftmaxComponent: bad <Dim>");
+  ExpectToken(is, binary, "<ValueSum>");
+  value_sum_ = kio::ReadDoubleVector(is, binary);
+  ExpectToken(is, binary, "<DerivSum>");
+  deriv_sum_ = kio::ReadDoubleVector(is, binary);
+  ExpectToken(is, binary, "<Count>");
+  count_ = kio::ReadDouble(is, binary);
+  ExpectToken(is, binary, "</SoftmaxComponent>");
+}
+// ---------------------------------------------------------------------------
 // AffineComponent (nnet-component.cc:1125-1274)
 // ---------------------------------------------------------------------------
 void AffineComponent::InitFromString(std::string args, Rng &rng) {
@@ -1013,6 +1062,32 @@ MinibatchStats NnetCtcUpdater::ComputeForMinibatch(const float *feats, int T_max
   if (pending_) throw std::logic_error("ComputeForMinibatch with queued minibatches (Finish them first)");
   Enqueue(feats, T_max, N, num_frames, flat_labels, label_lengths);
   return Finish();
+}
+
+const CuMatrixBase &NnetCtcUpdater::Forward(const float *feats, int T_max, int N) {
+  if (pending_) throw std::logic_error("Forward with queued minibatches (Finish them first)");
+  if (N <= 0 || T_max <= 0) throw std::invalid_argument("empty minibatch");
+  const int C = nnet_->NumComponents();
+  set_minibatch(nnet_, N);
+  err_word_.ensure(256);
+  KCTC_HIP_CHECK(hipMemsetAsync(err_word_.p, 0, sizeof(unsigned), S()));
+  for (int c = 0; c < C; c++)
+    if (auto *r = dynamic_cast<CuDNNRecurrentComponent *>(&nnet_->GetComponent(c)))
+      r->SetErrorWord(static_cast<unsigned *>(err_word_.p));
+  forward_data_.resize(C + 1);
+  chunk_info_.resize(C + 1);
+  for (int c = 0; c <= C; c++) {
+    chunk_info_[c].num_chunks = N;
+    chunk_info_[c].chunk_size = T_max;
+    chunk_info_[c].feat_dim = c == 0 ? nnet_->InputDim() : nnet_->GetComponent(c - 1).OutputDim();
+  }
+  forward_data_[0].SetView(const_cast<float *>(feats), (long)T_max * N, nnet_->InputDim());
+  Propagate(T_max, N);
+  unsigned herr = 0;
+  KCTC_HIP_CHECK(hipMemcpyAsync(&herr, err_word_.p, sizeof(unsigned), hipMemcpyDeviceToHost, S()));
+  KCTC_HIP_CHECK(hipStreamSynchronize(S()));
+  if (herr) throw std::runtime_error("recurrence hand-off timed out (device error word set)");
+  return forward_data_[C];
 }
 
 void NnetCtcUpdater::Enqueue(const float *feats, int T_max, int N, const int *num_frames,

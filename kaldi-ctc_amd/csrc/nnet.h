@@ -305,6 +305,30 @@ class ClipGradientComponent : public Component {
   ClipGradientComponent *shadow_ = nullptr;
 };
 
+// SoftmaxComponent (nnet-component.cc:929-946): the output layer the recipe
+// appends for decoding (egs/wsj/s5/steps/ctc/train.sh:471-477); forward only
+// on this path (CTC training runs on the un-normalised affine output).
+// The NonlinearComponent statistics are kept for the model file.
+class SoftmaxComponent : public Component {
+ public:
+  std::string Type() const override { return "SoftmaxComponent"; }
+  int InputDim() const override { return dim_; }
+  int OutputDim() const override { return dim_; }
+  void InitFromString(std::string args, Rng &rng) override;
+  bool BackpropNeedsInput() const override { return false; }
+  void Propagate(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &in,
+                 CuMatrixBase *out) const override;
+  void Backprop(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &, const CuMatrixBase &,
+                const CuMatrixBase &, Component *, CuMatrixBase *) const override;
+  void Write(std::ostream &os, bool binary) const override;
+  void Read(std::istream &is, bool binary) override;
+
+ private:
+  int dim_ = 0;
+  std::vector<double> value_sum_, deriv_sum_;
+  double count_ = 0;
+};
+
 class AffineComponent : public UpdatableComponent {
  public:
   std::string Type() const override { return "AffineComponent"; }
@@ -389,6 +413,9 @@ class NnetCtcUpdater {
   int Pending() const { return pending_; }
   MinibatchStats Finish();
   void SetExchange(GradExchange *ex) { exchange_ = ex; }
+  // NnetComputation (src/nnet2/nnet-compute.cc): forward only, N sequences
+  // time-major; the output stays valid until the next minibatch
+  const CuMatrixBase &Forward(const float *feats, int T_max, int N);
   // best-path ids ([T_max*N], FindRowMaxId) of the last minibatch Finish()ed
   const std::vector<int> &LastBestPath() const { return last_ids_; }
   // per-utterance CTC costs (-log p, warp-ctc `costs`) of that minibatch

@@ -1,6 +1,7 @@
 // train_api.cpp -- C ABI of include/kaldi_ctc_train.h: the nnet2 trainer,
 // RCCL data parallelism, FormatNnetInput and the synthetic minibatch generator.
 #include "kaldi_ctc_train.h"
+#include "kaldi_ctc_decode.h"
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -14,6 +15,7 @@
 #include <vector>
 
 #include "common.h"
+#include "decodable.h"
 #include "egs.h"
 #include "kaldi_io.h"
 #include "nnet.h"
@@ -621,6 +623,107 @@ int kctc_nnet_train_simple(kctcNnet_t n, struct kctcEgsReader_ *r, long max_mini
     if (tot_weight) *tot_weight = w;
     if (tot_objf) *tot_objf = objf;
     if (tot_accuracy) *tot_accuracy = acc;
+  });
+}
+
+size_t kctc_ctc_decodable_scratch_bytes(int T) { return kctc::ctc_decodable_scratch_bytes(T > 0 ? T : 1) + 256; }
+
+int kctc_softmax_rows(struct ihipStream_t *stream, const float *in, long rows, int cols, float *out) {
+  return guarded([&] {
+    KCTC_REQUIRE(in && out && rows >= 0 && cols > 0, "kctc_softmax_rows: bad argument");
+    kctc::softmax_rows(stream, in, rows, cols, out);
+    KCTC_HIP_CHECK(hipGetLastError());
+  });
+}
+
+int kctc_ctc_decodable(struct ihipStream_t *stream, const float *probs, int T, int A, const float *priors,
+                       float prob_scale, float blank_threshold, float floor_value, float *out, void *scratch,
+                       int *num_kept) {
+  return guarded([&] {
+    KCTC_REQUIRE(probs && out && scratch && num_kept && T > 0 && A > 0, "kctc_ctc_decodable: bad argument");
+    int *kept_dev = reinterpret_cast<int *>(static_cast<char *>(scratch) + kctc::ctc_decodable_scratch_bytes(T));
+    kctc::ctc_decodable(stream, probs, T, A, priors, prob_scale, blank_threshold, floor_value, out, scratch,
+                        kept_dev);
+    KCTC_HIP_CHECK(hipGetLastError());
+    KCTC_HIP_CHECK(hipMemcpyAsync(num_kept, kept_dev, sizeof(int), hipMemcpyDeviceToHost, stream));
+    KCTC_HIP_CHECK(hipStreamSynchronize(stream));
+  });
+}
+
+int kctc_nnet_propagate(kctcNnet_t n, const float *feats_dev, int T_max, int N, float *out_dev, long len) {
+  return guarded([&] {
+    KCTC_REQUIRE(n && feats_dev && out_dev, "kctc_nnet_propagate: null argument");
+    n->activate();
+    const auto &o = n->evaluator.Forward(feats_dev, T_max, N);
+    KCTC_REQUIRE(len == o.NumRows() * (long)o.NumCols(), "kctc_nnet_propagate: len != T_max*N*output_dim");
+    KCTC_HIP_CHECK(hipMemcpyAsync(out_dev, o.Data(), sizeof(float) * len, hipMemcpyDeviceToDevice, n->stream));
+    KCTC_HIP_CHECK(hipStreamSynchronize(n->stream));
+  });
+}
+
+int kctc_am_nnet_decodable(kctcNnet_t n, const float *feats_dev, int T, float prob_scale, float blank_threshold,
+                           float *out_host, int *num_rows) {
+  return guarded([&] {
+    KCTC_REQUIRE(n && feats_dev && out_host && num_rows && T > 0, "kctc_am_nnet_decodable: bad argument");
+    n->activate();
+    // left/right context of this path are 0: every input row gives an output row
+    const auto &o = n->evaluator.Forward(feats_dev, T, 1);
+    const int A = o.NumCols();
+    kctc::nnet2::DevBuf pri, out, scratch;
+    const float *pd = nullptr;
+    if (!n->priors.empty()) {
+      KCTC_REQUIRE((int)n->priors.size() == A, "priors dimension != network output dimension");
+      pri.ensure(sizeof(float) * A);
+      KCTC_HIP_CHECK(hipMemcpyAsync(pri.p, n->priors.data(), sizeof(float) * A, hipMemcpyHostToDevice, n->stream));
+      pd = pri.f();
+    }
+    out.ensure(sizeof(float) * (size_t)T * A);
+    scratch.ensure(kctc_ctc_decodable_scratch_bytes(T));
+    int kept = 0;
+    const int st = kctc_ctc_decodable(n->stream, o.Data(), T, A, pd, prob_scale, blank_threshold, 1.0e-10f, out.f(),
+                                      scratch.p, &kept);
+    if (st) throw std::runtime_error(g_err);
+    KCTC_HIP_CHECK(hipMemcpy(out_host, out.p, sizeof(float) * (size_t)kept * A, hipMemcpyDeviceToHost));
+    *num_rows = kept;
+  });
+}
+
+int kctc_nnet_compute_prob(kctcNnet_t n, const char *rspecifier, long *num_examples, double *tot_like,
+                           double *tot_accuracy, double *tot_weight) {
+  return guarded([&] {
+    KCTC_REQUIRE(n && rspecifier, "kctc_nnet_compute_prob: null argument");
+    n->activate();
+    kctc::egs::ArchiveReader reader(rspecifier);
+    std::vector<kctc::egs::Example> batch;
+    long ne = 0;
+    double like = 0, acc = 0, w = 0;
+    auto run = [&]() {  // ComputeNnetObjf on one batch (ctc-nnet-update.cc:426-431)
+      std::unique_ptr<kctc::egs::Minibatch> mb = kctc::egs::pack_minibatch(batch, 0, 0);
+      if (mb->InputDim() != n->nnet.InputDim())
+        throw std::invalid_argument("egs input dim " + std::to_string(mb->InputDim()) + " != nnet input dim " +
+                                    std::to_string(n->nnet.InputDim()));
+      n->egs_feats.ensure(sizeof(float) * (size_t)mb->T_max * mb->N * mb->InputDim());
+      n->egs_scratch.ensure(kctc::egs::format_scratch_bytes(*mb));
+      kctc::egs::format_on_device(*mb, n->egs_feats.f(), n->egs_scratch.p, n->egs_scratch.bytes, n->stream);
+      const auto st = n->evaluator.ComputeForMinibatch(n->egs_feats.f(), mb->T_max, mb->N, mb->num_frames.data(),
+                                                       mb->labels.data(), mb->label_lengths.data());
+      like += st.tot_objf;
+      acc += st.tot_accuracy;
+      w += st.tot_weight;  // TotalNnetTrainingWeight: sum of label counts
+      batch.clear();
+    };
+    kctc::egs::Example eg;
+    while (reader.Next(&eg)) {
+      if (batch.size() == 10) run();
+      batch.push_back(std::move(eg));
+      eg = kctc::egs::Example();
+      ne++;
+    }
+    if (!batch.empty()) run();
+    if (num_examples) *num_examples = ne;
+    if (tot_like) *tot_like = like;
+    if (tot_accuracy) *tot_accuracy = acc;
+    if (tot_weight) *tot_weight = w;
   });
 }
 

@@ -122,6 +122,47 @@ void oracle_find_row_max_id_f32(const float *m, int rows, int cols, int *ids) {
   }
 }
 
+/* SoftmaxComponent::Propagate (src/nnet2/nnet-component.cc:929-946): per row
+ * exp(x - max) / sum, floored at 1e-20 (computed in double, rounded once). */
+void oracle_softmax_rows_f32(const float *in, long rows, int cols, float *out) {
+  for (long r = 0; r < rows; r++) {
+    const float *x = in + r * cols;
+    double m = x[0], s = 0;
+    for (int j = 1; j < cols; j++) m = x[j] > m ? x[j] : m;
+    for (int j = 0; j < cols; j++) s += exp((double)x[j] - m);
+    for (int j = 0; j < cols; j++) {
+      double v = exp((double)x[j] - m) / s;
+      out[r * cols + j] = (float)(v > 1e-20 ? v : 1e-20);
+    }
+  }
+}
+
+/* CtcDecodableAmNnet (src/ctc/ctc-decodable-am-nnet.cc:28-80) on the network
+ * output probs [T][A]: blank-threshold frame skip (probs[t][0] <
+ * blank_threshold keeps t; none kept -> all kept), ApplyFloor(floor_v),
+ * ApplyLog, AddVecToRows(-1, log(priors)) when priors, Scale(prob_scale).
+ * Returns the number of rows written to out. */
+int oracle_ctc_decodable_f32(const float *probs, int T, int A, const float *priors, float prob_scale,
+                             float blank_threshold, float floor_v, float *out) {
+  int kept = 0;
+  for (int pass = 0; pass < 2 && kept == 0; pass++) {
+    const int skip = pass == 0 && blank_threshold < 1.0f;
+    kept = 0;
+    for (int t = 0; t < T; t++) {
+      if (skip && !(probs[(long)t * A] < blank_threshold)) continue;
+      for (int a = 0; a < A; a++) {
+        float p = probs[(long)t * A + a];
+        float v = logf(p > floor_v ? p : floor_v);
+        if (priors) v += -1.0f * logf(priors[a]);
+        out[(long)kept * A + a] = v * prob_scale;
+      }
+      kept++;
+    }
+    if (!skip) break;
+  }
+  return kept;
+}
+
 double oracle_ctc_accuracy(const int *best_ids, int T_max, int N,
                            const int *num_frames, const int *flat_labels,
                            const int *label_lengths, double *tot_weight) {

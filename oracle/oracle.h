@@ -90,6 +90,12 @@ void oracle_find_row_max_id_f32(const float *m, int rows, int cols, int *ids);
 /* The CPU-only FindRowMaxId (src/cudamatrix/cu-matrix.cc:1630-1644): first
  * maximum above -1e21, else -1.  Not on the CTC path (kept for comparison). */
 void oracle_find_row_max_id_cpu_f32(const float *m, int rows, int cols, int *ids);
+/* SoftmaxComponent::Propagate (nnet-component.cc:929-946), floored at 1e-20 */
+void oracle_softmax_rows_f32(const float *in, long rows, int cols, float *out);
+/* CtcDecodableAmNnet (src/ctc/ctc-decodable-am-nnet.cc:28-80): blank skip,
+ * floor, log, minus log prior (priors nullable), scale; returns rows kept */
+int oracle_ctc_decodable_f32(const float *probs, int T, int A, const float *priors, float prob_scale,
+                             float blank_threshold, float floor_v, float *out);
 /* ComputeTotAccuracy (src/ctc/ctc-nnet-update.cc:261-317): returns sum_n L_n -
  * sum_n Levenshtein(ref_n, collapse(best ids)); *tot_weight = sum_n L_n. */
 double oracle_ctc_accuracy(const int *best_ids, int T_max, int N,

@@ -40,7 +40,7 @@ def layers(kctc, only=None):
         S.save(f"{case}.dx", S.sketch(dx, seed + 1), out)
         S.save(f"{case}.dw", S.sketch(dw, seed + 2), out)
         # per-region norms of dW (W, R, biases of both directions)
-        nlin = 8
+        nlin = 8 if c["mode"] == 2 else 6
         regs = []
         for pl in range(2):
             for lin in range(nlin):

@@ -77,6 +77,11 @@ def lib():
         L.oracle_find_row_max_id_f32.argtypes = [f32p, ctypes.c_int, ctypes.c_int, i32p]
         L.oracle_find_row_max_id_cpu_f32.argtypes = [f32p, ctypes.c_int, ctypes.c_int, i32p]
         L.oracle_num_threads.restype = ctypes.c_int
+        L.oracle_softmax_rows_f32.argtypes = [f32p, ctypes.c_long, ctypes.c_int, f32p]
+        L.oracle_softmax_rows_f32.restype = None
+        L.oracle_ctc_decodable_f32.argtypes = [f32p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_float,
+                                               ctypes.c_float, ctypes.c_float, f32p]
+        L.oracle_ctc_decodable_f32.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -141,6 +146,24 @@ def find_row_max_id(m, cpu_rule=False):
     fn = lib().oracle_find_row_max_id_cpu_f32 if cpu_rule else lib().oracle_find_row_max_id_f32
     fn(m, rows, cols, ids)
     return ids
+
+
+def softmax_rows(x):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty_like(x)
+    lib().oracle_softmax_rows_f32(x, x.shape[0], x.shape[1], out)
+    return out
+
+
+def ctc_decodable(probs, priors=None, prob_scale=1.0, blank_threshold=1.0, floor=1e-10):
+    """CtcDecodableAmNnet restatement -> [kept, A] log-likelihoods."""
+    probs = np.ascontiguousarray(probs, dtype=np.float32)
+    T, A = probs.shape
+    out = np.empty_like(probs)
+    pr = np.ascontiguousarray(priors, dtype=np.float32) if priors is not None else None
+    k = lib().oracle_ctc_decodable_f32(probs, T, A, pr.ctypes.data if pr is not None else None, prob_scale,
+                                       blank_threshold, floor, out)
+    return out[:k].copy()
 
 
 def accuracy(best_ids, T, N, num_frames, flat_labels, label_lengths):

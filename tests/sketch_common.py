@@ -69,7 +69,9 @@ def compare(a, ref, seed, tol):
 LAYER_CASES = {"lstm512_d40": dict(mode=2, T=2000, N=16, D=40, H=512, seed=11),
                "lstm512_d1024": dict(mode=2, T=2000, N=16, D=1024, H=512, seed=12),
                # configs[2]: frame_subsampling_factor 3 -> T_max 667, minibatch 64
-               "lstm512_d1024_n64": dict(mode=2, T=667, N=64, D=1024, H=512, seed=13)}
+               "lstm512_d1024_n64": dict(mode=2, T=667, N=64, D=1024, H=512, seed=13),
+               # configs[4]: BGRU-1024 layers 2-5 (D = 2H), minibatch 32, run in bf16
+               "gru1024_d2048_n32": dict(mode=3, T=2000, N=32, D=2048, H=1024, seed=14, prec="bf16")}
 
 
 def recipe_rnn_params(oracle, mode, D, H, seed, stddev=0.02, bias=0.2):

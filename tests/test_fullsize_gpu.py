@@ -29,6 +29,10 @@ def test_layer_full_length_matches_oracle(kctc, gpu, oracle, case):
     T, N, D, H = c["T"], c["N"], c["D"], c["H"]
     w, x, dy = S.layer_inputs(kctc, oracle, case)
     r = kctc.Rnn(c["mode"], D, H, 1, True)
+    bf16 = c.get("prec") == "bf16"
+    if bf16:
+        r.set_precision("bf16")
+    tol = 1e-2 if bf16 else TOL  # bf16 operands (configs[4]): 2^-9 rounding, fp32 accumulation
     ws_b, res_b = r.sizes(T, N)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
     wd, xd, dyd = t(w), t(x), t(dy)
@@ -44,22 +48,26 @@ def test_layer_full_length_matches_oracle(kctc, gpu, oracle, case):
     assert r.device_status() == 0
     y, dx, dw = y.cpu().numpy(), dx.cpu().numpy(), dw.cpu().numpy()
     seed = c["seed"]
-    errs = {"y": S.compare(y, S.load(g, f"{case}.y"), seed, TOL),
-            "dx": S.compare(dx, S.load(g, f"{case}.dx"), seed + 1, TOL),
-            "dw": S.compare(dw, S.load(g, f"{case}.dw"), seed + 2, TOL)}
+    errs = {"y": S.compare(y, S.load(g, f"{case}.y"), seed, tol),
+            "dx": S.compare(dx, S.load(g, f"{case}.dx"), seed + 1, tol),
+            "dw": S.compare(dw, S.load(g, f"{case}.dw"), seed + 2, tol)}
     print(case, {k: {kk: f"{vv:.2e}" for kk, vv in v.items() if kk != "ok"} for k, v in errs.items()})
     for k, e in errs.items():
         assert e["ok"], (k, e)
     # every dW region (W, R, bW, bR of both directions) keeps its norm
     regs = []
     for pl in range(2):
-        for lin in range(8):
+        for lin in range(8 if c["mode"] == 2 else 6):
             for isb in (0, 1):
                 off, (h, cc) = r.lin_offset(pl, lin, isb)
                 regs.append(np.linalg.norm(dw[off:off + h * cc].astype(np.float64)))
     ref = g[f"{case}.dw_region_norms"]
-    np.testing.assert_allclose(regs, ref, rtol=TOL)
-    np.testing.assert_allclose(y[0, :, :H], g[f"{case}.y_t0_fwd"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(regs, ref, rtol=tol)
+    # t = 0 of the forward direction depends on x[0] only: element-wise; in bf16
+    # the projection over D = 2048 terms of ~0.02 * 0.8 carries ~sqrt(D) 2^-9
+    # of that scale per element (~1.5e-3 rms)
+    np.testing.assert_allclose(y[0, :, :H], g[f"{case}.y_t0_fwd"], rtol=1e-5 if not bf16 else 1e-2,
+                               atol=1e-6 if not bf16 else 8e-3)
 
 
 def test_train_step_full_size_matches_oracle(kctc, gpu, oracle):
