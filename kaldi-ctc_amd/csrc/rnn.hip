@@ -1669,10 +1669,10 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
 #pragma unroll
         for (int i = 0; i < 4; i++) o[i] = BF ? acc[c][i] : ldexpf(acc[c][i], ex[i]);
         const int off = (int)((obase + ((long)(w * CTW + c) * 64 + lane) * 4) * 4);
-        // write-through (sc1) payload in either mode: the stored lines leave
-        // the XCD's L2, so the consumers' sc1 loads read them from the
-        // Infinity Cache; only the flag stays in the shared L2 when local
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ro, off, 0, 16);
+        // local: plain stores keep the lines in the XCD's shared L2, where the
+        // consumers' sc1 loads find them; else write-through (sc1)
+        if (local) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ro, off, 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ro, off, 0, 16);
       }
     }
     REC_TRACE(ks, 7);
@@ -2026,7 +2026,8 @@ static void launch_mode(bool fwd, const RecParams &p, dim3 grid, size_t lds, hip
 // H / U producers in groups of 512 / (4 U) for the backward)
 template <int U, int H, int NTH>
 constexpr bool v6_shape_ok() {
-  return NTH == (U == 32 ? 512 : 256) && H % (16 * (NTH / 64)) == 0 && (H / U) % (NTH / (4 * U)) == 0;
+  return (NTH == (U == 32 ? 512 : 256) || (U == 16 && NTH == 512 && H == 512)) && H % (16 * (NTH / 64)) == 0 &&
+         (H / U) % (NTH / (4 * U)) == 0;
 }
 template <int MODE, int U, int H, int NTH, int P>
 static void launch6_shape(bool fwd, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
@@ -2053,20 +2054,24 @@ static void launch6_h(bool fwd, const RecParams &p, dim3 grid, size_t lds, hipSt
   }
 }
 template <int MODE, int P>
-static void launch6_u(bool fwd, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
+static void launch6_u(bool fwd, int nth, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
   switch (p.U) {
     case 8: launch6_h<MODE, 8, 256, P>(fwd, p, grid, lds, s); break;
-    case 16: launch6_h<MODE, 16, 256, P>(fwd, p, grid, lds, s); break;
+    case 16:
+      if (nth == 512) launch6_h<MODE, 16, 512, P>(fwd, p, grid, lds, s);
+      else launch6_h<MODE, 16, 256, P>(fwd, p, grid, lds, s);
+      break;
     default: launch6_h<MODE, 32, 512, P>(fwd, p, grid, lds, s); break;
   }
 }
-static void launch6(bool fwd, int mode, int prec, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
+static void launch6(bool fwd, int mode, int prec, int nth, const RecParams &p, dim3 grid, size_t lds,
+                    hipStream_t s) {
   if (mode == kLstm) {
-    if (prec == kPrecBf16) launch6_u<kLstm, kPrecBf16>(fwd, p, grid, lds, s);
-    else launch6_u<kLstm, kPrecX3>(fwd, p, grid, lds, s);
+    if (prec == kPrecBf16) launch6_u<kLstm, kPrecBf16>(fwd, nth, p, grid, lds, s);
+    else launch6_u<kLstm, kPrecX3>(fwd, nth, p, grid, lds, s);
   } else {
-    if (prec == kPrecBf16) launch6_u<kGru, kPrecBf16>(fwd, p, grid, lds, s);
-    else launch6_u<kGru, kPrecX3>(fwd, p, grid, lds, s);
+    if (prec == kPrecBf16) launch6_u<kGru, kPrecBf16>(fwd, nth, p, grid, lds, s);
+    else launch6_u<kGru, kPrecX3>(fwd, nth, p, grid, lds, s);
   }
 }
 static void launch_rec(bool fwd, int mode, const RecParams &p, dim3 grid, size_t lds, hipStream_t s,
@@ -2211,7 +2216,8 @@ static V6Cfg pick6(const RnnDesc &d, int N, bool fwd) {
   };
   auto take = [&](int U) {
     c.U = U;
-    c.nth = U == 32 ? 512 : 256;
+    // U = 16 at 512 threads (H = 512): K split over 8 waves (KCTC_FWD_NTH / KCTC_BWD_NTH)
+    c.nth = U == 32 ? 512 : (U == 16 && d.H == 512 && env_int(fwd ? "KCTC_FWD_NTH" : "KCTC_BWD_NTH", 256) == 512) ? 512 : 256;
     c.rg = rg;
     return c;
   };
@@ -2487,7 +2493,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     const hipEvent_t fork = chained ? fork_event(s) : nullptr;
     {
       ProfSpan ps(s, "rnn_fwd_rec");
-      if (ver == 6) launch6(true, d.mode, d.prec, p, grid, lds, s);
+      if (ver == 6) launch6(true, d.mode, d.prec, c6.nth, p, grid, lds, s);
       else launch_rec(true, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
@@ -2616,7 +2622,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     const hipEvent_t fork = streamed ? fork_event(s) : nullptr;
     {
       ProfSpan ps(s, "rnn_bwd_rec");
-      if (ver == 6) launch6(false, d.mode, d.prec, p, grid, lds, s);
+      if (ver == 6) launch6(false, d.mode, d.prec, c6.nth, p, grid, lds, s);
       else launch_rec(false, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
