@@ -1544,6 +1544,11 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   const int pos = tid % POS, pg = tid / POS;
   const int pln = U >= 16 ? pos : (pos >> 3) * 16 + fr0 + (pos & 7);
   const long coff = (long)grp * xgrp + (long)d * NWG * PSTR + ((long)ct_own * 64 + pln) * 4 + (long)pg * PSTR;
+  // a C-fragment lane holds rows 4 (lane / 16) .. +3 of the group: quads past N
+  // are neither stored nor loaded (a group of fewer than 16 sequences moves
+  // only its own rows)
+  const bool crow_live = n0 + 4 * ((pln & 63) >> 4) < N;
+  const bool prow_live = n0 + 4 * fq < N;
   // where element (en, eu) finds its sum: own tile eu / 16, lane (en / 4) * 16
   // + (eu % 16) (U = 8: compacted to 8 per row quad), register en % 4
   const int epos = (eu >> 4) * 64 + (en >> 2) * (U < 16 ? U : 16) + (eu & 15);
@@ -1553,6 +1558,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   unsigned *myflag = flag6(p, grp, d, g, NWG);
   if (tid == 0) loc_lds = 0;
   const int local = (p.xpd && p.allow_local) ? probe6(p, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
+  if (p.trace && tid == 0) p.trace[(long)blockIdx.x * 16 + 9] = (unsigned long long)(local + 1);  // step 0, slot 9
   int t_prev = -1;
   for (int k = T - 1; k >= 0 && !bad; k--) {
     const int t = d == 0 ? k : T - 1 - k;
@@ -1564,7 +1570,8 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
       const auto rs = rsrc(p.xch + (long)(ks - 1) * xstep, (unsigned)(xstep * 4));
       u32x4 v[PER];
 #pragma unroll
-      for (int i = 0; i < PER; i++) v[i] = ld_sc1(rs, (unsigned)((coff + (long)i * NGRP * PSTR) * 4));
+      for (int i = 0; i < PER; i++)
+        v[i] = crow_live ? ld_sc1(rs, (unsigned)((coff + (long)i * NGRP * PSTR) * 4)) : u32x4{0u, 0u, 0u, 0u};
       floatx4 sm = __builtin_bit_cast(floatx4, v[0]);
 #pragma unroll
       for (int i = 1; i < PER; i++) sm += __builtin_bit_cast(floatx4, v[i]);
@@ -1671,8 +1678,12 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
         const int off = (int)((obase + ((long)(w * CTW + c) * 64 + lane) * 4) * 4);
         // local: plain stores keep the lines in the XCD's shared L2, where the
         // consumers' sc1 loads find them; else write-through (sc1)
-        if (local) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ro, off, 0, 0);
-        else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ro, off, 0, 16);
+        if (!prow_live) {
+        } else if (local) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ro, off, 0, 0);
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ro, off, 0, 16);
+        }
       }
     }
     REC_TRACE(ks, 7);
@@ -1876,6 +1887,8 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // publish geometry: store thread s < NP * 16 * CH: part = s / (16 CH), row, chunk
   const int sp = tid / (16 * CH), sn = (tid / CH) % 16, sch = tid % CH;
   const int kb0 = u0 >> 5, koff = (u0 & 31) + sch * 8;
+  // rows past N (a group of fewer than 16 sequences) are neither loaded nor stored
+  const bool arow_live = n0 + fr < N;
   const long gimg = (long)grp * XG;
   int t_prev = -1;
   for (int k = 0; k < T && !bad; k++) {
@@ -1892,10 +1905,12 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
 #pragma unroll
       for (int i = 0; i < KBW; i++) {
         const int kb = w + NWV * i;
-        if (kb < KB) {
+        if (kb < KB && arow_live) {
           const long o = gimg + ((((long)d * KB + kb) * NP) * 16 + fr) * 32 + fq * 8;
           ah[i] = ld_sc1(rs, (unsigned)(o * sizeof(AT)));
           if constexpr (!BF) al[i] = ld_sc1(rs, (unsigned)((o + 16 * 32) * sizeof(AT)));
+        } else {
+          ah[i] = al[i] = u32x4{0u, 0u, 0u, 0u};
         }
       }
 #pragma unroll
@@ -1966,7 +1981,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
       }
     }
     __syncthreads();
-    if (tid < NP * 16 * CH) {
+    if (tid < NP * 16 * CH && n0 + sn < N) {
       const u32x4 v = *reinterpret_cast<const u32x4 *>(stg + (sp * 16 + sn) * U + sch * 8);
       const long o = gimg + ((((long)d * KB + kb0) * NP + sp) * 16 + sn) * 32 + koff;
       __builtin_amdgcn_raw_buffer_store_b128(v, rsrc(xch + (long)t * XS, (unsigned)(XS * sizeof(AT))),
@@ -2026,7 +2041,7 @@ static void launch_mode(bool fwd, const RecParams &p, dim3 grid, size_t lds, hip
 // H / U producers in groups of 512 / (4 U) for the backward)
 template <int U, int H, int NTH>
 constexpr bool v6_shape_ok() {
-  return (NTH == (U == 32 ? 512 : 256) || (U == 16 && NTH == 512 && H == 512)) && H % (16 * (NTH / 64)) == 0 &&
+  return (NTH == (U == 32 ? 512 : 256) || (U == 16 && (NTH == 512 || NTH == 1024) && H == 512)) && H % (16 * (NTH / 64)) == 0 &&
          (H / U) % (NTH / (4 * U)) == 0;
 }
 template <int MODE, int U, int H, int NTH, int P>
@@ -2058,7 +2073,8 @@ static void launch6_u(bool fwd, int nth, const RecParams &p, dim3 grid, size_t l
   switch (p.U) {
     case 8: launch6_h<MODE, 8, 256, P>(fwd, p, grid, lds, s); break;
     case 16:
-      if (nth == 512) launch6_h<MODE, 16, 512, P>(fwd, p, grid, lds, s);
+      if (nth == 1024) launch6_h<MODE, 16, 1024, P>(fwd, p, grid, lds, s);
+      else if (nth == 512) launch6_h<MODE, 16, 512, P>(fwd, p, grid, lds, s);
       else launch6_h<MODE, 16, 256, P>(fwd, p, grid, lds, s);
       break;
     default: launch6_h<MODE, 32, 512, P>(fwd, p, grid, lds, s); break;
@@ -2216,8 +2232,12 @@ static V6Cfg pick6(const RnnDesc &d, int N, bool fwd) {
   };
   auto take = [&](int U) {
     c.U = U;
-    // U = 16 at 512 threads (H = 512): K split over 8 waves (KCTC_FWD_NTH / KCTC_BWD_NTH)
-    c.nth = U == 32 ? 512 : (U == 16 && d.H == 512 && env_int(fwd ? "KCTC_FWD_NTH" : "KCTC_BWD_NTH", 256) == 512) ? 512 : 256;
+    // U = 16 at H = 512 runs 512 threads (K split over 8 waves; measured on
+    // BLSTM-512 N=16: forward 31.9 -> 28.4, backward 34.4 -> 32.9 ms/step of
+    // recurrence vs 256 threads; 1024 threads 30.5 / 33.5); KCTC_FWD_NTH /
+    // KCTC_BWD_NTH = 256 | 512 | 1024 override
+    const int want_nth = env_int(fwd ? "KCTC_FWD_NTH" : "KCTC_BWD_NTH", d.H == 512 ? 512 : 256);
+    c.nth = U == 32 ? 512 : (U == 16 && d.H == 512 && (want_nth == 512 || want_nth == 1024)) ? want_nth : 256;
     c.rg = rg;
     return c;
   };

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Full check: GPU test suite (one process), then the measurement script
+# (smoke, bench with CPU baseline, rocprofv3 stats, PMC traffic passes).
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/gpu_tests.log; exit 1; }
+tail -1 gpurun_out/gpu_tests.log
+bash scripts/gpu_bench_prof.sh || exit 1
+python scripts/timeline.py gpurun_out/prof/run_kernel_trace.csv 50 > gpurun_out/timeline.txt 2>&1 || true

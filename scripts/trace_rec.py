@@ -23,6 +23,9 @@ def main(path):
         members = [list(range(d * nwg, (d + 1) * nwg)) for d in range(dirs)]
     active = sorted(b for m in members for b in m)
     tr = tr[:, active, :]
+    loc = tr[0, :, 9]
+    if loc.max() > 0 and loc.max() < 8:  # v6 backward: hand-off mode per workgroup (1 sc1, 2 XCD-local)
+        print(f"  XCD-local workgroups: {int((loc == 2).sum())} of {len(loc)}")
     idx = {b: i for i, b in enumerate(active)}
     us = 1e-2  # 100 MHz
     names = ["start->flags", "flags->loads", "loads->reduced", "reduced->published", "published->end"]
