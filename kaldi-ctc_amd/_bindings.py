@@ -26,6 +26,7 @@ SIGS = {
     "kcm_add_mat_mat": (ci, [vp, ci, ci, ci, ci, ci, cf, vp, cl, vp, cl, cf, vp, cl]),
     "kcm_add_mat_mat_x3_workspace": (sz, [ci, ci, ci]),
     "kcm_add_mat_mat_x3": (ci, [vp, ci, ci, ci, ci, ci, cf, vp, cl, vp, cl, cf, vp, cl, vp]),
+    "kcm_bench_gemm_packed": (cf, [vp, ci, ci, ci, ci, ci, ci]),
     "kcm_find_row_max_id": (ci, [vp, vp, cl, ci, vp]),
     "kcm_clip_gradient_rows": (ci, [vp, vp, cl, ci, cf, vp]),
     "kcm_add_vec_clipped": (ci, [vp, vp, vp, cl, cf, cf]),

@@ -77,6 +77,13 @@ struct X3PArgs {
   bool bf16 = false;
 };
 void gemm_x3p(hipStream_t s, const X3PArgs &g);
+// shapes gemm_x3p runs on 256 x 256 tiles (KCTC_GEMM256=0 turns them off)
+bool x3p_use_256(int M, int N);
+// split-K for gemm_x3p on a (M x N, KB k-blocks, batch) problem so that the
+// tiles fill the chip (callers size ws for it: split * batch * M * N floats)
+int x3p_pick_split(int M, int N, int KB, int batch);
+// ms per gemm_x3p on random packed operands (M x K times N x K), iters launches
+float x3p_bench(hipStream_t s, int M, int N, int K, bool bf16, int iters, int split);
 // bf16-packed operands for gemm_x3p(bf16): rows (out[b][r][KB][64], KB =
 // ceil(K / 64)) and columns (the transpose, source row k - shift), zero pad
 void bf16_pack_rows(hipStream_t s, const float *X, long ldx, int R, int K, __bf16 *out, int batch = 1, long sX = 0,

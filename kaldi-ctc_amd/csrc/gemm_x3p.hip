@@ -501,6 +501,165 @@ __global__ __launch_bounds__(NTH, 2) void gemm_x3p_kernel(PParams p) {
   }
 }
 
+// ---- 256 x 256 tiles for the large GEMMs ----------------------------------
+// Same packed operands and swizzled 128-B row images as x3p_tile, at 4x the
+// tile area: 512 threads = 8 waves as 2 (M) x 4 (N), each wave a 128 x 64
+// block of C (8 x 4 accumulators).  Per stage (one 128-B k block of both
+// operands, 64 KB) a wave issues 96 split-fp16 (or 64 bf16) MFMAs against 24
+// fragment reads, so the stage's LDS-DMA of the next block (8 x 16 B per
+// thread) lands behind ~3000 SIMD cycles of matrix work; two stages (128 KB
+// LDS), one workgroup per CU, one barrier per stage.  Tile ids are dealt to
+// the XCDs in contiguous runs (decode_tile's remap) so that the blocks of an
+// XCD share A and B panels in its L2.
+constexpr int TB2 = 256, NTH2 = 512, TILEB2 = TB2 * ROWB;  // 32 KB per operand tile per stage
+constexpr size_t kLds256 = 2 * 2 * (size_t)TILEB2 + 16;
+
+__device__ __forceinline__ void issue_tile256(const _Float16 *__restrict__ P, int rows, int r0, int KB, int kb,
+                                              unsigned char *dst) {
+  // wave w fills rows [32 w, 32 w + 32): 4 instructions of 8 rows x 128 B
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int q = w * 4 + i;
+    const int r = q * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (r & 7);
+    int gr = r0 + r;
+    gr = gr < rows ? gr : rows - 1;  // rows past the edge: any valid row (results discarded)
+    __builtin_amdgcn_global_load_lds(P + ((long)gr * KB + kb) * 64 + c * 8, dst + q * 1024, 16, 0, 0);
+  }
+}
+
+template <bool BFM>
+__device__ __forceinline__ void p256_tile(const PParams &p, unsigned char *lds, int tm, int tn, int b, int ks) {
+  const _Float16 *A = p.A + (long)b * p.sA;
+  const _Float16 *B = p.B + (long)b * p.sB;
+  const int m0 = tm * TB2, n0 = tn * TB2;
+  const int kb0 = ks * p.kbchunk, kb1 = min(p.KB, kb0 + p.kbchunk);
+  const int nk = kb1 > kb0 ? kb1 - kb0 : 0;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = (wid >> 2) * 128, wn = (wid & 3) * 64;
+  const int fr = lane & 15, fq = lane >> 4;
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (nk > 0) {
+    issue_tile256(A, p.M, m0, p.KB, kb0, lds);
+    issue_tile256(B, p.N, n0, p.KB, kb0, lds + TILEB2);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int it = 0; it < nk; it++) {
+    unsigned char *cur = lds + (it & 1) * 2 * TILEB2;
+    unsigned char *nxt = lds + ((it + 1) & 1) * 2 * TILEB2;
+    if (it + 1 < nk) {
+      issue_tile256(A, p.M, m0, p.KB, kb0 + it + 1, nxt);
+      issue_tile256(B, p.N, n0, p.KB, kb0 + it + 1, nxt + TILEB2);
+    }
+    halfx8 bh[4], bl[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      bh[j] = frag(cur + TILEB2, wn + j * 16 + fr, fq);
+      bl[j] = frag(cur + TILEB2, wn + j * 16 + fr, 4 + fq);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const halfx8 ah = frag(cur, wm + i * 16 + fr, fq);
+      const halfx8 al = frag(cur, wm + i * 16 + fr, 4 + fq);
+      if constexpr (BFM) {
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ah),
+                                                              __builtin_bit_cast(bf16x8, bh[j]), acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al),
+                                                              __builtin_bit_cast(bf16x8, bl[j]), acc[i][j], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // epilogue: acc[i][j][r] -> C[m0+wm+16i+4fq+r][n0+wn+16j+fr], times 2^-(eA + eB)
+  const int *eA = p.eA ? p.eA + (long)b * p.seA : nullptr;
+  const int *eB = p.eB ? p.eB + (long)b * p.seB : nullptr;
+  int eb[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int col = n0 + wn + j * 16 + fr;
+    eb[j] = col < p.N ? (eB ? eB[col] : p.eB0) : 0;
+  }
+  float *W = p.split > 1 ? p.ws + ((long)ks * p.batch + b) * (long)p.M * p.N : nullptr;
+  float *C = p.C + (long)b * p.sC;
+  const float *bias = p.bias ? p.bias + (long)b * p.sBias : nullptr;
+  const float *bias2 = p.bias2 ? p.bias2 + (long)b * p.sBias : nullptr;
+  float badd[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int col = n0 + wn + j * 16 + fr;
+    badd[j] = 0.f;
+    if (!W && col < p.N) {
+      if (bias) badd[j] += bias[col];
+      if (bias2) badd[j] += bias2[col];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int row = m0 + wm + i * 16 + fq * 4 + r;
+      if (row >= p.M) continue;
+      const int ea = eA ? eA[row] : p.eA0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int col = n0 + wn + j * 16 + fr;
+        if (col >= p.N) continue;
+        const float v = ldexpf(acc[i][j][r], -(ea + eb[j]));
+        if (W) {
+          W[(long)row * p.N + col] = v;
+        } else {
+          float *c = C + (long)row * p.ldc + col;
+          float o = p.alpha * v + badd[j];
+          if (p.beta != 0.f) o += p.beta * *c;
+          *c = o;
+        }
+      }
+    }
+}
+
+template <bool BFM>
+__global__ __launch_bounds__(NTH2, 1) void gemm_p256_kernel(PParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];  // ONE shared array
+  int *next = reinterpret_cast<int *>(lds + 2 * 2 * TILEB2);
+  const int total = p.tiles * p.batch * p.split;
+  if (p.counter) {  // dynamic scheduling (beside a persistent kernel)
+    while (true) {
+      if (threadIdx.x == 0) *next = atomicAdd(p.counter, 1);
+      __syncthreads();
+      const int id = __builtin_amdgcn_readfirstlane(*next);
+      __syncthreads();
+      if (id >= total) break;
+      int tm, tn, b, ks;
+      decode_tile(p, id, total, false, tm, tn, b, ks);
+      p256_tile<BFM>(p, lds, tm, tn, b, ks);
+    }
+    return;
+  }
+  for (int id = blockIdx.x; id < total; id += gridDim.x) {
+    int tm, tn, b, ks;
+    decode_tile(p, id, total, true, tm, tn, b, ks);
+    p256_tile<BFM>(p, lds, tm, tn, b, ks);
+  }
+}
+
 __global__ __launch_bounds__(256) void x3p_splitk_reduce(PParams p) {
   const long total = (long)p.batch * p.M * p.N;
   const long MN = (long)p.M * p.N;
@@ -813,6 +972,68 @@ void x3p_pack_cols(hipStream_t s, const float *X, long ldx, int R, int Cn, int s
                      sX, out, sOut, eout, sE, cmax, sCm, bound);
 }
 
+namespace {
+// uniform [-1, 1) halves (fp16 or bf16 bit patterns) from a counter hash
+__global__ void fill_halves_kernel(unsigned short *p, long n, unsigned seed, int bf16) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    unsigned x = (unsigned)i * 2654435761u ^ seed;
+    x ^= x >> 15; x *= 2246822519u; x ^= x >> 13; x *= 3266489917u; x ^= x >> 16;
+    const float v = (float)(x >> 8) * (2.0f / 16777216.0f) - 1.0f;
+    p[i] = bf16 ? __builtin_bit_cast(unsigned short, (__bf16)v) : __builtin_bit_cast(unsigned short, (_Float16)v);
+  }
+}
+}  // namespace
+
+float x3p_bench(hipStream_t s, int M, int N, int K, bool bf16, int iters, int split) {
+  const int KB = bf16 ? (K + 63) / 64 : (K + 31) / 32;
+  const long na = (long)M * KB * 64, nb = (long)N * KB * 64;
+  _Float16 *A = nullptr, *B = nullptr;
+  float *C = nullptr, *ws = nullptr;
+  KCTC_HIP_CHECK(hipMalloc(&A, na * 2));
+  KCTC_HIP_CHECK(hipMalloc(&B, nb * 2));
+  KCTC_HIP_CHECK(hipMalloc(&C, (long)M * N * 4));
+  if (split > 1) KCTC_HIP_CHECK(hipMalloc(&ws, (long)split * M * N * 4));
+  hipLaunchKernelGGL(fill_halves_kernel, dim3(1024), dim3(256), 0, s, reinterpret_cast<unsigned short *>(A), na, 1u,
+                     bf16 ? 1 : 0);
+  hipLaunchKernelGGL(fill_halves_kernel, dim3(1024), dim3(256), 0, s, reinterpret_cast<unsigned short *>(B), nb, 2u,
+                     bf16 ? 1 : 0);
+  X3PArgs g;
+  g.M = M; g.N = N; g.KB = KB; g.A = A; g.B = B; g.C = C; g.ldc = N; g.bf16 = bf16;
+  g.split_k = split; g.ws = ws;
+  for (int i = 0; i < 2; i++) gemm_x3p(s, g);
+  hipEvent_t e0, e1;
+  KCTC_HIP_CHECK(hipEventCreate(&e0));
+  KCTC_HIP_CHECK(hipEventCreate(&e1));
+  KCTC_HIP_CHECK(hipEventRecord(e0, s));
+  for (int i = 0; i < iters; i++) gemm_x3p(s, g);
+  KCTC_HIP_CHECK(hipEventRecord(e1, s));
+  KCTC_HIP_CHECK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  KCTC_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
+  (void)hipFree(A); (void)hipFree(B); (void)hipFree(C);
+  if (ws) (void)hipFree(ws);
+  return ms / iters;
+}
+
+bool x3p_use_256(int M, int N) {
+  static const int on = [] {
+    const char *e = getenv("KCTC_GEMM256");
+    return e ? atoi(e) : 1;
+  }();
+  return on && M >= 192 && N >= 192;
+}
+
+int x3p_pick_split(int M, int N, int KB, int batch) {
+  const int tb = x3p_use_256(M, N) ? TB2 : TB;
+  const long tiles = (long)ceil_div(M, tb) * ceil_div(N, tb) * batch;
+  if (tiles >= 384 || KB < 16) return 1;
+  long want = (512 + tiles - 1) / tiles;
+  want = std::min<long>(want, KB / 8);
+  want = std::min<long>(want, 32);
+  return want < 1 ? 1 : (int)want;
+}
+
 void gemm_x3p(hipStream_t s, const X3PArgs &g) {
   if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return;
   PParams p;
@@ -826,6 +1047,12 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
   p.kbchunk = p.split > 1 ? ceil_div(g.KB, p.split) : (g.KB > 0 ? g.KB : 1);
   if (p.split > 1) p.split = ceil_div(g.KB, p.kbchunk);
   p.ws = g.ws;
+  // large shapes on 256 x 256 tiles (KCTC_GEMM256=0: 128 x 128 everywhere)
+  const bool t256 = !g.stream_flags && x3p_use_256(g.M, g.N);
+  if (t256) {
+    p.gx = ceil_div(g.N, TB2);
+    p.tiles = p.gx * ceil_div(g.M, TB2);
+  }
   const int total = p.tiles * p.batch * p.split;
   int blocks = total;
   if (g.max_blocks > 0 && total > g.max_blocks) blocks = std::max(8, g.max_blocks / 8 * 8);
@@ -843,9 +1070,17 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBase));
     KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_x3p_kernel<true>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsStream));
+    KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_p256_kernel<false>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds256));
+    KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_p256_kernel<true>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds256));
     attr = true;
   }
-  if (g.bf16) {
+  if (t256) {
+    if (g.bf16 && (p.eA || p.eB)) throw std::invalid_argument("gemm_x3p: bf16 operands take no exponents");
+    if (g.bf16) hipLaunchKernelGGL(gemm_p256_kernel<true>, dim3(blocks), dim3(NTH2), kLds256, s, p);
+    else hipLaunchKernelGGL(gemm_p256_kernel<false>, dim3(blocks), dim3(NTH2), kLds256, s, p);
+  } else if (g.bf16) {
     if (p.sflags || p.eA || p.eB) throw std::invalid_argument("gemm_x3p: bf16 operands take no exponents / streaming");
     hipLaunchKernelGGL((gemm_x3p_kernel<false, true>), dim3(blocks), dim3(NTH), kLdsBase, s, p);
   } else if (p.sflags) {

@@ -87,11 +87,12 @@ RnnReserveLayout rnn_reserve_layout(const RnnDesc &d, int T, int N) {
 static long drec_split_floats(const RnnDesc &d, int T, int N) {
   long need = 0;
   const int G4 = d.nw() * d.H;
+  const int KB = (int)(((long)T * N + 31) / 32);  // packed k blocks over the frames (x3; bf16 needs fewer)
   for (int l = 0; l < d.layers; l++) {
     const long K = (long)(T > 1 ? T - 1 : 1) * N;
-    int s = gemm_pick_split(G4, d.H, (int)K, d.dirs);
+    int s = std::max(gemm_pick_split(G4, d.H, (int)K, d.dirs), x3p_pick_split(G4, d.H, KB, d.dirs));
     if (s > 1) need = std::max(need, (long)s * d.dirs * G4 * d.H);
-    s = gemm_pick_split(G4, d.din(l), (int)((long)T * N), d.dirs);
+    s = std::max(gemm_pick_split(G4, d.din(l), (int)((long)T * N), d.dirs), x3p_pick_split(G4, d.din(l), KB, d.dirs));
     if (s > 1) need = std::max(need, (long)s * d.dirs * G4 * d.din(l));
   }
   return need;
@@ -1580,8 +1581,8 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
     }
     asm volatile("" ::: "memory");
     // behind the hand-off loads: next step's operands, last step's row-major dGates
-    if (t_prev >= 0) e_store(t_prev);
-    if (k > 0 && !p.nopf) prefetch(k - 1);
+    if (t_prev >= 0 && !(p.nopf & 2)) e_store(t_prev);
+    if (k > 0 && !(p.nopf & 1)) prefetch(k - 1);
     __syncthreads();
     if (has_e) {
       float dhr = 0.f;
@@ -1934,8 +1935,8 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     }
     asm volatile("" ::: "memory");
     // behind the hand-off loads: last step's row-major outputs, next step's input projection
-    if (t_prev >= 0) out_store(t_prev);
-    if (k + 1 < T && !p.nopf) gin_load(d == 0 ? t + 1 : t - 1, gnx);
+    if (t_prev >= 0 && !(p.nopf & 2)) out_store(t_prev);
+    if (k + 1 < T && !(p.nopf & 1)) gin_load(d == 0 ? t + 1 : t - 1, gnx);
 #pragma unroll
     for (int ct = 0; ct < CT; ct++)
 #pragma unroll
@@ -2781,7 +2782,8 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
         x.B = reinterpret_cast<const _Float16 *>(Xt);
         x.C = dwl; x.ldc = Din; x.beta = 1.f;
         x.batch = dirs; x.sC = pls;
-        x.split_k = g.split_k; x.ws = ws; x.max_blocks = g.max_blocks; x.tile_counter = g.tile_counter;
+        x.split_k = x3p_pick_split((int)G4, Din, KB, dirs); x.ws = ws;
+        x.max_blocks = g.max_blocks; x.tile_counter = g.tile_counter;
         ProfSpan ps(s, "gemm_bwd_w");
         gemm_x3p(s, x);
       }
@@ -2793,7 +2795,7 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
         x.B = reinterpret_cast<const _Float16 *>(Yt); x.sB = (long)H * KB * 64;
         x.C = dwl + (d.lin_offset(l * dirs, NW, false) - pl0); x.ldc = H; x.beta = 1.f;
         x.batch = dirs; x.sC = pls;
-        x.split_k = gemm_pick_split((int)G4, H, (int)((long)(T - 1) * N), dirs); x.ws = ws;
+        x.split_k = x3p_pick_split((int)G4, H, KB, dirs); x.ws = ws;
         x.max_blocks = max_blocks;
         if (max_blocks > 0) x.tile_counter = reinterpret_cast<int *>(fl + 1009);
         ProfSpan ps(s, "gemm_bwd_r");
@@ -2839,7 +2841,8 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       x.B = Xt; x.eB = eX;
       x.C = dwl; x.ldc = Din; x.beta = 1.f;
       x.batch = dirs; x.sC = pls;
-      x.split_k = g.split_k; x.ws = ws; x.max_blocks = g.max_blocks; x.tile_counter = g.tile_counter;
+      x.split_k = x3p_pick_split((int)G4, Din, KBt, dirs); x.ws = ws;
+      x.max_blocks = g.max_blocks; x.tile_counter = g.tile_counter;
       ProfSpan ps(s, "gemm_bwd_w");
       gemm_x3p(s, x);
     } else {
@@ -2872,7 +2875,8 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
         x.B = Yt; x.eB = eY; x.sB = (long)H * KBt * 64; x.seB = H;
         x.C = r.C; x.ldc = H; x.beta = 1.f;
         x.batch = dirs; x.sC = pls;
-        x.split_k = r.split_k; x.ws = ws; x.max_blocks = max_blocks; x.tile_counter = r.tile_counter;
+        x.split_k = x3p_pick_split((int)G4, H, KBt, dirs); x.ws = ws;
+        x.max_blocks = max_blocks; x.tile_counter = r.tile_counter;
         gemm_x3p(s, x);
       } else {
         gemm_f32(s, r);

@@ -210,7 +210,9 @@ def test_gemm_matches_numpy(kctc, gpu, ta, tb, M, N, K):
 
 
 @pytest.mark.parametrize("ta,tb,M,N,K", [(0, 0, 77, 41, 40), (0, 1, 300, 130, 257), (1, 0, 64, 96, 1000),
-                                         (1, 1, 33, 17, 9), (0, 1, 1024, 1024, 1024), (1, 0, 512, 256, 4000)])
+                                         (1, 1, 33, 17, 9), (0, 1, 1024, 1024, 1024), (1, 0, 512, 256, 4000),
+                                         # 256 x 256 tiles with ragged edges in both dimensions
+                                         (0, 1, 300, 260, 257), (1, 0, 700, 450, 3000)])
 def test_gemm_x3_matches_numpy(kctc, gpu, ta, tb, M, N, K):
     """Split-fp16 GEMM: fp32-class accuracy, also for rows / columns whose
     magnitudes differ by many orders (per-row / per-column power-of-two scaling)."""
