@@ -237,6 +237,7 @@ struct RecParams {
   int poll_sleep;   // v6: s_sleep between flag polls
   int nopf;         // diagnostic (KCTC_DIAG_NOPF): skip the operand prefetch (wrong results)
   int e_sc1;        // v6 backward: dGates rows written through (sc1) for a streaming consumer
+  int wwait;        // v6: per-wave waits on the producers a wave reads (else wave 0 waits for all)
   unsigned *cmax;   // v6 backward: column max |DX| [dirs * nW * H] (GRU: then |E|), as float bits
 };
 
@@ -1368,6 +1369,28 @@ __device__ __forceinline__ void wait_flags6(const unsigned *f0, int nwg, unsigne
   __syncthreads();
   if (*bad_lds) bad = 1;
 }
+// Per-wave wait (KCTC_FWD_WWAIT / KCTC_BWD_WWAIT): a wave waits only for the
+// producers whose rows IT loads -- lane j polls producer prod (-1: none) --
+// and goes on to its own loads and MFMAs while the other waves still wait, so
+// the hand-off of the last producer to publish costs only the loads of the
+// waves that read it.  No workgroup barrier (the step's next one follows the
+// K reduction); a timeout sets *bad_lds for the barrier after.
+__device__ __forceinline__ bool wave_wait_prod(const unsigned *f0, int prod, unsigned epoch, unsigned *err,
+                                               int *bad_lds, int sleep) {
+  int spins = 0;
+  while (true) {
+    const bool ok =
+        prod < 0 || __hip_atomic_load(f0 + (long)prod * kFlagStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= epoch;
+    if (__all(ok)) return true;
+    if (++spins > kSpinLimit ||
+        ((spins & 255) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+      if ((threadIdx.x & 63) == 0) *bad_lds = 1;
+      return false;
+    }
+    if (sleep) __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 // Placement probe of a v6 launch in XCD-slot mapping: 1 iff every workgroup of
 // direction d reads the same HW_REG_XCC_ID (then the hand-off may stay in that
 // XCD's L2: plain payload and flag stores, sc1 loads).  Publishes epoch 1.
@@ -1550,6 +1573,13 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   // only its own rows)
   const bool crow_live = n0 + 4 * ((pln & 63) >> 4) < N;
   const bool prow_live = n0 + 4 * fq < N;
+  // per-wave wait: the producers of the groups this wave's threads sum
+  int wprod = -1;
+  {
+    const int pgA = (tid & ~63) / POS, pgB = min(NGRP - 1, ((tid & ~63) + 63) / POS);
+    const int gi = lane / PER, i = lane - gi * PER;
+    if (pgA + gi <= pgB) wprod = pgA + gi + i * NGRP;
+  }
   // where element (en, eu) finds its sum: own tile eu / 16, lane (en / 4) * 16
   // + (eu % 16) (U = 8: compacted to 8 per row quad), register en % 4
   const int epos = (eu >> 4) * 64 + (en >> 2) * (U < 16 ? U : 16) + (eu & 15);
@@ -1566,7 +1596,11 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
     const int ks = T - 1 - k;  // steps done before this one
     REC_TRACE(ks, 0);
     if (ks > 0) {
-      wait_flags6(flag6(p, grp, d, 0, NWG), NWG, (unsigned)(ks + 1), p.err, bad, &bad_lds, p.poll_sleep);
+      if (p.wwait) {
+        if (!wave_wait_prod(flag6(p, grp, d, 0, NWG), wprod, (unsigned)(ks + 1), p.err, &bad_lds, p.poll_sleep)) bad = 1;
+      } else {
+        wait_flags6(flag6(p, grp, d, 0, NWG), NWG, (unsigned)(ks + 1), p.err, bad, &bad_lds, p.poll_sleep);
+      }
       REC_TRACE(ks, 1);
       const auto rs = rsrc(p.xch + (long)(ks - 1) * xstep, (unsigned)(xstep * 4));
       u32x4 v[PER];
@@ -1584,6 +1618,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
     if (t_prev >= 0 && !(p.nopf & 2)) e_store(t_prev);
     if (k > 0 && !(p.nopf & 1)) prefetch(k - 1);
     __syncthreads();
+    if (bad_lds) bad = 1;
     if (has_e) {
       float dhr = 0.f;
       if (ks > 0) {
@@ -1890,6 +1925,13 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   const int kb0 = u0 >> 5, koff = (u0 & 31) + sch * 8;
   // rows past N (a group of fewer than 16 sequences) are neither loaded nor stored
   const bool arow_live = n0 + fr < N;
+  // per-wave wait: the producers of the k blocks this wave loads (32 / U per block)
+  int wprod = -1;
+  {
+    constexpr int PPK = 32 / U;
+    const int i = lane / PPK, kb = w + NWV * i;
+    if (i < KBW && kb < KB) wprod = kb * PPK + lane % PPK;
+  }
   const long gimg = (long)grp * XG;
   int t_prev = -1;
   for (int k = 0; k < T && !bad; k++) {
@@ -1899,7 +1941,11 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     for (int ct = 0; ct < CT; ct++) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
     REC_TRACE(k, 0);
     if (k > 0) {
-      wait_flags6(flag6(p, grp, d, 0, NWG), NWG, (unsigned)(k + 1), p.err, bad, &bad_lds, p.poll_sleep);
+      if (p.wwait) {
+        if (!wave_wait_prod(flag6(p, grp, d, 0, NWG), wprod, (unsigned)(k + 1), p.err, &bad_lds, p.poll_sleep)) bad = 1;
+      } else {
+        wait_flags6(flag6(p, grp, d, 0, NWG), NWG, (unsigned)(k + 1), p.err, bad, &bad_lds, p.poll_sleep);
+      }
       REC_TRACE(k, 1);
       const auto rs = rsrc(xch + (long)tp * XS, (unsigned)(XS * sizeof(AT)));
       u32x4 ah[KBW], al[KBW];
@@ -1942,6 +1988,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
 #pragma unroll
       for (int i = 0; i < 4; i++) red[(w * 16 + fq * 4 + i) * RP + ct * 16 + fr] = acc[ct][i];
     __syncthreads();
+    if (bad_lds) bad = 1;
     REC_TRACE(k, 3);
     if (has_e) {
       float rh[NW];
@@ -2507,6 +2554,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
     p.poll_sleep = env_int("KCTC_POLL_SLEEP", 1);
     p.nopf = env_int("KCTC_DIAG_NOPF", 0);
+    p.wwait = env_int("KCTC_FWD_WWAIT", 1);  // measured: forward recurrence 29.7 -> 28.6 ms/step
     const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : dirs * p.nwg * p.rg);
     RecTrace tr;
     if (tr.arm("fwd", grid.x)) p.trace = tr.dev;
@@ -2621,6 +2669,10 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
       p.allow_local = env_int("KCTC_LOCAL", 1);
       p.poll_sleep = env_int("KCTC_POLL_SLEEP", 1);
       p.nopf = env_int("KCTC_DIAG_NOPF", 0);
+      // off: the backward's waves 0-3 still have the step's write-through
+      // dGates rows outstanding when they would poll (their first poll waits
+      // for them): measured 34.2 -> 35.4 ms/step with per-wave waits
+      p.wwait = env_int("KCTC_BWD_WWAIT", 0);
       p.xch = xch_acquire(sizeof(float) * (size_t)T * dirs * p.nwg * (16 * H + 64) * p.rg, s);
     } else {
       p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
