@@ -70,10 +70,12 @@ struct X3PArgs {
   const unsigned *stream_flags = nullptr;
   int stream_nwg = 0, stream_T = 0, stream_N = 0;
   long stream_step = 0;              // halves per producer step image (A = image of step 0)
+  int stream_rg = 1;                  // producer row groups (N > 16): flags and image parts per group
+  long stream_group_step = 0;         // halves per row group's part of a step image
   unsigned *stream_err = nullptr;    // set (bit 2) if the producer stops publishing
   // bf16 operands (bf16_pack_rows / _cols: [rows][KB][64] bf16, KB = 64-k
   // blocks, no exponents): two v_mfma_f32_16x16x32_bf16 per stage, fp32
-  // accumulation; not with streaming
+  // accumulation; streaming: A = a bf16 v6 forward's h images (eA0 = 0)
   bool bf16 = false;
 };
 void gemm_x3p(hipStream_t s, const X3PArgs &g);
@@ -113,8 +115,10 @@ struct X3PBwdStream {
   int *cnt = nullptr;                  // x3p_bwd_stream_ints(M, N) ints (zeroed here)
   const unsigned *flags = nullptr;     // producer flag lines
   int nwg = 0, T = 0, Nf = 0;
+  int rg = 1;                          // producer row groups of 16 sequences
   unsigned *err = nullptr;
   int blocks = 0;                      // persistent blocks (each takes a CU: 96 KB LDS)
+  bool bf16 = false;                   // rows packed as bf16 ([M][KB][64], KB 64-k blocks), B bf16, no exponents
 };
 size_t x3p_bwd_stream_ints(int M, int N);
 void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a);

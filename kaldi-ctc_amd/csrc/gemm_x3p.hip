@@ -53,8 +53,10 @@ struct PParams {
   int eA0, eB0;
   const unsigned *sflags;  // streaming mode: producer flag lines
   int snwg, sT, sN;
+  int srg;                 // producer row groups of 16 sequences (flag lines and images per group)
   int nrt;                 // row tiles
   long sxs;                // halves per producer step image
+  long sxg;                // halves per row group's part of a step image
   unsigned *serr;          // producer's error word (wait timeout)
   // backward stream (x3p_bwd_stream_kernel)
   const float *E;          // source rows of direction d: E + row * lde + d * edoff (KB * 32 floats)
@@ -99,7 +101,8 @@ __device__ __forceinline__ void load_tile_xch(const PParams &p, const _Float16 *
     const int c = (lane & 7) ^ (r & 7);
     const int gr = min(r0 + r, p.M - 1);
     const int t = gr / p.sN, n = gr - t * p.sN;
-    const long off = (long)t * p.sxs + (((long)kb * 2 + (c >> 2)) * 16 + n) * 32 + (c & 3) * 8;
+    const long off = (long)t * p.sxs + (long)(n >> 4) * p.sxg + (((long)kb * 2 + (c >> 2)) * 16 + (n & 15)) * 32 +
+                     (c & 3) * 8;
     reg[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off * 2), 0, 16 /* sc1 */);
   }
 }
@@ -196,8 +199,12 @@ __device__ void x3p_wait_rows(const PParams &p, int m0, int *prog) {
     int s0 = 0, s1 = 0, spins = 0;
     bool failed = false;
     while (true) {
-      s0 = (int)wave_flags_min(p.sflags, p.snwg) - 2;  // epochs: step + 2
-      s1 = (int)wave_flags_min(p.sflags + 32L * p.snwg, p.snwg) - 2;
+      // epochs: step + 2; the slowest row group decides ([group][dir][wg] lines)
+      s0 = s1 = 1 << 30;
+      for (int gi = 0; gi < p.srg; gi++) {
+        s0 = min(s0, (int)wave_flags_min(p.sflags + 32L * (2 * gi) * p.snwg, p.snwg) - 2);
+        s1 = min(s1, (int)wave_flags_min(p.sflags + 32L * (2 * gi + 1) * p.snwg, p.snwg) - 2);
+      }
       if (s0 >= need0 && s1 >= need1) break;
       failed = wave_timed_out(p.serr, spins++, ts);
       if (failed) break;  // the producer stopped: flag it, finish on whatever is there
@@ -240,7 +247,9 @@ __device__ void wait_epoch(const PParams &p, int d, int need, int *seen) {
     bool failed = false;
     int m = 0, spins = 0;
     while (true) {
-      m = (int)wave_flags_min(p.sflags + 32L * d * p.snwg, p.snwg);
+      m = 1 << 30;
+      for (int gi = 0; gi < p.srg; gi++)
+        m = min(m, (int)wave_flags_min(p.sflags + 32L * (2 * gi + d) * p.snwg, p.snwg));
       if (m >= need) break;
       failed = wave_timed_out(p.serr, spins++, t0);
       if (failed) break;
@@ -399,7 +408,7 @@ __device__ __forceinline__ void x3p_tile(const PParams &p, unsigned char *lds, i
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int row = m0 + wm + i * 16 + fq * 4 + r;
-      ea[i][r] = row >= p.M ? 0
+      ea[i][r] = row >= p.M || BFM ? 0
                  : SM == 2  ? __hip_atomic_load(eA + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                  : p.eA     ? eA[row]
                             : p.eA0;
@@ -484,7 +493,7 @@ __global__ __launch_bounds__(NTH, 2) void gemm_x3p_kernel(PParams p) {
         const int rest = id / p.gx;
         b = rest % p.batch;
         tm = stream_row_tile(rest / p.batch, p.nrt, p.sT, p.sN);
-        x3p_tile<1>(p, lds, tm, tn, b, 0, prog);
+        x3p_tile<1, BFM>(p, lds, tm, tn, b, 0, prog);
       } else {
         decode_tile(p, id, total, false, tm, tn, b, ks);
         x3p_tile<0, BFM>(p, lds, tm, tn, b, ks, prog);
@@ -748,10 +757,10 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(const float *__restrict_
 // (wait done == P, then the tile with sc1 LDS-DMA, combine epilogue).  Slots
 // alternate directions in production order; jobs are taken from one counter,
 // so a GEMM job only ever waits for pack jobs that running blocks own.
-template <int KW>
+template <int KW, bool BFM>
 __device__ __forceinline__ void bwd_pack_rows(const PParams &p, int d, int r0, int r1) {
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int K = p.KB * 32;
+  const int K = p.KB * (BFM ? 64 : 32);
   for (int r = r0 + w; r < r1; r += 4) {
     const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p.E + (long)r * p.lde + d * p.edoff), 0,
                                                       K * 4, 0x00020000);
@@ -764,10 +773,24 @@ __device__ __forceinline__ void bwd_pack_rows(const PParams &p, int d, int r0, i
       if (k < K) v[i] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rx, k * 4, 0, 16));
       mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[i][0]), fabsf(v[i][1])), fmaxf(fabsf(v[i][2]), fabsf(v[i][3]))));
     }
-    mx = wave_max_l63(mx);
-    const int e = split_exp_d(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 63)));
     const auto ro = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16 *>(p.A) + (long)d * p.sA + (long)r * p.KB * 64, 0, p.KB * 128,
                                                       0x00020000);
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    if constexpr (BFM) {  // bf16 rows [KB][64], no exponent
+#pragma unroll
+      for (int i = 0; i < KW; i++) {
+        const int k = 4 * lane + 256 * i;
+        if (k < K) {
+          bf16x4 h;
+#pragma unroll
+          for (int j = 0; j < 4; j++) h[j] = (__bf16)v[i][j];
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h), ro, k * 2, 0, 16);
+        }
+      }
+      continue;
+    }
+    mx = wave_max_l63(mx);
+    const int e = split_exp_d(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 63)));
 #pragma unroll
     for (int i = 0; i < KW; i++) {
       const int k = 4 * lane + 256 * i;
@@ -775,7 +798,6 @@ __device__ __forceinline__ void bwd_pack_rows(const PParams &p, int d, int r0, i
         halfx4 h, l;
         split4(v[i], e, h, l);
         const int kb = k >> 5, off = k & 31;
-        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h), ro, (kb * 64 + off) * 2, 0, 16);
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, l), ro, (kb * 64 + 32 + off) * 2, 0, 16);
       }
@@ -785,7 +807,7 @@ __device__ __forceinline__ void bwd_pack_rows(const PParams &p, int d, int r0, i
   }
 }
 
-template <int KW>
+template <int KW, bool BFM>
 __global__ __launch_bounds__(NTH, 2) void x3p_bwd_stream_kernel(PParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   int *next = reinterpret_cast<int *>(lds + 2 * 2 * TILEB);
@@ -808,7 +830,7 @@ __global__ __launch_bounds__(NTH, 2) void x3p_bwd_stream_kernel(PParams p) {
         // (s = steps done before it; the last step gets epoch T + 2 at exit)
         const int ta = ra / p.sN, tb = (rb - 1) / p.sN;
         wait_epoch(p, d, d == 0 ? p.sT + 2 - ta : tb + 3, seen);
-        bwd_pack_rows<KW>(p, d, ra, rb);
+        bwd_pack_rows<KW, BFM>(p, d, ra, rb);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -820,7 +842,7 @@ __global__ __launch_bounds__(NTH, 2) void x3p_bwd_stream_kernel(PParams p) {
       __syncthreads();
     } else {
       wait_count(p.done + d * p.nrt + rt, p.P, p.serr);
-      x3p_tile<2>(p, lds, rt, r - p.P, d, 0, bc);
+      x3p_tile<2, BFM>(p, lds, rt, r - p.P, d, 0, bc);
       __syncthreads();
     }
   }
@@ -1059,6 +1081,7 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
   p.counter = g.tile_counter;
   p.eA0 = g.eA0; p.eB0 = g.eB0;
   p.sflags = g.stream_flags; p.snwg = g.stream_nwg; p.sT = g.stream_T; p.sN = g.stream_N;
+  p.srg = g.stream_rg; p.sxg = g.stream_group_step;
   p.nrt = ceil_div(g.M, TB);
   p.sxs = g.stream_step; p.serr = g.stream_err;
   if (p.counter) KCTC_HIP_CHECK(hipMemsetAsync(p.counter, 0, sizeof(int), s));
@@ -1070,6 +1093,8 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBase));
     KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_x3p_kernel<true>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsStream));
+    KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_x3p_kernel<true, true>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsStream));
     KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_p256_kernel<false>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds256));
     KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_p256_kernel<true>),
@@ -1080,8 +1105,8 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
     if (g.bf16 && (p.eA || p.eB)) throw std::invalid_argument("gemm_x3p: bf16 operands take no exponents");
     if (g.bf16) hipLaunchKernelGGL(gemm_p256_kernel<true>, dim3(blocks), dim3(NTH2), kLds256, s, p);
     else hipLaunchKernelGGL(gemm_p256_kernel<false>, dim3(blocks), dim3(NTH2), kLds256, s, p);
-  } else if (g.bf16) {
-    if (p.sflags || p.eA || p.eB) throw std::invalid_argument("gemm_x3p: bf16 operands take no exponents / streaming");
+  } else if (g.bf16 && !p.sflags) {
+    if (p.eA || p.eB) throw std::invalid_argument("gemm_x3p: bf16 operands take no exponents");
     hipLaunchKernelGGL((gemm_x3p_kernel<false, true>), dim3(blocks), dim3(NTH), kLdsBase, s, p);
   } else if (p.sflags) {
     if (!p.counter || p.split > 1 || g.stream_N <= 0 || g.stream_step <= 0 ||
@@ -1090,7 +1115,12 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
     // persistent blocks, each owning its CU's LDS, so the producer's
     // workgroups always find free CUs (max_blocks = CUs left to this GEMM)
     const int sb = std::min(stream_total(p), g.max_blocks > 0 ? g.max_blocks : 176);
-    hipLaunchKernelGGL(gemm_x3p_kernel<true>, dim3(sb), dim3(NTH), kLdsStream, s, p);
+    if (g.bf16) {  // A: the producer's bf16 h images (same chunk addressing, 64 k per block)
+      if (p.eB) throw std::invalid_argument("gemm_x3p: bf16 operands take no exponents");
+      hipLaunchKernelGGL((gemm_x3p_kernel<true, true>), dim3(sb), dim3(NTH), kLdsStream, s, p);
+    } else {
+      hipLaunchKernelGGL(gemm_x3p_kernel<true>, dim3(sb), dim3(NTH), kLdsStream, s, p);
+    }
     return;
   } else {
     hipLaunchKernelGGL(gemm_x3p_kernel<false>, dim3(blocks), dim3(NTH), kLdsBase, s, p);
@@ -1108,7 +1138,7 @@ size_t x3p_bwd_stream_ints(int M, int N) {
 
 void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a) {
   if (a.M <= 0 || a.N <= 0) return;
-  const int K = a.KB * 32;
+  const int K = a.KB * (a.bf16 ? 64 : 32);
   if (K > 4096 || a.Nf <= 0 || (long)a.M * a.N * 4 >= (1L << 31) || (long)a.M * a.KB * 128 >= (1L << 31) ||
       (a.lde & 3) || (a.edoff & 3))
     throw std::invalid_argument("gemm_x3p_bwd_stream: unsupported shape");
@@ -1123,7 +1153,7 @@ void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a) {
   p.P = 4;
   p.counter = a.cnt; p.done = a.cnt + 1; p.arrive = a.cnt + 1 + 2 * p.nrt;
   p.part = a.part;
-  p.sflags = a.flags; p.snwg = a.nwg; p.sT = a.T; p.sN = a.Nf; p.serr = a.err;
+  p.sflags = a.flags; p.snwg = a.nwg; p.sT = a.T; p.sN = a.Nf; p.serr = a.err; p.srg = a.rg;
   KCTC_HIP_CHECK(hipMemsetAsync(a.cnt, 0, sizeof(int) * x3p_bwd_stream_ints(a.M, a.N), s));
   const int total = 2 * p.nrt * (p.P + p.gx);
   const dim3 grid(std::min(total, a.blocks > 0 ? a.blocks : 96));
@@ -1136,9 +1166,15 @@ void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a) {
     }
     hipLaunchKernelGGL(kern, grid, dim3(NTH), kLdsStream, s, p);
   };
-  if (K <= 1024) go(x3p_bwd_stream_kernel<4>);
-  else if (K <= 2048) go(x3p_bwd_stream_kernel<8>);
-  else go(x3p_bwd_stream_kernel<16>);
+  if (a.bf16) {
+    if (K <= 1024) go(x3p_bwd_stream_kernel<4, true>);
+    else if (K <= 2048) go(x3p_bwd_stream_kernel<8, true>);
+    else go(x3p_bwd_stream_kernel<16, true>);
+  } else {
+    if (K <= 1024) go(x3p_bwd_stream_kernel<4, false>);
+    else if (K <= 2048) go(x3p_bwd_stream_kernel<8, false>);
+    else go(x3p_bwd_stream_kernel<16, false>);
+  }
 }
 
 }  // namespace kctc

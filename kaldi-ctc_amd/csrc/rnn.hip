@@ -2402,8 +2402,15 @@ void join_stream(hipStream_t s, hipStream_t other) {
 bool chain_ok(const RnnDesc &d, int ver, int T, int N, const RnnFwdChain *c) {
   if (!c || !c->d || !c->side || ver != 6 || d.dirs != 2 || !env_int("KCTC_FWD_STREAM", 1)) return false;
   const RnnDesc &n = *c->d;
-  if (n.D != d.dirs * d.H || !use_x3(n.D) || N > 16 || d.prec != kPrecX3 || n.prec != kPrecX3) return false;
-  const long xs = 2L * (d.H / 32) * 2 * 16 * 32;  // halves per step image (rnn_fwd_rec6)
+  // split-fp16 into split-fp16, or bf16 images into a bf16 projection
+  if (n.D != d.dirs * d.H || !use_x3(n.D) || N > 64 || d.prec != n.prec) return false;
+  // default: split-fp16 at N <= 16 only.  Row groups and bf16 run (and are
+  // tested) under KCTC_STREAM_ALL=1, but are slower on the recipe shapes: at
+  // N = 64 / T = 667 (configs[2]) and bf16 N = 32 (configs[4]) the GEMM on
+  // the CUs left beside the 128-workgroup recurrence outlasts it (990k ->
+  // 728k and 560k -> 389k frames/s measured), the 256-tile GEMM after it wins
+  if ((N > 16 || d.prec == kPrecBf16) && !env_int("KCTC_STREAM_ALL", 0)) return false;
+  const long xs = 2L * (d.H / 32) * (d.prec == kPrecBf16 ? 1 : 2) * 16 * 32 * ((N + 15) / 16);  // halves per step image
   if ((long)T * xs * 2 >= (1L << 31)) return false;
   return c->ws_bytes >= rnn_workspace_bytes(n, T, N) &&
          c->res_bytes >= sizeof(float) * (size_t)rnn_reserve_layout(n, T, N).total;
@@ -2414,15 +2421,19 @@ void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
                        unsigned *err) {
   KCTC_HIP_CHECK(hipStreamWaitEvent(c.side, fork, 0));  // after the producer's flag reset
   const RnnDesc &n = *c.d;
-  const int NW = n.nw(), G = NW * n.H, Din = n.D, KB = Din / 32;
+  const bool bf = n.prec == kPrecBf16;
+  const int NW = n.nw(), G = NW * n.H, Din = n.D, KB = Din / (bf ? 64 : 32);
   const long pl0 = n.lin_offset(0, 0, false), pls = n.pl_size(0);
   const float *wl = c.w + pl0;
   const PackLay pl = pack_layout(n, T, N);
   _Float16 *Bp = pk<_Float16>(c.workspace, n, T, N, pl.b);
-  int *eB = pk<int>(c.workspace, n, T, N, pl.eb);
+  int *eB = bf ? nullptr : pk<int>(c.workspace, n, T, N, pl.eb);
   {
     ProfSpan ps(c.side, "x3_pack_chain");
-    x3p_pack_rows(c.side, wl, Din, G, Din, Bp, eB, 0.f, n.dirs, pls, (long)G * KB * 64, (long)G);
+    if (bf)
+      bf16_pack_rows(c.side, wl, Din, G, Din, reinterpret_cast<__bf16 *>(Bp), n.dirs, pls, (long)G * KB * 64);
+    else
+      x3p_pack_rows(c.side, wl, Din, G, Din, Bp, eB, 0.f, n.dirs, pls, (long)G * KB * 64, (long)G);
   }
   const RnnReserveLayout lay = rnn_reserve_layout(n, T, N);
   static int cus = 0;
@@ -2432,19 +2443,21 @@ void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
     KCTC_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   }
   X3PArgs x;
+  x.bf16 = bf;
   x.M = T * N; x.N = G; x.KB = KB;
-  x.A = reinterpret_cast<const _Float16 *>(p.xch); x.eA0 = 14;
+  x.A = reinterpret_cast<const _Float16 *>(p.xch); x.eA0 = bf ? 0 : 14;  // x3 images hold h 2^14
   x.B = Bp; x.eB = eB;
   x.C = static_cast<float *>(c.reserve) + lay.G; x.ldc = (long)n.dirs * G;
   x.bias = wl + (n.lin_offset(0, 0, true) - pl0);
   x.bias2 = n.mode == kGru ? nullptr : wl + (n.lin_offset(0, NW, true) - pl0);
-  x.batch = n.dirs; x.sB = (long)G * KB * 64; x.seB = G; x.sC = G; x.sBias = pls;
+  x.batch = n.dirs; x.sB = (long)G * KB * 64; x.seB = bf ? 0 : G; x.sC = G; x.sBias = pls;
   x.tile_counter = reinterpret_cast<int *>(static_cast<char *>(c.workspace) + flags_offset(n, T, N));
   x.stream_flags = p.flags + 1024; x.stream_nwg = p.nwg; x.stream_T = T; x.stream_N = N;
-  x.stream_step = 2L * (d.H / 32) * 2 * 16 * 32; x.stream_err = err;
+  x.stream_group_step = 2L * (d.H / 32) * (bf ? 1 : 2) * 16 * 32;  // rnn_fwd_rec6's XG
+  x.stream_rg = p.rg; x.stream_step = x.stream_group_step * p.rg; x.stream_err = err;
   // every producer workgroup needs a CU of its own (96 KB LDS); the GEMM's
   // persistent blocks (96 KB each) take the rest minus a margin
-  x.max_blocks = env_int("KCTC_STREAM_BLOCKS", std::max(8, cus - d.dirs * p.nwg - 16));
+  x.max_blocks = env_int("KCTC_STREAM_BLOCKS", std::max(8, cus - d.dirs * p.nwg * p.rg - 16));
   {
     ProfSpan ps(c.side, "fwd_proj_stream");
     gemm_x3p(c.side, x);
@@ -2583,7 +2596,8 @@ namespace {
 void launch_bwd_stream(const RnnDesc &d, const RecParams &p, int l, const float *w, float *dxl, void *workspace,
                        int T, int N, hipStream_t ov, hipEvent_t fork, unsigned *err) {
   KCTC_HIP_CHECK(hipStreamWaitEvent(ov, fork, 0));  // after the flag reset, not after the recurrence
-  const int NW = d.nw(), H = d.H, G4 = NW * H, KB = G4 / 32, Din = d.din(l);
+  const bool bf = d.prec == kPrecBf16;
+  const int NW = d.nw(), H = d.H, G4 = NW * H, KB = G4 / (bf ? 64 : 32), Din = d.din(l);
   const long TN = (long)T * N;
   const long pl0 = d.lin_offset(l * d.dirs, 0, false), pls = d.pl_size(l);
   const float *wl = w + pl0;
@@ -2594,20 +2608,25 @@ void launch_bwd_stream(const RnnDesc &d, const RecParams &p, int l, const float 
   {
     ProfSpan ps(ov, "x3_pack_bwd_stream");
     for (int dir = 0; dir < 2; dir++) {
+      if (bf) {
+        bf16_pack_cols(ov, wl + dir * pls, Din, G4, Din, 0, reinterpret_cast<__bf16 *>(Bp) + (long)dir * Din * KB * 64);
+        continue;
+      }
       absmax_f32(ov, wl + dir * pls, Din, G4, Din, nullptr, cm + dir * Din);
       x3p_pack_cols(ov, wl + dir * pls, Din, G4, Din, 0, Bp + (long)dir * Din * KB * 64, eB + dir * Din,
                     cm + dir * Din, 0.f);
     }
   }
   X3PBwdStream a;
+  a.bf16 = bf;
   a.M = (int)TN; a.N = Din; a.KB = KB;
   a.E = p.DX; a.lde = 2L * G4; a.edoff = G4;
   a.Ap = Ap; a.eA = eA;
-  a.B = Bp; a.eB = eB; a.sB = (long)Din * KB * 64; a.seB = Din;
+  a.B = Bp; a.eB = bf ? nullptr : eB; a.sB = (long)Din * KB * 64; a.seB = Din;
   a.C = dxl; a.ldc = Din;
   a.part = pk<float>(workspace, d, T, N, pl.part);
   a.cnt = pk<int>(workspace, d, T, N, pl.cnt);
-  a.flags = p.flags + 1024; a.nwg = p.nwg; a.T = T; a.Nf = N; a.err = err;
+  a.flags = p.flags + 1024; a.nwg = p.nwg; a.T = T; a.Nf = N; a.err = err; a.rg = p.rg;
   a.blocks = env_int("KCTC_BWD_STREAM_BLOCKS", 96);
   ProfSpan ps(ov, "bwd_data_stream");
   gemm_x3p_bwd_stream(ov, a);
@@ -2683,8 +2702,10 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     // dx_l = sum_dir DX_dir W_dir   (lower layer's dy, or the caller's dx)
     float *dxl = (l == 0) ? dx : res + lay.per_layer * (l - 1) + lay.dout;
     // streamed: computed on `overlap` while the recurrence runs, from its rows as they appear
-    const bool streamed = dxl && overlap && ver == 6 && dirs == 2 && !p.xpd && p.rg == 1 && d.prec == kPrecX3 &&
-                          use_x3(NW * H) && NW * H <= 4096 && (long)TN * Din * 4 < (1L << 31) &&
+    const bool streamed = dxl && overlap && ver == 6 && dirs == 2 && !p.xpd &&
+                          ((d.prec == kPrecX3 && p.rg == 1) || env_int("KCTC_STREAM_ALL", 0)) && use_x3(NW * H) &&
+                          NW * H <= 4096 &&
+                          (d.prec == kPrecX3 || (NW * H) % 64 == 0) && (long)TN * Din * 4 < (1L << 31) &&
                           env_int("KCTC_BWD_STREAM", 1);
     p.e_sc1 = env_int("KCTC_DIAG_ESC1", streamed ? 1 : 0);  // diagnostic override (0 with streaming: wrong dx)
     if (ver == 6) {

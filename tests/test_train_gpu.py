@@ -200,8 +200,11 @@ def test_model_write_read_roundtrip(kctc, gpu, tmp_path):
 
 
 @pytest.mark.parametrize("knob", ["KCTC_FWD_STREAM", "KCTC_BWD_STREAM"])
-@pytest.mark.parametrize("mode,H,T,N", [(2, 512, 300, 16), (2, 256, 97, 5), (3, 256, 64, 16)])
-def test_streamed_gemms_match_unstreamed(kctc, gpu, monkeypatch, knob, mode, H, T, N):
+@pytest.mark.parametrize("mode,H,T,N,prec", [(2, 512, 300, 16, 0), (2, 256, 97, 5, 0), (3, 256, 64, 16, 0),
+                                             # row groups (N > 16: ragged last group), bf16 images / operands
+                                             (2, 256, 64, 40, 0), (3, 256, 50, 32, 0), (3, 256, 64, 16, 1),
+                                             (2, 256, 48, 24, 1)])
+def test_streamed_gemms_match_unstreamed(kctc, gpu, monkeypatch, knob, mode, H, T, N, prec):
     """GEMMs that run while the recurrence producing their rows is still going
     (knob=1, the default) against the same GEMMs after it (knob=0):
     KCTC_FWD_STREAM -- RNN -> ClipGradient -> RNN, the second RNN's input
@@ -217,18 +220,24 @@ def test_streamed_gemms_match_unstreamed(kctc, gpu, monkeypatch, knob, mode, H, 
     feats, nf, fl, ll = kctc.synth_minibatch(17, T, N, D, A, 0.125)
     f = torch.from_numpy(feats).to(gpu)
     res = {}
+    if N > 16 or prec:  # the general streaming path (off by default on these shapes)
+        monkeypatch.setenv("KCTC_STREAM_ALL", "1")
     for flag in ("0", "1"):
         monkeypatch.setenv(knob, flag)
         net = kctc.Nnet(cfg, seed=8)
+        if prec:
+            net.set_precision("bf16")
         o = net.compute_objf(f, T, N, nf, fl, ll)[0]
         net.train_step(f, T, N, nf, fl, ll)
         o2 = net.compute_objf(f, T, N, nf, fl, ll)[0]
         res[flag] = (o, o2, [net.get_params(c).astype(np.float64) for c in range(net.num_components)
                              if net.num_params(c) > 0])
-    np.testing.assert_allclose(res["1"][0], res["0"][0], rtol=2e-6)
-    np.testing.assert_allclose(res["1"][1], res["0"][1], rtol=2e-6)
+    # bf16: the same bf16 operands either way (h rounded once), fp32 sums in another order
+    tol = 2e-5 if prec else 2e-6
+    np.testing.assert_allclose(res["1"][0], res["0"][0], rtol=tol)
+    np.testing.assert_allclose(res["1"][1], res["0"][1], rtol=tol)
     for a, b in zip(res["1"][2], res["0"][2]):
-        assert rel_err(a, b) < 1e-6
+        assert rel_err(a, b) < tol / 2
 
 
 def test_rccl_dp_single_rank_matches_plain(kctc, gpu):
