@@ -238,6 +238,7 @@ struct RecParams {
   int nopf;         // diagnostic (KCTC_DIAG_NOPF): skip the operand prefetch (wrong results)
   int e_sc1;        // v6 backward: dGates rows written through (sc1) for a streaming consumer
   int wwait;        // v6: per-wave waits on the producers a wave reads (else wave 0 waits for all)
+  int bfpart;       // v6 backward, bf16 mode: partial dh exchanged as bf16 (KCTC_BF16_PARTIALS)
   unsigned *cmax;   // v6 backward: column max |DX| [dirs * nW * H] (GRU: then |E|), as float bits
 };
 
@@ -1331,6 +1332,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
 // sc1 loads) into a per-step image that is never rewritten within a launch.
 typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 // products of the v6 recurrences: split-fp16 (fp32-class) or bf16
 enum { kPrecX3 = 0, kPrecBf16 = 1 };
 // max over each aligned group of U (8, 16, 32) lanes, all lanes active
@@ -1465,7 +1467,11 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   const long ldy = (long)dirs * H, ldg = (long)dirs * NW * H;
   // floats per producer block (16 x H) + 256 B, so that the 1-KB chunks a
   // consumer reads from consecutive producers fall in different L2 channels
-  constexpr long PSTR = (long)CTT * 64 * 4 + 64;
+  // bf16 mode (p.bfpart): the partials travel as bf16 (8 B per lane and tile,
+  // summed in fp32 by the consumer), half the bytes of the fp32 images
+  const bool bfp = BF && p.bfpart;
+  const long PSTR = bfp ? (long)CTT * 64 * 2 + 64 : (long)CTT * 64 * 4 + 64;
+  const int LW = bfp ? 2 : 4;  // floats-worth per lane and tile
   const long xgrp = (long)dirs * NWG * PSTR;  // one row group's images of a step
   const long xstep = xgrp * p.rg;
   AT *Ahi = reinterpret_cast<AT *>(smem);  // [16][AP]
@@ -1567,7 +1573,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   // C-fragment chunks) of producers pg, pg + NGRP, ...
   const int pos = tid % POS, pg = tid / POS;
   const int pln = U >= 16 ? pos : (pos >> 3) * 16 + fr0 + (pos & 7);
-  const long coff = (long)grp * xgrp + (long)d * NWG * PSTR + ((long)ct_own * 64 + pln) * 4 + (long)pg * PSTR;
+  const long coff = (long)grp * xgrp + (long)d * NWG * PSTR + ((long)ct_own * 64 + pln) * LW + (long)pg * PSTR;
   // a C-fragment lane holds rows 4 (lane / 16) .. +3 of the group: quads past N
   // are neither stored nor loaded (a group of fewer than 16 sequences moves
   // only its own rows)
@@ -1603,13 +1609,30 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
       }
       REC_TRACE(ks, 1);
       const auto rs = rsrc(p.xch + (long)(ks - 1) * xstep, (unsigned)(xstep * 4));
-      u32x4 v[PER];
+      floatx4 sm = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (bfp) {
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        u32x2 v[PER];
 #pragma unroll
-      for (int i = 0; i < PER; i++)
-        v[i] = crow_live ? ld_sc1(rs, (unsigned)((coff + (long)i * NGRP * PSTR) * 4)) : u32x4{0u, 0u, 0u, 0u};
-      floatx4 sm = __builtin_bit_cast(floatx4, v[0]);
+        for (int i = 0; i < PER; i++)
+          v[i] = crow_live ? __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                                 rs, (int)((coff + (long)i * NGRP * PSTR) * 4), 0, 16 /* sc1 */))
+                           : u32x2{0u, 0u};
 #pragma unroll
-      for (int i = 1; i < PER; i++) sm += __builtin_bit_cast(floatx4, v[i]);
+        for (int i = 0; i < PER; i++) {
+          const bf16x4 b = __builtin_bit_cast(bf16x4, v[i]);
+#pragma unroll
+          for (int j = 0; j < 4; j++) sm[j] += (float)b[j];
+        }
+      } else {
+        u32x4 v[PER];
+#pragma unroll
+        for (int i = 0; i < PER; i++)
+          v[i] = crow_live ? ld_sc1(rs, (unsigned)((coff + (long)i * NGRP * PSTR) * 4)) : u32x4{0u, 0u, 0u, 0u};
+        sm = __builtin_bit_cast(floatx4, v[0]);
+#pragma unroll
+        for (int i = 1; i < PER; i++) sm += __builtin_bit_cast(floatx4, v[i]);
+      }
       st4(red + (long)(pg * POS + pos) * 4, sm);
       REC_TRACE(ks, 2);
     }
@@ -1711,10 +1734,17 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
         floatx4 o;
 #pragma unroll
         for (int i = 0; i < 4; i++) o[i] = BF ? acc[c][i] : ldexpf(acc[c][i], ex[i]);
-        const int off = (int)((obase + ((long)(w * CTW + c) * 64 + lane) * 4) * 4);
+        const int off = (int)((obase + ((long)(w * CTW + c) * 64 + lane) * LW) * 4);
         // local: plain stores keep the lines in the XCD's shared L2, where the
         // consumers' sc1 loads find them; else write-through (sc1)
         if (!prow_live) {
+        } else if (bfp) {
+          typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+          bf16x4 b;
+#pragma unroll
+          for (int i = 0; i < 4; i++) b[i] = (__bf16)o[i];
+          if (local) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, b), ro, off, 0, 0);
+          else __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, b), ro, off, 0, 16);
         } else if (local) {
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ro, off, 0, 0);
         } else {
@@ -2692,6 +2722,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
       // dGates rows outstanding when they would poll (their first poll waits
       // for them): measured 34.2 -> 35.4 ms/step with per-wave waits
       p.wwait = env_int("KCTC_BWD_WWAIT", 0);
+      p.bfpart = env_int("KCTC_BF16_PARTIALS", 1);
       p.xch = xch_acquire(sizeof(float) * (size_t)T * dirs * p.nwg * (16 * H + 64) * p.rg, s);
     } else {
       p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
