@@ -289,6 +289,21 @@ def main():
                                 "frac": round(tf / PEAK_X3_TFLOPS, 4),
                                 "note": "peak = 2.5 PF dense f16 / 3 MFMAs per split-fp16 product; "
                                         "vs the fp32 MFMA peak it is " + str(round(tf / PEAK_FP32_TFLOPS, 3))}
+        if "gate_gemm" in aux and rank == 0:
+            # the same kernel on the same shape, alone on the chip (the in-step
+            # figure above shares the CUs and memory system with a recurrence)
+            G4, din = nw * H, 2 * H
+            Ms, Ns, Ks = G4, din, T * N
+            split = 4 if bf16 else 8
+            ms_s = k.lib().kcm_bench_gemm_packed(None, Ms, Ns, Ks, 1 if bf16 else 0, 5, split)
+            if ms_s > 0:
+                tf_s = 2.0 * Ms * Ns * Ks / (ms_s / 1e3) / 1e12
+                aux["gate_gemm"]["standalone"] = {
+                    "shape": f"M={Ms} N={Ns} K={Ks} split-K {split} (dW of a BLSTM layer, one direction)",
+                    "ms": round(ms_s, 4), "achieved": round(tf_s, 2),
+                    "frac": round(tf_s / (PEAK_F16_TFLOPS if bf16 else PEAK_X3_TFLOPS), 4),
+                    "mfma_issue_frac": round(tf_s * (1 if bf16 else 3) / PEAK_F16_TFLOPS, 4),
+                    "note": "kcm_bench_gemm_packed: random packed operands, 5 launches after 2 warm-ups"}
         if "ctc_alpha_beta" in prof:
             ms_c, n_c = prof["ctc_alpha_beta"]
             byts = 0.0
