@@ -57,6 +57,7 @@ struct PParams {
   int nrt;                 // row tiles
   long sxs;                // halves per producer step image
   long sxg;                // halves per row group's part of a step image
+  int backoff;             // streaming waits sleep in proportion to the producer's distance (KCTC_STREAM_BACKOFF)
   unsigned *serr;          // producer's error word (wait timeout)
   // backward stream (x3p_bwd_stream_kernel)
   const float *E;          // source rows of direction d: E + row * lde + d * edoff (KB * 32 floats)
@@ -181,6 +182,18 @@ __device__ __forceinline__ void wave_fail(unsigned *err) {
   if ((threadIdx.x & 63) == 0 && err) atomicOr(err, 2u);
 }
 
+// Waiting for a producer that is `gap` steps (~3 us each) short: sleep for
+// gap - 1 steps instead of re-polling its flag lines every ~0.2 us -- up to
+// 176 blocks poll the same lines the recurrence itself polls and stores
+__device__ __forceinline__ void backoff(int gap) {
+  if (gap > 2) {
+    const int n = min(gap - 1, 64);
+    for (int i = 0; i < n; i++) __builtin_amdgcn_s_sleep(80);  // 80 x 64 clocks: ~2.4 us at 2.1 GHz
+  } else {
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+
 // (Inside the polling loops every branch is wave-uniform; the single-lane
 // stores of the outcome come after the loop: a lane-0 store in front of a
 // `break` let the compiler leave lane 0 of wave 0 switched off, observed as
@@ -208,7 +221,7 @@ __device__ void x3p_wait_rows(const PParams &p, int m0, int *prog) {
       if (s0 >= need0 && s1 >= need1) break;
       failed = wave_timed_out(p.serr, spins++, ts);
       if (failed) break;  // the producer stopped: flag it, finish on whatever is there
-      __builtin_amdgcn_s_sleep(8);
+      backoff(p.backoff ? max(need0 - s0, need1 - s1) : 0);
     }
     if (failed) s0 = s1 = 1 << 30;
     if (threadIdx.x == 0) { prog[0] = s0; prog[1] = s1; }
@@ -253,7 +266,7 @@ __device__ void wait_epoch(const PParams &p, int d, int need, int *seen) {
       if (m >= need) break;
       failed = wave_timed_out(p.serr, spins++, t0);
       if (failed) break;
-      __builtin_amdgcn_s_sleep(8);
+      backoff(p.backoff ? need - m : 0);
     }
     if (threadIdx.x == 0) seen[d] = failed ? 1 << 30 : m;
     if (failed) wave_fail(p.serr);
@@ -1038,6 +1051,11 @@ float x3p_bench(hipStream_t s, int M, int N, int K, bool bf16, int iters, int sp
   return ms / iters;
 }
 
+static int env_backoff() {
+  const char *e = getenv("KCTC_STREAM_BACKOFF");
+  return e ? atoi(e) : 1;
+}
+
 bool x3p_use_256(int M, int N) {
   static const int on = [] {
     const char *e = getenv("KCTC_GEMM256");
@@ -1082,6 +1100,7 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
   p.eA0 = g.eA0; p.eB0 = g.eB0;
   p.sflags = g.stream_flags; p.snwg = g.stream_nwg; p.sT = g.stream_T; p.sN = g.stream_N;
   p.srg = g.stream_rg; p.sxg = g.stream_group_step;
+  p.backoff = env_backoff();
   p.nrt = ceil_div(g.M, TB);
   p.sxs = g.stream_step; p.serr = g.stream_err;
   if (p.counter) KCTC_HIP_CHECK(hipMemsetAsync(p.counter, 0, sizeof(int), s));
@@ -1154,6 +1173,7 @@ void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a) {
   p.counter = a.cnt; p.done = a.cnt + 1; p.arrive = a.cnt + 1 + 2 * p.nrt;
   p.part = a.part;
   p.sflags = a.flags; p.snwg = a.nwg; p.sT = a.T; p.sN = a.Nf; p.serr = a.err; p.srg = a.rg;
+  p.backoff = env_backoff();
   KCTC_HIP_CHECK(hipMemsetAsync(a.cnt, 0, sizeof(int) * x3p_bwd_stream_ints(a.M, a.N), s));
   const int total = 2 * p.nrt * (p.P + p.gx);
   const dim3 grid(std::min(total, a.blocks > 0 ? a.blocks : 96));
