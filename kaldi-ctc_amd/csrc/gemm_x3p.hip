@@ -53,7 +53,8 @@ struct PParams {
   int eA0, eB0;
   const unsigned *sflags;  // streaming mode: producer flag lines
   int snwg, sT, sN;
-  int srg;                 // producer row groups of 16 sequences (flag lines and images per group)
+  int srg;                 // producer row groups (flag lines and images per group)
+  int sgsh;                // log2 of the sequences per row group (4: 16, 3: 8)
   int nrt;                 // row tiles
   long sxs;                // halves per producer step image
   long sxg;                // halves per row group's part of a step image
@@ -102,7 +103,8 @@ __device__ __forceinline__ void load_tile_xch(const PParams &p, const _Float16 *
     const int c = (lane & 7) ^ (r & 7);
     const int gr = min(r0 + r, p.M - 1);
     const int t = gr / p.sN, n = gr - t * p.sN;
-    const long off = (long)t * p.sxs + (long)(n >> 4) * p.sxg + (((long)kb * 2 + (c >> 2)) * 16 + (n & 15)) * 32 +
+    const long off = (long)t * p.sxs + (long)(n >> p.sgsh) * p.sxg +
+                     (((long)kb * 2 + (c >> 2)) * 16 + (n & ((1 << p.sgsh) - 1))) * 32 +
                      (c & 3) * 8;
     reg[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off * 2), 0, 16 /* sc1 */);
   }
@@ -1100,6 +1102,7 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
   p.eA0 = g.eA0; p.eB0 = g.eB0;
   p.sflags = g.stream_flags; p.snwg = g.stream_nwg; p.sT = g.stream_T; p.sN = g.stream_N;
   p.srg = g.stream_rg; p.sxg = g.stream_group_step;
+  p.sgsh = g.stream_gs == 8 ? 3 : 4;
   p.backoff = env_backoff();
   p.nrt = ceil_div(g.M, TB);
   p.sxs = g.stream_step; p.serr = g.stream_err;

@@ -76,7 +76,7 @@ RnnReserveLayout rnn_reserve_layout(const RnnDesc &d, int T, int N) {
   r.aux = p;  p += al64(TN * dirs * H);
   r.E = p;    p += al64(TN * dirs * nw * H);
   r.DX = p;   p += (d.mode == kGru) ? al64(TN * dirs * nw * H) : 0;
-  r.bias = p; p += al64(dirs * 2 * nw * H * (long)((N + 15) / 16));  // v6: per row group
+  r.bias = p; p += al64(dirs * 2 * nw * H * (long)((N + 7) / 8));  // v6: per row group (>= 8 rows each)
   r.out = p;  p += (d.layers > 1) ? al64(TN * dirs * H) : 0;
   r.dout = p; p += (d.layers > 1) ? al64(TN * dirs * H) : 0;
   r.per_layer = p;
@@ -215,7 +215,8 @@ __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); 
 
 struct RecParams {
   int T, N, H, dirs, U, nwg, ncol, Npad;
-  int rg;           // v6: row groups of 16 sequences (independent recurrences)
+  int rg;           // v6: row groups (independent recurrences) of gs sequences
+  int gs;           // v6: sequences per row group (16, or 8: two groups of a 16-row batch run side by side)
   const float *w;   // params base of this stacked layer's pseudo-layer 0
   long pl_stride;   // floats between the two directions' blocks
   long r_off;       // R within a pseudo-layer block
@@ -1461,7 +1462,8 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   const int g = p.xpd ? (blockIdx.x >> 3) : (blockIdx.x / dirs) % NWG;
   const int grp = p.xpd ? 0 : blockIdx.x / (dirs * NWG);
   if (d >= dirs || g >= NWG || grp >= p.rg) return;
-  const int N = p.N, T = p.T, n0 = grp * 16;
+  // rows n0 .. nend-1 of the batch (p.gs <= 16 of the 16 MFMA rows)
+  const int N = p.N, T = p.T, n0 = grp * p.gs, nend = min(N, n0 + p.gs);
   const int u0 = g * U, ct_own = u0 >> 4, fr0 = u0 & 15;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
   const long ldy = (long)dirs * H, ldg = (long)dirs * NW * H;
@@ -1529,7 +1531,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   const bool has_e = tid < 16 * U;
   const int en = tid / U, eu = tid - en * U;
   const int n = n0 + en;
-  const bool live = has_e && n < N;
+  const bool live = has_e && n < nend;
   float carry = 0.f, bsx[NW], bsh[NW], dxk[NW], eg[NW], cg[NW], ng[NW], cmx[NW], cme[NW];
   float cdy = 0.f, ca = 0.f, cap = 0.f, ndy = 0.f, na = 0.f, nap = 0.f;
 #pragma unroll
@@ -1577,8 +1579,8 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   // a C-fragment lane holds rows 4 (lane / 16) .. +3 of the group: quads past N
   // are neither stored nor loaded (a group of fewer than 16 sequences moves
   // only its own rows)
-  const bool crow_live = n0 + 4 * ((pln & 63) >> 4) < N;
-  const bool prow_live = n0 + 4 * fq < N;
+  const bool crow_live = n0 + 4 * ((pln & 63) >> 4) < nend;
+  const bool prow_live = n0 + 4 * fq < nend;
   // per-wave wait: the producers of the groups this wave's threads sum
   int wprod = -1;
   {
@@ -1762,7 +1764,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
       // for them (4-B write-through stores per element cost ~8 us per step)
       constexpr int CPR = NW * U / 4;  // chunks per row
       const int rn = tid / CPR, c = tid - rn * CPR;
-      if (rn < 16 && n0 + rn < N) {
+      if (rn < 16 && n0 + rn < nend) {
         const int q = (c * 4) / U, u = (c * 4) % U;
         const u32x4 v = *reinterpret_cast<const u32x4 *>(estg + rn * NW * U + c * 4);
         const int off = (int)(((long)(n0 + rn) * ldg + (long)d * NW * H + q * H + u0 + u) * 4);
@@ -1855,7 +1857,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   const int dirs = p.dirs;
   const int d = blockIdx.x % dirs, g = (blockIdx.x / dirs) % NWG, grp = blockIdx.x / (dirs * NWG);
   if (grp >= p.rg) return;
-  const int N = p.N, T = p.T, n0 = grp * 16;
+  const int N = p.N, T = p.T, n0 = grp * p.gs, nend = min(N, n0 + p.gs);
   const int u0 = g * U;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
   const long ldy = (long)dirs * H, ldg = (long)dirs * NW * H;
@@ -1926,7 +1928,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   const bool has_e = tid < 16 * U;
   const int en = tid / U, eu = tid - en * U;
   const int n = n0 + en;
-  const bool live = has_e && n < N;
+  const bool live = has_e && n < nend;
   float cst = 0.f, hpv = 0.f, cnew = 0.f, hval = 0.f;
   float gin[NW], gnx[NW], bR[NW], act[NW];
 #pragma unroll
@@ -1954,7 +1956,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   const int sp = tid / (16 * CH), sn = (tid / CH) % 16, sch = tid % CH;
   const int kb0 = u0 >> 5, koff = (u0 & 31) + sch * 8;
   // rows past N (a group of fewer than 16 sequences) are neither loaded nor stored
-  const bool arow_live = n0 + fr < N;
+  const bool arow_live = n0 + fr < nend;
   // per-wave wait: the producers of the k blocks this wave loads (32 / U per block)
   int wprod = -1;
   {
@@ -2059,7 +2061,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
       }
     }
     __syncthreads();
-    if (tid < NP * 16 * CH && n0 + sn < N) {
+    if (tid < NP * 16 * CH && n0 + sn < nend) {
       const u32x4 v = *reinterpret_cast<const u32x4 *>(stg + (sp * 16 + sn) * U + sch * 8);
       const long o = gimg + ((((long)d * KB + kb0) * NP + sp) * 16 + sn) * 32 + koff;
       __builtin_amdgcn_raw_buffer_store_b128(v, rsrc(xch + (long)t * XS, (unsigned)(XS * sizeof(AT))),
@@ -2292,16 +2294,29 @@ static int pick_bwd_u4(const RnnDesc &d, int N) {
 // for the GEMMs that overlap the recurrences).  Preference U = 16, then 32,
 // then 8 (measured on BLSTM-512 N=16: U=16 34.2 ms/step of forward
 // recurrence, U=8 37.1).  KCTC_FWD_U / KCTC_BWD_U force U.
+// Sequences per v6 row group: 16 (one MFMA row tile), or 8 for 9 <= N <= 32
+// -- the batch then runs as ceil(N / 8) independent recurrences side by side,
+// each moving half the hand-off rows per step.  Default: 8 in the forward
+// (configs[1]: 28.0 -> 27.0 ms/step of forward recurrence), 16 in the
+// backward (34.3 -> 34.7, and the weight GEMMs beside it get 64 CUs fewer).
+// KCTC_REC_GS sets both, KCTC_REC_GS_FWD / KCTC_REC_GS_BWD one direction.
+// (The default 8 applies to N <= 16; a set knob to N <= 32.)  pick6 falls
+// back to 16 when no workgroup partition fits the groups of 8.
+static int v6_group_rows(int N, bool fwd) {
+  const int dflt = fwd && N <= 16 ? 8 : 16;
+  const int want = env_int(fwd ? "KCTC_REC_GS_FWD" : "KCTC_REC_GS_BWD", env_int("KCTC_REC_GS", dflt));
+  return (want == 8 && N > 8 && N <= 32) ? 8 : 16;
+}
 struct V6Cfg {
-  int U = 0, nth = 0, rg = 0;
+  int U = 0, nth = 0, rg = 0, gs = 16;
   explicit operator bool() const { return U > 0; }
 };
-static V6Cfg pick6(const RnnDesc &d, int N, bool fwd) {
+static V6Cfg pick6(const RnnDesc &d, int N, bool fwd, int gs_force = 0) {
   V6Cfg c;
   if (env_int(fwd ? "KCTC_FWD_REC" : "KCTC_BWD_REC", 6) != 6 || rec_version() != 4) return c;
   if ((d.mode != kLstm && d.mode != kGru) || N <= 0 || N > 64 || d.dirs > 2) return c;
   if (d.H != 256 && d.H != 320 && d.H != 512 && d.H != 1024) return c;
-  const int rg = (N + 15) / 16;
+  const int gs = gs_force ? gs_force : v6_group_rows(N, fwd), rg = (N + gs - 1) / gs;
   const int max_wg = env_int("KCTC_REC_MAX_WG", 128);
   auto ok = [&](int U) {
     const int nth = U == 32 ? 512 : 256, nwv = nth / 64;
@@ -2317,16 +2332,20 @@ static V6Cfg pick6(const RnnDesc &d, int N, bool fwd) {
     const int want_nth = env_int(fwd ? "KCTC_FWD_NTH" : "KCTC_BWD_NTH", d.H == 512 ? 512 : 256);
     c.nth = U == 32 ? 512 : (U == 16 && d.H == 512 && (want_nth == 512 || want_nth == 1024)) ? want_nth : 256;
     c.rg = rg;
+    c.gs = gs;
     return c;
   };
   const int want = env_int(fwd ? "KCTC_FWD_U" : "KCTC_BWD_U", 0);
-  if (want) return ok(want) ? take(want) : c;
-  for (int U : {16, 32, 8})
-    if (ok(U)) {
-      // rg = 1 keeps the measured N <= 16 choice even above the budget
-      if (rg == 1 || (long)d.dirs * (d.H / U) * rg <= max_wg) return take(U);
-    }
-  return c;
+  if (want) {
+    if (ok(want)) return take(want);
+  } else {
+    for (int U : {16, 32, 8})
+      if (ok(U)) {
+        // rg = 1 keeps the measured N <= 16 choice even above the budget
+        if (rg == 1 || (long)d.dirs * (d.H / U) * rg <= max_wg) return take(U);
+      }
+  }
+  return gs == 8 ? pick6(d, N, fwd, 16) : c;
 }
 static int pick_fwd_u6(const RnnDesc &d, int N) { return pick6(d, N, true).U; }
 static int pick_bwd_u6(const RnnDesc &d, int N) { return pick6(d, N, false).U; }
@@ -2440,7 +2459,7 @@ bool chain_ok(const RnnDesc &d, int ver, int T, int N, const RnnFwdChain *c) {
   // the CUs left beside the 128-workgroup recurrence outlasts it (990k ->
   // 728k and 560k -> 389k frames/s measured), the 256-tile GEMM after it wins
   if ((N > 16 || d.prec == kPrecBf16) && !env_int("KCTC_STREAM_ALL", 0)) return false;
-  const long xs = 2L * (d.H / 32) * (d.prec == kPrecBf16 ? 1 : 2) * 16 * 32 * ((N + 15) / 16);  // halves per step image
+  const long xs = 2L * (d.H / 32) * (d.prec == kPrecBf16 ? 1 : 2) * 16 * 32 * pick6(d, N, true).rg;  // halves per step image
   if ((long)T * xs * 2 >= (1L << 31)) return false;
   return c->ws_bytes >= rnn_workspace_bytes(n, T, N) &&
          c->res_bytes >= sizeof(float) * (size_t)rnn_reserve_layout(n, T, N).total;
@@ -2484,7 +2503,7 @@ void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
   x.tile_counter = reinterpret_cast<int *>(static_cast<char *>(c.workspace) + flags_offset(n, T, N));
   x.stream_flags = p.flags + 1024; x.stream_nwg = p.nwg; x.stream_T = T; x.stream_N = N;
   x.stream_group_step = 2L * (d.H / 32) * (bf ? 1 : 2) * 16 * 32;  // rnn_fwd_rec6's XG
-  x.stream_rg = p.rg; x.stream_step = x.stream_group_step * p.rg; x.stream_err = err;
+  x.stream_rg = p.rg; x.stream_gs = p.gs; x.stream_step = x.stream_group_step * p.rg; x.stream_err = err;
   // every producer workgroup needs a CU of its own (96 KB LDS); the GEMM's
   // persistent blocks (96 KB each) take the rest minus a margin
   x.max_blocks = env_int("KCTC_STREAM_BLOCKS", std::max(8, cus - d.dirs * p.nwg * p.rg - 16));
@@ -2594,6 +2613,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     const size_t lds = ver == 6 ? fwd6_lds_bytes(d, c6) : fwd_lds_bytes(d, N, U);
     p.xpd = ver == 4 ? v4_xpd(d, U) : 1;
     p.rg = ver == 6 ? c6.rg : 1;
+    p.gs = ver == 6 ? c6.gs : 16;
     p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
     p.poll_sleep = env_int("KCTC_POLL_SLEEP", 1);
     p.nopf = env_int("KCTC_DIAG_NOPF", 0);
@@ -2709,6 +2729,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     const size_t lds = ver == 6 ? bwd6_lds_bytes(d, c6) : bwd_lds_bytes(d, N, U, ver);
     p.xpd = ver == 4 ? v4_xpd(d, U) : 1;
     p.rg = ver == 6 ? c6.rg : 1;
+    p.gs = ver == 6 ? c6.gs : 16;
     if (ver == 6) {
       // XCD-slot mapping when a direction's workgroups fit one XCD
       // (measured slower, 37.2 vs 33.6 ms/step of backward recurrence: the 32
@@ -2734,7 +2755,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     float *dxl = (l == 0) ? dx : res + lay.per_layer * (l - 1) + lay.dout;
     // streamed: computed on `overlap` while the recurrence runs, from its rows as they appear
     const bool streamed = dxl && overlap && ver == 6 && dirs == 2 && !p.xpd &&
-                          ((d.prec == kPrecX3 && p.rg == 1) || env_int("KCTC_STREAM_ALL", 0)) && use_x3(NW * H) &&
+                          ((d.prec == kPrecX3 && N <= 16) || env_int("KCTC_STREAM_ALL", 0)) && use_x3(NW * H) &&
                           NW * H <= 4096 &&
                           (d.prec == kPrecX3 || (NW * H) % 64 == 0) && (long)TN * Din * 4 < (1L << 31) &&
                           env_int("KCTC_BWD_STREAM", 1);
@@ -2991,7 +3012,8 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     const long bW = d.lin_offset(l * dirs, 0, true) - pl0;
     const long bR = d.lin_offset(l * dirs, NW, true) - pl0;
     // (v6: one partial per row group, [group][dir][2][G], added in group order)
-    const int rg = pick_bwd_u6(d, N) ? (N + 15) / 16 : 1;
+    const V6Cfg c6b = pick6(d, N, false);
+    const int rg = c6b ? c6b.rg : 1;
     for (int gi = 0; gi < rg; gi++)
       for (int dir = 0; dir < dirs; dir++) {
         const float *part = R0 + lay.bias + ((long)gi * dirs + dir) * 2 * G4;

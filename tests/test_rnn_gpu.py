@@ -89,6 +89,23 @@ def test_rnn_matches_oracle(kctc, gpu, oracle, case):
                 assert rel_err(dw[sl], rdw[sl]) < 2e-4, (pl, lin, isb)
 
 
+GS8_CASES = [
+    # KCTC_REC_GS=8: a batch of 9..32 sequences runs as groups of 8 (side by side)
+    (2, 24, 16, 40, 512, 1, True),   # configs[1] width: 2 groups of 8, U=16 on 512-thread workgroups
+    (3, 20, 13, 48, 256, 1, True),   # ragged last group (5 rows)
+    (2, 14, 12, 16, 256, 2, False),  # stacked uni
+    (2, 12, 30, 40, 512, 1, True),   # 4 groups (the last one 6 rows), U=32
+]
+
+
+@pytest.mark.parametrize("case", GS8_CASES, ids=[f"m{c[0]}_T{c[1]}_N{c[2]}_H{c[4]}_L{c[5]}" for c in GS8_CASES])
+def test_rnn_group8_matches_oracle(kctc, gpu, oracle, monkeypatch, case):
+    """Row groups of 8 sequences (rows n0..n0+7 of each group's 16-row MFMA
+    tile live, the other rows neither stored nor loaded) against the oracle."""
+    monkeypatch.setenv("KCTC_REC_GS", "8")
+    test_rnn_matches_oracle(kctc, gpu, oracle, case)
+
+
 BF16_CASES = [
     # (mode, T, N, D, H, layers, bidir): configs[4] shapes in miniature
     (3, 20, 32, 64, 1024, 1, True),   # BGRU-1024, 2 row groups, U=32

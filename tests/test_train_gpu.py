@@ -240,6 +240,22 @@ def test_streamed_gemms_match_unstreamed(kctc, gpu, monkeypatch, knob, mode, H, 
         assert rel_err(a, b) < tol / 2
 
 
+@pytest.mark.parametrize("knob", ["KCTC_FWD_STREAM", "KCTC_BWD_STREAM"])
+@pytest.mark.parametrize("mode,H,T,N", [(2, 512, 300, 16), (3, 256, 64, 13)])
+def test_streamed_gemms_group8(kctc, gpu, monkeypatch, knob, mode, H, T, N):
+    """KCTC_REC_GS=8: the streamed GEMMs read two row groups' images / flags
+    (readiness = the slower group) and equal the GEMMs run after the recurrence."""
+    monkeypatch.setenv("KCTC_REC_GS", "8")
+    test_streamed_gemms_match_unstreamed(kctc, gpu, monkeypatch, knob, mode, H, T, N, 0)
+
+
+@pytest.mark.parametrize("mode,H,T,N", [(2, 512, 20, 16), (3, 256, 24, 11)])
+def test_train_step_group8_matches_oracle(kctc, gpu, oracle, monkeypatch, mode, H, T, N):
+    """A whole train step with the recurrences in row groups of 8 sequences."""
+    monkeypatch.setenv("KCTC_REC_GS", "8")
+    test_train_step_row_groups_match_oracle(kctc, gpu, oracle, mode, H, T, N)
+
+
 def test_rccl_dp_single_rank_matches_plain(kctc, gpu):
     """kctc_nnet_enable_dp at world size 1 builds the RCCL exchange
     (ncclCommInitRank on a one-rank communicator): every component's bucket is
