@@ -72,6 +72,10 @@ struct X3PArgs {
   long stream_step = 0;              // halves per producer step image (A = image of step 0)
   int stream_rg = 1;                  // producer row groups (N > 16): flags and image parts per group
   int stream_gs = 16;                 // sequences per producer row group (16 or 8)
+  // direction-split streaming (gemm_x3p_kernel's fwd_combine): [row tiles][batch][col tiles]
+  // zeroed ints; null: whole-K jobs after both directions' rows are in
+  int *stream_arrive = nullptr;
+  float *stream_part = nullptr;         // [row tiles][batch][col tiles][128 x 128] half-K partials
   long stream_group_step = 0;         // halves per row group's part of a step image
   unsigned *stream_err = nullptr;    // set (bit 2) if the producer stops publishing
   // bf16 operands (bf16_pack_rows / _cols: [rows][KB][64] bf16, KB = 64-k

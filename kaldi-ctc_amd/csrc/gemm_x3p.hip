@@ -59,6 +59,8 @@ struct PParams {
   long sxs;                // halves per producer step image
   long sxg;                // halves per row group's part of a step image
   int backoff;             // streaming waits sleep in proportion to the producer's distance (KCTC_STREAM_BACKOFF)
+  int sdir;                // streaming: K split by producer direction (two half-K jobs per C tile, see fwd_combine)
+  int dbg;                 // KCTC_STREAM_DBG diagnostics: 1 no combine wait, 2 wait for both directions, 4 no combine
   unsigned *serr;          // producer's error word (wait timeout)
   // backward stream (x3p_bwd_stream_kernel)
   const float *E;          // source rows of direction d: E + row * lde + d * edoff (KB * 32 floats)
@@ -200,12 +202,13 @@ __device__ __forceinline__ void backoff(int gap) {
 // stores of the outcome come after the loop: a lane-0 store in front of a
 // `break` let the compiler leave lane 0 of wave 0 switched off, observed as
 // EXEC = ...fffe and a workgroup running on without its thread 0.)
-__device__ void x3p_wait_rows(const PParams &p, int m0, int *prog) {
+__device__ void x3p_wait_rows(const PParams &p, int m0, int *prog, int pd) {
   // prog[0..1]: steps known published by directions 0 / 1 (LDS cache; every
-  // wave reads it before the barrier, wave 0 writes it only after)
+  // wave reads it before the barrier, wave 0 writes it only after).
+  // pd = 0 / 1: only that producer direction's rows are needed (-1: both)
   const int r1 = min(p.M, m0 + TB) - 1;
   const int t0 = m0 / p.sN, t1 = r1 / p.sN;
-  const int need0 = t1, need1 = p.sT - 1 - t0;
+  const int need0 = pd == 1 ? -1 : t1, need1 = pd == 0 ? -1 : p.sT - 1 - t0;
   const bool ok = __builtin_amdgcn_readfirstlane(prog[0] >= need0 && prog[1] >= need1);
   __syncthreads();
   if (ok) return;
@@ -308,11 +311,75 @@ __device__ __forceinline__ void bwd_combine(const PParams &p, floatx4 (&acc)[4][
         }
       }
     }
+  // unconditional barrier (see fwd_combine)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (first && threadIdx.x == 0) __hip_atomic_fetch_add(arr, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Direction-split streaming (p.sdir): the K of the projection is [h_fwd |
+// h_bwd], and the forward half of frame t is ready at producer step t, the
+// backward half at step T-1-t -- so each C tile is two half-K jobs, taken in
+// the order their rows appear (forward half: row tiles ascending, backward
+// half: descending), and the work is spread over the whole recurrence instead
+// of its second half.  The halves meet in C: the first to arrive stores its
+// partial (sc1), the second adds it, its own and the bias and writes C.
+// (v0 + v1) + bias is the same either way round, so C does not depend on the
+// order of arrival.
+__device__ __forceinline__ void fwd_combine(const PParams &p, floatx4 (&acc)[4][4], const int (&ea)[4][4],
+                                            const int (&eb)[4], int tm, int tn, int b, int m0, int n0, int wm, int wn,
+                                            int fr, int fq, int *bc) {
+  const long tile = ((long)tm * p.batch + b) * p.gx + tn;
+  int *arr = p.arrive + tile;
+  if (threadIdx.x == 0) *bc = __hip_atomic_fetch_add(arr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const bool first = __builtin_amdgcn_readfirstlane(*bc) == 0;
+  // the partial travels in the accumulator layout: thread t's (i, j) fragment
+  // is 16 B at [tile][i * 4 + j][t], so both halves store / load whole,
+  // coalesced 16-B chunks (sc1: the other half may run on another XCD)
+  const auto rp = __builtin_amdgcn_make_buffer_rsrc(p.part + tile * (TB * TB), 0, TB * TB * 4, 0x00020000);
+  floatx4 v[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) v[i][j][r] = ldexpf(acc[i][j][r], -(ea[i][r] + eb[j]));
   if (first) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(arr, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[i][j]), rp,
+                                               ((i * 4 + j) * NTH + (int)threadIdx.x) * 16, 0, 16);
+  } else {
+    if (!(p.dbg & 1)) wait_count(arr, 4, p.serr);
+    float *C = p.C + (long)b * p.sC;
+    const float *bias = p.bias ? p.bias + (long)b * p.sBias : nullptr;
+    const float *bias2 = p.bias2 ? p.bias2 + (long)b * p.sBias : nullptr;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const floatx4 o = __builtin_bit_cast(
+            floatx4, __builtin_amdgcn_raw_buffer_load_b128(rp, ((i * 4 + j) * NTH + (int)threadIdx.x) * 16, 0, 16));
+        const int col = n0 + wn + j * 16 + fr;
+        if (col >= p.N) continue;
+        float badd = 0.f;
+        if (bias) badd += bias[col];
+        if (bias2) badd += bias2[col];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int row = m0 + wm + i * 16 + fq * 4 + r;
+          if (row < p.M) C[(long)row * p.ldc + col] = (v[i][j][r] + o[r]) + badd;
+        }
+      }
   }
+  // the barrier is unconditional: under `if (first)` (as bwd_combine had it)
+  // the compiler let waves of this inlined copy skip it (observed: a hang)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (first && threadIdx.x == 0) __hip_atomic_fetch_add(arr, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // SM (source mode): 0 packed A via LDS-DMA; 1 A = a forward producer's
@@ -340,7 +407,7 @@ __device__ __forceinline__ void x3p_tile(const PParams &p, unsigned char *lds, i
 #pragma unroll
     for (int j = 0; j < 4; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  if (STREAM) x3p_wait_rows(p, m0, prog);
+  if (STREAM) x3p_wait_rows(p, m0, prog, p.sdir && !(p.dbg & 2) ? ks : -1);
   // LDS: [2 stages][A tile | B tile]
   u32x4 ra[4];
   if (nk > 0) {
@@ -432,6 +499,10 @@ __device__ __forceinline__ void x3p_tile(const PParams &p, unsigned char *lds, i
     bwd_combine(p, acc, ea, eb, tm, tn, m0, n0, wm, wn, fr, fq, prog);
     return;
   }
+  if (STREAM && p.sdir && !(p.dbg & 4)) {
+    fwd_combine(p, acc, ea, eb, tm, tn, b, m0, n0, wm, wn, fr, fq, prog + 2);
+    return;
+  }
   if (p.split > 1) {
     float *W = p.ws + ((long)ks * p.batch + b) * (long)p.M * p.N;
 #pragma unroll
@@ -474,7 +545,7 @@ __device__ __forceinline__ void x3p_tile(const PParams &p, unsigned char *lds, i
 }
 
 constexpr size_t kLdsBase = 2 * 2 * TILEB + 16, kLdsStream = 96 * 1024;
-__host__ __device__ inline int stream_total(const PParams &p) { return p.nrt * p.batch * p.gx; }
+__host__ __device__ inline int stream_total(const PParams &p) { return p.nrt * p.batch * p.gx * (p.sdir ? 2 : 1); }
 
 __device__ __forceinline__ void decode_tile(const PParams &p, int id, int total, bool remap, int &tm, int &tn,
                                             int &b, int &ks) {
@@ -507,8 +578,14 @@ __global__ __launch_bounds__(NTH, 2) void gemm_x3p_kernel(PParams p) {
         tn = id % p.gx;
         const int rest = id / p.gx;
         b = rest % p.batch;
-        tm = stream_row_tile(rest / p.batch, p.nrt, p.sT, p.sN);
-        x3p_tile<1, BFM>(p, lds, tm, tn, b, 0, prog);
+        const int slot = rest / p.batch;
+        if (p.sdir) {  // slot = 2 j + producer direction: its K half of row tile j (dir 0) / nrt-1-j (dir 1)
+          const int pd = slot & 1, j = slot >> 1;
+          x3p_tile<1, BFM>(p, lds, pd == 0 ? j : p.nrt - 1 - j, tn, b, pd, prog);
+        } else {
+          tm = stream_row_tile(slot, p.nrt, p.sT, p.sN);
+          x3p_tile<1, BFM>(p, lds, tm, tn, b, 0, prog);
+        }
       } else {
         decode_tile(p, id, total, false, tm, tn, b, ks);
         x3p_tile<0, BFM>(p, lds, tm, tn, b, ks, prog);
@@ -1106,6 +1183,16 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
   p.backoff = env_backoff();
   p.nrt = ceil_div(g.M, TB);
   p.sxs = g.stream_step; p.serr = g.stream_err;
+  p.sdir = 0;
+  p.arrive = nullptr;
+  p.dbg = getenv("KCTC_STREAM_DBG") ? atoi(getenv("KCTC_STREAM_DBG")) : 0;
+  if (g.stream_flags && g.stream_arrive && g.stream_part && g.KB % 2 == 0 && (long)g.M * g.ldc * 4 + (long)(g.batch - 1) * g.sC * 4 < (1L << 31)) {
+    p.sdir = 1;
+    p.kbchunk = g.KB / 2;  // the producer's two directions
+    p.arrive = g.stream_arrive;
+    p.part = g.stream_part;
+    KCTC_HIP_CHECK(hipMemsetAsync(p.arrive, 0, sizeof(int) * (size_t)stream_total(p) / 2, s));
+  }
   if (p.counter) KCTC_HIP_CHECK(hipMemsetAsync(p.counter, 0, sizeof(int), s));
   static bool attr = false;  // dynamic LDS above 64 KB
   if (!attr) {

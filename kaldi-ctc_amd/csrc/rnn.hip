@@ -120,7 +120,7 @@ static size_t xch_bytes(const RnnDesc &d, int T, int N) {
 //               shifted output^T [dirs*H][TN]
 // plus int exponents and float-bit column maxima (G = nW*H).
 struct PackLay {
-  size_t a, b, c, d, ea, eb, ec, ed, cm, part, cnt, cme, total;
+  size_t a, b, c, d, ea, eb, ec, ed, cm, part, cnt, cme, fcnt, fpart, total;
 };
 static PackLay pack_layout(const RnnDesc &d, int T, int N) {
   const long TN = (long)T * N, G = (long)d.nw() * d.H, Dm = std::max(d.D, d.dirs * d.H), dirs = d.dirs;
@@ -143,6 +143,9 @@ static PackLay pack_layout(const RnnDesc &d, int T, int N) {
   p.part = o; o = align_up(o + sizeof(float) * TN * Dm, 256);            // backward stream partials
   p.cnt = o; o = align_up(o + sizeof(int) * x3p_bwd_stream_ints((int)TN, (int)Dm), 256);
   p.cme = o; o = align_up(o + sizeof(unsigned) * 2 * dirs * G, 256);  // dGates column maxima (v6 backward)
+  // arrival counters of the direction-split streamed projection (this component as its consumer)
+  p.fcnt = o; o = align_up(o + sizeof(int) * ((TN + 127) / 128 * dirs * ((G + 127) / 128) + 64), 256);
+  p.fpart = o; o = align_up(o + sizeof(float) * ((TN + 127) / 128) * dirs * ((G + 127) / 128) * 128 * 128, 256);
   p.total = o;
   return p;
 }
@@ -2504,6 +2507,12 @@ void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
   x.stream_flags = p.flags + 1024; x.stream_nwg = p.nwg; x.stream_T = T; x.stream_N = N;
   x.stream_group_step = 2L * (d.H / 32) * (bf ? 1 : 2) * 16 * 32;  // rnn_fwd_rec6's XG
   x.stream_rg = p.rg; x.stream_gs = p.gs; x.stream_step = x.stream_group_step * p.rg; x.stream_err = err;
+  // K split by producer direction: the work is ready from the first steps
+  // (KCTC_STREAM_DIRSPLIT=0: whole-K tiles from the middle of the sequence outwards)
+  if (env_int("KCTC_STREAM_DIRSPLIT", 1)) {
+    x.stream_arrive = pk<int>(c.workspace, n, T, N, pl.fcnt);
+    x.stream_part = pk<float>(c.workspace, n, T, N, pl.fpart);
+  }
   // every producer workgroup needs a CU of its own (96 KB LDS); the GEMM's
   // persistent blocks (96 KB each) take the rest minus a margin
   x.max_blocks = env_int("KCTC_STREAM_BLOCKS", std::max(8, cus - d.dirs * p.nwg * p.rg - 16));

@@ -232,8 +232,13 @@ def test_streamed_gemms_match_unstreamed(kctc, gpu, monkeypatch, knob, mode, H, 
         o2 = net.compute_objf(f, T, N, nf, fl, ll)[0]
         res[flag] = (o, o2, [net.get_params(c).astype(np.float64) for c in range(net.num_components)
                              if net.num_params(c) > 0])
-    # bf16: the same bf16 operands either way (h rounded once), fp32 sums in another order
-    tol = 2e-5 if prec else 2e-6
+    # bf16: the same bf16 operands either way (h rounded once), fp32 sums in
+    # another order (the direction-split projection adds two half-K partials);
+    # a last-bit difference in a gate pre-activation can flip the bf16
+    # rounding of an h, which the bf16 recurrence carries on (measured 2.5e-5
+    # on the objective after a step; the bf16 path is held to the fp64
+    # oracle in test_train_step_bf16_matches_oracle)
+    tol = 1e-4 if prec else 2e-6
     np.testing.assert_allclose(res["1"][0], res["0"][0], rtol=tol)
     np.testing.assert_allclose(res["1"][1], res["0"][1], rtol=tol)
     for a, b in zip(res["1"][2], res["0"][2]):
@@ -247,6 +252,15 @@ def test_streamed_gemms_group8(kctc, gpu, monkeypatch, knob, mode, H, T, N):
     (readiness = the slower group) and equal the GEMMs run after the recurrence."""
     monkeypatch.setenv("KCTC_REC_GS", "8")
     test_streamed_gemms_match_unstreamed(kctc, gpu, monkeypatch, knob, mode, H, T, N, 0)
+
+
+@pytest.mark.parametrize("mode,H,T,N", [(2, 512, 300, 16), (3, 256, 50, 32)])
+def test_streamed_projection_whole_k(kctc, gpu, monkeypatch, mode, H, T, N):
+    """KCTC_STREAM_DIRSPLIT=0: the streamed projection's tiles take the whole K
+    (both producer directions) once a row tile is complete, instead of two
+    half-K jobs per tile meeting in C."""
+    monkeypatch.setenv("KCTC_STREAM_DIRSPLIT", "0")
+    test_streamed_gemms_match_unstreamed(kctc, gpu, monkeypatch, "KCTC_FWD_STREAM", mode, H, T, N, 0)
 
 
 @pytest.mark.parametrize("mode,H,T,N", [(2, 512, 20, 16), (3, 256, 24, 11)])
