@@ -60,7 +60,8 @@ struct PParams {
   long sxg;                // halves per row group's part of a step image
   int backoff;             // streaming waits sleep in proportion to the producer's distance (KCTC_STREAM_BACKOFF)
   int sdir;                // streaming: K split by producer direction (two half-K jobs per C tile, see fwd_combine)
-  int dbg;                 // KCTC_STREAM_DBG diagnostics: 1 no combine wait, 2 wait for both directions, 4 no combine
+  int dbg;                 // KCTC_STREAM_DBG diagnostics: 1 no combine wait, 2 wait for both directions, 4 no combine,
+                           // 32 register-A k loop without the two-deep prefetch
   unsigned *serr;          // producer's error word (wait timeout)
   // backward stream (x3p_bwd_stream_kernel)
   const float *E;          // source rows of direction d: E + row * lde + d * edoff (KB * 32 floats)
@@ -389,6 +390,102 @@ __device__ __forceinline__ void fwd_combine(const PParams &p, floatx4 (&acc)[4][
 // BFM: the operands are bf16-packed ([row][KB][64] bf16, 64 consecutive k per
 // 128-B block): a stage is two v_mfma_f32_16x16x32_bf16 (chunks fq and 4 + fq)
 // instead of the three split-fp16 products, no exponents.
+// one k block of MFMAs on the LDS stage `cur` (A and B tiles)
+template <bool BFM>
+__device__ __forceinline__ void x3p_kblock(const unsigned char *cur, int wm, int wn, int fr, int fq,
+                                           floatx4 (&acc)[4][4]) {
+  halfx8 ah[4], al[4], bh[4], bl[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    ah[i] = frag(cur, wm + i * 16 + fr, fq);
+    al[i] = frag(cur, wm + i * 16 + fr, 4 + fq);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    bh[j] = frag(cur + TILEB, wn + j * 16 + fr, fq);
+    bl[j] = frag(cur + TILEB, wn + j * 16 + fr, 4 + fq);
+  }
+  if constexpr (BFM) {
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ah[i]),
+                                                            __builtin_bit_cast(bf16x8, bh[j]), acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al[i]),
+                                                            __builtin_bit_cast(bf16x8, bl[j]), acc[i][j], 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+  }
+}
+
+// k loop of the register-loaded A modes (SM 1: a forward producer's images,
+// SM 2: rows packed by other workgroups; both sc1 loads whose latency is a
+// MALL / other-XCD round trip): A is prefetched TWO k blocks ahead in a
+// two-slot register ring (the loop is unrolled by two so the ring indices are
+// static), B by LDS-DMA one block ahead, and the stage hand-over waits with a
+// counted vmcnt that leaves the newest A prefetch in flight plus a raw
+// s_barrier (a __syncthreads() would drain it).  Issue order per block it:
+// B(it + 1) then A(it + 2), so vmcnt(4) at the end of block it means B(it + 1)
+// and A(it + 1) have landed.  The body is straight-line (the loads past the
+// last block re-read it, clamped, and are drained after the loop): with the
+// loads under branches the compiler put a vmcnt(0) in front of every
+// prefetch.  Even block counts only (the caller falls back otherwise).
+template <int SM, bool BFM>
+__device__ __forceinline__ void x3p_kloop_reg(const PParams &p, unsigned char *lds, const _Float16 *A,
+                                              const _Float16 *B, int m0, int n0, int kb0, int nk, int wm, int wn,
+                                              int fr, int fq, floatx4 (&acc)[4][4]) {
+  u32x4 r0[4], r1[4];
+  const int kbl = kb0 + nk - 1;
+  auto loadA = [&](int kb, u32x4 (&r)[4]) {
+    if constexpr (SM == 1) load_tile_xch(p, A, m0, min(kb, kbl), r);
+    else load_tile_sc1(A, p.M, m0, p.KB, min(kb, kbl), r);
+  };
+  auto stage_wait = [&]() {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  loadA(kb0, r0);
+  issue_tile(B, p.N, n0, p.KB, kb0, lds + TILEB);
+  loadA(kb0 + 1, r1);
+  store_tile_lds(lds, r0);
+  stage_wait();
+  // block it: cur holds A(it), B(it); rn holds A(it + 1); rf is free
+  auto body = [&](int it, u32x4 (&rf)[4], u32x4 (&rn)[4]) {
+    unsigned char *cur = lds + (it & 1) * 2 * TILEB;
+    unsigned char *nxt = lds + ((it + 1) & 1) * 2 * TILEB;
+    issue_tile(B, p.N, n0, p.KB, min(kb0 + it + 1, kbl), nxt + TILEB);
+    loadA(kb0 + it + 2, rf);
+    x3p_kblock<BFM>(cur, wm, wn, fr, fq, acc);
+    store_tile_lds(nxt, rn);
+    stage_wait();
+  };
+  for (int it = 0; it < nk; it += 2) {
+    body(it, r0, r1);
+    body(it + 1, r1, r0);
+  }
+  // the clamped loads past the last block land before anyone reuses the stages
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
 template <int SM, bool BFM = false>
 __device__ __forceinline__ void x3p_tile(const PParams &p, unsigned char *lds, int tm, int tn, int b, int ks, int *prog) {
   constexpr bool STREAM = SM == 1;
@@ -408,6 +505,13 @@ __device__ __forceinline__ void x3p_tile(const PParams &p, unsigned char *lds, i
     for (int j = 0; j < 4; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   if (STREAM) x3p_wait_rows(p, m0, prog, p.sdir && !(p.dbg & 2) ? ks : -1);
+  if constexpr (SM != 0) {
+    if (!(p.dbg & 32) && nk >= 2 && !(nk & 1)) {
+      x3p_kloop_reg<SM, BFM>(p, lds, A, B, m0, n0, kb0, nk, wm, wn, fr, fq, acc);
+      goto epilogue;
+    }
+  }
+  {
   // LDS: [2 stages][A tile | B tile]
   u32x4 ra[4];
   if (nk > 0) {
@@ -475,6 +579,8 @@ __device__ __forceinline__ void x3p_tile(const PParams &p, unsigned char *lds, i
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+  }
+epilogue:
 
   // epilogue: acc[i][j][r] -> C[m0+wm+16i+4fq+r][n0+wn+16j+fr], times 2^-(eA + eB)
   const int *eA = p.eA ? p.eA + (long)b * p.seA : nullptr;
@@ -1264,6 +1370,7 @@ void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a) {
   p.part = a.part;
   p.sflags = a.flags; p.snwg = a.nwg; p.sT = a.T; p.sN = a.Nf; p.serr = a.err; p.srg = a.rg;
   p.backoff = env_backoff();
+  p.dbg = getenv("KCTC_STREAM_DBG") ? atoi(getenv("KCTC_STREAM_DBG")) : 0;
   KCTC_HIP_CHECK(hipMemsetAsync(a.cnt, 0, sizeof(int) * x3p_bwd_stream_ints(a.M, a.N), s));
   const int total = 2 * p.nrt * (p.P + p.gx);
   const dim3 grid(std::min(total, a.blocks > 0 ? a.blocks : 96));

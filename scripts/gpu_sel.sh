@@ -13,7 +13,7 @@ i=0
 for E in "$@"; do
   i=$((i+1))
   if [ "$E" = "-" ]; then E=""; fi
-  env $E timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench_$i.log 2>&1 || { echo BENCH_FAILED $E; tail -20 gpurun_out/bench_$i.log; exit 1; }
+  env $E timeout -k 10 300 python bench.py --no-cpu-baseline $BARGS > gpurun_out/bench_$i.log 2>&1 || { echo BENCH_FAILED $E; tail -20 gpurun_out/bench_$i.log; exit 1; }
   python3 -c "
 import json,sys
 d=json.loads(open('gpurun_out/bench_$i.log').read().strip().splitlines()[-1])
