@@ -2299,14 +2299,14 @@ static int pick_bwd_u4(const RnnDesc &d, int N) {
 // recurrence, U=8 37.1).  KCTC_FWD_U / KCTC_BWD_U force U.
 // Sequences per v6 row group: 16 (one MFMA row tile), or 8 for 9 <= N <= 32
 // -- the batch then runs as ceil(N / 8) independent recurrences side by side,
-// each moving half the hand-off rows per step.  Default: 8 in the forward
-// (configs[1]: 28.0 -> 27.0 ms/step of forward recurrence), 16 in the
-// backward (34.3 -> 34.7, and the weight GEMMs beside it get 64 CUs fewer).
-// KCTC_REC_GS sets both, KCTC_REC_GS_FWD / KCTC_REC_GS_BWD one direction.
-// (The default 8 applies to N <= 16; a set knob to N <= 32.)  pick6 falls
-// back to 16 when no workgroup partition fits the groups of 8.
+// each moving half the hand-off rows per step.  Default 8 for N <= 16
+// (configs[1]: forward 28.0 -> 27.0, backward 34.2 -> 33.0 ms/step of
+// recurrence; the weight GEMMs beside the backward get 64 CUs fewer and take
+// twice as long, still hidden).  KCTC_REC_GS sets both, KCTC_REC_GS_FWD /
+// KCTC_REC_GS_BWD one direction; a set knob applies up to N = 32.  pick6
+// falls back to 16 when no workgroup partition fits the groups of 8.
 static int v6_group_rows(int N, bool fwd) {
-  const int dflt = fwd && N <= 16 ? 8 : 16;
+  const int dflt = N <= 16 ? 8 : 16;
   const int want = env_int(fwd ? "KCTC_REC_GS_FWD" : "KCTC_REC_GS_BWD", env_int("KCTC_REC_GS", dflt));
   return (want == 8 && N > 8 && N <= 32) ? 8 : 16;
 }
