@@ -464,6 +464,41 @@ void CuDNNRecurrentComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
                                        const CuMatrixBase &out_deriv, Component *to_update_in,
                                        CuMatrixBase *in_deriv) const {
   const int N = mini_batch_, T = seq_length_;
+  auto &dev0 = CuDevice::Instantiate();
+  // the bottom component (no input derivative): its weight gradients are
+  // streamed off its own backward recurrence on the side stream (rnn.h
+  // RnnWgradStream) instead of following it
+  if (to_update_in && !in_deriv && dev0.side && rnn_wgrad_stream_ok(desc_, T, N)) {
+    auto *to_update = dynamic_cast<CuDNNRecurrentComponent *>(to_update_in);
+    if (!to_update) throw std::invalid_argument("CuDNNRecurrentComponent: bad to_update");
+    hipStream_t ws = dev0.side;
+    dev0.Fork();
+    to_update->grad_stream_ = ws;
+    KCTC_HIP_CHECK(hipMemsetAsync(to_update->grad_.p, 0, sizeof(float) * NumParameters(), ws));
+    RnnWgradStream wg;
+    wg.side = ws;
+    if (const char *e = getenv("KCTC_WGRAD_CHUNKS")) wg.chunks = atoi(e);
+    wg.x = in_value.Data();
+    wg.dw = to_update->grad_.f();
+    wg.max_blocks = side_gemm_blocks();
+    wg.in_bound = input_bound_;
+    {
+      ProfScope ps("layer_rnn_backward_data");
+      int st = rnn_backward_data(desc_, S(), T, N, out_value.Data(), out_deriv.Data(), params_.f(), nullptr,
+                                 workspace_.p, workspace_.bytes, reserve_.p, reserve_.bytes, DeviceError(),
+                                 dev0.stream2, &wg);
+      if (st) throw std::runtime_error("rnn_backward_data failed: " + std::to_string(st));
+    }
+    if (!wg.done) {
+      dev0.Fork();
+      ProfScope ps("layer_rnn_backward_weights", ws);
+      int st = rnn_backward_weights(desc_, ws, T, N, in_value.Data(), out_value.Data(), workspace_.p,
+                                    workspace_.bytes, to_update->grad_.f(), reserve_.p, reserve_.bytes,
+                                    side_gemm_blocks(), input_bound_);
+      if (st) throw std::runtime_error("rnn_backward_weights failed: " + std::to_string(st));
+    }
+    return;
+  }
   {
     ProfScope ps("layer_rnn_backward_data");
     int st = rnn_backward_data(desc_, S(), T, N, out_value.Data(), out_deriv.Data(), params_.f(),

@@ -65,10 +65,29 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
                          const float *w, float *y, void *workspace, size_t ws_bytes,
                          void *reserve, size_t res_bytes, unsigned *err, RnnFwdChain *chain = nullptr,
                          bool input_projected = false);
+// Weight gradients of a one-layer bidirectional split-fp16 LSTM computed off
+// its RUNNING backward recurrence (the bottom component, which has no dx to
+// stream): the frames are cut into `chunks` per direction in the order the
+// recurrence finishes them (direction 0 from the last frame down, direction
+// 1 from the first up); on `side`, a one-wave gate kernel waits for the
+// recurrence's flags to pass a chunk, then that chunk's transposes are packed
+// and its dW / dR GEMMs accumulate (beta = 1) into dw; the bias sums follow
+// the recurrence.  `dw` must be zeroed on `side` before.  done = launched.
+struct RnnWgradStream {
+  hipStream_t side = nullptr;
+  int chunks = 4;
+  const float *x = nullptr;  // the layer input
+  float *dw = nullptr;       // gradient (cuDNN layout)
+  int max_blocks = 0;
+  float in_bound = 0.f;
+  bool done = false;
+};
+bool rnn_wgrad_stream_ok(const RnnDesc &d, int T, int N);
 int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float *y,
                       const float *dy, const float *w, float *dx, void *workspace,
                       size_t ws_bytes, void *reserve, size_t res_bytes, unsigned *err,
-                      hipStream_t overlap = nullptr);  // overlap: stream for the streamed dx GEMM
+                      hipStream_t overlap = nullptr,  // overlap: stream for the streamed dx GEMM
+                      RnnWgradStream *wgrad = nullptr);
 int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *y, void *workspace, size_t ws_bytes, float *dw,
                          void *reserve, size_t res_bytes, int max_blocks = 0,

@@ -2693,12 +2693,142 @@ void launch_bwd_stream(const RnnDesc &d, const RecParams &p, int l, const float 
 }  // namespace
 
 // ---------------------------------------------------------------------------
+// streamed weight gradients of the bottom component (rnn.h RnnWgradStream)
+// ---------------------------------------------------------------------------
+namespace {
+// One wave: returns once every v6 flag line (stride kFlagStride words) holds
+// >= epoch, the recurrence reported an error, or after 3 s (then err bit 3).
+// Every exit decision is wave-uniform; the error store follows the loop.
+__global__ __launch_bounds__(64) void rec_gate_kernel(const unsigned *flags, int nlines, unsigned epoch,
+                                                      unsigned *err) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  int spins = 0;
+  bool late = false;
+  while (true) {
+    bool ok = true;
+    for (int i = threadIdx.x; i < nlines; i += 64)
+      ok &= __hip_atomic_load(flags + (long)i * kFlagStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= epoch;
+    if (__all(ok)) break;
+    if ((++spins & 255) == 0) {
+      const unsigned e = __builtin_amdgcn_readfirstlane(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if (e) break;
+      late = __builtin_amdgcn_s_memrealtime() - t0 > 300000000ull;
+      if (late) break;
+    }
+    __builtin_amdgcn_s_sleep(16);
+  }
+  if (late && threadIdx.x == 0) atomicOr(err, 8u);
+}
+
+// dW_dir += DX_dir^T x and dR_dir += DX_dir^T h_prev over the frames [ta, tb)
+// of direction dir (layer 0 of a one-layer component, split-fp16, LSTM: E == DX)
+void wgrad_frames(const RnnDesc &d, hipStream_t s, int T, int N, const float *x, const float *y, void *workspace,
+                  float *dw, void *reserve, int max_blocks, float in_bound, int dir, int ta, int tb) {
+  if (tb <= ta) return;
+  const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
+  const int NW = d.nw(), H = d.H, dirs = d.dirs, G4 = NW * H, Din = d.din(0);
+  const long ldg = (long)dirs * G4, ldy = (long)dirs * H;
+  const int R = (tb - ta) * N, KB = (R + 31) / 32;
+  const float *DX = static_cast<const float *>(reserve) + lay.E;
+  const PackLay pl = pack_layout(d, T, N);
+  _Float16 *DXt = pk<_Float16>(workspace, d, T, N, pl.a), *Xt = pk<_Float16>(workspace, d, T, N, pl.b);
+  _Float16 *Yt = pk<_Float16>(workspace, d, T, N, pl.c);
+  int *eDX = pk<int>(workspace, d, T, N, pl.ea), *eX = pk<int>(workspace, d, T, N, pl.eb);
+  int *eY = pk<int>(workspace, d, T, N, pl.ec);
+  unsigned *cm = pk<unsigned>(workspace, d, T, N, pl.cm);
+  unsigned *fl = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
+  float *ws = static_cast<float *>(workspace);
+  const long ws_floats = drec_split_floats(d, T, N);
+  {
+    ProfSpan ps(s, "x3_pack_w");
+    const float *src = DX + (long)ta * N * ldg + (long)dir * G4;
+    absmax_f32(s, src, ldg, R, G4, nullptr, cm);
+    x3p_pack_cols(s, src, ldg, R, G4, 0, DXt, eDX, cm, 0.f);
+    const float *xs = x + (long)ta * N * Din;
+    if (!(in_bound > 0.f)) absmax_f32(s, xs, Din, R, Din, nullptr, cm + G4);
+    x3p_pack_cols(s, xs, Din, R, Din, 0, Xt, eX, cm + G4, in_bound > 0.f ? in_bound : 0.f);
+    // h_prev: direction 0 pairs frame t with y(t - 1), direction 1 with y(t + 1);
+    // frames outside the sequence contribute zero (pack_cols zero-fills k - shift outside [0, R))
+    const float *yd = y + (long)dir * H;
+    if (dir == 0) {
+      if (ta == 0) x3p_pack_cols(s, yd, ldy, R, H, N, Yt, eY, nullptr, 1.f);
+      else x3p_pack_cols(s, yd + (long)(ta - 1) * N * ldy, ldy, R, H, 0, Yt, eY, nullptr, 1.f);
+    } else {
+      if (tb == T) x3p_pack_cols(s, yd + (long)ta * N * ldy, ldy, R, H, -N, Yt, eY, nullptr, 1.f);
+      else x3p_pack_cols(s, yd + (long)(ta + 1) * N * ldy, ldy, R, H, 0, Yt, eY, nullptr, 1.f);
+    }
+  }
+  auto split_for = [&](int n) {
+    int sp = x3p_pick_split(G4, n, KB, 1);
+    while (sp > 1 && (long)sp * G4 * n > ws_floats) sp--;
+    return sp;
+  };
+  const long pl0 = d.lin_offset(dir, 0, false);
+  {
+    X3PArgs a;
+    a.M = G4; a.N = Din; a.KB = KB;
+    a.A = DXt; a.eA = eDX; a.B = Xt; a.eB = eX;
+    a.C = dw + pl0; a.ldc = Din; a.beta = 1.f; a.batch = 1;
+    a.split_k = split_for(Din); a.ws = ws;
+    a.max_blocks = max_blocks;
+    if (max_blocks > 0) a.tile_counter = reinterpret_cast<int *>(fl + 1008);
+    ProfSpan ps(s, "gemm_bwd_w");
+    gemm_x3p(s, a);
+  }
+  {
+    X3PArgs a;
+    a.M = G4; a.N = H; a.KB = KB;
+    a.A = DXt; a.eA = eDX; a.B = Yt; a.eB = eY;
+    a.C = dw + d.lin_offset(dir, NW, false); a.ldc = H; a.beta = 1.f; a.batch = 1;
+    a.split_k = split_for(H); a.ws = ws;
+    a.max_blocks = max_blocks;
+    if (max_blocks > 0) a.tile_counter = reinterpret_cast<int *>(fl + 1009);
+    ProfSpan ps(s, "gemm_bwd_r");
+    gemm_x3p(s, a);
+  }
+}
+
+// dbW += sum dGx, dbR += sum dGh of layer l from the recurrence's per-group partials
+void wgrad_bias(const RnnDesc &d, hipStream_t s, int T, int N, float *dw, void *reserve, int l) {
+  const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
+  const int NW = d.nw(), H = d.H, dirs = d.dirs, G4 = NW * H;
+  const float *R0 = static_cast<const float *>(reserve) + lay.per_layer * l;
+  const long pl0 = d.lin_offset(l * dirs, 0, false), pls = d.pl_size(l);
+  float *dwl = dw + pl0;
+  const long bW = d.lin_offset(l * dirs, 0, true) - pl0;
+  const long bR = d.lin_offset(l * dirs, NW, true) - pl0;
+  // (v6: one partial per row group, [group][dir][2][G], added in group order)
+  const V6Cfg c6b = pick6(d, N, false);
+  const int rg = c6b ? c6b.rg : 1;
+  for (int gi = 0; gi < rg; gi++)
+    for (int dir = 0; dir < dirs; dir++) {
+      const float *part = R0 + lay.bias + ((long)gi * dirs + dir) * 2 * G4;
+      clip_sgd_update(s, dwl + dir * pls + bW, part, G4, 1.f, 0.f);
+      clip_sgd_update(s, dwl + dir * pls + bR, part + G4, G4, 1.f, 0.f);
+    }
+}
+}  // namespace
+
+// Off by default (KCTC_WGRAD_STREAM=1 turns it on): measured on configs[1]
+// 470.4k -> 467.0k (2 chunks), 466.1k (4), 454.5k (8) frames/s: the chunk
+// GEMMs beside the backward recurrence slow it (33.0 -> 33.3-33.5 ms/step)
+// and the per-chunk transposes add packing, more than the 1 ms tail saved.
+bool rnn_wgrad_stream_ok(const RnnDesc &d, int T, int N) {
+  if (!env_int("KCTC_WGRAD_STREAM", 0) || d.layers != 1 || d.dirs != 2 || d.mode != kLstm ||
+      d.prec != kPrecX3 || T < 8 || N > 16)
+    return false;
+  if (!pick6(d, N, false) || !use_x3((int)((long)T * N)) || !use_x3(d.nw() * d.H)) return false;
+  return (long)T * N * d.din(0) * 4 < (1L << 31);
+}
+
+// ---------------------------------------------------------------------------
 // host: backward data (dGates into the reserve, dx)
 // ---------------------------------------------------------------------------
 int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float *y,
                       const float *dy, const float *w, float *dx, void *workspace,
                       size_t ws_bytes, void *reserve, size_t res_bytes, unsigned *err,
-                      hipStream_t overlap) {
+                      hipStream_t overlap, RnnWgradStream *wgrad) {
+  if (wgrad) wgrad->done = false;
   if (T <= 0 || N <= 0 || N > 16 * kMaxRT || d.H % 16) return KRNN_NOT_SUPPORTED;
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
   if (res_bytes < sizeof(float) * (size_t)lay.total) return KRNN_BAD_PARAM;
@@ -2768,13 +2898,17 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
                           NW * H <= 4096 &&
                           (d.prec == kPrecX3 || (NW * H) % 64 == 0) && (long)TN * Din * 4 < (1L << 31) &&
                           env_int("KCTC_BWD_STREAM", 1);
-    p.e_sc1 = env_int("KCTC_DIAG_ESC1", streamed ? 1 : 0);  // diagnostic override (0 with streaming: wrong dx)
+    // weight gradients streamed off this recurrence (the bottom component):
+    // its dGates rows must be written through too
+    const bool wstream = wgrad && wgrad->side && !dxl && ver == 6 && !p.xpd && d.layers == 1 &&
+                         rnn_wgrad_stream_ok(d, T, N);
+    p.e_sc1 = env_int("KCTC_DIAG_ESC1", (streamed || wstream) ? 1 : 0);  // diagnostic override (0 with streaming: wrong dx)
     if (ver == 6) {
       p.cmax = pk<unsigned>(workspace, d, T, N, pack_layout(d, T, N).cme);
       if (p.rg > 1)  // max over the row groups by atomicMax on the float bits
         KCTC_HIP_CHECK(hipMemsetAsync(p.cmax, 0, sizeof(unsigned) * 2 * dirs * NW * H, s));
     }
-    const hipEvent_t fork = streamed ? fork_event(s) : nullptr;
+    const hipEvent_t fork = (streamed || wstream) ? fork_event(s) : nullptr;
     {
       ProfSpan ps(s, "rnn_bwd_rec");
       if (ver == 6) launch6(false, d.mode, d.prec, c6.nth, p, grid, lds, s);
@@ -2784,6 +2918,27 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     if (streamed) {
       launch_bwd_stream(d, p, l, w, dxl, workspace, T, N, overlap, fork, err);
       join_stream(s, overlap);
+    }
+    if (wstream) {
+      // chunk c of C: direction 0 frames [T - b(c+1), T - b(c)), direction 1
+      // [b(c), b(c+1)), b(c) = c T / C; complete once every flag line holds
+      // epoch b(c+1) + 2 (rows of step k are out at epoch k + 3)
+      hipStream_t ws2 = wgrad->side;
+      KCTC_HIP_CHECK(hipStreamWaitEvent(ws2, fork, 0));  // after the flag reset
+      const int C = std::max(1, std::min(wgrad->chunks, T / 4));
+      const unsigned *lines = p.flags + 1024;
+      const int nlines = p.rg * dirs * p.nwg;
+      for (int c = 0; c < C; c++) {
+        const int b0 = (int)((long)c * T / C), b1 = (int)((long)(c + 1) * T / C);
+        hipLaunchKernelGGL(rec_gate_kernel, dim3(1), dim3(64), 0, ws2, lines, nlines, (unsigned)(b1 + 2), err);
+        wgrad_frames(d, ws2, T, N, wgrad->x, y, workspace, wgrad->dw, reserve, wgrad->max_blocks, wgrad->in_bound, 0,
+                     T - b1, T - b0);
+        wgrad_frames(d, ws2, T, N, wgrad->x, y, workspace, wgrad->dw, reserve, wgrad->max_blocks, wgrad->in_bound, 1,
+                     b0, b1);
+      }
+      join_stream(ws2, s);  // the bias partials are written after the last flag
+      wgrad_bias(d, ws2, T, N, wgrad->dw, reserve, 0);
+      wgrad->done = true;
     }
     if (ver == 6) xch_release(s);
     tr.dump("bwd", s, grid.x, p.nwg, T, dirs, ver, ver == 6 ? (p.xpd ? 1 : 0) : p.xpd);

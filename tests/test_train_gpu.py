@@ -270,6 +270,32 @@ def test_train_step_group8_matches_oracle(kctc, gpu, oracle, monkeypatch, mode, 
     test_train_step_row_groups_match_oracle(kctc, gpu, oracle, mode, H, T, N)
 
 
+@pytest.mark.parametrize("H,T,N,chunks", [(512, 64, 16, 4), (256, 50, 7, 3), (256, 33, 12, 8)])
+def test_wgrad_stream_matches_whole(kctc, gpu, monkeypatch, H, T, N, chunks):
+    """The bottom component's weight gradients streamed off its running
+    backward recurrence (frame chunks gated on its flags, KCTC_WGRAD_STREAM=1,
+    the default) against the whole-sequence weight GEMMs after it (=0):
+    equal up to fp32 rounding of the chunked sums."""
+    import torch
+    D, A = 40, 41
+    cfg = kctc.recipe_config(num_rnn=2, input_dim=D, hidden=H, num_targets=A, rnn_mode=2,
+                             learning_rate=1e-3, param_stddev=0.05)
+    feats, nf, fl, ll = kctc.synth_minibatch(19, T, N, D, A, 0.125)
+    f = torch.from_numpy(feats).to(gpu)
+    monkeypatch.setenv("KCTC_WGRAD_CHUNKS", str(chunks))
+    res = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("KCTC_WGRAD_STREAM", flag)
+        net = kctc.Nnet(cfg, seed=9)
+        for _ in range(2):
+            net.train_step(f, T, N, nf, fl, ll)
+        res[flag] = (net.compute_objf(f, T, N, nf, fl, ll)[0],
+                     [net.get_params(c).astype(np.float64) for c in range(net.num_components) if net.num_params(c) > 0])
+    np.testing.assert_allclose(res["1"][0], res["0"][0], rtol=2e-6)
+    for a, b in zip(res["1"][1], res["0"][1]):
+        assert rel_err(a, b) < 1e-6
+
+
 def test_rccl_dp_single_rank_matches_plain(kctc, gpu):
     """kctc_nnet_enable_dp at world size 1 builds the RCCL exchange
     (ncclCommInitRank on a one-rank communicator): every component's bucket is
