@@ -138,6 +138,36 @@ def test_rnn_bf16_matches_oracle(kctc, gpu, oracle, case):
     assert rel_err(y2, ry) < 1e-5 < errs["y"]
 
 
+def test_gemm_x3_rarely_active_columns(kctc, gpu):
+    """dW-shaped split-fp16 GEMM (C = A^T B over K frames) whose A columns are
+    "rarely active" gate units: a few frames O(1), the rest down to 1e-9 (a
+    saturated sigmoid's derivative), so an output element can be dominated by
+    terms far below the column maximum the power-of-two scale is taken from
+    (their lo parts fall into fp16 subnormals).  Element-wise against fp64,
+    normalised by the element's own sum of |terms| -- the bound an fp32 sgemm
+    is held to -- and next to numpy's fp32 sgemm on the same operands."""
+    import torch
+    rng = np.random.default_rng(5)
+    K, M, N = 6000, 192, 96
+    A = rng.standard_normal((K, M)).astype(np.float32)
+    act = rng.uniform(size=(K, M)) < np.array([1.0, 0.1, 0.01, 0.001])[np.arange(M) % 4]
+    A = np.where(act, A, A * (10.0 ** rng.uniform(-9, -3, (K, M)))).astype(np.float32)
+    B = np.tanh(rng.standard_normal((K, N))).astype(np.float32)   # h in (-1, 1)
+    B[rng.uniform(size=(K, N)) < 0.3] = 0.0                       # units off at many frames
+    C = torch.zeros((M, N), dtype=torch.float32, device=gpu)
+    kctc.add_mat_mat_x3(C, torch.from_numpy(A).to(gpu), torch.from_numpy(B).to(gpu), True, False,
+                        alpha=1.0, beta=0.0)
+    torch.cuda.synchronize()
+    ref = A.T.astype(np.float64) @ B.astype(np.float64)
+    den = np.abs(A.T).astype(np.float64) @ np.abs(B).astype(np.float64) + 1e-300
+    e_x3 = np.abs(C.cpu().numpy().astype(np.float64) - ref) / den
+    e_f32 = np.abs((A.T @ B).astype(np.float64) - ref) / den
+    print(f"max element error / sum|terms|: x3 {e_x3.max():.2e}, fp32 sgemm {e_f32.max():.2e}")
+    # measured: x3 2.3e-6, numpy fp32 sgemm 1.2e-6 (both far inside the 1e-4 bar)
+    assert e_x3.max() < 1e-5
+    assert e_x3.max() < 5 * max(e_f32.max(), 6e-8)
+
+
 def test_rnn_golden_layout(kctc, gpu):
     """The torch-fp64 golden fixture through the HIP path (cuDNN layout)."""
     import torch
