@@ -47,7 +47,7 @@ struct UttDesc {
 };
 
 struct Layout {
-  size_t desc, labels, costs, logz, lp, spill, offs, total;
+  size_t desc, labels, links, owner, costs, logz, lp, spill, offs, total;
   int T_max;
   long long spill_floats, off_doubles;
 };
@@ -77,6 +77,8 @@ static bool make_layout(const int *label_lengths, const int *input_lengths, int 
   size_t p = 0;
   l.desc = p;   p = align_up(p + sizeof(UttDesc) * N, 256);
   l.labels = p; p = align_up(p + sizeof(int) * (nlab > 0 ? nlab : 1), 256);
+  l.links = p;  p = align_up(p + sizeof(int) * (nlab > 0 ? nlab : 1), 256);  // next position of the same label
+  l.owner = p;  p = align_up(p + sizeof(int) * (size_t)N * A, 256);          // first position of each label
   l.costs = p;  p = align_up(p + sizeof(double) * N, 256);
   l.logz = p;   p = align_up(p + sizeof(float) * (size_t)T_max * N + 4, 256);
   l.lp = p;     p = align_up(p + sizeof(float) * (size_t)T_max * N * A + 4, 256);
@@ -333,7 +335,7 @@ __global__ __launch_bounds__(kABThreads) void ctc_alpha_beta(
 __global__ __launch_bounds__(kThreads) void ctc_grad(
     const float *__restrict__ acts, const float *__restrict__ logz, float *__restrict__ grads,
     int N, int A, int T_max, int blank, const UttDesc *__restrict__ descs,
-    const int *__restrict__ labels, const float *__restrict__ spill,
+    const int *__restrict__ links, const int *__restrict__ owners, const float *__restrict__ spill,
     const double *__restrict__ offs, const double *__restrict__ costs) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = blockIdx.y, t0 = blockIdx.x * kFR, tid = threadIdx.x;
@@ -352,19 +354,10 @@ __global__ __launch_bounds__(kThreads) void ctc_grad(
   int *owner = nxt + (L > 0 ? L : 1);
   float *gblank = reinterpret_cast<float *>(owner + A);
   float *gtot = gblank + kFR;
-  const int *lab = labels + d.lab_off;
-  for (int a = tid; a < A; a += kThreads) owner[a] = -1;
-  __syncthreads();
-  for (int j = tid; j < L; j += kThreads) {
-    int k = lab[j], nx = -1;
-    for (int i = j + 1; i < L; i++)
-      if (lab[i] == k) { nx = i; break; }
-    nxt[j] = nx;
-    bool first = true;
-    for (int i = 0; i < j; i++)
-      if (lab[i] == k) { first = false; break; }
-    if (first) owner[k] = j;
-  }
+  // label chains (first position of each label, next position of the same
+  // label), computed once per call on the host and staged with the labels
+  for (int a = tid; a < A; a += kThreads) owner[a] = owners[(long)n * A + a];
+  for (int j = tid; j < L; j += kThreads) nxt[j] = links[d.lab_off + j];
   const double logp = -costs[n];
   const float *al = spill + d.ab_off;
   const float *be = al + (long long)T * S;
@@ -466,6 +459,23 @@ static ctcStatus_t launch(const float *acts, float *grads, const int *flat_label
   if (!stage) return CTC_STATUS_MEMOPS_FAILED;
   memcpy(stage + lay.desc, descs.data(), sizeof(UttDesc) * N);
   if (nlab) memcpy(stage + lay.labels, flat_labels, sizeof(int) * nlab);
+  {
+    // per utterance: owner[a] = first position of label a (-1: absent),
+    // links[j] = next position holding the same label as j (-1: last)
+    int *links = reinterpret_cast<int *>(stage + lay.links), *owner = reinterpret_cast<int *>(stage + lay.owner);
+    std::fill(owner, owner + (size_t)N * A, -1);
+    long long off = 0;
+    for (int n = 0; n < N; n++) {
+      const int L = label_lengths[n];
+      int *own = owner + (size_t)n * A;
+      for (int j = L - 1; j >= 0; j--) {
+        const int k = flat_labels[off + j];
+        links[off + j] = own[k];
+        own[k] = j;
+      }
+      off += L;
+    }
+  }
   if (hipMemcpyAsync(ws, stage, lay.costs, hipMemcpyHostToDevice, stream) != hipSuccess)
     return CTC_STATUS_MEMOPS_FAILED;
   staging_release(stream);
@@ -517,8 +527,9 @@ static ctcStatus_t launch(const float *acts, float *grads, const int *flat_label
     if (shm > 160 * 1024) return CTC_STATUS_INVALID_VALUE;
     ProfSpan ps(stream, "ctc_grad");
     hipLaunchKernelGGL(ctc_grad, dim3(ceil_div(lay.T_max, kFR), N), dim3(kThreads), shm, stream,
-                       acts, d_logz, grads, N, A, lay.T_max, blank, d_desc, d_lab, d_spill,
-                       d_offs, costs_dev);
+                       acts, d_logz, grads, N, A, lay.T_max, blank, d_desc,
+                       reinterpret_cast<const int *>(ws + lay.links), reinterpret_cast<const int *>(ws + lay.owner),
+                       d_spill, d_offs, costs_dev);
   }
   if (hipGetLastError() != hipSuccess) return CTC_STATUS_EXECUTION_FAILED;
   return CTC_STATUS_SUCCESS;
