@@ -134,6 +134,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-h2d-pass", action="store_true")
+    ap.add_argument("--average-every", type=int, default=0,
+                    help="N>1: the recipe's model averaging every K steps instead of the per-step "
+                         "gradient all-reduce (kctc_nnet_set_dp_mode 1)")
     args = ap.parse_args()
     cf = CONFIGS[args.config]
 
@@ -163,6 +166,8 @@ def main():
         uid = k.dp_unique_id() if rank == 0 else bytes(128)
         obj = [uid]
         dist.broadcast_object_list(obj, src=0)
+        if args.average_every > 0:
+            net.set_dp_mode("average")
         net.enable_dp(obj[0], rank, world)
 
     total = args.warmup + args.steps
@@ -208,6 +213,9 @@ def main():
             if r is not None:
                 stats.append(r)
             frames += int(nf.sum())
+            if world > 1 and args.average_every > 0 and (i + 1) % args.average_every == 0:
+                stats += net.train_flush()
+                net.average_params()
         stats += net.train_flush()
         evs[-1].record(ext)
         barrier()

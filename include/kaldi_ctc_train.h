@@ -137,6 +137,16 @@ int kctc_nnet_enable_dp(kctcNnet_t nnet, const void *uid128, int rank, int world
  * (several processes sharing one GPU, CPU-side rendezvous). */
 typedef void (*kctc_host_allreduce_fn)(float *buf, long n, void *user);
 int kctc_nnet_enable_dp_host(kctcNnet_t nnet, kctc_host_allreduce_fn allreduce, void *user, int world_size);
+/* Data-parallel mode.  0 (default): the gradient of every step is summed over
+ * the ranks before the update (kctc_nnet_enable_dp).  1: model averaging --
+ * the ranks step independently and kctc_nnet_average_params replaces every
+ * updatable component's parameters by their mean over the ranks: the recipe's
+ * per-iteration nnet-am-average (egs/wsj/s5/steps/ctc/train.sh:434-435,
+ * src/nnet2bin/nnet-am-average.cc:185-241, default weights 1/num-models),
+ * e.g. called every K minibatches.  ClipGradient counters and momentum
+ * deltas stay per rank (nnet-am-average only averages updatable components). */
+int kctc_nnet_set_dp_mode(kctcNnet_t nnet, int mode);
+int kctc_nnet_average_params(kctcNnet_t nnet);
 
 /* Arithmetic of every CuDNNRecurrentComponent's recurrences and gate GEMMs:
  * 0 fp32-class (default), 1 bf16 operands with fp32 accumulation and fp32

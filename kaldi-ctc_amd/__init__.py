@@ -517,6 +517,14 @@ class Nnet:
         buf = ctypes.create_string_buffer(bytes(uid), 128)
         _tcheck(lib().kctc_nnet_enable_dp(self.h, buf, rank, world), "enable_dp")
 
+    def set_dp_mode(self, mode):
+        """"grad" (sum the gradients every step) or "average" (independent steps,
+        average_params() = nnet-am-average over the ranks)."""
+        _tcheck(lib().kctc_nnet_set_dp_mode(self.h, {"grad": 0, "average": 1}[mode]), "set_dp_mode")
+
+    def average_params(self):
+        _tcheck(lib().kctc_nnet_average_params(self.h), "average_params")
+
     def enable_dp_host(self, allreduce, world):
         """Gradient exchange over a host transport: allreduce(np.float32 array)
         must sum it in place across the ranks (e.g. gloo)."""

@@ -69,6 +69,8 @@ SIGS = {
     "kctc_dp_unique_id": (ci, [vp]),
     "kctc_nnet_enable_dp": (ci, [vp, vp, ci, ci]),
     "kctc_nnet_enable_dp_host": (ci, [vp, vp, vp, ci]),
+    "kctc_nnet_set_dp_mode": (ci, [vp, ci]),
+    "kctc_nnet_average_params": (ci, [vp]),
     "kctc_nnet_set_momentum": (ci, [vp, cf]),
     "kctc_nnet_set_precision": (ci, [vp, ci]),
     "krnnSetPrecision": (ci, [vp, ci]),

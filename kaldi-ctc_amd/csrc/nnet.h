@@ -160,6 +160,8 @@ class UpdatableComponent : public Component {
   virtual void UnVectorize(const float *host) = 0;
   // gradient produced by the last Backprop (device), in Vectorize order
   virtual float *GradData() = 0;
+  // the parameters (device), in Vectorize order
+  virtual float *ParamData() = 0;
   // stream on which GradData() was produced (the exchange waits on it)
   hipStream_t GradStream() const;
   // params += lr * (clipped) grad; skipped on device when *skip != 0 (the
@@ -221,6 +223,7 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   void Vectorize(float *host) const override;
   void UnVectorize(const float *host) override;
   float *GradData() override { return grad_.f(); }
+  float *ParamData() override { return params_.f(); }
   void ApplyUpdate(const unsigned *skip = nullptr) override;
   // device error word of the recurrences (hand-off timeout); the updater
   // points every RNN at its own per-step word (SetErrorWord)
@@ -348,6 +351,7 @@ class AffineComponent : public UpdatableComponent {
   void Vectorize(float *host) const override;  // linear (row-major) then bias
   void UnVectorize(const float *host) override;
   float *GradData() override { return grad_.f(); }
+  float *ParamData() override { return params_.f(); }
   void ApplyUpdate(const unsigned *skip = nullptr) override;
 
  private:
@@ -387,6 +391,8 @@ class GradExchange {
   virtual void GradReady(int component, float *grad, long n, hipStream_t producer) = 0;
   virtual void Finish() = 0;  // compute stream waits for every launched all-reduce
   virtual int WorldSize() const = 0;
+  // in-place sum of buf over the ranks, ordered on stream s (s waits for it)
+  virtual void AllReduceSum(float *buf, long n, hipStream_t s) = 0;
 };
 
 struct MinibatchStats {

@@ -17,6 +17,7 @@
 #include "common.h"
 #include "decodable.h"
 #include "egs.h"
+#include "elementwise.h"
 #include "kaldi_io.h"
 #include "nnet.h"
 
@@ -63,6 +64,14 @@ class RcclExchange : public kctc::nnet2::GradExchange {
     KCTC_HIP_CHECK(hipStreamWaitEvent(compute_, done_, 0));
   }
   int WorldSize() const override { return world_; }
+  void AllReduceSum(float *buf, long n, hipStream_t s) override {
+    KCTC_HIP_CHECK(hipEventRecord(ready_, s));
+    KCTC_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ready_, 0));
+    if (ncclAllReduce(buf, buf, (size_t)n, ncclFloat, ncclSum, comm_, comm_stream_) != ncclSuccess)
+      throw std::runtime_error("ncclAllReduce failed");
+    KCTC_HIP_CHECK(hipEventRecord(done_, comm_stream_));
+    KCTC_HIP_CHECK(hipStreamWaitEvent(s, done_, 0));
+  }
 
  private:
   int world_;
@@ -107,6 +116,10 @@ class HostExchange : public kctc::nnet2::GradExchange {
     buckets_.clear();
   }
   int WorldSize() const override { return world_; }
+  void AllReduceSum(float *buf, long n, hipStream_t s) override {
+    buckets_.push_back({buf, n, s});
+    Finish();
+  }
 
  private:
   struct Bucket {
@@ -136,6 +149,7 @@ struct kctcNnetImpl {
   kctc::nnet2::NnetCtcUpdater evaluator{&nnet, false};
   hipStream_t side = nullptr, stream2 = nullptr;
   kctc::nnet2::GradExchange *dp = nullptr;
+  bool dp_average = false;  // model averaging: no per-step gradient exchange
   kctc::nnet2::DevBuf egs_feats, egs_scratch;  // TrainNnetSimple staging
   // nnet2-ctc model file extras: the CtcTransitionModel exactly as read (opaque
   // bytes, in the mode of the file it came from) and AmNnet's priors
@@ -561,7 +575,7 @@ int kctc_nnet_enable_dp(kctcNnet_t n, const void *uid128, int rank, int world_si
     n->trainer.SetExchange(nullptr);
     if (world_size >= 1) {  // one rank included: the same communicator and all-reduce path
       n->dp = new RcclExchange(uid128, rank, world_size, n->stream);
-      n->trainer.SetExchange(n->dp);
+      n->trainer.SetExchange(n->dp_average ? nullptr : n->dp);
     }
   });
 }
@@ -573,7 +587,36 @@ int kctc_nnet_enable_dp_host(kctcNnet_t n, kctc_host_allreduce_fn fn, void *user
     n->activate();
     delete n->dp;
     n->dp = new HostExchange(fn, user, world_size, n->stream);
-    n->trainer.SetExchange(n->dp);
+    n->trainer.SetExchange(n->dp_average ? nullptr : n->dp);
+  });
+}
+
+int kctc_nnet_set_dp_mode(kctcNnet_t n, int mode) {
+  return guarded([&] {
+    KCTC_REQUIRE(n && (mode == 0 || mode == 1), "kctc_nnet_set_dp_mode: mode must be 0 or 1");
+    KCTC_REQUIRE(n->trainer.Pending() == 0, "kctc_nnet_set_dp_mode with minibatches in flight");
+    n->dp_average = mode == 1;
+    n->trainer.SetExchange(n->dp && !n->dp_average ? n->dp : nullptr);
+  });
+}
+
+// nnet-am-average over the data-parallel ranks (src/nnet2bin/nnet-am-average.cc:
+// 185-241 with the default weights 1/num-models): every updatable component's
+// parameters become the mean of the ranks' copies.  Sum in place through the
+// exchange (RCCL or host transport), then scale by 1/world, on the compute stream.
+int kctc_nnet_average_params(kctcNnet_t n) {
+  return guarded([&] {
+    KCTC_REQUIRE(n && n->dp, "kctc_nnet_average_params: data parallelism not enabled");
+    KCTC_REQUIRE(n->trainer.Pending() == 0, "kctc_nnet_average_params with minibatches in flight");
+    n->activate();
+    const int world = n->dp->WorldSize();
+    for (int c = 0; c < n->nnet.NumComponents(); c++) {
+      auto *u = dynamic_cast<kctc::nnet2::UpdatableComponent *>(&n->nnet.GetComponent(c));
+      if (!u) continue;
+      n->dp->AllReduceSum(u->ParamData(), u->NumParameters(), n->stream);
+      if (world > 1) kctc::scale_inplace(n->stream, u->ParamData(), u->NumParameters(), 1.f / (float)world);
+    }
+    KCTC_HIP_CHECK(hipStreamSynchronize(n->stream));
   });
 }
 

@@ -101,3 +101,69 @@ def test_two_rank_dp_equals_concatenated_minibatch(kctc, gpu):
     for a, b in zip(res[0][2], ref):
         assert rel_err(a.astype(np.float64), b.astype(np.float64)) < 1e-6
     net.close()
+
+
+def _avg_rank_main(rank, world, port, q):
+    try:
+        import torch
+        import torch.distributed as dist
+        sys.path.insert(0, ROOT)
+        import __graft_entry__ as ge
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        kctc = ge.load_package()
+        net = kctc.Nnet(_cfg(kctc), seed=21)
+
+        def allreduce(buf):
+            dist.all_reduce(torch.from_numpy(buf))
+
+        net.set_dp_mode("average")
+        net.enable_dp_host(allreduce, world)
+        for step in range(STEPS):
+            feats, nf, fl, ll = _batch(kctc, rank, step)
+            net.train_step(torch.from_numpy(feats).to("cuda:0"), T, N, nf, fl, ll)
+        before = [net.get_params(c) for c in range(net.num_components) if net.num_params(c)]
+        net.average_params()
+        after = [net.get_params(c) for c in range(net.num_components) if net.num_params(c)]
+        q.put((rank, before, after))
+        net.close()
+        dist.destroy_process_group()
+    except BaseException as e:  # report, never hang the parent
+        q.put((rank, repr(e), None))
+
+
+def test_two_rank_model_averaging(kctc, gpu):
+    """kctc_nnet_set_dp_mode(1): the ranks step independently (no gradient
+    exchange), then kctc_nnet_average_params makes every updatable
+    component the mean of the ranks' copies -- the recipe's nnet-am-average
+    (nnet-am-average.cc:185-241, weights 1/2).  Each rank's pre-average
+    parameters equal a lone trainer on that rank's minibatches; afterwards
+    both ranks hold (p0 + p1) / 2 bit for bit."""
+    import torch
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31500 + os.getpid() % 2000
+    procs = [ctx.Process(target=_avg_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r = q.get(timeout=200)
+        res[r[0]] = r
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        assert res[r][2] is not None, res[r][1]
+    for r in (0, 1):  # independent steps: a lone trainer on rank r's data
+        net = kctc.Nnet(_cfg(kctc), seed=21)
+        for step in range(STEPS):
+            feats, nf, fl, ll = _batch(kctc, r, step)
+            net.train_step(torch.from_numpy(feats).to(gpu), T, N, nf, fl, ll)
+        alone = [net.get_params(c) for c in range(net.num_components) if net.num_params(c)]
+        net.close()
+        for a, b in zip(res[r][1], alone):
+            np.testing.assert_array_equal(a, b)
+    for p0, p1, a0, a1 in zip(res[0][1], res[1][1], res[0][2], res[1][2]):
+        np.testing.assert_array_equal(a0, a1)
+        np.testing.assert_array_equal(a0, (p0 + p1) * np.float32(0.5))

@@ -318,6 +318,30 @@ def test_rccl_dp_single_rank_matches_plain(kctc, gpu):
             np.testing.assert_array_equal(nets[0].get_params(c), nets[1].get_params(c))
 
 
+def test_rccl_model_averaging_single_rank(kctc, gpu):
+    """Model-averaging mode over the RCCL communicator at world size 1: no
+    gradient exchange during the steps, and averaging one model is the
+    identity -- the parameters equal a plain trainer's bit for bit."""
+    import torch
+    D, A, T, N, H = 40, 41, 32, 4, 256
+    cfg = kctc.recipe_config(num_rnn=2, input_dim=D, hidden=H, num_targets=A, learning_rate=1e-3,
+                             param_stddev=0.05)
+    feats, nf, fl, ll = kctc.synth_minibatch(23, T, N, D, A, 0.125)
+    f = torch.from_numpy(feats).to(gpu)
+    nets = [kctc.Nnet(cfg, seed=4), kctc.Nnet(cfg, seed=4)]
+    nets[1].set_dp_mode("average")
+    nets[1].enable_dp(kctc.dp_unique_id(), 0, 1)
+    for net in nets:
+        for _ in range(2):
+            net.train_step(f, T, N, nf, fl, ll)
+    nets[1].average_params()
+    for c in range(nets[0].num_components):
+        if nets[0].num_params(c):
+            np.testing.assert_array_equal(nets[0].get_params(c), nets[1].get_params(c))
+    for net in nets:
+        net.close()
+
+
 def test_async_steps_equal_sync_steps(kctc, gpu):
     """kctc_nnet_train_step_async / train_flush: the same updates and the same
     per-minibatch stats as kctc_nnet_train_step, reported one step late."""
