@@ -228,6 +228,10 @@ def main():
     objf = sum(o for o, _, _ in stats)
     acc = sum(a for _, a, _ in stats)
     wt = sum(w for _, _, w in stats)
+    if world > 1:  # the loss / accuracy / label totals summed over the ranks
+        tot = torch.tensor([objf, acc, wt], dtype=torch.float64)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        objf, acc, wt = float(tot[0]), float(tot[1]), float(tot[2])
     fam_flops, _ = model_flops(T, N, D, H, A, L, nw=nw)
     if args.config != 1:
         # the committed PMC traffic was measured on configs[1]
