@@ -519,9 +519,12 @@ void CuDNNRecurrentComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
     to_update->grad_stream_ = ws;
     KCTC_HIP_CHECK(hipMemsetAsync(to_update->grad_.p, 0, sizeof(float) * NumParameters(), ws));
     ProfScope ps("layer_rnn_backward_weights", ws);
+    // the bottom component (no input derivative): its weight GEMMs are the
+    // step's tail, so dW runs beside dR on the (then idle) dx-stream queue
     int st = rnn_backward_weights(desc_, ws, T, N, in_value.Data(), out_value.Data(), workspace_.p,
                                   workspace_.bytes, to_update->grad_.f(), reserve_.p, reserve_.bytes,
-                                  dev.side ? side_gemm_blocks() : 0, input_bound_);
+                                  dev.side ? side_gemm_blocks() : 0, input_bound_,
+                                  (!in_deriv && dev.side) ? dev.stream2 : nullptr);
     if (st) throw std::runtime_error("rnn_backward_weights failed: " + std::to_string(st));
   }
 }

@@ -91,6 +91,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
 int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *y, void *workspace, size_t ws_bytes, float *dw,
                          void *reserve, size_t res_bytes, int max_blocks = 0,
-                         float in_bound = 0.f);  // > 0: |x| <= in_bound (an LSTM/GRU below)
+                         float in_bound = 0.f,  // > 0: |x| <= in_bound (an LSTM/GRU below)
+                         hipStream_t s2 = nullptr);  // second stream: dW beside dR (nothing else to overlap)
 
 }  // namespace kctc

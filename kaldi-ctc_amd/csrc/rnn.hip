@@ -85,16 +85,19 @@ RnnReserveLayout rnn_reserve_layout(const RnnDesc &d, int T, int N) {
 }
 
 static long drec_split_floats(const RnnDesc &d, int T, int N) {
-  long need = 0;
+  // the dR and dW split slabs of a layer side by side: with a second stream
+  // (rnn_backward_weights' s2) the two GEMMs run concurrently
+  long need = 0, needR = 0, needW = 0;
   const int G4 = d.nw() * d.H;
   const int KB = (int)(((long)T * N + 31) / 32);  // packed k blocks over the frames (x3; bf16 needs fewer)
   for (int l = 0; l < d.layers; l++) {
     const long K = (long)(T > 1 ? T - 1 : 1) * N;
     int s = std::max(gemm_pick_split(G4, d.H, (int)K, d.dirs), x3p_pick_split(G4, d.H, KB, d.dirs));
-    if (s > 1) need = std::max(need, (long)s * d.dirs * G4 * d.H);
+    if (s > 1) needR = std::max(needR, (long)s * d.dirs * G4 * d.H);
     s = std::max(gemm_pick_split(G4, d.din(l), (int)((long)T * N), d.dirs), x3p_pick_split(G4, d.din(l), KB, d.dirs));
-    if (s > 1) need = std::max(need, (long)s * d.dirs * G4 * d.din(l));
+    if (s > 1) needW = std::max(needW, (long)s * d.dirs * G4 * d.din(l));
   }
+  need = al64(needR) + needW;
   return need;
 }
 
@@ -3013,7 +3016,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
 // ---------------------------------------------------------------------------
 int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *y, void *workspace, size_t ws_bytes, float *dw,
-                         void *reserve, size_t res_bytes, int max_blocks, float in_bound) {
+                         void *reserve, size_t res_bytes, int max_blocks, float in_bound, hipStream_t s2) {
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
   if (res_bytes < sizeof(float) * (size_t)lay.total) return KRNN_BAD_PARAM;
   if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
@@ -3101,12 +3104,41 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     int *eDX = pk<int>(workspace, d, T, N, pl.ea), *eX = pk<int>(workspace, d, T, N, pl.eb);
     int *eY = pk<int>(workspace, d, T, N, pl.ec), *eE = d.mode == kGru ? pk<int>(workspace, d, T, N, pl.ed) : eDX;
     unsigned *cm = pk<unsigned>(workspace, d, T, N, pl.cm);
-    if (x3) {
+    // two streams (s2, the bottom component's tail, where nothing else
+    // overlaps): input^T and output^T are packed and dW runs on s2 while
+    // dGates^T is packed and dR runs on s (separate split slabs, tile
+    // counters and absmax scratch); s then waits for s2
+    const unsigned *cme0 = pick_bwd_u6(d, N) ? pk<unsigned>(workspace, d, T, N, pl.cme) : nullptr;
+    // (LSTM: dR's dGates^T is dW's, E == DX; the GRU's E^T pack stays on one stream)
+    const bool two = s2 && x3 && cme0 && d.mode == kLstm && d.layers == 1 && T > 1 && env_int("KCTC_WGRAD_2S", 1);
+    hipStream_t sx = two ? s2 : s;  // stream of the input / output packs and of dW
+    hipEvent_t ev_dx = nullptr, ev_y = nullptr;
+    if (two) {
+      KCTC_HIP_CHECK(hipEventCreateWithFlags(&ev_dx, hipEventDisableTiming));
+      KCTC_HIP_CHECK(hipEventCreateWithFlags(&ev_y, hipEventDisableTiming));
+      join_stream(s2, s);
+    }
+    if (two) {
+      ProfSpan ps(s, "x3_pack_w");
+      x3p_pack_cols(s, DX, ldg, (int)TN, (int)(dirs * G4), 0, DXt, eDX, cme0, 0.f);
+      KCTC_HIP_CHECK(hipEventRecord(ev_dx, s));
+      const bool xb = l == 0 && in_bound > 0.f;
+      // absmax scratch of its own: the GRU-only E^T exponent array (free for an LSTM)
+      unsigned *cmx = reinterpret_cast<unsigned *>(pk<int>(workspace, d, T, N, pl.ed));
+      if (!xb) absmax_f32(s2, in, Din, (int)TN, Din, nullptr, cmx);
+      x3p_pack_cols(s2, in, Din, (int)TN, Din, 0, Xt, eX, cmx, xb ? in_bound : 0.f);
+      for (int dir = 0; dir < dirs; dir++)
+        x3p_pack_cols(s2, out + (long)dir * H, ldy, (int)TN, H, dir == 0 ? N : -N, Yt + (long)dir * H * KBt * 64,
+                      eY + dir * H, nullptr, 1.f);
+      KCTC_HIP_CHECK(hipEventRecord(ev_y, s2));
+      KCTC_HIP_CHECK(hipStreamWaitEvent(s2, ev_dx, 0));
+      KCTC_HIP_CHECK(hipStreamWaitEvent(s, ev_y, 0));
+    } else if (x3) {
       // the transposes, packed over the frames: dGates^T (per-gate exponents),
       // input^T (per-dim), and for dR the output shifted by one step per direction
       ProfSpan ps(s, "x3_pack_w");
       // the v6 backward recurrence leaves the dGates column maxima behind
-      const unsigned *cme = pick_bwd_u6(d, N) ? pk<unsigned>(workspace, d, T, N, pl.cme) : nullptr;
+      const unsigned *cme = cme0;
       if (!cme) absmax_f32(s, DX, ldg, (int)TN, (int)(dirs * G4), nullptr, cm);
       x3p_pack_cols(s, DX, ldg, (int)TN, (int)(dirs * G4), 0, DXt, eDX, cme ? cme : cm, 0.f);
       if (d.mode == kGru) {
@@ -3130,10 +3162,12 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       x.B = Xt; x.eB = eX;
       x.C = dwl; x.ldc = Din; x.beta = 1.f;
       x.batch = dirs; x.sC = pls;
-      x.split_k = x3p_pick_split((int)G4, Din, KBt, dirs); x.ws = ws;
+      x.split_k = x3p_pick_split((int)G4, Din, KBt, dirs);
+      // concurrent with dR: its own split slab past dR's
+      x.ws = two ? ws + al64((long)x3p_pick_split((int)G4, H, KBt, dirs) * dirs * G4 * H) : ws;
       x.max_blocks = g.max_blocks; x.tile_counter = g.tile_counter;
-      ProfSpan ps(s, "gemm_bwd_w");
-      gemm_x3p(s, x);
+      ProfSpan ps(sx, "gemm_bwd_w");
+      gemm_x3p(sx, x);
     } else {
       ProfSpan ps(s, "gemm_bwd_w");
       gemm_f32(s, g);
@@ -3170,6 +3204,11 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       } else {
         gemm_f32(s, r);
       }
+    }
+    if (two) {
+      join_stream(s, s2);
+      (void)hipEventDestroy(ev_dx);
+      (void)hipEventDestroy(ev_y);
     }
     }  // x3 / fp32 weight GEMMs
     // biases: dbW += sum dGx, dbR += sum dGh (partials from the recurrence)

@@ -296,6 +296,28 @@ def test_wgrad_stream_matches_whole(kctc, gpu, monkeypatch, H, T, N, chunks):
         assert rel_err(a, b) < 1e-6
 
 
+def test_bottom_wgrad_two_streams_bit_identical(kctc, gpu, monkeypatch):
+    """The bottom component's weight GEMMs with dW beside dR on a second stream
+    (KCTC_WGRAD_2S=1, the default) equal the one-stream order bit for bit:
+    separate split slabs and tile counters, the same kernels and sums."""
+    import torch
+    D, A, T, N, H = 40, 41, 40, 16, 512
+    cfg = kctc.recipe_config(num_rnn=2, input_dim=D, hidden=H, num_targets=A, learning_rate=1e-3,
+                             param_stddev=0.05)
+    feats, nf, fl, ll = kctc.synth_minibatch(29, T, N, D, A, 0.125)
+    f = torch.from_numpy(feats).to(gpu)
+    res = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("KCTC_WGRAD_2S", flag)
+        net = kctc.Nnet(cfg, seed=12)
+        for _ in range(2):
+            net.train_step(f, T, N, nf, fl, ll)
+        res[flag] = [net.get_params(c) for c in range(net.num_components) if net.num_params(c) > 0]
+        net.close()
+    for a, b in zip(res["0"], res["1"]):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_rccl_dp_single_rank_matches_plain(kctc, gpu):
     """kctc_nnet_enable_dp at world size 1 builds the RCCL exchange
     (ncclCommInitRank on a one-rank communicator): every component's bucket is
