@@ -146,7 +146,7 @@ __device__ __forceinline__ float lse3(float a, float b, float c) {
 //   emit[2][F][SP] | col[2][CP] | wmax[2][8] | feasible flag
 struct AbLds {
   int F, SP, CP;
-  int pair;  // two frames per barrier (SPT == 1): KCTC_CTC_PAIR
+  int pair;  // frames per barrier (SPT == 1, 1..4): KCTC_CTC_PAIR
   __device__ __host__ size_t floats() const { return 2 * (size_t)F * SP + 2 * (size_t)CP + 2 * kABWaves + 4; }
 };
 
@@ -204,19 +204,22 @@ __device__ __forceinline__ void ab_body(
   // beta: transition s -> s+2 allowed iff l'_{s+2} != blank and != l'_s; for
   // odd s that is lab[(s+1)/2] != lab[(s-1)/2]; for even s, l'_{s+2} is blank.
 
-  // Two frames per barrier (SPT == 1): lanes 0 / 1 of each wave also carry a
-  // halo state of the neighbouring wave -- alpha: states 64 w - 2, 64 w - 1;
-  // beta: 64 w + 64, 64 w + 65 -- so that the second frame of a pair needs
-  // no exchange: its s - 1 / s - 2 (beta: s + 1 / s + 2) come from the
-  // first frame's values by wave shuffles, the halo filling the wave edge.
-  const int hs = is_beta ? 64 * wid + 64 + lane : 64 * wid - 2 + lane;
-  const bool hlive = lane < 2 && hs >= 0 && hs < S;
+  // Groups of m frames per barrier (SPT == 1, m = lay.pair in 2..4): lanes
+  // 0 .. 2(m-1)-1 of each wave also carry halo states of the neighbouring
+  // wave -- alpha: 64 w - 2(m-1) .. 64 w - 1; beta: 64 w + 64 .. -- so frames
+  // 2..m of a group need no exchange: their s - 1 / s - 2 (beta: s + 1 /
+  // s + 2) come from the previous frame's values by wave shuffles, the halo
+  // (shrinking by two states a frame) filling the wave edge.
+  const int gm = SPT == 1 ? max(1, min(lay.pair, 4)) : 1;
+  const int nh = 2 * (gm - 1);
+  const int hs = is_beta ? 64 * wid + 64 + lane : 64 * wid - nh + lane;
+  const bool hlive = lane < nh && hs >= 0 && hs < S;
   bool hskip = false;
   if (hlive && (hs & 1)) {
     if (!is_beta) hskip = (hs >= 2) && (lab[(hs - 1) >> 1] != lab[(hs - 3) >> 1]);
     else hskip = (hs + 2 < S) && (lab[(hs + 1) >> 1] != lab[(hs - 1) >> 1]);
   }
-  const bool pair_ok = SPT == 1 && lay.pair && (F % 2 == 0);
+  const bool pair_ok = gm > 1;
 
   const long tstride = (long)N * A;
   const float *lrow = lp + (long)n * A;  // + t * N * A
@@ -252,12 +255,10 @@ __device__ __forceinline__ void ab_body(
       const int k = c * F + f;
       const int t = tframe(k);
       if (pair_ok && k > 0 && f + 1 < fend) {
-        // frames k and k + 1 with one barrier; mu (the max of column k - 1)
+        // frames k .. k + g - 1 with one barrier; mu (the max of column k - 1)
         // renormalises frame k only
-        const int t1 = tframe(k + 1);
-        const int sid = min(tid, SP - 1);
-        const float ly0 = em[(size_t)f * SP + sid], ly1 = em[(size_t)(f + 1) * SP + sid];
-        const float hly = em[(size_t)f * SP + min(max(hs, 0), SP - 1)];
+        const int g = min(gm, fend - f);
+        const int sid = min(tid, SP - 1), hid = min(max(hs, 0), SP - 1);
         const float *wm = wmax + (cur ^ 1) * kABWaves;
         const float *pv = colb + (cur ^ 1) * CP;
         const int s0 = tid;
@@ -266,55 +267,71 @@ __device__ __forceinline__ void ab_body(
           pa = pv[min(s0, CP - 1)];
           pb = s0 >= 1 ? pv[max(s0 - 1, 0)] : -INFINITY;
           pc = skip[0] ? pv[max(s0 - 2, 0)] : -INFINITY;
-          ha = pv[min(max(hs, 0), CP - 1)];
+          ha = pv[min(hid, CP - 1)];
           hb = hs >= 1 ? pv[min(max(hs - 1, 0), CP - 1)] : -INFINITY;
           hc = hskip ? pv[min(max(hs - 2, 0), CP - 1)] : -INFINITY;
         } else {
           pa = pv[min(s0, CP - 1)];
           pb = s0 + 1 < S ? pv[min(s0 + 1, CP - 1)] : -INFINITY;
           pc = skip[0] ? pv[min(s0 + 2, CP - 1)] : -INFINITY;
-          ha = pv[min(max(hs, 0), CP - 1)];
+          ha = pv[min(hid, CP - 1)];
           hb = hs + 1 < S ? pv[min(hs + 1, CP - 1)] : -INFINITY;
           hc = hskip ? pv[min(hs + 2, CP - 1)] : -INFINITY;
         }
         float mu = wm[0];
 #pragma unroll
         for (int w = 1; w < kABWaves; w++) mu = fmaxf(mu, wm[w]);
-        // frame k (own state and halo state)
-        const float v0 = lse3(pa, pb, pc) - mu;
-        const float q0 = s0 < S ? v0 + ly0 : -INFINITY;
-        const float hq = hlive ? (lse3(ha, hb, hc) - mu) + hly : -INFINITY;
-        if (SPILL && s0 < S) sp[(long)t * S + s0] = is_beta ? v0 : q0;
         off += (double)mu;
-        if (tid == 0 && SPILL) op[t] = off;
-        // frame k + 1 from q0 by shuffles (no renormalisation)
-        float pa1 = q0, pb1, pc1;
-        if (!is_beta) {
-          const float a1 = __shfl(q0, max(lane - 1, 0), kWave), a2 = __shfl(q0, max(lane - 2, 0), kWave);
-          const float h1 = __shfl(hq, 1, kWave);  // state 64 w - 1
-          pb1 = lane >= 1 ? a1 : h1;
-          pc1 = lane >= 2 ? a2 : hq;  // lane 1: own halo 64 w - 1; lane 0: own halo 64 w - 2
-          pb1 = s0 >= 1 ? pb1 : -INFINITY;
-          pc1 = skip[0] ? pc1 : -INFINITY;
-        } else {
-          const float a1 = __shfl(q0, min(lane + 1, 63), kWave), a2 = __shfl(q0, min(lane + 2, 63), kWave);
-          const float h0 = __shfl(hq, 0, kWave), h1 = __shfl(hq, 1, kWave);  // states 64 w + 64, + 65
-          pb1 = lane <= 62 ? a1 : h0;
-          pc1 = lane <= 61 ? a2 : (lane == 62 ? h0 : h1);
-          pb1 = s0 + 1 < S ? pb1 : -INFINITY;
-          pc1 = skip[0] ? pc1 : -INFINITY;
+        float q = 0.f, hq = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          if (j >= g) break;
+          const int tj = tframe(k + j);
+          const float ly = em[(size_t)(f + j) * SP + sid];
+          const float hly = em[(size_t)(f + j) * SP + hid];
+          if (j > 0) {
+            // the previous frame's values of s - 1, s - 2 (beta: s + 1, s + 2)
+            // from the neighbouring lanes, the halo at the wave edge
+            if (!is_beta) {
+              const float a1 = __shfl(q, max(lane - 1, 0), kWave), a2 = __shfl(q, max(lane - 2, 0), kWave);
+              const float e1 = __shfl(hq, nh - 1, kWave), e2 = __shfl(hq, nh - 2, kWave);  // 64 w - 1, - 2
+              const float g1 = __shfl(hq, max(lane - 1, 0), kWave), g2 = __shfl(hq, max(lane - 2, 0), kWave);
+              pa = q;
+              pb = lane >= 1 ? a1 : e1;
+              pc = lane >= 2 ? a2 : (lane == 1 ? e1 : e2);
+              pb = s0 >= 1 ? pb : -INFINITY;
+              pc = skip[0] ? pc : -INFINITY;
+              ha = hq;
+              hb = lane >= 1 && hs >= 1 ? g1 : -INFINITY;
+              hc = lane >= 2 && hskip ? g2 : -INFINITY;
+            } else {
+              const float a1 = __shfl(q, min(lane + 1, 63), kWave), a2 = __shfl(q, min(lane + 2, 63), kWave);
+              const float e0 = __shfl(hq, 0, kWave), e1 = __shfl(hq, 1, kWave);  // 64 w + 64, + 65
+              const float g1 = __shfl(hq, min(lane + 1, 63), kWave), g2 = __shfl(hq, min(lane + 2, 63), kWave);
+              pa = q;
+              pb = lane <= 62 ? a1 : e0;
+              pc = lane <= 61 ? a2 : (lane == 62 ? e0 : e1);
+              pb = s0 + 1 < S ? pb : -INFINITY;
+              pc = skip[0] ? pc : -INFINITY;
+              ha = hq;
+              hb = lane + 1 < nh && hs + 1 < S ? g1 : -INFINITY;
+              hc = lane + 2 < nh && hskip ? g2 : -INFINITY;
+            }
+          }
+          const float m = j == 0 ? mu : 0.f;
+          const float v = lse3(pa, pb, pc) - m;
+          q = s0 < S ? v + ly : -INFINITY;
+          hq = hlive ? (lse3(ha, hb, hc) - m) + hly : -INFINITY;
+          if (SPILL && s0 < S) sp[(long)tj * S + s0] = is_beta ? v : q;
+          if (tid == 0 && SPILL) op[tj] = off;
         }
-        const float v1 = lse3(pa1, pb1, pc1);
-        const float q1 = s0 < S ? v1 + ly1 : -INFINITY;
         float *cc = colb + cur * CP;
-        cc[s0] = q1;
-        if (SPILL && s0 < S) sp[(long)t1 * S + s0] = is_beta ? v1 : q1;
-        if (tid == 0 && SPILL) op[t1] = off;
-        float lm = wave_max_l63(q1);
+        cc[s0] = q;
+        float lm = wave_max_l63(q);
         if (lane == 63) wmax[cur * kABWaves + wid] = lm;
         lds_barrier();
         cur ^= 1;
-        f++;
+        f += g - 1;
         continue;
       }
       float ly[SPT];
@@ -577,7 +594,7 @@ static ctcStatus_t launch(const float *acts, float *grads, const int *flat_label
     int Smax = 1;
     for (int n = 0; n < N; n++) Smax = 2 * label_lengths[n] + 1 > Smax ? 2 * label_lengths[n] + 1 : Smax;
     AbLds al;
-    al.pair = getenv("KCTC_CTC_PAIR") ? atoi(getenv("KCTC_CTC_PAIR")) : 1;
+    al.pair = getenv("KCTC_CTC_PAIR") ? atoi(getenv("KCTC_CTC_PAIR")) : 4;  // measured: 4 < 3 < 1 < 2 (ms)
     al.SP = (Smax + 63) / 64 * 64;
     al.CP = std::max((Smax + 4 + 3) / 4 * 4, (Smax <= kABThreads ? 1 : kSPT) * kABThreads);
     // chunk depth: as many frames as fit 96 KB of double-buffered emissions (4..32)
