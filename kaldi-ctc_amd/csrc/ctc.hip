@@ -146,7 +146,7 @@ __device__ __forceinline__ float lse3(float a, float b, float c) {
 //   emit[2][F][SP] | col[2][CP] | wmax[2][8] | feasible flag
 struct AbLds {
   int F, SP, CP;
-  int pair;  // frames per barrier (SPT == 1, 1..4): KCTC_CTC_PAIR
+  int pair;  // frames per barrier (SPT == 1, 1..8): KCTC_CTC_PAIR
   __device__ __host__ size_t floats() const { return 2 * (size_t)F * SP + 2 * (size_t)CP + 2 * kABWaves + 4; }
 };
 
@@ -204,13 +204,13 @@ __device__ __forceinline__ void ab_body(
   // beta: transition s -> s+2 allowed iff l'_{s+2} != blank and != l'_s; for
   // odd s that is lab[(s+1)/2] != lab[(s-1)/2]; for even s, l'_{s+2} is blank.
 
-  // Groups of m frames per barrier (SPT == 1, m = lay.pair in 2..4): lanes
+  // Groups of m frames per barrier (SPT == 1, m = lay.pair in 2..8): lanes
   // 0 .. 2(m-1)-1 of each wave also carry halo states of the neighbouring
   // wave -- alpha: 64 w - 2(m-1) .. 64 w - 1; beta: 64 w + 64 .. -- so frames
   // 2..m of a group need no exchange: their s - 1 / s - 2 (beta: s + 1 /
   // s + 2) come from the previous frame's values by wave shuffles, the halo
   // (shrinking by two states a frame) filling the wave edge.
-  const int gm = SPT == 1 ? max(1, min(lay.pair, 4)) : 1;
+  const int gm = SPT == 1 ? max(1, min(lay.pair, 8)) : 1;
   const int nh = 2 * (gm - 1);
   const int hs = is_beta ? 64 * wid + 64 + lane : 64 * wid - nh + lane;
   const bool hlive = lane < nh && hs >= 0 && hs < S;
@@ -284,7 +284,7 @@ __device__ __forceinline__ void ab_body(
         off += (double)mu;
         float q = 0.f, hq = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < 8; j++) {
           if (j >= g) break;
           const int tj = tframe(k + j);
           const float ly = em[(size_t)(f + j) * SP + sid];
@@ -594,7 +594,7 @@ static ctcStatus_t launch(const float *acts, float *grads, const int *flat_label
     int Smax = 1;
     for (int n = 0; n < N; n++) Smax = 2 * label_lengths[n] + 1 > Smax ? 2 * label_lengths[n] + 1 : Smax;
     AbLds al;
-    al.pair = getenv("KCTC_CTC_PAIR") ? atoi(getenv("KCTC_CTC_PAIR")) : 4;  // measured: 4 < 3 < 1 < 2 (ms)
+    al.pair = getenv("KCTC_CTC_PAIR") ? atoi(getenv("KCTC_CTC_PAIR")) : 8;  // measured: 8 < 6 < 4 < 3 < 1 < 2 (ms)
     al.SP = (Smax + 63) / 64 * 64;
     al.CP = std::max((Smax + 4 + 3) / 4 * 4, (Smax <= kABThreads ? 1 : kSPT) * kABThreads);
     // chunk depth: as many frames as fit 96 KB of double-buffered emissions (4..32)
