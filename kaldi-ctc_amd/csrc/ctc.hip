@@ -24,6 +24,7 @@
 //                      Deterministic (fixed summation order, no atomics).
 #include <algorithm>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "common.h"
@@ -292,27 +293,38 @@ __device__ __forceinline__ void ab_body(
           if (j > 0) {
             // the previous frame's values of s - 1, s - 2 (beta: s + 1, s + 2)
             // from the neighbouring lanes, the halo at the wave edge
+            // whole-wave DPP shifts (wave_shr:1 / wave_shl:1); the edge lane
+            // takes `old` -- the halo value broadcast by readlane
+            constexpr int kShr1 = 0x138, kShl1 = 0x130;
+            auto dpp = [](float old, float src, auto ctrl) {
+              return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src),
+                                                                decltype(ctrl)::value, 0xf, 0xf, false));
+            };
+            const int ninf = __float_as_int(-INFINITY);
+            (void)ninf;
             if (!is_beta) {
-              const float a1 = __shfl(q, max(lane - 1, 0), kWave), a2 = __shfl(q, max(lane - 2, 0), kWave);
-              const float e1 = __shfl(hq, nh - 1, kWave), e2 = __shfl(hq, nh - 2, kWave);  // 64 w - 1, - 2
-              const float g1 = __shfl(hq, max(lane - 1, 0), kWave), g2 = __shfl(hq, max(lane - 2, 0), kWave);
+              const float e1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hq), nh - 1));  // 64 w - 1
+              const float e2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hq), nh - 2));  // 64 w - 2
+              using R = std::integral_constant<int, kShr1>;
+              const float b1 = dpp(e1, q, R{});   // lane l: q[l-1]; lane 0: 64 w - 1
+              const float c1 = dpp(e2, b1, R{});  // lane l: q[l-2]; lane 1: 64 w - 1; lane 0: 64 w - 2
+              const float g1 = dpp(-INFINITY, hq, R{}), g2 = dpp(-INFINITY, g1, R{});
               pa = q;
-              pb = lane >= 1 ? a1 : e1;
-              pc = lane >= 2 ? a2 : (lane == 1 ? e1 : e2);
-              pb = s0 >= 1 ? pb : -INFINITY;
-              pc = skip[0] ? pc : -INFINITY;
+              pb = s0 >= 1 ? b1 : -INFINITY;
+              pc = skip[0] ? c1 : -INFINITY;
               ha = hq;
-              hb = lane >= 1 && hs >= 1 ? g1 : -INFINITY;
-              hc = lane >= 2 && hskip ? g2 : -INFINITY;
+              hb = hs >= 1 ? g1 : -INFINITY;
+              hc = hskip ? g2 : -INFINITY;
             } else {
-              const float a1 = __shfl(q, min(lane + 1, 63), kWave), a2 = __shfl(q, min(lane + 2, 63), kWave);
-              const float e0 = __shfl(hq, 0, kWave), e1 = __shfl(hq, 1, kWave);  // 64 w + 64, + 65
-              const float g1 = __shfl(hq, min(lane + 1, 63), kWave), g2 = __shfl(hq, min(lane + 2, 63), kWave);
+              const float e0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hq), 0));  // 64 w + 64
+              const float e1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hq), 1));  // 64 w + 65
+              using L = std::integral_constant<int, kShl1>;
+              const float b1 = dpp(e0, q, L{});   // lane l: q[l+1]; lane 63: 64 w + 64
+              const float c1 = dpp(e1, b1, L{});  // lane l: q[l+2]; lane 62: 64 w + 64; lane 63: 64 w + 65
+              const float g1 = dpp(-INFINITY, hq, L{}), g2 = dpp(-INFINITY, g1, L{});
               pa = q;
-              pb = lane <= 62 ? a1 : e0;
-              pc = lane <= 61 ? a2 : (lane == 62 ? e0 : e1);
-              pb = s0 + 1 < S ? pb : -INFINITY;
-              pc = skip[0] ? pc : -INFINITY;
+              pb = s0 + 1 < S ? b1 : -INFINITY;
+              pc = skip[0] ? c1 : -INFINITY;
               ha = hq;
               hb = lane + 1 < nh && hs + 1 < S ? g1 : -INFINITY;
               hc = lane + 2 < nh && hskip ? g2 : -INFINITY;
