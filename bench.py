@@ -327,7 +327,7 @@ def main():
             aux["ctc_alpha_beta"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
                                      "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
                                      "ms_per_launch": round(ms_c / n_c, 4),
-                                     "note": "serial over T (one barrier per frame): latency-bound"}
+                                     "note": "serial over T (one barrier per group of 8 frames): latency-bound"}
         roof["secondary"] = aux
 
     cpu = None
