@@ -9,17 +9,30 @@ generator, seed 20161015 + 1000*rank + step), fp32.  Inputs are resident in
 HBM when the timed region starts (a second pass with the H2D copy inside
 every step is reported beside it).  frames = sum of real frames T_n.
 
-Multi-GPU: one process per GPU (torch.distributed.run); each rank trains its
-own N=16 shard, weight gradients are summed with RCCL (kctc_nnet_enable_dp),
-so per-GPU work is fixed ("weak" scaling).
+Multi-GPU: one process per GPU; each rank trains its own N=16 shard and the
+weight gradients are summed with RCCL (kctc_nnet_enable_dp), so per-GPU work
+is fixed ("weak" scaling).  `--gpus N` with no WORLD_SIZE in the environment
+starts the N rank processes itself (torchrun-style env, LOCAL_RANK = device)
+before anything touches the GPU; under torch.distributed.run it is one rank.
+`--dp-transport host` sums the gradients through gloo on the host instead
+(kctc_nnet_enable_dp_host): ranks may then share a device, each on its own
+CU-masked share of it (kctc_set_cu_partition) -- a rehearsal of the N-rank
+path on a one-GPU box, not a throughput configuration.
+
+Before the timed region the bench checks the loss: one train step of the
+committed full-size fixture (tests/golden/sketch_step.npz, fp64 oracle, same
+parameters and minibatch) must match at 1e-4 (`loss_match`).
 
 Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (HIP
 events on the trainer's stream over the timed region) and a CPU baseline
-(the oracle's fp32 restatement, OpenMP, bounded sample; rank 0 at N=1 only).
+(the oracle's fp32 restatement, OpenMP, on utterances of the GPU run's own
+first timed minibatch with the run's initial parameters; rank 0 at N=1 only).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,6 +48,7 @@ PEAK_F16_TFLOPS = 2500.0   # dense f16/bf16 MFMA
 # a split-fp16 ("x3") fp32-class product issues 3 f16 MFMAs: its ceiling on
 # the engine it runs on is a third of the dense f16 peak
 PEAK_X3_TFLOPS = PEAK_F16_TFLOPS / 3
+LOSS_BAR = 1e-4            # north_star: loss / grads within 1e-4 relative
 
 # BASELINE.json configs this bench measures (--config): T_max, N/GPU, hidden,
 # rnn mode, labels per frame (12.5 phones/s: 1/8 per 10-ms frame, 3/8 after
@@ -51,6 +65,92 @@ CONFIGS = {
 }
 
 
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=1, choices=sorted(CONFIGS),
+                    help="BASELINE.json configs[i] to measure (1: the metric's config)")
+    ap.add_argument("--T", type=int, default=0)
+    ap.add_argument("--N", type=int, default=0)
+    ap.add_argument("--hidden", type=int, default=0)
+    ap.add_argument("--layers", type=int, default=5)
+    ap.add_argument("--dp-transport", choices=("rccl", "host"), default="rccl",
+                    help="N>1: gradient sum over RCCL (one GPU per rank) or gloo on the host "
+                         "(ranks may share a GPU)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-h2d-pass", action="store_true")
+    ap.add_argument("--no-loss-match", action="store_true")
+    ap.add_argument("--average-every", type=int, default=0,
+                    help="N>1: the recipe's model averaging every K steps instead of the per-step "
+                         "gradient all-reduce (kctc_nnet_set_dp_mode 1)")
+    return ap.parse_args(argv)
+
+
+# ---- rank launcher ------------------------------------------------------------
+def rank_envs(n, port, base=None):
+    """torch.distributed.run-style environments of n local ranks (one node)."""
+    base = dict(os.environ if base is None else base)
+    out = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+        out.append(e)
+    return out
+
+
+def device_of(local_rank, local_world, ndev, transport):
+    """(device, cu part, cu parts) of a local rank: one device per rank over
+    RCCL; over the host transport ranks wrap around the devices and the ranks
+    on one device split its CUs."""
+    if transport == "rccl":
+        if local_rank >= ndev:
+            raise SystemExit(f"bench.py: rank {local_rank} needs GPU {local_rank} but {ndev} are visible "
+                             "(RCCL: one GPU per rank; --dp-transport host lets ranks share a GPU)")
+        return local_rank, 0, 1
+    dev = local_rank % ndev
+    nparts = len(range(dev, local_world, ndev))
+    return dev, local_rank // ndev, nparts
+
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv, script=None):
+    """Start n rank processes of this script (fresh children: nothing here has
+    touched the GPU) and wait for all of them; a failed rank stops the rest
+    and its exit status is returned.  Rank 0 prints the JSON line (the ranks
+    sum their totals among themselves)."""
+    port = free_port()
+    procs = [subprocess.Popen([sys.executable, "-u", script or os.path.abspath(__file__)] + list(argv), env=e)
+             for e in rank_envs(n, port)]
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                r = p.poll()
+                if r is None:
+                    continue
+                procs.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r
+                    for q in procs:
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            p.kill()
+    return rc
+
+
+# ---- work and byte models -------------------------------------------------------
 def step_flops_per_frame(D, H, A, L, nw=4, dirs=2):
     """Algorithmic train-step FLOPs per frame (forward =
     sum_layers 2*dirs*nW*H*(D_in+H) + affine 2*2H*A; train = 3x forward)."""
@@ -70,9 +170,26 @@ def model_flops(T, N, D, H, A, L, nw=4, dirs=2):
     f["gemm_bwd_data"] = sum(2.0 * TN * nw * H * dirs * d for d in din[1:])  # layer 1 dx not needed
     f["gemm_bwd_w"] = sum(2.0 * TN * nw * H * dirs * d for d in din)
     f["gemm_bwd_r"] = L * 2.0 * (T - 1) * N * nw * H * H * dirs
-    launches = {"gemm_fwd_proj": L, "rnn_fwd_rec": L, "rnn_bwd_rec": L, "gemm_bwd_data": 2 * (L - 1),
-                "gemm_bwd_w": L, "gemm_bwd_r": L}
-    return f, launches
+    return f
+
+
+def ctc_bytes(T_max, A, num_frames, label_lengths):
+    """Algorithmic HBM bytes of one minibatch's CTC kernels (ctc.hip), per
+    utterance n with T_n frames and S_n = 2 L_n + 1 extended labels:
+      ctc_logz       reads the T_max*N*A activations, writes the normalised
+                     log-probs (T_max*N*A) and the per-frame log-normaliser;
+      ctc_alpha_beta the alpha block and the beta block each read the T_n
+                     emission rows (A floats) and write their spilled column
+                     (T_n*S_n floats) and fp64 frame offsets (T_n);
+      ctc_grad       reads both spills, both offset vectors, the activations
+                     and the normaliser, writes the gradient (padding rows too)."""
+    T = np.asarray(num_frames, np.float64)
+    S = 2.0 * np.asarray(label_lengths, np.float64) + 1.0
+    N = T.size
+    rows = float(T_max * N)
+    return {"ctc_logz": rows * A * 4 * 2 + rows * 4,
+            "ctc_alpha_beta": float(np.sum(2 * (4 * T * A + 4 * T * S + 8 * T))),
+            "ctc_grad": float(np.sum(8 * T * S + 16 * T + 4 * T * A + 4 * T)) + rows * A * 4}
 
 
 def pmc_traffic(kernel):
@@ -92,52 +209,90 @@ def pmc_traffic(kernel):
     return None, None
 
 
-def cpu_baseline(T, D, H, A, L, steps_seed, ratio=0.125, mode=2, Ns=4):
+# ---- checks and baselines ---------------------------------------------------------
+def loss_match(k, dev):
+    """One train step of the committed full-size fixture (tests/golden/
+    sketch_step.npz, generated by tests/golden/make_sketch.py with the fp64
+    oracle): 5 x BLSTM-512, N=16, T_max=2000, the fixture's parameters and
+    bench.py's first minibatch.  Reports the per-utterance cost error, the
+    network output's and every applied gradient's sketch error (norm-wise
+    relative, tests/sketch_common.py) and the best-path flips against the
+    fp64 output, with the 1e-4 bar."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import sketch_common as S
+    g = np.load(os.path.join(ROOT, "tests", "golden", "sketch_step.npz"))
+    s = S.STEP
+    T, N, D, H, A, R = s["T"], s["N"], s["D"], s["H"], s["A"], s["R"]
+    rnn, Wa, ba = S.step_params(S.ProductLayout(k))
+    feats, nf, fl, ll = S.step_inputs(k)
+    net = k.Nnet(k.recipe_config(num_rnn=R, input_dim=D, hidden=H, num_targets=A, learning_rate=s["lr"],
+                                 max_seq_length=T), seed=1, device=dev.index)
+    rnn_idx = [1 + 2 * c for c in range(R)]
+    aff_idx = 2 * R + 1
+    for c, i in enumerate(rnn_idx):
+        net.set_params(i, rnn[c])
+    net.set_params(aff_idx, np.concatenate([Wa.ravel(), ba]))
+    net.srand(0)
+    objf, acc, wt = net.train_step(torch.from_numpy(feats).to(dev), T, N, nf, fl, ll)
+    costs = net.last_costs(N)
+    rc = np.abs(costs - g["costs"]) / np.abs(g["costs"])
+    logits = net.last_output(T, N, A)
+    e_log = S.compare(logits, S.load(g, "logits"), 500, LOSS_BAR)
+    errs = [S.compare(np.clip(net.get_grad(i).astype(np.float64), -5.0, 5.0), S.load(g, f"g{c}"), 600 + c,
+                      LOSS_BAR) for c, i in enumerate(rnn_idx)]
+    errs.append(S.compare(net.get_grad(aff_idx).astype(np.float64), S.load(g, "gaff"), 700, LOSS_BAR))
+    ids = net.last_best_path(T, N)
+    net.close()
+    out = {"fixture": "tests/golden/sketch_step.npz (fp64 oracle, configs[1] step, params pseed 77, "
+                      "minibatch seed 20161015)",
+           "max_rel_cost": float(rc.max()),
+           "tot_objf_rel": abs(objf - float(g["tot_objf"])) / abs(float(g["tot_objf"])),
+           "logits_sketch_err": max(e_log["norm"], e_log["proj"]),
+           "grad_sketch_err": max(max(e["norm"], e["proj"]) for e in errs),
+           "best_path_flips": int(np.sum(ids != g["ids"])), "frames": int(ids.size),
+           "objf_per_label": objf / wt, "bar": LOSS_BAR}
+    out["pass"] = bool(out["max_rel_cost"] < LOSS_BAR and out["tot_objf_rel"] < LOSS_BAR and
+                       out["logits_sketch_err"] < LOSS_BAR and out["grad_sketch_err"] < LOSS_BAR and
+                       wt == float(g["tot_weight"]))
+    return out
+
+
+def cpu_baseline(params0, batch, T, D, H, A, L, ratio=0.125, mode=2, Ns=4):
     """The oracle's fp32 restatement (warp-ctc-CPU-style CTC + blocked-GEMM
-    LSTM/affine, OpenMP) on a bounded sample: 4 utterances of the same shape
-    (about 7 s of CPU work, so it does not dominate the bench's lease)."""
+    LSTM/affine, OpenMP) on a bounded sample of the GPU run's own bytes: the
+    first Ns utterances of its first timed minibatch, the run's initial
+    parameters (about 8 s of CPU work)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
-    import __graft_entry__ as ge
-    k = ge.load_package()
     s = O.NnetSpec()
     s.num_rnn, s.mode, s.hidden, s.dirs, s.layers_per_rnn = L, mode, H, 2, 1
     s.input_dim, s.num_targets = D, A
     s.clip_threshold, s.repair_threshold, s.repair_scale, s.repair_target = 30.0, 0.01, 1.0, 0.0
     s.rnn_clip_gradient, s.lr_rnn, s.lr_affine = 5.0, 5e-4, 5e-4
-    rng = np.random.default_rng(0)
-    ps = [(rng.standard_normal(O.params_size(mode, D if i == 0 else 2 * H, H, 1, 2)) * 0.02).astype(np.float32)
-          for i in range(L)]
-    Wa = (rng.standard_normal((A, 2 * H)) / np.sqrt(2 * H)).astype(np.float32)
-    ba = rng.standard_normal(A).astype(np.float32)
-    feats, nf, fl, ll = k.synth_minibatch(steps_seed, T, Ns, D, A, ratio)
+    rnn_p, aff = params0
+    ps = [p.copy() for p in rnn_p]
+    Wa = np.ascontiguousarray(aff[:A * 2 * H].reshape(A, 2 * H))
+    ba = aff[A * 2 * H:].copy()
+    feats, nf, fl, ll = batch
+    N = nf.size
+    sub = np.ascontiguousarray(feats.reshape(T, N, D)[:, :Ns, :])
+    nlab = int(np.sum(ll[:Ns]))
     t0 = time.time()
-    O.train_step(s, ps, Wa, ba, feats.reshape(T, Ns, D), nf, fl, ll)
+    O.train_step(s, ps, Wa, ba, sub, nf[:Ns], fl[:nlab], ll[:Ns])
     dt = time.time() - t0
-    return {"value": float(nf.sum() / dt), "unit": "frames/s", "cores": int(O.lib().oracle_num_threads()),
+    frames = int(nf[:Ns].sum())
+    return {"value": float(frames / dt), "unit": "frames/s", "cores": int(O.lib().oracle_num_threads()),
             "kind": "port",
-            "sample": f"one full train step ({L}x{'BLSTM' if mode == 2 else 'BGRU'}-{H} fwd+CTC+bwd+SGD, fp32) on {Ns} utterances "
-                      f"x T_max={T} ({int(nf.sum())} frames) in {dt:.1f}s"}
+            "sample": f"one full train step ({L}x{'BLSTM' if mode == 2 else 'BGRU'}-{H} fwd+CTC+bwd+SGD, fp32) on "
+                      f"utterances 0..{Ns - 1} of the GPU run's first timed minibatch (T_max={T}, {frames} frames, "
+                      f"the run's initial parameters) in {dt:.1f}s"}
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=1, choices=sorted(CONFIGS),
-                    help="BASELINE.json configs[i] to measure (1: the metric's config)")
-    ap.add_argument("--T", type=int, default=0)
-    ap.add_argument("--N", type=int, default=0)
-    ap.add_argument("--hidden", type=int, default=0)
-    ap.add_argument("--layers", type=int, default=5)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--no-h2d-pass", action="store_true")
-    ap.add_argument("--average-every", type=int, default=0,
-                    help="N>1: the recipe's model averaging every K steps instead of the per-step "
-                         "gradient all-reduce (kctc_nnet_set_dp_mode 1)")
-    args = ap.parse_args()
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     cf = CONFIGS[args.config]
 
     import torch
@@ -147,39 +302,62 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     if world > 1:
-        dist.init_process_group("gloo", init_method="env://")  # rendezvous only; data path is RCCL
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        dist.init_process_group("gloo", init_method="env://")  # rendezvous (+ host transport)
+    device, part, nparts = device_of(local, local_world, max(1, torch.cuda.device_count()), args.dp_transport)
     k = ge.load_package()
+    if nparts > 1:
+        k.set_cu_partition(part, nparts)
+    torch.cuda.set_device(device)
+    dev = torch.device("cuda", device)
     T, N, H = args.T or cf["T"], args.N or cf["N"], args.hidden or cf["H"]
     D, A, L, mode, ratio = 40, 41, args.layers, cf["mode"], cf["ratio"]
     nw = 4 if mode == 2 else 3
     cfg = k.recipe_config(num_rnn=L, input_dim=D, hidden=H, num_targets=A, learning_rate=5e-4,
                           max_seq_length=T, rnn_mode=mode)
-    net = k.Nnet(cfg, seed=20161015, device=local)  # same init on every rank
+    net = k.Nnet(cfg, seed=20161015, device=device)  # same init on every rank
     bf16 = cf.get("prec") == "bf16"
     if bf16:
         net.set_precision("bf16")
-    peak_mfma = PEAK_F16_TFLOPS if bf16 else PEAK_FP32_TFLOPS
+    rnn_idx = [1 + 2 * c for c in range(L)]
+    params0 = ([net.get_params(i) for i in rnn_idx], net.get_params(2 * L + 1))
+    dp_info = None
     if world > 1:
-        uid = k.dp_unique_id() if rank == 0 else bytes(128)
-        obj = [uid]
-        dist.broadcast_object_list(obj, src=0)
         if args.average_every > 0:
             net.set_dp_mode("average")
-        net.enable_dp(obj[0], rank, world)
+        if args.dp_transport == "rccl":
+            uid = k.dp_unique_id() if rank == 0 else bytes(128)
+            obj = [uid]
+            dist.broadcast_object_list(obj, src=0)
+            net.enable_dp(obj[0], rank, world)
+        else:
+            def allreduce(buf):
+                dist.all_reduce(torch.from_numpy(buf))
+            net.enable_dp_host(allreduce, world)
+        dp_info = {"transport": args.dp_transport, "ranks": world,
+                   "devices": len({device_of(r, local_world, max(1, torch.cuda.device_count()),
+                                             args.dp_transport)[0] for r in range(local_world)}),
+                   "ranks_per_device_cu_share": f"1/{nparts}" if nparts > 1 else "all",
+                   "mode": "model averaging every %d steps" % args.average_every if args.average_every > 0
+                   else "gradient sum every step"}
+
+    lm = None
+    if rank == 0 and not args.no_loss_match and args.config == 1 and (T, N, H, L) == (2000, 16, 512, 5):
+        lm = loss_match(k, dev)
 
     total = args.warmup + args.steps
-    batches = []
+    batches, host_batches = [], []
     for step in range(total):
         feats, nf, fl, ll = k.synth_minibatch(20161015 + 1000 * rank + step, T, N, D, A, ratio)
         batches.append((torch.from_numpy(feats).to(dev), nf, fl, ll, torch.from_numpy(feats).pin_memory()))
+        host_batches.append((feats, nf, fl, ll) if step == args.warmup else None)
     torch.cuda.synchronize()
 
+    warm_stats = []
     for step in range(args.warmup):
         f, nf, fl, ll, _ = batches[step]
-        net.train_step(f, T, N, nf, fl, ll)
+        warm_stats.append(net.train_step(f, T, N, nf, fl, ll))
 
     profile = not args.no_profile
     net.set_profiling(profile)
@@ -225,6 +403,7 @@ def main():
         return dt, frames, stats, step_ms
 
     dt, frames, stats, step_ms = timed_pass(False)
+    traj = np.array([[o, w] for o, _, w in warm_stats + stats], np.float64)
     objf = sum(o for o, _, _ in stats)
     acc = sum(a for _, a, _ in stats)
     wt = sum(w for _, _, w in stats)
@@ -232,10 +411,10 @@ def main():
         tot = torch.tensor([objf, acc, wt], dtype=torch.float64)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         objf, acc, wt = float(tot[0]), float(tot[1]), float(tot[2])
-    fam_flops, _ = model_flops(T, N, D, H, A, L, nw=nw)
-    if args.config != 1:
-        # the committed PMC traffic was measured on configs[1]
-        globals()["pmc_traffic"] = lambda kernel: (None, None)
+        tt = torch.from_numpy(np.ascontiguousarray(traj))
+        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+        traj = tt.numpy()
+    fam_flops = model_flops(T, N, D, H, A, L, nw=nw)
     prof = {}
     if profile:
         # *_stream / x3_pack_chain / x3_pack_bwd_stream: GEMMs and packs on the
@@ -263,7 +442,19 @@ def main():
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         dt, frames, med_ms = float(mx[0]), int(sm[1]), float(mx[2])
         frames_per_step = frames / args.steps
+        if h2d:
+            t2 = torch.tensor([h2d[0], float(h2d[1])], dtype=torch.float64)
+            mx2 = t2.clone()
+            dist.all_reduce(mx2, op=dist.ReduceOp.MAX)
+            dist.all_reduce(t2, op=dist.ReduceOp.SUM)
+            h2d = (float(mx2[0]), int(t2[1]), h2d[2])
 
+    # the split-fp16 ("x3") products deliver fp32-class results on the f16
+    # matrix cores: priced against the fp32 MFMA peak (the precision class,
+    # the contract's `peak` for dtype f32) and against the engine they issue on
+    peak_mfma = PEAK_F16_TFLOPS if bf16 else PEAK_FP32_TFLOPS
+    peak_engine = PEAK_F16_TFLOPS if bf16 else PEAK_X3_TFLOPS
+    engine = "bf16 MFMA (dense 2.5 PF)" if bf16 else "split-fp16 x3 on the f16 MFMA (2.5 PF / 3)"
     roof = None
     if prof:
         dom = max((f for f in prof if f in fam_flops), key=lambda f: prof[f][0])
@@ -271,72 +462,70 @@ def main():
         avg_s = ms / n / 1e3
         flops_per_launch = fam_flops[dom] / (n / args.steps)
         achieved = flops_per_launch / avg_s / 1e12
-        traffic, tsrc = pmc_traffic(dom)
-        # the recurrences multiply on the split-fp16 (x3) path: priced against
-        # the fp32 MFMA peak (the precision class they deliver) and, as
-        # issue_frac, against what the f16 engine they run on could do
+        traffic, tsrc = pmc_traffic(dom) if args.config == 1 else (None, None)
         roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak_mfma, "unit": "TFLOP/s",
                 "frac": round(achieved / peak_mfma, 4), "traffic": traffic, "traffic_source": tsrc,
-                "kernel": dom,
-                "avg_launch_ms": round(ms / n, 4),
-                "flops_per_launch": flops_per_launch,
-                "issue_frac_x3_on_f16": None if bf16 else round(achieved / PEAK_X3_TFLOPS, 4),
+                "kernel": dom, "avg_launch_ms": round(ms / n, 4), "flops_per_launch": flops_per_launch,
+                "engine": {"name": engine, "peak": round(peak_engine, 1),
+                           "frac": round(achieved / peak_engine, 4)},
                 "families_ms_per_step": {f: round(prof[f][0] / args.steps, 3) for f in prof}}
         aux = {}
+        # the recurrences are serial over T: their step latency is the figure
+        # that bounds them
+        aux["recurrence_step_us"] = {f: round(prof[f][0] / prof[f][1] / T * 1e3, 3)
+                                     for f in ("rnn_fwd_rec", "rnn_bwd_rec") if f in prof}
         # the input projections and dx GEMMs of layers 2..L stream off the
         # recurrences (no kernel time of their own to price); the weight-gradient
-        # GEMM dW = dGates^T [x | 1] is the same packed split-fp16 kernel, timed
-        # on its own (side stream); its ceiling is the f16 engine / 3
-        if "gemm_bwd_w" in prof and bf16:
+        # GEMM dW = dGates^T [x | 1] is the same packed kernel, timed on its own
+        # (side stream, sharing the chip with a backward recurrence)
+        if "gemm_bwd_w" in prof:
             ms_g, n_g = prof["gemm_bwd_w"]
             tf = fam_flops["gemm_bwd_w"] * args.steps / (ms_g / 1e3) / 1e12
-            aux["gate_gemm"] = {"bound": "mfma", "kernel": "gemm_bwd_w (gemm_x3p, bf16 operands)",
-                                "achieved": round(tf, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
-                                "frac": round(tf / PEAK_F16_TFLOPS, 4)}
-        elif "gemm_bwd_w" in prof:
-            ms_g, n_g = prof["gemm_bwd_w"]
-            tf = fam_flops["gemm_bwd_w"] * args.steps / (ms_g / 1e3) / 1e12
-            aux["gate_gemm"] = {"bound": "mfma", "kernel": "gemm_bwd_w (gemm_x3p, split-fp16)", "achieved": round(tf, 2),
-                                "peak": round(PEAK_X3_TFLOPS, 1), "unit": "TFLOP/s (fp32-class)",
-                                "frac": round(tf / PEAK_X3_TFLOPS, 4),
-                                "note": "peak = 2.5 PF dense f16 / 3 MFMAs per split-fp16 product; "
-                                        "vs the fp32 MFMA peak it is " + str(round(tf / PEAK_FP32_TFLOPS, 3))}
-        if "gate_gemm" in aux and rank == 0:
-            # the same kernel on the same shape, alone on the chip (the in-step
-            # figure above shares the CUs and memory system with a recurrence)
-            G4, din = nw * H, 2 * H
-            Ms, Ns, Ks = G4, din, T * N
-            split = 4 if bf16 else 8
-            ms_s = k.lib().kcm_bench_gemm_packed(None, Ms, Ns, Ks, 1 if bf16 else 0, 5, split)
-            if ms_s > 0:
-                tf_s = 2.0 * Ms * Ns * Ks / (ms_s / 1e3) / 1e12
-                aux["gate_gemm"]["standalone"] = {
-                    "shape": f"M={Ms} N={Ns} K={Ks} split-K {split} (dW of a BLSTM layer, one direction)",
-                    "ms": round(ms_s, 4), "achieved": round(tf_s, 2),
-                    "frac": round(tf_s / (PEAK_F16_TFLOPS if bf16 else PEAK_X3_TFLOPS), 4),
-                    "mfma_issue_frac": round(tf_s * (1 if bf16 else 3) / PEAK_F16_TFLOPS, 4),
-                    "note": "kcm_bench_gemm_packed: random packed operands, 5 launches after 2 warm-ups"}
-        if "ctc_alpha_beta" in prof:
-            ms_c, n_c = prof["ctc_alpha_beta"]
-            byts = 0.0
-            for step in range(args.warmup, total):
-                _, nf, fl, ll, _ = batches[step]
-                S = 2 * np.asarray(ll, np.float64) + 1
-                byts += float(np.sum(2 * (8.0 * np.asarray(nf) * S + 8.0 * np.asarray(nf))))
-            gbs = byts / (ms_c / 1e3) / 1e9
-            aux["ctc_alpha_beta"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
-                                     "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
-                                     "ms_per_launch": round(ms_c / n_c, 4),
-                                     "note": "serial over T (one barrier per group of 8 frames): latency-bound"}
+            aux["gate_gemm"] = {"bound": "mfma",
+                                "kernel": "gemm_bwd_w (gemm_x3p, %s)" % ("bf16" if bf16 else "split-fp16"),
+                                "achieved": round(tf, 2), "peak": round(peak_engine, 1),
+                                "unit": "TFLOP/s" if bf16 else "TFLOP/s (fp32-class)",
+                                "frac": round(tf / peak_engine, 4), "where": "in step, beside a recurrence"}
+            if rank == 0:
+                # the same kernel on the same shape, alone on the chip
+                G4, din = nw * H, 2 * H
+                Ms, Ns, Ks = G4, din, T * N
+                split = 4 if bf16 else 8
+                ms_s = k.lib().kcm_bench_gemm_packed(None, Ms, Ns, Ks, 1 if bf16 else 0, 5, split)
+                if ms_s > 0:
+                    tf_s = 2.0 * Ms * Ns * Ks / (ms_s / 1e3) / 1e12
+                    aux["gate_gemm"]["standalone"] = {
+                        "shape": f"M={Ms} N={Ns} K={Ks} split-K {split} (dW of a BLSTM layer, one direction)",
+                        "ms": round(ms_s, 4), "achieved": round(tf_s, 2), "frac": round(tf_s / peak_engine, 4),
+                        "note": "kcm_bench_gemm_packed: random packed operands, 5 launches after 2 warm-ups"}
+        # CTC: each kernel against its own algorithmic bytes
+        cb = {"ctc_logz": 0.0, "ctc_alpha_beta": 0.0, "ctc_grad": 0.0}
+        for step in range(args.warmup, total):
+            _, nf, _, ll, _ = batches[step]
+            for key, v in ctc_bytes(T, A, nf, ll).items():
+                cb[key] += v
+        for key, byts in cb.items():
+            if key in prof:
+                ms_c, n_c = prof[key]
+                gbs = byts / (ms_c / 1e3) / 1e9
+                aux[key] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                            "frac": round(gbs / PEAK_HBM_GBS, 4), "ms_per_launch": round(ms_c / n_c, 4),
+                            "bytes_per_launch": round(byts / n_c)}
+        if "ctc_alpha_beta" in aux:
+            aux["ctc_alpha_beta"]["us_per_frame"] = round(aux["ctc_alpha_beta"]["ms_per_launch"] / T * 1e3, 4)
+            aux["ctc_alpha_beta"]["note"] = ("serial over T (one barrier per group of 8 frames): latency-bound; "
+                                             "bytes = emission rows read + alpha/beta spill + fp64 offsets written")
         roof["secondary"] = aux
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(T, D, H, A, L, 20161015, ratio, mode=mode, Ns=2 if H > 512 else 4)
+        cpu = cpu_baseline(params0, host_batches[args.warmup], T, D, H, A, L, ratio, mode=mode,
+                           Ns=2 if H > 512 else 4)
 
     if rank == 0:
         value = frames / dt
         fpf = step_flops_per_frame(D, H, A, L, nw=nw)
+        step_tf = value * fpf / 1e12
         out = {"metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if bf16 else "f32",
@@ -346,22 +535,31 @@ def main():
                           f"custom: {L}x{'BLSTM' if mode == 2 else 'BGRU'}-{H}, minibatch={N}/GPU, T_max={T}",
                           "model": f"{L}x{'BLSTM' if mode == 2 else 'BGRU'}-{H}+affine-{A}", "global_batch": N * world,
                           "seq_len": T, "parallelism": f"dp{world}"},
+               "loss_match": lm,
                # per-step device time (HIP events on the trainer's stream): the
                # median of the K steps beside the whole-job mean
                "median_step_ms": round(med_ms, 3),
                "value_median": round(frames_per_step / (med_ms / 1e3), 1),
-               # whole train step against the fp32 MFMA peak (algorithmic
-               # FLOPs/frame x frames/s; BASELINE.md's whole-step fraction)
-               "step_roofline": {"flops_per_frame": fpf, "achieved_tflops": round(value * fpf / 1e12, 2),
-                                 "peak": peak_mfma, "frac": round(value * fpf / 1e12 / peak_mfma, 4)},
-               "loss": {"objf_per_label": round(objf / max(wt, 1), 4), "accuracy": round(acc / max(wt, 1), 4)},
-               "roofline": roof, "cpu_baseline": cpu}
+               # whole train step: algorithmic FLOPs/frame x frames/s against the
+               # engine the products run on; the fp32 MFMA peak beside it as a
+               # ratio (the x3 engine is faster than fp32 MFMA, so it may pass 1)
+               "step_roofline": {"flops_per_frame": fpf, "achieved_tflops": round(step_tf, 2),
+                                 "engine": engine, "peak": round(peak_engine, 1),
+                                 "frac": round(step_tf / peak_engine, 4),
+                                 "ratio_to_fp32_mfma_peak": None if bf16 else round(step_tf / PEAK_FP32_TFLOPS, 4)},
+               "loss": {"objf_per_label": round(objf / max(wt, 1), 4), "accuracy": round(acc / max(wt, 1), 4),
+                        # warm-up + timed steps in order (summed over the ranks);
+                        # the growth is the reference's own SGD on this synthetic
+                        # data: summed minibatch gradients at lr 5e-4 (tests/
+                        # test_train_gpu.py::test_multistep_trajectory_matches_oracle)
+                        "objf_per_label_by_step": [round(o / max(w, 1), 3) for o, w in traj]},
+               "dp": dp_info, "roofline": roof, "cpu_baseline": cpu}
         if h2d:
             out["h2d_inclusive"] = {"value": round(h2d[1] / h2d[0], 1),
                                     "median_step_ms": round(float(np.median(h2d[2])), 3),
                                     "note": "features copied from pinned host memory on the trainer's stream "
                                             "inside every step (not `value`)"}
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

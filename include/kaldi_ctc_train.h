@@ -148,6 +148,26 @@ int kctc_nnet_enable_dp_host(kctcNnet_t nnet, kctc_host_allreduce_fn allreduce, 
 int kctc_nnet_set_dp_mode(kctcNnet_t nnet, int mode);
 int kctc_nnet_average_params(kctcNnet_t nnet);
 
+/* A step whose device error word is set on ANY rank (a recurrence's bounded
+ * spin timed out) is skipped on every rank: the word is summed over the ranks
+ * through the exchange after the gradient buckets, before the updates, and
+ * the train step then fails on every rank with the parameters unchanged.
+ * Test hook: the next minibatch of `nnet` starts with error word `word`. */
+int kctc_nnet_inject_step_error(kctcNnet_t nnet, unsigned word);
+
+/* CU budget.  RCCL's kernels are capped at KCTC_COMM_CTAS
+ * blocks (default 16, ncclConfig_t.maxCTAs) and the streamed GEMMs beside a
+ * backward recurrence leave that many CUs free.  kctc_nnet_enable_cu_probe is
+ * the test of that budget: a one-rank exchange whose every gradient bucket
+ * launches a kernel holding `blocks` whole CUs for `usec` microseconds on the
+ * comm stream (gradients untouched); blocks 0 switches it off. */
+int kctc_nnet_enable_cu_probe(kctcNnet_t nnet, int blocks, double usec);
+/* Ranks sharing one device (host-transport data parallelism on one GPU):
+ * the nnets created afterwards in this process run on CU-masked streams
+ * holding CU share `part` of `nparts`, and the persistent kernels size
+ * themselves for that share.  Call before kctc_nnet_create. */
+int kctc_set_cu_partition(int part, int nparts);
+
 /* Arithmetic of every CuDNNRecurrentComponent's recurrences and gate GEMMs:
  * 0 fp32-class (default), 1 bf16 operands with fp32 accumulation and fp32
  * master weights (BASELINE configs[4]).  Affine, CTC and the updates stay

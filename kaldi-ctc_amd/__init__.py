@@ -76,6 +76,8 @@ def lib():
     L.mictc_compute_ctc_loss_async.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int,
                                                vp, vp, vp, ctypes.c_int]
     L.mictc_compute_ctc_loss_async.restype = ctypes.c_int
+    L.mictc_set_frame_group.argtypes = [ctypes.c_int]
+    L.mictc_set_frame_group.restype = ctypes.c_int
     _bind_optional(L)
     _lib = L
     return L
@@ -119,6 +121,12 @@ def _stream_handle(stream):
         import torch
         return torch.cuda.current_stream().cuda_stream
     return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+
+def ctc_frame_group(m=0):
+    """Frames per barrier of the alpha/beta kernel (mictc_set_frame_group):
+    sets it when m > 0; returns the previous value."""
+    return lib().mictc_set_frame_group(int(m))
 
 
 def ctc_workspace_size(label_lengths, input_lengths, alphabet_size):
@@ -535,7 +543,25 @@ class Nnet:
                 "enable_dp_host")
 
 
+    def inject_step_error(self, word=1):
+        """Test hook: the next minibatch starts with device error word `word`
+        (as after a recurrence timeout): its updates are skipped -- on every
+        data-parallel rank -- and the step raises."""
+        _tcheck(lib().kctc_nnet_inject_step_error(self.h, int(word)), "inject_step_error")
+
+    def enable_cu_probe(self, blocks, usec):
+        """CU-budget probe: every gradient bucket launches a kernel holding
+        `blocks` whole CUs for `usec` us on a comm stream (blocks 0: off)."""
+        _tcheck(lib().kctc_nnet_enable_cu_probe(self.h, int(blocks), float(usec)), "enable_cu_probe")
+
+
 _HOST_ALLREDUCE = ctypes.CFUNCTYPE(None, ctypes.POINTER(ctypes.c_float), ctypes.c_long, ctypes.c_void_p)
+
+
+def set_cu_partition(part, nparts):
+    """Ranks sharing one device: nnets created afterwards in this process run
+    on CU share `part` of `nparts` (kctc_set_cu_partition)."""
+    _tcheck(lib().kctc_set_cu_partition(int(part), int(nparts)), "kctc_set_cu_partition")
 
 
 def softmax_rows(x, stream=None):

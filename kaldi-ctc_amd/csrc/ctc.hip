@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cstring>
 #include <type_traits>
+#include <atomic>
 #include <vector>
 
 #include "common.h"
@@ -548,6 +549,20 @@ static void staging_release(hipStream_t stream) {
   if (hipEventRecord(g_stage.ev, stream) == hipSuccess) g_stage.pending = true;
 }
 
+// frames per barrier of ctc_alpha_beta (mictc_set_frame_group)
+static std::atomic<int> g_frame_group{0};
+static int frame_group() {
+  int m = g_frame_group.load(std::memory_order_relaxed);
+  if (m <= 0) {
+    const char *e = getenv("KCTC_CTC_PAIR");
+    m = std::max(1, std::min(e && *e ? atoi(e) : 8, 8));
+    int expect = 0;
+    g_frame_group.compare_exchange_strong(expect, m);
+    m = g_frame_group.load(std::memory_order_relaxed);
+  }
+  return m;
+}
+
 static ctcStatus_t launch(const float *acts, float *grads, const int *flat_labels,
                           const int *label_lengths, const int *input_lengths, int A, int N,
                           double *costs_dev, void *workspace, hipStream_t stream, int blank) {
@@ -606,7 +621,7 @@ static ctcStatus_t launch(const float *acts, float *grads, const int *flat_label
     int Smax = 1;
     for (int n = 0; n < N; n++) Smax = 2 * label_lengths[n] + 1 > Smax ? 2 * label_lengths[n] + 1 : Smax;
     AbLds al;
-    al.pair = getenv("KCTC_CTC_PAIR") ? atoi(getenv("KCTC_CTC_PAIR")) : 8;  // measured: 8 < 6 < 4 < 3 < 1 < 2 (ms)
+    al.pair = frame_group();  // measured: 8 < 6 < 4 < 3 < 1 < 2 (ms)
     al.SP = (Smax + 63) / 64 * 64;
     al.CP = std::max((Smax + 4 + 3) / 4 * 4, (Smax <= kABThreads ? 1 : kSPT) * kABThreads);
     // chunk depth: as many frames as fit 96 KB of double-buffered emissions (4..32)
@@ -654,6 +669,12 @@ using namespace kctc::ctcimpl;
 extern "C" {
 
 int get_warpctc_version(void) { return 2; }
+
+int mictc_set_frame_group(int m) {
+  const int prev = frame_group();
+  if (m > 0) g_frame_group.store(std::max(1, std::min(m, 8)));
+  return prev;
+}
 
 const char *ctcGetStatusString(ctcStatus_t status) {
   switch (status) {

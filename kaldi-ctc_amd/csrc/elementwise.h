@@ -26,4 +26,16 @@ void sum_rows(hipStream_t s, const float *X, long rows, int cols, float alpha, f
 void fill(hipStream_t s, float *p, long n, float v);
 void scale_inplace(hipStream_t s, float *p, long n, float alpha);
 
+// Data-parallel agreement on a failed step: the step's device error word (set
+// by a recurrence's bounded-spin timeout) as a 0/1 float that the gradient
+// exchange sums over the ranks, and back: a positive sum sets kErrPeerFailed,
+// so every rank skips the updates of a step that failed on any rank.
+constexpr unsigned kErrPeerFailed = 1u << 8;
+void err_word_to_flag(hipStream_t s, const unsigned *err, float *flag);
+void flag_to_err_word(hipStream_t s, const float *flag, unsigned *err);
+
+// Holds `blocks` whole CUs (1024 threads and 160 KB LDS each) for `usec`
+// microseconds: the stand-in for a communication kernel in the CU-budget test.
+void cu_hold(hipStream_t s, int blocks, double usec);
+
 }  // namespace kctc

@@ -222,4 +222,37 @@ void scale_inplace(hipStream_t s, float *p, long n, float alpha) {
   hipLaunchKernelGGL(k_scale, dim3(grid_for(n)), dim3(256), 0, s, p, n, alpha);
 }
 
+// ---- data-parallel step agreement ------------------------------------------
+__global__ void k_err_to_flag(const unsigned *err, float *flag) { flag[0] = err[0] ? 1.f : 0.f; }
+__global__ void k_flag_to_err(const float *flag, unsigned *err) {
+  if (flag[0] > 0.f) err[0] |= kErrPeerFailed;
+}
+
+void err_word_to_flag(hipStream_t s, const unsigned *err, float *flag) {
+  hipLaunchKernelGGL(k_err_to_flag, dim3(1), dim3(1), 0, s, err, flag);
+}
+void flag_to_err_word(hipStream_t s, const float *flag, unsigned *err) {
+  hipLaunchKernelGGL(k_flag_to_err, dim3(1), dim3(1), 0, s, flag, err);
+}
+
+// ---- CU occupancy probe ----------------------------------------------------
+// Every block takes a whole CU (1024 threads, the dynamic LDS below) and
+// stays resident for `ticks` of the 100-MHz constant clock; every wave leaves
+// on the same time test, so the grid always drains.
+__global__ __launch_bounds__(1024) void k_cu_hold(unsigned long long ticks) {
+  extern __shared__ float hold_lds[];
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) hold_lds[0] = 0.f;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
+}
+
+void cu_hold(hipStream_t s, int blocks, double usec) {
+  if (blocks <= 0 || usec <= 0) return;
+  const int lds = 160 * 1024;
+  KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(k_cu_hold),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  hipLaunchKernelGGL(k_cu_hold, dim3(blocks), dim3(1024), lds, s, (unsigned long long)(usec * 100.0));
+  KCTC_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace kctc

@@ -1140,6 +1140,11 @@ void NnetCtcUpdater::Enqueue(const float *feats, int T_max, int N, const int *nu
   // updates of a step that set it are skipped on the device
   err_word_.ensure(256);
   KCTC_HIP_CHECK(hipMemsetAsync(err_word_.p, 0, sizeof(unsigned), S()));
+  if (inject_err_) {
+    KCTC_HIP_CHECK(hipMemcpyAsync(err_word_.p, &inject_err_, sizeof(unsigned), hipMemcpyHostToDevice, S()));
+    KCTC_HIP_CHECK(hipStreamSynchronize(S()));  // the source is a member that is reset next
+    inject_err_ = 0;
+  }
   for (int c = 0; c < C; c++)
     if (auto *r = dynamic_cast<CuDNNRecurrentComponent *>(&nnet_->GetComponent(c)))
       r->SetErrorWord(static_cast<unsigned *>(err_word_.p));
@@ -1242,10 +1247,14 @@ MinibatchStats NnetCtcUpdater::Finish() {
   const unsigned *herr = reinterpret_cast<const unsigned *>(hids + rows);
   last_ids_.assign(hids, hids + rows);
   last_costs_.assign(hcost, hcost + N);
-  for (int i = 0; i < sl.nerr; i++)
-    if (herr[i])
+  for (int i = 0; i < sl.nerr; i++) {
+    if (herr[i] & ~kErrPeerFailed)
       throw std::runtime_error("recurrence hand-off timed out (device error word set); this minibatch's "
                                "updates were skipped, the parameters are those before it");
+    if (herr[i])
+      throw std::runtime_error("the step failed on another data-parallel rank; every rank skipped this "
+                               "minibatch's updates, the parameters are those before it");
+  }
   const int *num_frames = sl.num_frames.data(), *flat_labels = sl.labels.data();
   const int *label_lengths = sl.label_lengths.data();
   MinibatchStats st;
@@ -1346,6 +1355,15 @@ void NnetCtcUpdater::Backprop(int T, int N) {  // :320-348
   }
   CuDevice::Instantiate().Join();
   if (exchange_) exchange_->Finish();
+  if (exchange_ && exchange_->WorldSize() > 1 && err_word_.p) {
+    // the gradients just summed include every rank's: a step that failed on
+    // ANY rank is skipped on all of them, so the replicas stay identical
+    unsigned *err = static_cast<unsigned *>(err_word_.p);
+    err_flag_.ensure(256);
+    err_word_to_flag(S(), err, err_flag_.f());
+    exchange_->AllReduceSum(err_flag_.f(), 1, S());
+    flag_to_err_word(S(), err_flag_.f(), err);
+  }
   for (int c : updated) {
     ProfScope ps("update");
     static_cast<UpdatableComponent *>(&nnet_->GetComponent(c))->ApplyUpdate(err_word_.p ? static_cast<const unsigned *>(err_word_.p) : nullptr);

@@ -432,6 +432,9 @@ class NnetCtcUpdater {
   // default 0) that ClipGradient self-repair draws from
   void Srand(unsigned seed) { repair_rng_.Seed(seed); }
   long RandCalls() const { return repair_rng_.Calls(); }
+  // test hook: the next minibatch's device error word starts as `word` (as if
+  // a recurrence had timed out), so its updates are skipped and Finish throws
+  void InjectStepError(unsigned word) { inject_err_ = word; }
 
  private:
   void Propagate(int T, int N);
@@ -448,6 +451,8 @@ class NnetCtcUpdater {
   CuMatrix deriv_a_, deriv_b_;
   DevBuf ctc_ws_, costs_dev_, ids_dev_;
   DevBuf err_word_;  // this step's recurrence error word (all RNNs), cleared per step
+  DevBuf err_flag_;  // the word as a 0/1 float, summed over the data-parallel ranks
+  unsigned inject_err_ = 0;
   struct Slot {  // one minibatch in flight: pinned readback + what its stats need
     char *pinned = nullptr;
     size_t bytes = 0;

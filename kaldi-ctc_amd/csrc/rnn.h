@@ -37,6 +37,19 @@ struct RnnReserveLayout {
 RnnReserveLayout rnn_reserve_layout(const RnnDesc &d, int T, int N);
 size_t rnn_workspace_bytes(const RnnDesc &d, int T, int N);
 
+// CU budget of the persistent kernels.  A v6 recurrence needs
+// all of its workgroups resident at once (one per CU, >= 96 KB LDS) and the
+// streamed GEMMs' persistent blocks (one per CU as well) spin on its flags,
+// so everything that may hold a CU beside them has to fit:
+//   recurrence WGs + streamed blocks + comm CUs + 16 (margin) <= usable CUs.
+// `cus`: the CUs this process may use (0: the device's; a smaller number
+// when ranks share a device through CU-masked streams); `comm`: CUs the
+// gradient exchange's kernels (RCCL, capped by maxCTAs) may hold during a
+// backward pass.  Streaming is switched off when fewer than 8 blocks fit.
+void rnn_set_cu_budget(int cus, int comm);
+int rnn_usable_cus();
+int rnn_comm_cus();
+
 // Status codes of the RNN ABI (include/kaldi_rnn.h)
 enum { KRNN_OK = 0, KRNN_BAD_PARAM = 1, KRNN_NOT_SUPPORTED = 2, KRNN_EXEC_FAILED = 3,
        KRNN_TIMEOUT = 4 };

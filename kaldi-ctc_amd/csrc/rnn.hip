@@ -2323,7 +2323,8 @@ static V6Cfg pick6(const RnnDesc &d, int N, bool fwd, int gs_force = 0) {
   if ((d.mode != kLstm && d.mode != kGru) || N <= 0 || N > 64 || d.dirs > 2) return c;
   if (d.H != 256 && d.H != 320 && d.H != 512 && d.H != 1024) return c;
   const int gs = gs_force ? gs_force : v6_group_rows(N, fwd), rg = (N + gs - 1) / gs;
-  const int max_wg = env_int("KCTC_REC_MAX_WG", 128);
+  // never more workgroups than the CUs this process may use (all must be resident)
+  const int max_wg = std::min(env_int("KCTC_REC_MAX_WG", 128), rnn_usable_cus());
   auto ok = [&](int U) {
     const int nth = U == 32 ? 512 : 256, nwv = nth / 64;
     if (d.H % U || d.H % (16 * nwv) || (d.H / U) % (nth / (4 * U))) return false;
@@ -2439,6 +2440,15 @@ namespace {
 // BEFORE the recurrence launch, and the GEMM is enqueued AFTER it: should the
 // two streams share a hardware queue, the GEMM then merely runs after the
 // recurrence instead of blocking it (its blocks only wait for recurrence flags).
+int g_usable_cus = 0, g_comm_cus = 0;
+
+// persistent blocks a streamed GEMM may run beside a recurrence of `rec_wgs`
+// workgroups (rnn.h, CU budget); 0: too few to stream
+int stream_block_budget(int rec_wgs, bool backward) {
+  const int left = rnn_usable_cus() - rec_wgs - (backward ? rnn_comm_cus() : 0) - 16;
+  return left >= 8 ? left : 0;
+}
+
 hipEvent_t fork_event(hipStream_t s) {
   static thread_local hipEvent_t ev = nullptr;
   if (!ev) KCTC_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -2465,6 +2475,8 @@ bool chain_ok(const RnnDesc &d, int ver, int T, int N, const RnnFwdChain *c) {
   // the CUs left beside the 128-workgroup recurrence outlasts it (990k ->
   // 728k and 560k -> 389k frames/s measured), the 256-tile GEMM after it wins
   if ((N > 16 || d.prec == kPrecBf16) && !env_int("KCTC_STREAM_ALL", 0)) return false;
+  const V6Cfg c6 = pick6(d, N, true);
+  if (!c6 || !stream_block_budget(d.dirs * (d.H / c6.U) * c6.rg, false)) return false;
   const long xs = 2L * (d.H / 32) * (d.prec == kPrecBf16 ? 1 : 2) * 16 * 32 * pick6(d, N, true).rg;  // halves per step image
   if ((long)T * xs * 2 >= (1L << 31)) return false;
   return c->ws_bytes >= rnn_workspace_bytes(n, T, N) &&
@@ -2491,12 +2503,6 @@ void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
       x3p_pack_rows(c.side, wl, Din, G, Din, Bp, eB, 0.f, n.dirs, pls, (long)G * KB * 64, (long)G);
   }
   const RnnReserveLayout lay = rnn_reserve_layout(n, T, N);
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    KCTC_HIP_CHECK(hipGetDevice(&dev));
-    KCTC_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  }
   X3PArgs x;
   x.bf16 = bf;
   x.M = T * N; x.N = G; x.KB = KB;
@@ -2517,8 +2523,10 @@ void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
     x.stream_part = pk<float>(c.workspace, n, T, N, pl.fpart);
   }
   // every producer workgroup needs a CU of its own (96 KB LDS); the GEMM's
-  // persistent blocks (96 KB each) take the rest minus a margin
-  x.max_blocks = env_int("KCTC_STREAM_BLOCKS", std::max(8, cus - d.dirs * p.nwg * p.rg - 16));
+  // persistent blocks (96 KB each) take the rest minus a margin (chain_ok
+  // checked that at least 8 fit).  No gradient exchange runs during a
+  // forward pass: the updates of the previous step waited for it.
+  x.max_blocks = env_int("KCTC_STREAM_BLOCKS", stream_block_budget(d.dirs * p.nwg * p.rg, false));
   {
     ProfSpan ps(c.side, "fwd_proj_stream");
     gemm_x3p(c.side, x);
@@ -2527,6 +2535,20 @@ void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
 }
 
 }  // namespace
+
+void rnn_set_cu_budget(int cus, int comm) {
+  g_usable_cus = std::max(0, cus);
+  g_comm_cus = std::max(0, comm);
+}
+int rnn_usable_cus() {
+  static int dev_cus[64] = {0};
+  int dev = 0;
+  KCTC_HIP_CHECK(hipGetDevice(&dev));
+  int &c = dev_cus[dev & 63];
+  if (!c) KCTC_HIP_CHECK(hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev));
+  return g_usable_cus > 0 ? std::min(g_usable_cus, c) : c;
+}
+int rnn_comm_cus() { return g_comm_cus; }
 
 int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *w, float *y, void *workspace, size_t ws_bytes,
@@ -2689,7 +2711,9 @@ void launch_bwd_stream(const RnnDesc &d, const RecParams &p, int l, const float 
   a.part = pk<float>(workspace, d, T, N, pl.part);
   a.cnt = pk<int>(workspace, d, T, N, pl.cnt);
   a.flags = p.flags + 1024; a.nwg = p.nwg; a.T = T; a.Nf = N; a.err = err; a.rg = p.rg;
-  a.blocks = env_int("KCTC_BWD_STREAM_BLOCKS", 96);
+  // 96 measured best at configs[1]; never more than the CU budget leaves
+  // beside the recurrence and the exchange's kernels (rnn.h)
+  a.blocks = env_int("KCTC_BWD_STREAM_BLOCKS", std::min(96, stream_block_budget(d.dirs * p.nwg * p.rg, true)));
   ProfSpan ps(ov, "bwd_data_stream");
   gemm_x3p_bwd_stream(ov, a);
 }
@@ -2900,7 +2924,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
                           ((d.prec == kPrecX3 && N <= 16) || env_int("KCTC_STREAM_ALL", 0)) && use_x3(NW * H) &&
                           NW * H <= 4096 &&
                           (d.prec == kPrecX3 || (NW * H) % 64 == 0) && (long)TN * Din * 4 < (1L << 31) &&
-                          env_int("KCTC_BWD_STREAM", 1);
+                          stream_block_budget((int)grid.x, true) && env_int("KCTC_BWD_STREAM", 1);
     // weight gradients streamed off this recurrence (the bottom component):
     // its dGates rows must be written through too
     const bool wstream = wgrad && wgrad->side && !dxl && ver == 6 && !p.xpd && d.layers == 1 &&
@@ -3163,8 +3187,10 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       x.C = dwl; x.ldc = Din; x.beta = 1.f;
       x.batch = dirs; x.sC = pls;
       x.split_k = x3p_pick_split((int)G4, Din, KBt, dirs);
-      // concurrent with dR: its own split slab past dR's
-      x.ws = two ? ws + al64((long)x3p_pick_split((int)G4, H, KBt, dirs) * dirs * G4 * H) : ws;
+      // concurrent with dR: its own split slab past dR's (none when dR is not
+      // split: drec_split_floats reserves a dR slab only for a split > 1)
+      const long sR = x3p_pick_split((int)G4, H, KBt, dirs);
+      x.ws = two && sR > 1 ? ws + al64(sR * dirs * G4 * H) : ws;
       x.max_blocks = g.max_blocks; x.tile_counter = g.tile_counter;
       ProfSpan ps(sx, "gemm_bwd_w");
       gemm_x3p(sx, x);

@@ -23,6 +23,8 @@
 
 using kctc::nnet2::CuDevice;
 
+int kctc_usable_cus_override();
+
 namespace {
 
 thread_local std::string g_err;
@@ -34,19 +36,38 @@ thread_local std::string g_err;
 // per-rank minibatches equals the gradient of their concatenation, then the
 // reference's per-component clip (+-clip-gradient) and SGD run identically
 // on every rank, so replicas stay bit-identical.
+//
+// CU budget: the all-reduces run during the backward pass,
+// beside the persistent recurrence and the streamed dx GEMM, whose blocks must
+// all be resident.  RCCL's kernels are capped at kctc_comm_ctas() blocks
+// (ncclConfig_t.maxCTAs) and the streamed GEMMs leave that many CUs free
+// (rnn_set_cu_budget), so even if every RCCL block kept a CU to itself the
+// recurrence's workgroups still find theirs.
+int kctc_comm_ctas() {
+  const char *e = getenv("KCTC_COMM_CTAS");
+  const int v = e && *e ? atoi(e) : 16;
+  return std::max(1, std::min(v, 64));
+}
+
 class RcclExchange : public kctc::nnet2::GradExchange {
  public:
   RcclExchange(const void *uid, int rank, int world, hipStream_t compute)
       : world_(world), compute_(compute) {
     ncclUniqueId id;
     memcpy(&id, uid, sizeof(id));
-    if (ncclCommInitRank(&comm_, world, id, rank) != ncclSuccess)
-      throw std::runtime_error("ncclCommInitRank failed");
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 1;
+    cfg.maxCTAs = kctc_comm_ctas();
+    cfg.minCTAs = std::min(cfg.maxCTAs, 4);
+    if (ncclCommInitRankConfig(&comm_, world, id, rank, &cfg) != ncclSuccess)
+      throw std::runtime_error("ncclCommInitRankConfig failed");
+    kctc::rnn_set_cu_budget(kctc_usable_cus_override(), cfg.maxCTAs);
     KCTC_HIP_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
     KCTC_HIP_CHECK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
     KCTC_HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
   }
   ~RcclExchange() override {
+    kctc::rnn_set_cu_budget(kctc_usable_cus_override(), 0);
     (void)hipStreamSynchronize(comm_stream_);
     ncclCommDestroy(comm_);
     (void)hipStreamDestroy(comm_stream_);
@@ -137,7 +158,59 @@ class HostExchange : public kctc::nnet2::GradExchange {
   std::vector<Bucket> buckets_;
 };
 
+// CU-budget probe (kctc_nnet_enable_cu_probe): a one-rank exchange whose
+// "all-reduce" of every gradient bucket is a kernel holding `blocks` whole CUs
+// for `usec` on the comm stream -- the worst case of an exchange kernel that
+// keeps its CUs to itself while the next component's backward recurrence and
+// streamed dx GEMM run.  The gradients are not touched (a sum over one rank).
+class CuProbeExchange : public kctc::nnet2::GradExchange {
+ public:
+  CuProbeExchange(int blocks, double usec, hipStream_t compute) : blocks_(blocks), usec_(usec), compute_(compute) {
+    KCTC_HIP_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
+    KCTC_HIP_CHECK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
+    KCTC_HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+    kctc::rnn_set_cu_budget(kctc_usable_cus_override(), blocks);
+  }
+  ~CuProbeExchange() override {
+    kctc::rnn_set_cu_budget(kctc_usable_cus_override(), 0);
+    (void)hipStreamSynchronize(comm_stream_);
+    (void)hipStreamDestroy(comm_stream_);
+    (void)hipEventDestroy(ready_);
+    (void)hipEventDestroy(done_);
+  }
+  void GradReady(int, float *, long, hipStream_t producer) override {
+    KCTC_HIP_CHECK(hipEventRecord(ready_, producer));
+    KCTC_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ready_, 0));
+    kctc::cu_hold(comm_stream_, blocks_, usec_);
+    launches_++;
+  }
+  void Finish() override {
+    KCTC_HIP_CHECK(hipEventRecord(done_, comm_stream_));
+    KCTC_HIP_CHECK(hipStreamWaitEvent(compute_, done_, 0));
+  }
+  int WorldSize() const override { return 1; }
+  void AllReduceSum(float *, long, hipStream_t) override {}
+  long launches_ = 0;
+
+ private:
+  int blocks_;
+  double usec_;
+  hipStream_t compute_, comm_stream_ = nullptr;
+  hipEvent_t ready_ = nullptr, done_ = nullptr;
+};
+
 }  // namespace
+
+// CUs of the device this process may use: all of them, or its share when
+// ranks share a device (kctc_set_cu_partition)
+static int g_part = 0, g_nparts = 1;
+int kctc_usable_cus_override() {
+  if (g_nparts <= 1) return 0;
+  int dev = 0, cus = 0;
+  KCTC_HIP_CHECK(hipGetDevice(&dev));
+  KCTC_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  return cus / g_nparts;
+}
 
 void kctc_set_error(const char *msg) { g_err = msg ? msg : ""; }
 
@@ -151,6 +224,10 @@ struct kctcNnetImpl {
   kctc::nnet2::GradExchange *dp = nullptr;
   bool dp_average = false;  // model averaging: no per-step gradient exchange
   kctc::nnet2::DevBuf egs_feats, egs_scratch;  // TrainNnetSimple staging
+  // decodable (per utterance): device priors, uploaded again only when they
+  // change, and the output / scratch buffers, grown and kept
+  kctc::nnet2::DevBuf dec_priors, dec_out, dec_scratch;
+  std::vector<float> dec_priors_host;
   // nnet2-ctc model file extras: the CtcTransitionModel exactly as read (opaque
   // bytes, in the mode of the file it came from) and AmNnet's priors
   std::string trans_model;
@@ -173,6 +250,18 @@ struct kctcNnetImpl {
   // the weight-gradient side stream at the lowest; KCTC_OVERLAP=0 keeps
   // everything on one stream
   void create_streams() {
+    if (g_nparts > 1) {  // ranks sharing the device: this rank's streams on its CU share only
+      int cus = 0;
+      KCTC_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+      const int per = cus / g_nparts, first = g_part * per;
+      std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+      for (int c = first; c < first + per; c++) mask[c / 32] |= 1u << (c % 32);
+      KCTC_HIP_CHECK(hipExtStreamCreateWithCUMask(&stream, (uint32_t)mask.size(), mask.data()));
+      KCTC_HIP_CHECK(hipExtStreamCreateWithCUMask(&side, (uint32_t)mask.size(), mask.data()));
+      KCTC_HIP_CHECK(hipExtStreamCreateWithCUMask(&stream2, (uint32_t)mask.size(), mask.data()));
+      kctc::rnn_set_cu_budget(per, kctc::rnn_comm_cus());
+      return;
+    }
     int lo = 0, hi = 0;
     KCTC_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     KCTC_HIP_CHECK(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, hi));
@@ -591,6 +680,37 @@ int kctc_nnet_enable_dp_host(kctcNnet_t n, kctc_host_allreduce_fn fn, void *user
   });
 }
 
+int kctc_nnet_enable_cu_probe(kctcNnet_t n, int blocks, double usec) {
+  return guarded([&] {
+    KCTC_REQUIRE(n && blocks >= 0 && usec >= 0, "kctc_nnet_enable_cu_probe: bad argument");
+    KCTC_REQUIRE(n->trainer.Pending() == 0, "kctc_nnet_enable_cu_probe with minibatches in flight");
+    n->activate();
+    delete n->dp;
+    n->dp = nullptr;
+    n->trainer.SetExchange(nullptr);
+    if (blocks > 0) {
+      n->dp = new CuProbeExchange(blocks, usec, n->stream);
+      n->trainer.SetExchange(n->dp);
+    }
+  });
+}
+
+int kctc_set_cu_partition(int part, int nparts) {
+  return guarded([&] {
+    KCTC_REQUIRE(nparts >= 1 && nparts <= 8 && part >= 0 && part < nparts, "kctc_set_cu_partition: bad partition");
+    g_part = part;
+    g_nparts = nparts;
+    kctc::rnn_set_cu_budget(kctc_usable_cus_override(), kctc::rnn_comm_cus());
+  });
+}
+
+int kctc_nnet_inject_step_error(kctcNnet_t n, unsigned word) {
+  return guarded([&] {
+    KCTC_REQUIRE(n, "null nnet");
+    n->trainer.InjectStepError(word);
+  });
+}
+
 int kctc_nnet_set_dp_mode(kctcNnet_t n, int mode) {
   return guarded([&] {
     KCTC_REQUIRE(n && (mode == 0 || mode == 1), "kctc_nnet_set_dp_mode: mode must be 0 or 1");
@@ -712,13 +832,18 @@ int kctc_am_nnet_decodable(kctcNnet_t n, const float *feats_dev, int T, float pr
     // left/right context of this path are 0: every input row gives an output row
     const auto &o = n->evaluator.Forward(feats_dev, T, 1);
     const int A = o.NumCols();
-    kctc::nnet2::DevBuf pri, out, scratch;
+    auto &out = n->dec_out, &scratch = n->dec_scratch;
     const float *pd = nullptr;
     if (!n->priors.empty()) {
       KCTC_REQUIRE((int)n->priors.size() == A, "priors dimension != network output dimension");
-      pri.ensure(sizeof(float) * A);
-      KCTC_HIP_CHECK(hipMemcpyAsync(pri.p, n->priors.data(), sizeof(float) * A, hipMemcpyHostToDevice, n->stream));
-      pd = pri.f();
+      if (n->dec_priors_host != n->priors) {
+        n->dec_priors.ensure(sizeof(float) * A);
+        KCTC_HIP_CHECK(hipMemcpyAsync(n->dec_priors.p, n->priors.data(), sizeof(float) * A, hipMemcpyHostToDevice,
+                                      n->stream));
+        KCTC_HIP_CHECK(hipStreamSynchronize(n->stream));  // the source is the host vector
+        n->dec_priors_host = n->priors;
+      }
+      pd = n->dec_priors.f();
     }
     out.ensure(sizeof(float) * (size_t)T * A);
     scratch.ensure(kctc_ctc_decodable_scratch_bytes(T));
@@ -726,6 +851,7 @@ int kctc_am_nnet_decodable(kctcNnet_t n, const float *feats_dev, int T, float pr
     const int st = kctc_ctc_decodable(n->stream, o.Data(), T, A, pd, prob_scale, blank_threshold, 1.0e-10f, out.f(),
                                       scratch.p, &kept);
     if (st) throw std::runtime_error(g_err);
+    KCTC_HIP_CHECK(hipStreamSynchronize(n->stream));
     KCTC_HIP_CHECK(hipMemcpy(out_host, out.p, sizeof(float) * (size_t)kept * A, hipMemcpyDeviceToHost));
     *num_rows = kept;
   });

@@ -74,6 +74,27 @@ LAYER_CASES = {"lstm512_d40": dict(mode=2, T=2000, N=16, D=40, H=512, seed=11),
                "gru1024_d2048_n32": dict(mode=3, T=2000, N=32, D=2048, H=1024, seed=14, prec="bf16")}
 
 
+class ProductLayout:
+    """params_size / lin_offset (the cuDNN-v5 opaque layout) through the
+    library's own krnn ABI, for callers that must not load the oracle
+    (bench.py's loss match); equal to the oracle's (tests/test_abi.py)."""
+
+    def __init__(self, kctc):
+        self.k, self._rnns = kctc, {}
+
+    def _rnn(self, mode, D, H, layers, dirs):
+        key = (mode, D, H, layers, dirs)
+        if key not in self._rnns:
+            self._rnns[key] = self.k.Rnn(mode, D, H, layers, dirs == 2)
+        return self._rnns[key]
+
+    def params_size(self, mode, D, H, layers, dirs):
+        return self._rnn(mode, D, H, layers, dirs).num_params
+
+    def lin_offset(self, mode, D, H, layers, dirs, pl, lin, isb):
+        return self._rnn(mode, D, H, layers, dirs).lin_offset(pl, lin, isb)[0]
+
+
 def recipe_rnn_params(oracle, mode, D, H, seed, stddev=0.02, bias=0.2):
     P = oracle.params_size(mode, D, H, 1, 2)
     w = (np.random.default_rng([seed, 1]).standard_normal(P) * stddev).astype(np.float32)

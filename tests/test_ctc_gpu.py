@@ -40,14 +40,25 @@ def test_ctc_matches_golden(kctc, gpu, name):
         assert np.all(grads[tn:, n, :] == 0)
 
 
+@pytest.fixture(params=[8, 1, 2, 5], ids=lambda m: f"group{m}")
+def frame_group(kctc, request):
+    """Frames per barrier of the alpha/beta kernel (default 8): the halo
+    lanes and DPP shifts of every group depth give the same results."""
+    prev = kctc.ctc_frame_group(request.param)
+    yield request.param
+    kctc.ctc_frame_group(prev)
+
+
 @pytest.mark.parametrize("seed,T,N,L,A,rep", [
     (1, 2000, 16, 237, 41, False),     # configs[1] shape: T_max=2000, N=16, L=T/8
     (2, 667, 8, 250, 41, False),       # configs[2] (fs=3): L = 3T/8
     (3, 300, 4, 60, 41, True),         # repeats in labels
     (4, 1300, 2, 639, 41, False),      # maximum label length (MAX_WARPCTC_LABEL_LENGTH)
     (5, 50, 3, 5, 300, False),         # large alphabet
+    (6, 37, 5, 9, 41, True),           # T not a multiple of any group depth, short utterances
 ])
-def test_ctc_matches_oracle(kctc, gpu, oracle, seed, T, N, L, A, rep):
+def test_ctc_matches_oracle(kctc, gpu, oracle, frame_group, seed, T, N, L, A, rep):
+    assert kctc.ctc_frame_group() == frame_group
     rng = np.random.default_rng(seed)
     acts = (rng.standard_normal((T, N, A)) * 3).astype(np.float32)
     lens = [T - int(rng.integers(0, T // 10 + 1)) if n else T for n in range(N)]

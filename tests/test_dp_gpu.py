@@ -167,3 +167,71 @@ def test_two_rank_model_averaging(kctc, gpu):
     for p0, p1, a0, a1 in zip(res[0][1], res[1][1], res[0][2], res[1][2]):
         np.testing.assert_array_equal(a0, a1)
         np.testing.assert_array_equal(a0, (p0 + p1) * np.float32(0.5))
+
+
+def _fail_rank_main(rank, world, port, q):
+    try:
+        import torch
+        import torch.distributed as dist
+        sys.path.insert(0, ROOT)
+        import __graft_entry__ as ge
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        kctc = ge.load_package()
+        net = kctc.Nnet(_cfg(kctc), seed=21)
+
+        def allreduce(buf):
+            dist.all_reduce(torch.from_numpy(buf))
+
+        net.enable_dp_host(allreduce, world)
+        params, errors = [], []
+        for step in range(3):
+            feats, nf, fl, ll = _batch(kctc, rank, step)
+            if step == 1 and rank == 1:
+                net.inject_step_error(1)  # as if rank 1's recurrence had timed out
+            try:
+                net.train_step(torch.from_numpy(feats).to("cuda:0"), T, N, nf, fl, ll)
+                errors.append(None)
+            except Exception as e:  # noqa: BLE001 -- the failed step raises on every rank
+                errors.append(str(e))
+            params.append([net.get_params(c) for c in range(net.num_components) if net.num_params(c)])
+        q.put((rank, errors, params))
+        net.close()
+        dist.destroy_process_group()
+    except BaseException as e:  # report, never hang the parent
+        q.put((rank, repr(e), None))
+
+
+def test_failed_step_on_one_rank_is_skipped_on_all(kctc, gpu):
+    """a step whose device error word is set on ONE rank
+    must not be applied anywhere -- the gradients were already summed into
+    every rank's buffers.  The word is summed over the ranks before the
+    updates: both ranks skip step 1 (parameters equal to after step 0), both
+    raise, the local rank with the timeout message and the other with the
+    peer message, and the replicas stay bit-identical through step 2."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 33500 + os.getpid() % 2000
+    procs = [ctx.Process(target=_fail_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r = q.get(timeout=200)
+        res[r[0]] = r
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        assert res[r][2] is not None, res[r][1]
+    e0, e1 = res[0][1], res[1][1]
+    assert e0[0] is None and e1[0] is None and e0[2] is None and e1[2] is None
+    assert e1[1] is not None and "timed out" in e1[1]
+    assert e0[1] is not None and "another data-parallel rank" in e0[1]
+    for r in (0, 1):
+        for a, b in zip(res[r][2][0], res[r][2][1]):
+            np.testing.assert_array_equal(a, b)  # step 1 skipped
+    for step in range(3):
+        for a, b in zip(res[0][2][step], res[1][2][step]):
+            np.testing.assert_array_equal(a, b)  # replicas identical
+    assert any(np.any(a != b) for a, b in zip(res[0][2][1], res[0][2][2]))  # step 2 applied
