@@ -1,6 +1,7 @@
 """Generate the full-size sketch fixtures (tests/golden/sketch_*.npz) from the
 fp64 oracle.  TEST INFRASTRUCTURE: run once in the build container
-(`python tests/golden/make_sketch.py`, ~5 min on 8 cores); the GPU tests in
+(`python tests/golden/make_sketch.py [layers|step|step_cfg2|step_cfg4|<layer case>]`,
+~5 min on 8 cores for the layers and the configs[1] step; step_cfg4 ~30 min); the GPU tests in
 tests/test_fullsize_gpu.py regenerate the same inputs and compare sketches
 (tests/sketch_common.py).  Nothing here reads /root/reference.
 """
@@ -55,13 +56,13 @@ def layers(kctc, only=None):
     np.savez_compressed(path, **out)
 
 
-def step(kctc):
-    s = S.STEP
+def step(kctc, case="cfg1"):
+    s = S.STEPS[case]
     t0 = time.time()
-    rnn, Wa, ba = S.step_params(O)
-    feats, nf, fl, ll = S.step_inputs(kctc)
+    rnn, Wa, ba = S.step_params(O, case)
+    feats, nf, fl, ll = S.step_inputs(kctc, case)
     spec = O.NnetSpec()
-    spec.num_rnn, spec.mode, spec.hidden, spec.dirs, spec.layers_per_rnn = s["R"], 2, s["H"], 2, 1
+    spec.num_rnn, spec.mode, spec.hidden, spec.dirs, spec.layers_per_rnn = s["R"], s["mode"], s["H"], 2, 1
     spec.input_dim, spec.num_targets = s["D"], s["A"]
     spec.clip_threshold, spec.repair_threshold, spec.repair_scale, spec.repair_target = 30.0, 0.01, 1.0, 0.0
     spec.rnn_clip_gradient, spec.lr_rnn, spec.lr_affine = 5.0, s["lr"], s["lr"]
@@ -84,8 +85,8 @@ def step(kctc):
         S.save(f"g{c}", S.sketch((p[c] - rnn[c].astype(np.float64)) / s["lr"], 600 + c), out)
     daff = np.concatenate([(Wd - Wa.astype(np.float64)).ravel(), bd - ba.astype(np.float64)]) / s["lr"]
     S.save("gaff", S.sketch(daff, 700), out)
-    np.savez_compressed(os.path.join(HERE, "sketch_step.npz"), **out)
-    print(f"step: {time.time() - t0:.1f}s objf {tot:.8g} acc {acc} weight {wt} clipped {cnc}", flush=True)
+    np.savez_compressed(os.path.join(HERE, s["file"] + ".npz"), **out)
+    print(f"step {case}: {time.time() - t0:.1f}s objf {tot:.8g} acc {acc} weight {wt} clipped {cnc}", flush=True)
 
 
 if __name__ == "__main__":
@@ -96,3 +97,6 @@ if __name__ == "__main__":
         layers(kctc, cases or None)
     if "step" in what:
         step(kctc)
+    for case in ("cfg2", "cfg4"):
+        if "step_" + case in what:
+            step(kctc, case)

@@ -119,15 +119,24 @@ def layer_inputs(kctc, oracle, case):
     return w, x, dy
 
 
-# (ii) one configs[1] train step (bench.py's first minibatch, seed 20161015):
-#      5 x BLSTM-512, N=16, T_max=2000, lr 5e-4; recipe init, affine
-#      N(0, 1/1024) / N(0, 1) (nnet-component.cc:1169-1174).
-STEP = dict(T=2000, N=16, D=40, H=512, A=41, R=5, lr=5e-4, seed=20161015, pseed=77)
+# (ii) one whole train step of bench.py's first minibatch (seed 20161015) per
+#      BASELINE config, lr 5e-4; recipe init, affine N(0, 1/2H) / N(0, 1)
+#      (nnet-component.cc:1169-1174):
+#      cfg1  configs[1]: 5 x BLSTM-512, N=16, T_max=2000 (fixture sketch_step.npz)
+#      cfg2  configs[2]: 5 x BLSTM-512, fs=3: N=64, T_max=667, 3/8 labels per frame
+#      cfg4  configs[4]: 5 x BGRU-1024, N=32, T_max=2000, run in bf16 on the GPU
+STEPS = {"cfg1": dict(T=2000, N=16, D=40, H=512, A=41, R=5, mode=2, lr=5e-4, seed=20161015, pseed=77,
+                      ratio=0.125, file="sketch_step"),
+         "cfg2": dict(T=667, N=64, D=40, H=512, A=41, R=5, mode=2, lr=5e-4, seed=20161015, pseed=78,
+                      ratio=0.375, file="sketch_step_cfg2"),
+         "cfg4": dict(T=2000, N=32, D=40, H=1024, A=41, R=5, mode=3, lr=5e-4, seed=20161015, pseed=79,
+                      ratio=0.125, file="sketch_step_cfg4", prec="bf16")}
+STEP = STEPS["cfg1"]
 
 
-def step_params(oracle):
-    s = STEP
-    rnn = [recipe_rnn_params(oracle, 2, s["D"] if c == 0 else 2 * s["H"], s["H"], s["pseed"] + c)
+def step_params(oracle, case="cfg1"):
+    s = STEPS[case]
+    rnn = [recipe_rnn_params(oracle, s["mode"], s["D"] if c == 0 else 2 * s["H"], s["H"], s["pseed"] + c)
            for c in range(s["R"])]
     rng = np.random.default_rng([s["pseed"], 9])
     Wa = (rng.standard_normal((s["A"], 2 * s["H"])) / np.sqrt(2 * s["H"])).astype(np.float32)
@@ -135,6 +144,39 @@ def step_params(oracle):
     return rnn, Wa, ba
 
 
-def step_inputs(kctc):
-    s = STEP
-    return kctc.synth_minibatch(s["seed"], s["T"], s["N"], s["D"], s["A"], 0.125)
+def step_inputs(kctc, case="cfg1"):
+    s = STEPS[case]
+    return kctc.synth_minibatch(s["seed"], s["T"], s["N"], s["D"], s["A"], s["ratio"])
+
+
+# ---- bf16 error model (configs[4]) ---------------------------------------------
+BF16_EPS = 2.0 ** -9  # relative rounding of a bf16 operand: 8 significant bits, half an ulp
+
+
+def bf16_tol(stages, k=3.0):
+    """Norm-wise relative tolerance of a result computed through `stages`
+    chained matrix products of bf16-rounded operands with fp32 accumulation.
+    Each operand rounding is uniform in +-2^-9 relative (rms 2^-9/sqrt(3)), so
+    a product of two rounded operands carries rms sqrt(2/3) 2^-9; a K-term
+    fp32 sum of such products keeps that norm-wise (independent errors: both
+    the error and the sum grow like sqrt(K); the fp32 accumulation adds
+    ~sqrt(K) 2^-24, negligible); errors of chained stages add in quadrature.
+    k = 3 standard deviations."""
+    return k * np.sqrt(stages) * np.sqrt(2.0 / 3.0) * BF16_EPS
+
+
+def layer_stages(what, layers=1):
+    """bf16 product stages behind the outputs of `layers` stacked layers:
+    y = (x W) then (h R) per step and layer; dx and dW add, per layer, the
+    backward recurrence's dGates R^T and the dx / dW GEMM."""
+    return {"y": 2 * layers, "dx": 4 * layers, "dw": 4 * layers}[what]
+
+
+def step_stages(R, what, c=0):
+    """bf16 product stages behind a whole train step's outputs (R stacked
+    layers, 2 stages each forward): the logits and the costs see the forward
+    path (2R); component c's gradient (0 = bottom) also the backward through
+    the R-1-c layers above it (2 each) and its own dW GEMM (2)."""
+    if what in ("logits", "costs", "affine"):
+        return 2 * R
+    return 2 * R + 2 * (R - 1 - c) + 2

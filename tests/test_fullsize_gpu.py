@@ -32,7 +32,8 @@ def test_layer_full_length_matches_oracle(kctc, gpu, oracle, case):
     bf16 = c.get("prec") == "bf16"
     if bf16:
         r.set_precision("bf16")
-    tol = 1e-2 if bf16 else TOL  # bf16 operands (configs[4]): 2^-9 rounding, fp32 accumulation
+    # bf16 operands (configs[4]): the error model of sketch_common.bf16_tol
+    tols = {w: S.bf16_tol(S.layer_stages(w)) if bf16 else TOL for w in ("y", "dx", "dw")}
     ws_b, res_b = r.sizes(T, N)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
     wd, xd, dyd = t(w), t(x), t(dy)
@@ -48,9 +49,9 @@ def test_layer_full_length_matches_oracle(kctc, gpu, oracle, case):
     assert r.device_status() == 0
     y, dx, dw = y.cpu().numpy(), dx.cpu().numpy(), dw.cpu().numpy()
     seed = c["seed"]
-    errs = {"y": S.compare(y, S.load(g, f"{case}.y"), seed, tol),
-            "dx": S.compare(dx, S.load(g, f"{case}.dx"), seed + 1, tol),
-            "dw": S.compare(dw, S.load(g, f"{case}.dw"), seed + 2, tol)}
+    errs = {"y": S.compare(y, S.load(g, f"{case}.y"), seed, tols["y"]),
+            "dx": S.compare(dx, S.load(g, f"{case}.dx"), seed + 1, tols["dx"]),
+            "dw": S.compare(dw, S.load(g, f"{case}.dw"), seed + 2, tols["dw"])}
     print(case, {k: {kk: f"{vv:.2e}" for kk, vv in v.items() if kk != "ok"} for k, v in errs.items()})
     for k, e in errs.items():
         assert e["ok"], (k, e)
@@ -62,7 +63,7 @@ def test_layer_full_length_matches_oracle(kctc, gpu, oracle, case):
                 off, (h, cc) = r.lin_offset(pl, lin, isb)
                 regs.append(np.linalg.norm(dw[off:off + h * cc].astype(np.float64)))
     ref = g[f"{case}.dw_region_norms"]
-    np.testing.assert_allclose(regs, ref, rtol=tol)
+    np.testing.assert_allclose(regs, ref, rtol=tols["dw"])
     # t = 0 of the forward direction depends on x[0] only: element-wise; in bf16
     # the projection over D = 2048 terms of ~0.02 * 0.8 carries ~sqrt(D) 2^-9
     # of that scale per element (~1.5e-3 rms)
@@ -70,15 +71,24 @@ def test_layer_full_length_matches_oracle(kctc, gpu, oracle, case):
                                atol=1e-6 if not bf16 else 8e-3)
 
 
-def test_train_step_full_size_matches_oracle(kctc, gpu, oracle):
+@pytest.mark.parametrize("case", sorted(S.STEPS))
+def test_train_step_full_size_matches_oracle(kctc, gpu, oracle, case):
+    """One whole train step per BASELINE config at full size: configs[1]
+    (5 x BLSTM-512, N=16, T=2000), configs[2] (N=64, T=667) at the fp32 bar,
+    configs[4] (5 x BGRU-1024 bf16, N=32, T=2000) at the bf16 error model's
+    tolerance per output (sketch_common.bf16_tol / step_stages)."""
     import torch
-    g = golden("sketch_step")
-    s = S.STEP
+    s = S.STEPS[case]
+    g = golden(s["file"])
     T, N, D, H, A, R = s["T"], s["N"], s["D"], s["H"], s["A"], s["R"]
-    rnn, Wa, ba = S.step_params(oracle)
-    feats, nf, fl, ll = S.step_inputs(kctc)
+    bf16 = s.get("prec") == "bf16"
+    tol = (lambda what, c=0: S.bf16_tol(S.step_stages(R, what, c))) if bf16 else (lambda what, c=0: TOL)
+    rnn, Wa, ba = S.step_params(oracle, case)
+    feats, nf, fl, ll = S.step_inputs(kctc, case)
     net = kctc.Nnet(kctc.recipe_config(num_rnn=R, input_dim=D, hidden=H, num_targets=A, learning_rate=s["lr"],
-                                       max_seq_length=T), seed=1)
+                                       max_seq_length=T, rnn_mode=s["mode"]), seed=1)
+    if bf16:
+        net.set_precision("bf16")
     rnn_idx = [1 + 2 * c for c in range(R)]
     aff_idx = 2 * R + 1
     for c, i in enumerate(rnn_idx):
@@ -87,11 +97,12 @@ def test_train_step_full_size_matches_oracle(kctc, gpu, oracle):
     net.srand(0)
     objf, acc, wt = net.train_step(torch.from_numpy(feats).to(gpu), T, N, nf, fl, ll)
     costs = net.last_costs(N)
-    np.testing.assert_allclose(costs, g["costs"], rtol=TOL)
-    np.testing.assert_allclose(objf, float(g["tot_objf"]), rtol=TOL)
+    print(case, "max cost rel err %.2e" % float(np.max(np.abs(costs - g["costs"]) / np.abs(g["costs"]))))
+    np.testing.assert_allclose(costs, g["costs"], rtol=tol("costs"))
+    np.testing.assert_allclose(objf, float(g["tot_objf"]), rtol=tol("costs"))
     assert wt == float(g["tot_weight"])
     logits = net.last_output(T, N, A)
-    e = S.compare(logits, S.load(g, "logits"), 500, TOL)
+    e = S.compare(logits, S.load(g, "logits"), 500, tol("logits"))
     assert e["ok"], ("logits", e)
     # best path: bit-exact on the GPU's own output; vs the fp64 output only
     # near-ties may flip
@@ -99,15 +110,15 @@ def test_train_step_full_size_matches_oracle(kctc, gpu, oracle):
     np.testing.assert_array_equal(ids, oracle.find_row_max_id(logits))
     assert acc == oracle.accuracy(ids, T, N, nf, fl, ll)[0]
     flips = int(np.sum(ids != g["ids"]))
-    assert flips <= 1e-3 * ids.size, flips
+    assert flips <= (2e-2 if bf16 else 1e-3) * ids.size, flips
     # the applied gradients (the fp32 parameters cannot carry an lr-scaled
     # update exactly: compare the gradient the update used, +-5 clipped for
     # the RNNs, against the oracle's fp64 (W_after - W_before) / lr)
     report = {}
     for c, i in enumerate(rnn_idx):
         gc = np.clip(net.get_grad(i).astype(np.float64), -5.0, 5.0)
-        report[f"rnn{c}"] = S.compare(gc, S.load(g, f"g{c}"), 600 + c, TOL)
-    report["affine"] = S.compare(net.get_grad(aff_idx).astype(np.float64), S.load(g, "gaff"), 700, TOL)
+        report[f"rnn{c}"] = S.compare(gc, S.load(g, f"g{c}"), 600 + c, tol("grad", c))
+    report["affine"] = S.compare(net.get_grad(aff_idx).astype(np.float64), S.load(g, "gaff"), 700, tol("affine"))
     print({k: {kk: f"{vv:.2e}" for kk, vv in v.items() if kk != "ok"} for k, v in report.items()},
           "flips", flips)
     for k, e in report.items():

@@ -139,7 +139,9 @@ def test_train_step_row_groups_match_oracle(kctc, gpu, oracle, mode, H, T, N):
 def test_train_step_bf16_matches_oracle(kctc, gpu, oracle, mode, H, T, N):
     """kctc_nnet_set_precision(1): bf16 recurrences and gate GEMMs, fp32
     master weights, affine / CTC / updates in fp32 (configs[4]).  Tolerance
-    for bf16 operands: objective 1e-3 relative, updates 5e-2 norm-wise."""
+    for bf16 operands: objective 1e-3 relative (measured ~1e-4); every
+    component's update at the error model's bound for its stages
+    (sketch_common.bf16_tol / step_stages)."""
     import torch
     R, D, A, lr = 2, 40, 41, 0.02
     cfg = kctc.recipe_config(num_rnn=R, input_dim=D, hidden=H, num_targets=A, rnn_mode=mode,
@@ -161,10 +163,12 @@ def test_train_step_bf16_matches_oracle(kctc, gpu, oracle, mode, H, T, N):
     assert wt == rwt
     ids = net.last_best_path(T, N)
     np.testing.assert_array_equal(ids, oracle.find_row_max_id(net.last_output(T, N, A)))
-    for c, p, q in zip(upd, params, p0):
+    import sketch_common as S
+    for k, (c, p, q) in enumerate(zip(upd, params, p0)):
         e = rel_err(net.get_params(c).astype(np.float64) - q, p - q)
-        print(c, f"{e:.2e}")
-        assert e < 5e-2, (c, e)
+        bound = S.bf16_tol(S.step_stages(R, "affine" if k == R else "grad", k))
+        print(c, f"{e:.2e} (bound {bound:.2e})")
+        assert e < bound, (c, e, bound)
 
 
 def test_train_loss_decreases_and_objf_only(kctc, gpu):
@@ -389,3 +393,45 @@ def test_async_steps_equal_sync_steps(kctc, gpu):
     for c in range(a.num_components):
         if a.num_params(c):
             np.testing.assert_array_equal(a.get_params(c), b.get_params(c))
+
+
+def test_multistep_trajectory_matches_oracle(kctc, gpu, oracle):
+    """bench.py's objf-per-label trajectory swings by 10-100x from step to
+    step (16.7 -> 1111 -> 336 -> ... at configs[1]).  That is the reference's
+    own SGD on the synthetic data: the minibatch gradient is a SUM over all
+    frames (6,400 here, 30,000 at configs[1]) at lr 5e-4, the affine update is
+    not clipped, so the first steps over-shoot.  The fp64 oracle (the same
+    recipe init, lr, clipping and self-repair semantics) follows the same
+    trajectory: here 20.9 -> 48.7 -> 37.8 -> 9.2 per label, and the GPU
+    matches it step by step."""
+    import torch
+    R, H, T, N, D, A, lr, steps = 2, 64, 400, 16, 40, 41, 5e-4, 4
+    import sketch_common as S
+    rnn = [S.recipe_rnn_params(oracle, 2, D if c == 0 else 2 * H, H, 77 + c) for c in range(R)]
+    rng = np.random.default_rng([77, 9])
+    Wa = (rng.standard_normal((A, 2 * H)) / np.sqrt(2 * H)).astype(np.float32)
+    ba = rng.standard_normal(A).astype(np.float32)
+    cfg = kctc.recipe_config(num_rnn=R, input_dim=D, hidden=H, num_targets=A, learning_rate=lr)
+    net = kctc.Nnet(cfg, seed=1)
+    for c in range(R):
+        net.set_params(1 + 2 * c, rnn[c])
+    net.set_params(2 * R + 1, np.concatenate([Wa.ravel(), ba]))
+    net.srand(0)
+    spec = _oracle_spec(oracle, R, 2, H, 2, D, A, 30.0, lr)
+    rp = [p.astype(np.float64) for p in rnn]
+    Wd, bd = Wa.astype(np.float64), ba.astype(np.float64)
+    cnc, cc = np.zeros(R), np.zeros(R)
+    draws = glibc_rand_uniforms(0, steps * R)
+    got, ref = [], []
+    for step in range(steps):
+        feats, nf, fl, ll = kctc.synth_minibatch(20161015 + step, T, N, D, A, 0.125)
+        o, _, w = net.train_step(torch.from_numpy(feats).to(gpu), T, N, nf, fl, ll)
+        d = np.array(draws[step * R:(step + 1) * R][::-1], np.float32)  # top clip component draws first
+        ro, _, rw = oracle.train_step(spec, rp, Wd, bd, feats.reshape(T, N, D).astype(np.float64), nf, fl, ll,
+                                      repair_draws=d, clip_num_clipped=cnc, clip_count=cc)
+        assert w == rw
+        got.append(o / w)
+        ref.append(ro / rw)
+    print("gpu", [round(x, 4) for x in got], "oracle fp64", [round(x, 4) for x in ref])
+    np.testing.assert_allclose(got, ref, rtol=1e-4)
+    assert max(ref) > 2 * ref[0]  # the over-shooting first steps
