@@ -63,6 +63,7 @@ struct PParams {
   int dbg;                 // KCTC_STREAM_DBG diagnostics: 1 no combine wait, 2 wait for both directions, 4 no combine,
                            // 32 register-A k loop without the two-deep prefetch
   unsigned *serr;          // producer's error word (wait timeout)
+  int p256v;               // 256-tile k loop: 2 DMA spread over the MFMAs (default), 1 DMA block per stage
   // backward stream (x3p_bwd_stream_kernel)
   const float *E;          // source rows of direction d: E + row * lde + d * edoff (KB * 32 floats)
   long lde, edoff;
@@ -736,6 +737,84 @@ __device__ __forceinline__ void issue_tile256(const _Float16 *__restrict__ P, in
   }
 }
 
+// one row block (16 rows of the wave's 128) of a k block: 4 (bf16: 2 x 4)
+// or 12 (split-fp16) MFMAs against the wave's B fragments
+template <bool BFM>
+__device__ __forceinline__ void p256_row(floatx4 (&acc)[4], halfx8 ah, halfx8 al, const halfx8 (&bh)[4],
+                                         const halfx8 (&bl)[4]) {
+  if constexpr (BFM) {
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ah), __builtin_bit_cast(bf16x8, bh[j]),
+                                                       acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al), __builtin_bit_cast(bf16x8, bl[j]),
+                                                       acc[j], 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; j++) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[j], acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; j++) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[j], acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; j++) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acc[j], 0, 0, 0);
+  }
+}
+
+// k loop with the next stage's LDS-DMA spread over the MFMAs: the wave's 8
+// pieces (4 of A, 4 of B) are issued two per row block over the first four of
+// its eight row blocks, between the MFMAs,
+// instead of as one block of address arithmetic + m0 writes at the top of the
+// iteration (where both waves of a SIMD issued them at once, right after the
+// barrier, with no matrix work to hide behind).  Source pointers are computed
+// once per tile; the loads of the last iteration re-read the last k block
+// (clamped) so the body is straight-line.  KCTC_P256=1: the previous loop.
+template <bool BFM>
+__device__ __forceinline__ void p256_kloop_spread(const _Float16 *A, const _Float16 *B, int M, int N, int KB, int m0,
+                                                  int n0, int kb0, int nk, unsigned char *lds, int wm, int wn, int fr,
+                                                  int fq, floatx4 (&acc)[8][4]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const _Float16 *src[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int q = w * 4 + (i & 3);
+    const int r = q * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (r & 7);
+    const int gr = i < 4 ? min(m0 + r, M - 1) : min(n0 + r, N - 1);
+    src[i] = (i < 4 ? A : B) + ((long)gr * KB + kb0) * 64 + c * 8;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    __builtin_amdgcn_global_load_lds(src[i], lds + (i < 4 ? 0 : TILEB2) + (w * 4 + (i & 3)) * 1024, 16, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int it = 0; it < nk; it++) {
+    unsigned char *cur = lds + (it & 1) * 2 * TILEB2;
+    unsigned char *nxt = lds + ((it + 1) & 1) * 2 * TILEB2;
+    const long adv = (long)min(it + 1, nk - 1) * 64;
+    halfx8 bh[4], bl[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      bh[j] = frag(cur + TILEB2, wn + j * 16 + fr, fq);
+      bl[j] = frag(cur + TILEB2, wn + j * 16 + fr, 4 + fq);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      if (i < 4) {  // two pieces per row block of the first half: the last lands behind half the MFMAs
+#pragma unroll
+        for (int h = 2 * i; h < 2 * i + 2; h++)
+          __builtin_amdgcn_global_load_lds(src[h] + adv, nxt + (h < 4 ? 0 : TILEB2) + (w * 4 + (h & 3)) * 1024, 16, 0,
+                                           0);
+      }
+      const halfx8 ah = frag(cur, wm + i * 16 + fr, fq);
+      const halfx8 al = frag(cur, wm + i * 16 + fr, 4 + fq);
+      p256_row<BFM>(acc[i], ah, al, bh, bl);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+}
+
 template <bool BFM>
 __device__ __forceinline__ void p256_tile(const PParams &p, unsigned char *lds, int tm, int tn, int b, int ks) {
   const _Float16 *A = p.A + (long)b * p.sA;
@@ -751,6 +830,9 @@ __device__ __forceinline__ void p256_tile(const PParams &p, unsigned char *lds, 
   for (int i = 0; i < 8; i++)
 #pragma unroll
     for (int j = 0; j < 4; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (p.p256v == 2) {
+    if (nk > 0) p256_kloop_spread<BFM>(A, B, p.M, p.N, p.KB, m0, n0, kb0, nk, lds, wm, wn, fr, fq, acc);
+  } else {
   if (nk > 0) {
     issue_tile256(A, p.M, m0, p.KB, kb0, lds);
     issue_tile256(B, p.N, n0, p.KB, kb0, lds + TILEB2);
@@ -794,6 +876,7 @@ __device__ __forceinline__ void p256_tile(const PParams &p, unsigned char *lds, 
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  }
   }
   // epilogue: acc[i][j][r] -> C[m0+wm+16i+4fq+r][n0+wn+16j+fr], times 2^-(eA + eB)
   const int *eA = p.eA ? p.eA + (long)b * p.seA : nullptr;
@@ -1292,6 +1375,8 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
   p.sdir = 0;
   p.arrive = nullptr;
   p.dbg = getenv("KCTC_STREAM_DBG") ? atoi(getenv("KCTC_STREAM_DBG")) : 0;
+  static const int p256v = getenv("KCTC_P256") ? atoi(getenv("KCTC_P256")) : 2;
+  p.p256v = p256v;
   if (g.stream_flags && g.stream_arrive && g.stream_part && g.KB % 2 == 0 && (long)g.M * g.ldc * 4 + (long)(g.batch - 1) * g.sC * 4 < (1L << 31)) {
     p.sdir = 1;
     p.kbchunk = g.KB / 2;  // the producer's two directions

@@ -1,31 +1,44 @@
 // rnn.hip -- cuDNN-v5 compatible LSTM / GRU / RELU / TANH layers for gfx950.
 //
-// Forward (per stacked layer):
-//   1. G = x W^T + bW (+ bR for LSTM/RNN)      one batched fp32 MFMA GEMM for both
-//      directions (gemm.hip): the input projection of all T*N frames at once.
-//   2. rnn_fwd_rec<MODE>: ONE persistent launch runs the whole time recurrence of
-//      both directions.  Workgroup (dir, g) owns hidden units [g*U, g*U+U): its
-//      slice of R (nW*U rows x H, fp32) is loaded into LDS once, its cell
-//      state stays in registers for all T steps.  Per step it multiplies
-//      h_{t-1} [N x H] by the slice on the matrix cores (v_mfma_f32_16x16x4_f32,
-//      K split over the 4 waves, reduced through LDS), applies the gate
-//      nonlinearities and publishes its U columns of h_t.
-//      Inter-workgroup hand-off: the layer output y (= the h exchange buffer)
-//      is pre-filled with a NaN sentinel; h_t is published with write-through
-//      (sc1) 4-byte stores and consumers read h_{t-1} straight into MFMA
-//      A-operand registers with sc1 16-byte buffer loads, re-polling any
-//      fragment that still holds the sentinel (data-as-flag: no barrier, no
-//      flag word; each 4-byte store is a granule; MI355X_MICROARCH.md §R2).
-//      Spins are bounded; a timeout sets a device error word and every
-//      workgroup drains out.
-// Backward data: rnn_bwd_rec<MODE>, the mirror image: workgroup (dir, g) owns
-//   units [g*U, g*U+U) and keeps R^T's U rows (U x nW*H) in LDS; per step it
-//   polls dGates_{t+1} (all nW*H columns) from a sentinel-filled exchange
-//   buffer E, forms dh = dy + dGates_{t+1} R on the matrix cores, does the
-//   pointwise cell backward (dc carried in registers) and publishes its
-//   dGates_t columns.  E is kept in the reserve for backward-weights.
-// Backward weights: dW += dGx^T x, dR += dGh^T h_prev (time-shifted views of E
-//   and y; batched over directions), bias sums accumulated by the recurrence.
+// Replaces cudnnRNNForwardTraining / BackwardData / BackwardWeights as the
+// reference calls them (src/cudamatrix/cudnn-recurrent.cc:13-102 through
+// src/nnet2/nnet-cudnn-component.cc:508-614).  Per stacked layer:
+//
+// Forward
+//   1. G = x W^T + bW (+ bR): the input projection of all T*N frames of both
+//      directions as one packed split-fp16 GEMM (gemm_x3p.hip) -- or, for the
+//      layers above the first, streamed off the previous component's running
+//      recurrence (launch_chain_proj).
+//   2. rnn_fwd_rec6: ONE persistent launch runs the whole time recurrence of
+//      both directions (and of every row group of 8 or 16 sequences).  Work-
+//      group (group, dir, g) owns hidden units [g*U, g*U+U); its slice of R
+//      (nW*U gate rows x H) is held for the whole launch in REGISTERS as
+//      split-fp16 MFMA B fragments (bf16 in configs[4]'s precision).  Per step
+//      it loads h_{t-1} of its direction as fp16 hi/lo A fragments (sc1
+//      buffer loads of the step's exchange image), multiplies on
+//      v_mfma_f32_16x16x32_f16 (K split over the waves, reduced through LDS in
+//      a fixed order), applies the gates (cell state in registers) and
+//      publishes its U units of h_t as hi/lo fp16 with sc1 16-B stores.
+// Backward data
+//   rnn_bwd_rec6, reduce-scatter form: per step a workgroup sums the partial
+//   dh of its own units from the direction's H/U producers (fixed order), adds
+//   dy, does the pointwise cell backward (dc in registers), multiplies its
+//   dGates by its R rows (registers) and publishes the partial dh of ALL H
+//   units (MFMA C-fragment layout).  dGates rows go to the reserve, from where
+//   the dx GEMM of the layer below is streamed while the recurrence runs
+//   (x3p_bwd_stream_kernel).
+// Backward weights
+//   dW += dGx^T x, dR += dGh^T h_prev (time-shifted views), packed split-fp16
+//   GEMMs on a side stream beside the next component's backward recurrence;
+//   bias sums accumulated by the recurrence.
+// Hand-off protocol (both recurrences): payload sc1 stores -> every storing
+// wave's s_waitcnt vmcnt(0) -> workgroup barrier -> lane 0 stores the step
+// epoch into the workgroup's own 128-B flag line; consumers poll the flag
+// lines of their producers, then sc1 loads (MI355X_MICROARCH.md "Valid forms",
+// row 1).  Every spin is bounded (3 s); a timeout sets the device error word,
+// every workgroup drains out and the train step fails loudly.
+// v4 (fp32 MFMA, XCD-slot all-gather) and v3 remain for the shapes v6 does
+// not compile (RELU / TANH, other H, N > 64).
 //
 // Semantics follow cuDNN v5 as used by CuDNNRecurrentComponent: hx = cx = 0,
 // dhy = dcy = 0 (SetBufferZero, nnet-cudnn-component.cc:494-506), all N
