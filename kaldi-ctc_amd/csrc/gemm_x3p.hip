@@ -63,7 +63,7 @@ struct PParams {
   int dbg;                 // KCTC_STREAM_DBG diagnostics: 1 no combine wait, 2 wait for both directions, 4 no combine,
                            // 32 register-A k loop without the two-deep prefetch
   unsigned *serr;          // producer's error word (wait timeout)
-  int p256v;               // 256-tile k loop: 2 DMA spread over the MFMAs (default), 1 DMA block per stage
+  int p256v;               // 256-tile k loop (KCTC_P256): 2 DMA spread over the MFMAs, 1 DMA block per stage, 0 auto
   // backward stream (x3p_bwd_stream_kernel)
   const float *E;          // source rows of direction d: E + row * lde + d * edoff (KB * 32 floats)
   long lde, edoff;
@@ -830,7 +830,11 @@ __device__ __forceinline__ void p256_tile(const PParams &p, unsigned char *lds, 
   for (int i = 0; i < 8; i++)
 #pragma unroll
     for (int j = 0; j < 4; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  if (p.p256v == 2) {
+  // default: the spread loop for split-fp16 (measured +4..10 %: dW 0.476 ->
+  // 0.50-0.52, 8192^3 0.527 -> 0.555 of the f16 issue rate), the block loop
+  // for bf16 (equal or 1-3 % faster there: fewer MFMAs per stage to hide the
+  // DMA issue behind)
+  if (p.p256v == 2 || (p.p256v == 0 && !BFM)) {
     if (nk > 0) p256_kloop_spread<BFM>(A, B, p.M, p.N, p.KB, m0, n0, kb0, nk, lds, wm, wn, fr, fq, acc);
   } else {
   if (nk > 0) {
@@ -1375,7 +1379,7 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
   p.sdir = 0;
   p.arrive = nullptr;
   p.dbg = getenv("KCTC_STREAM_DBG") ? atoi(getenv("KCTC_STREAM_DBG")) : 0;
-  static const int p256v = getenv("KCTC_P256") ? atoi(getenv("KCTC_P256")) : 2;
+  static const int p256v = getenv("KCTC_P256") ? atoi(getenv("KCTC_P256")) : 0;
   p.p256v = p256v;
   if (g.stream_flags && g.stream_arrive && g.stream_part && g.KB % 2 == 0 && (long)g.M * g.ldc * 4 + (long)(g.batch - 1) * g.sC * 4 < (1L << 31)) {
     p.sdir = 1;
