@@ -151,32 +151,45 @@ def step_inputs(kctc, case="cfg1"):
 
 # ---- bf16 error model (configs[4]) ---------------------------------------------
 BF16_EPS = 2.0 ** -9  # relative rounding of a bf16 operand: 8 significant bits, half an ulp
+# variance units of one stage:
+#   a GEMM of bf16-rounded operands (fp32 accumulation)                       1
+#   a recurrence: h (or dh) is re-rounded every step and the earlier steps'
+#   errors are carried forward through the gates, an AR(1) process whose
+#   stationary error is 1/sqrt(1 - lam^2) times one step's; lam ~ 0.87
+#   (update / forget gates ~ 0.5 plus the R h feedback at the recipe init)
+#   gives a factor 2, i.e. 4 variance units                                  4
+GEMM, REC = 1, 4
 
 
-def bf16_tol(stages, k=3.0):
-    """Norm-wise relative tolerance of a result computed through `stages`
-    chained matrix products of bf16-rounded operands with fp32 accumulation.
-    Each operand rounding is uniform in +-2^-9 relative (rms 2^-9/sqrt(3)), so
-    a product of two rounded operands carries rms sqrt(2/3) 2^-9; a K-term
-    fp32 sum of such products keeps that norm-wise (independent errors: both
-    the error and the sum grow like sqrt(K); the fp32 accumulation adds
-    ~sqrt(K) 2^-24, negligible); errors of chained stages add in quadrature.
-    k = 3 standard deviations."""
-    return k * np.sqrt(stages) * np.sqrt(2.0 / 3.0) * BF16_EPS
+def bf16_tol(units, k=3.0):
+    """Tolerance on the sketch error (tests/sketch_common.compare: the max of
+    4 random projections of the difference, each ~ N(0, |a - b|^2)) of a
+    result computed through stages of bf16-rounded products with fp32
+    accumulation.  Each operand rounding is uniform in +-2^-9 relative (rms
+    2^-9/sqrt(3)), so a product of two rounded operands carries rms
+    sqrt(2/3) 2^-9, and a K-term fp32 sum of such products keeps that
+    norm-wise (independent errors: both the error and the sum grow like
+    sqrt(K); the fp32 accumulation adds ~sqrt(K) 2^-24, negligible).  Chained
+    stages add in quadrature (`units` variance units, see GEMM / REC), which
+    gives the expected norm-wise relative error; k = 3 covers the projection
+    estimator (P(max of 4 |N(0,1)| > 3) ~ 1 %)."""
+    return k * np.sqrt(units) * np.sqrt(2.0 / 3.0) * BF16_EPS
 
 
 def layer_stages(what, layers=1):
-    """bf16 product stages behind the outputs of `layers` stacked layers:
-    y = (x W) then (h R) per step and layer; dx and dW add, per layer, the
-    backward recurrence's dGates R^T and the dx / dW GEMM."""
-    return {"y": 2 * layers, "dx": 4 * layers, "dw": 4 * layers}[what]
+    """Variance units behind the outputs of `layers` stacked layers: forward
+    x W then the recurrence per layer; dx adds, per layer, the backward
+    recurrence and the dx GEMM; dW the backward recurrence and its GEMM."""
+    fwd = (GEMM + REC) * layers
+    return {"y": fwd, "dx": fwd + (REC + GEMM) * layers, "dw": fwd + (REC + GEMM) * layers}[what]
 
 
 def step_stages(R, what, c=0):
-    """bf16 product stages behind a whole train step's outputs (R stacked
-    layers, 2 stages each forward): the logits and the costs see the forward
-    path (2R); component c's gradient (0 = bottom) also the backward through
-    the R-1-c layers above it (2 each) and its own dW GEMM (2)."""
+    """Variance units behind a whole train step's outputs (R stacked layers):
+    the logits and the costs see the forward path; component c's gradient (0
+    = bottom) also the backward (recurrence + dx GEMM) of the R-1-c layers
+    above it, its own backward recurrence and its dW GEMM."""
+    fwd = (GEMM + REC) * R
     if what in ("logits", "costs", "affine"):
-        return 2 * R
-    return 2 * R + 2 * (R - 1 - c) + 2
+        return fwd
+    return fwd + (REC + GEMM) * (R - 1 - c) + REC + GEMM
