@@ -76,6 +76,9 @@ int kctc_egs_reader_close(kctcEgsReader_t r);
 
 /* --- a minibatch --- */
 int kctc_minibatch_info(kctcMinibatch_t mb, int *N, int *T_max, int *input_dim, long *total_labels);
+/* rows per output frame of the formatted input: 1 + the nnet left + right
+ * context the reader was opened with (FormatNnetInput's num_splice) */
+int kctc_minibatch_num_splice(kctcMinibatch_t mb);
 /* num_frames[N], label_lengths[N], flat_labels[total_labels] (host) */
 int kctc_minibatch_labels(kctcMinibatch_t mb, int *num_frames, int *label_lengths, int *flat_labels);
 /* key of example n (pointer valid until kctc_minibatch_free) */

@@ -46,6 +46,13 @@ const char *kctc_last_error(void);
 int kctc_nnet_create(kctcNnet_t *nnet, const char *config, unsigned long long seed, int device);
 int kctc_nnet_destroy(kctcNnet_t nnet);
 int kctc_nnet_num_components(kctcNnet_t nnet);
+/* Nnet::LeftContext / RightContext (src/nnet2/nnet-nnet.cc:52-73).  The
+ * network input of a minibatch is FormatNnetInput's layout for num_splice =
+ * 1 + left + right: [T_max*N*num_splice][input_dim], row (t*N+n)*num_splice+s
+ * = frame t+s of utterance n (src/ctc/ctc-nnet-update.cc:351-424); the
+ * train/objf calls take T_max = output frames and num_frames = the CTC input
+ * lengths (NumFrames - left_context - right context, :187-195). */
+int kctc_nnet_context(kctcNnet_t nnet, int *left, int *right);
 /* writes "<Type> dim info" of component c into buf */
 int kctc_nnet_component_info(kctcNnet_t nnet, int c, char *buf, size_t buflen);
 long kctc_nnet_num_params(kctcNnet_t nnet, int c);

@@ -288,13 +288,15 @@ def _tcheck(st, where):
 
 def recipe_config(num_rnn=5, input_dim=40, hidden=512, num_targets=41, rnn_mode=2, bidirectional=True,
                   learning_rate=5e-4, max_seq_length=2000, clipping_threshold=30.0, param_stddev=0.02,
-                  bias_stddev=0.2, num_layers=1, norm_based_clipping=True):
+                  bias_stddev=0.2, num_layers=1, norm_based_clipping=True, splice_context=(0,)):
     """Component config lines of the CTC recipe, as written by
     egs/wsj/s5/steps/ctc/nnet2/components.py:73-102 (AddRnnLayer ->
     CuDNNRecurrentComponent + ClipGradientComponent) and an output
-    AffineComponent; Splice with context 0 first (make_configs.py)."""
-    lines = [f"SpliceComponent input-dim={input_dim} context=0"]
-    dim = input_dim
+    AffineComponent; Splice first (make_configs.py: context 0; any sorted
+    offsets containing <= 0 and >= 0 values splice frames)."""
+    ctx = [int(c) for c in splice_context]
+    lines = [f"SpliceComponent input-dim={input_dim} context={':'.join(map(str, ctx))}"]
+    dim = input_dim * len(ctx)
     out = hidden * (2 if bidirectional else 1)
     for _ in range(num_rnn):
         lines.append(f"CuDNNRecurrentComponent input-dim={dim} output-dim={hidden} "
@@ -434,6 +436,14 @@ class Nnet:
         _tcheck(fn(self.h, _ptr(feats), T, N, nf.ctypes.data, fl.ctypes.data, ll.ctypes.data,
                    ctypes.byref(o), ctypes.byref(a), ctypes.byref(w)), fn.__name__)
         return o.value, a.value, w.value
+
+    @property
+    def context(self):
+        """(left, right) context of the network (kctc_nnet_context); the input
+        of a minibatch has (1 + left + right) rows per output frame."""
+        l, r = ctypes.c_int(), ctypes.c_int()
+        _tcheck(lib().kctc_nnet_context(self.h, ctypes.byref(l), ctypes.byref(r)), "context")
+        return l.value, r.value
 
     def train_step(self, feats, T, N, num_frames, flat_labels, label_lengths):
         """DoBackprop on one minibatch; feats: device [T*N, D]. -> (objf, accuracy, weight)"""
@@ -733,6 +743,7 @@ class Minibatch:
         _tcheck(L.kctc_minibatch_info(handle, ctypes.byref(N), ctypes.byref(T), ctypes.byref(D), ctypes.byref(tl)),
                 "kctc_minibatch_info")
         self.N, self.T_max, self.input_dim, self.total_labels = N.value, T.value, D.value, tl.value
+        self.num_splice = L.kctc_minibatch_num_splice(handle)  # rows per output frame of the formatted input
         self.num_frames = np.zeros(self.N, dtype=np.int32)
         self.label_lengths = np.zeros(self.N, dtype=np.int32)
         self.flat_labels = np.zeros(max(self.total_labels, 1), dtype=np.int32)
@@ -745,7 +756,7 @@ class Minibatch:
         return int(lib().kctc_minibatch_scratch_bytes(self._h))
 
     def format(self, out, scratch, stream=None):
-        """Stream-ordered FormatNnetInput on the GPU into out [T_max*N, input_dim] (device)."""
+        """Stream-ordered FormatNnetInput on the GPU into out [T_max*N*num_splice, input_dim] (device)."""
         _tcheck(lib().kctc_minibatch_format(self._h, _ptr(out), _ptr(scratch), int(scratch.numel()),
                                             ctypes.c_void_p(_stream_handle(stream))), "kctc_minibatch_format")
 

@@ -374,7 +374,8 @@ std::unique_ptr<Minibatch> pack_minibatch(std::vector<Example> &egs, int nnet_le
   if (egs.empty()) return nullptr;
   auto mb = std::make_unique<Minibatch>();
   const int num_splice = 1 + nnet_left + nnet_right;
-  if (num_splice != 1) throw std::invalid_argument("FormatNnetInput: only num_splice = 1 (context 0) is supported");
+  if (nnet_left < 0 || nnet_right < 0) throw std::invalid_argument("FormatNnetInput: negative context");
+  mb->num_splice = num_splice;
   const Example &e0 = egs[0];
   if (e0.NumFrames() < num_splice) throw std::invalid_argument("FormatNnetInput: example shorter than the splice");
   mb->feat_dim = e0.NumCols();

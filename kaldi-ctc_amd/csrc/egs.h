@@ -101,6 +101,7 @@ struct Minibatch {
   std::vector<std::string> keys;
   std::vector<int32_t> num_frames, label_lengths, labels;
   int N = 0, T_max = 0, feat_dim = 0, spk_dim = 0;
+  int num_splice = 1;  // 1 + nnet left + right context: rows per output frame of the formatted input
   std::vector<uint8_t> blob;
   hipEvent_t done = nullptr;  // recorded after the last use of `blob` by a copy
   ~Minibatch();

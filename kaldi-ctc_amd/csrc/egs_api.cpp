@@ -152,6 +152,8 @@ int kctc_minibatch_info(kctcMinibatch_t m, int *N, int *T_max, int *input_dim, l
   });
 }
 
+int kctc_minibatch_num_splice(kctcMinibatch_t m) { return m && m->mb ? m->mb->num_splice : -1; }
+
 int kctc_minibatch_labels(kctcMinibatch_t m, int *num_frames, int *label_lengths, int *flat_labels) {
   return guarded([&] {
     KCTC_REQUIRE(m && m->mb, "kctc_minibatch_labels: bad minibatch");

@@ -1,6 +1,8 @@
 // egs_format.hip -- FormatNnetInput on the GPU: CompressedMatrix decode of
 // every example of a minibatch straight into the time-major network input
-// [T_max*N][feat_dim + spk_dim] (row t*N+n, zero rows for t >= T_n).
+// [T_max*N*num_splice][feat_dim + spk_dim]: row (t*N+n)*num_splice + s holds
+// input frame first + t + s of example n (num_splice = 1 + the network's left
+// and right context, first = ignore_frames), zero rows for t >= T_n.
 //
 // Reference: FormatNnetInput (src/ctc/ctc-nnet-update.cc:351-424) decodes on
 // the CPU in the background thread (CompressedMatrix::CopyToMat,
@@ -36,13 +38,15 @@ __device__ __forceinline__ float dev_from_u8(float p0, float p25, float p75, flo
 }
 
 __global__ __launch_bounds__(256) void egs_format_kernel(const uint8_t *__restrict__ blob, int N, int T_max,
-                                                         int Df, int Ds, int R, float *__restrict__ out) {
+                                                         int Df, int Ds, int R, int NS, float *__restrict__ out) {
   extern __shared__ float lds[];
   const int n = blockIdx.y, t0 = blockIdx.x * R, tid = threadIdx.x;
   const EgDesc d = reinterpret_cast<const EgDesc *>(blob)[n];
   const int Dt = Df + Ds, LD = Df + 1;
   const int rows_here = min(R, T_max - t0);
-  const int valid = max(0, min(rows_here, d.frames - t0));  // rows of this tile with data
+  // input frames of this tile: the R output frames and their NS - 1 right neighbours
+  const int valid = max(0, min(rows_here + NS - 1, d.frames + NS - 1 - t0));  // tile rows with data
+  const int valid_out = max(0, min(rows_here, d.frames - t0));
   const uint8_t *body = blob + d.off;
   float *pc = lds;              // [4][Df]
   float *tile = lds + 4 * Df;   // [R][LD]
@@ -55,8 +59,9 @@ __global__ __launch_bounds__(256) void egs_format_kernel(const uint8_t *__restri
       }
       __syncthreads();
       const uint8_t *bytes = body + 8 * (long)Df + d.first + t0;
-      for (int idx = tid; idx < Df * R; idx += 256) {
-        const int c = idx / R, j = idx - c * R;
+      const int RI = R + NS - 1;
+      for (int idx = tid; idx < Df * RI; idx += 256) {
+        const int c = idx / RI, j = idx - c * RI;
         if (j < valid)
           tile[j * LD + c] = dev_from_u8(pc[c], pc[Df + c], pc[2 * Df + c], pc[3 * Df + c],
                                          bytes[(long)c * d.rows + j]);
@@ -71,17 +76,18 @@ __global__ __launch_bounds__(256) void egs_format_kernel(const uint8_t *__restri
   }
   __syncthreads();
   const float *spk = d.spk_off >= 0 ? reinterpret_cast<const float *>(blob + d.spk_off) : nullptr;
-  for (int idx = tid; idx < rows_here * Dt; idx += 256) {
-    const int j = idx / Dt, c = idx - j * Dt;
+  for (int idx = tid; idx < rows_here * NS * Dt; idx += 256) {
+    const int js = idx / Dt, c = idx - js * Dt;
+    const int j = js / NS, sp = js - j * NS;
     float v = 0.f;
-    if (j < valid) v = c < Df ? tile[j * LD + c] : spk[c - Df];
-    out[((long)(t0 + j) * N + n) * Dt + c] = v;
+    if (j < valid_out) v = c < Df ? tile[(j + sp) * LD + c] : spk[c - Df];
+    out[(((long)(t0 + j) * N + n) * NS + sp) * Dt + c] = v;
   }
 }
 
-int pick_rows(int Df) {
+int pick_rows(int Df, int NS) {
   int R = 64;
-  while (R > 1 && (size_t)(4 * Df + R * (Df + 1)) * 4 > 64 * 1024) R >>= 1;
+  while (R > 1 && (size_t)(4 * Df + (R + NS - 1) * (Df + 1)) * 4 > 64 * 1024) R >>= 1;
   return R;
 }
 
@@ -97,11 +103,14 @@ void format_on_device(Minibatch &mb, float *out, void *scratch, size_t scratch_b
   if (!mb.done) KCTC_HIP_CHECK(hipEventCreateWithFlags(&mb.done, hipEventDisableTiming));
   KCTC_HIP_CHECK(hipEventRecord(mb.done, stream));
   if (mb.T_max <= 0) return;
-  const int R = pick_rows(mb.feat_dim);
-  const size_t lds = (size_t)(4 * mb.feat_dim + R * (mb.feat_dim + 1)) * 4;
+  const int NS = mb.num_splice;
+  if (NS < 1 || NS > 64) throw std::invalid_argument("format: num_splice out of range");
+  const int R = pick_rows(mb.feat_dim, NS);
+  const size_t lds = (size_t)(4 * mb.feat_dim + (R + NS - 1) * (mb.feat_dim + 1)) * 4;
+  if (lds > 64 * 1024) throw std::invalid_argument("format: feature dim x context too large");
   dim3 grid(ceil_div(mb.T_max, R), mb.N);
   hipLaunchKernelGGL(egs_format_kernel, grid, dim3(256), lds, stream, static_cast<const uint8_t *>(scratch),
-                     mb.N, mb.T_max, mb.feat_dim, mb.spk_dim, R, out);
+                     mb.N, mb.T_max, mb.feat_dim, mb.spk_dim, R, NS, out);
   KCTC_HIP_CHECK(hipGetLastError());
 }
 

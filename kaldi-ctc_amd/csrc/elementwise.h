@@ -26,6 +26,17 @@ void sum_rows(hipStream_t s, const float *X, long rows, int cols, float alpha, f
 void fill(hipStream_t s, float *p, long n, float v);
 void scale_inplace(hipStream_t s, float *p, long n, float alpha);
 
+// SpliceComponent on the FormatNnetInput layout (nnet.h): output row j, block
+// c = input row j * ns + first + ctx[c] (dim - const_dim columns); the last
+// const_dim columns from input row j * ns.  Backward: the transpose (input
+// rows no block reads get zeros; the const part adds to the chunk's first
+// row).  At most kMaxSplice context offsets.
+constexpr int kMaxSplice = 32;
+void splice_rows(hipStream_t s, const float *in, int dim, int ns, long rows, const int *ctx, int nctx, int first,
+                 int const_dim, float *out);
+void splice_rows_backward(hipStream_t s, const float *out_deriv, int dim, int ns, long rows, const int *ctx, int nctx,
+                          int first, int const_dim, float *in_deriv);
+
 // Data-parallel agreement on a failed step: the step's device error word (set
 // by a recurrence's bounded-spin timeout) as a 0/1 float that the gradient
 // exchange sums over the ranks, and back: a positive sum sets kErrPeerFailed,

@@ -222,6 +222,69 @@ void scale_inplace(hipStream_t s, float *p, long n, float alpha) {
   hipLaunchKernelGGL(k_scale, dim3(grid_for(n)), dim3(256), 0, s, p, n, alpha);
 }
 
+// ---- SpliceComponent --------------------------------------------------------
+struct SpliceArgs {
+  int n, first, dim, const_dim, ns, out_dim;
+  int ctx[kMaxSplice];
+};
+// one thread per output element; rows of the same chunk are contiguous
+__global__ void k_splice(const float *__restrict__ in, long rows, SpliceArgs a, float *__restrict__ out) {
+  const long total = rows * a.out_dim;
+  const int sd = a.dim - a.const_dim;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long j = e / a.out_dim;
+    const int col = (int)(e - j * a.out_dim);
+    const int c = col / sd;
+    float v;
+    if (c < a.n) v = in[(j * a.ns + a.first + a.ctx[c]) * a.dim + (col - c * sd)];
+    else v = in[j * a.ns * a.dim + sd + (col - a.n * sd)];  // const part: the chunk's first row
+    out[e] = v;
+  }
+}
+// one thread per input element: a pure gather (no atomics): input row
+// j * ns + s gets block c of output row j when first + ctx[c] == s
+__global__ void k_splice_bwd(const float *__restrict__ od, long rows, SpliceArgs a, float *__restrict__ id) {
+  const long total = rows * a.ns * a.dim;
+  const int sd = a.dim - a.const_dim;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long r = e / a.dim;
+    const int col = (int)(e - r * a.dim);
+    const long j = r / a.ns;
+    const int sp = (int)(r - j * a.ns);
+    float v = 0.f;
+    if (col < sd) {
+      for (int c = 0; c < a.n; c++)
+        if (a.first + a.ctx[c] == sp) v += od[j * a.out_dim + c * sd + col];
+    } else if (sp == 0) {
+      v = od[j * a.out_dim + a.n * sd + (col - sd)];
+    }
+    id[e] = v;
+  }
+}
+
+static SpliceArgs splice_args(int dim, int ns, const int *ctx, int nctx, int first, int const_dim) {
+  if (nctx <= 0 || nctx > kMaxSplice) throw std::invalid_argument("splice: 1..32 context offsets");
+  SpliceArgs a{};
+  a.n = nctx; a.first = first; a.dim = dim; a.const_dim = const_dim; a.ns = ns;
+  a.out_dim = (dim - const_dim) * nctx + const_dim;
+  for (int c = 0; c < nctx; c++) a.ctx[c] = ctx[c];
+  return a;
+}
+
+void splice_rows(hipStream_t s, const float *in, int dim, int ns, long rows, const int *ctx, int nctx, int first,
+                 int const_dim, float *out) {
+  if (rows <= 0) return;
+  const SpliceArgs a = splice_args(dim, ns, ctx, nctx, first, const_dim);
+  hipLaunchKernelGGL(k_splice, dim3(grid_for(rows * a.out_dim)), dim3(256), 0, s, in, rows, a, out);
+}
+
+void splice_rows_backward(hipStream_t s, const float *out_deriv, int dim, int ns, long rows, const int *ctx, int nctx,
+                          int first, int const_dim, float *in_deriv) {
+  if (rows <= 0) return;
+  const SpliceArgs a = splice_args(dim, ns, ctx, nctx, first, const_dim);
+  hipLaunchKernelGGL(k_splice_bwd, dim3(grid_for(rows * ns * dim)), dim3(256), 0, s, out_deriv, rows, a, in_deriv);
+}
+
 // ---- data-parallel step agreement ------------------------------------------
 __global__ void k_err_to_flag(const unsigned *err, float *flag) { flag[0] = err[0] ? 1.f : 0.f; }
 __global__ void k_flag_to_err(const float *flag, unsigned *err) {

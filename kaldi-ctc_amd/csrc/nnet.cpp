@@ -278,74 +278,101 @@ Component *Component::NewComponentOfType(const std::string &type) {
 }
 
 // ---------------------------------------------------------------------------
-// SpliceComponent (nnet-component.cc:2517-2760), context {0} on this path
+// SpliceComponent (nnet-component.cc:2504-2820)
 // ---------------------------------------------------------------------------
-void SpliceComponent::InitFromString(std::string args, Rng &) {
+void SpliceComponent::Init(int input_dim, std::vector<int> context, int const_dim) {  // :2504-2513
+  if (context.empty() || input_dim <= 0 || context.front() > 0 || context.back() < 0)
+    throw std::invalid_argument("SpliceComponent: context must contain offsets <= 0 and >= 0");
+  for (size_t i = 1; i < context.size(); i++)
+    if (context[i] <= context[i - 1]) throw std::invalid_argument("SpliceComponent: context must be sorted and unique");
+  if (const_dim < 0 || const_dim >= input_dim) throw std::invalid_argument("SpliceComponent: bad const-component-dim");
+  input_dim_ = input_dim;
+  context_ = std::move(context);
+  const_dim_ = const_dim;
+}
+void SpliceComponent::InitFromString(std::string args, Rng &) {  // :2517-2540
   const std::string orig = args;
-  int left = 0, right = 0, cdim = 0;
-  bool in_ok = ParseFromString("input-dim", &args, &input_dim_);
-  bool ctx_ok = ParseFromString("context", &args, &context_);
+  int input_dim = 0, left = 0, right = 0, cdim = 0;
+  std::vector<int> context;
+  bool in_ok = ParseFromString("input-dim", &args, &input_dim);
+  bool ctx_ok = ParseFromString("context", &args, &context);
   bool lr_ok = ParseFromString("left-context", &args, &left) &&
                ParseFromString("right-context", &args, &right);
   ParseFromString("const-component-dim", &args, &cdim);
-  if (!(in_ok && (ctx_ok || lr_ok)) || !args.empty() || input_dim_ <= 0)
+  if (!(in_ok && (ctx_ok || lr_ok)) || !args.empty() || input_dim <= 0)
     throw std::invalid_argument("Invalid initializer for layer of type SpliceComponent: \"" + orig + "\"");
   if (lr_ok) {
-    context_.clear();
-    for (int i = -left; i <= right; i++) context_.push_back(i);
+    if (!context.empty()) throw std::invalid_argument("SpliceComponent: context and left/right-context both given");
+    for (int i = -left; i <= right; i++) context.push_back(i);
   }
-  if (context_ != std::vector<int>{0} || cdim != 0)
-    throw std::invalid_argument("SpliceComponent: only context=0 (the CTC recipe's splice) is "
-                                "supported on this path");
+  Init(input_dim, context, cdim);
 }
-void SpliceComponent::Propagate(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &in,
+void SpliceComponent::Propagate(const ChunkInfo &in_info, const ChunkInfo &out_info, const CuMatrixBase &in,
                                 CuMatrixBase *out) const {
-  if (out->Data() != in.Data())
-    KCTC_HIP_CHECK(hipMemcpyAsync(out->Data(), in.Data(), sizeof(float) * in.NumRows() * in.NumCols(),
-                                  hipMemcpyDeviceToDevice, S()));
+  if (IsIdentityForward()) {
+    if (out->Data() != in.Data())
+      KCTC_HIP_CHECK(hipMemcpyAsync(out->Data(), in.Data(), sizeof(float) * in.NumRows() * in.NumCols(),
+                                    hipMemcpyDeviceToDevice, S()));
+    return;
+  }
+  const long rows = out->NumRows();
+  if (rows <= 0 || in.NumRows() % rows) throw std::invalid_argument("SpliceComponent: input rows are not chunks of the output rows");
+  const int ns = (int)(in.NumRows() / rows);
+  // input row of output frame j for context offset 0: j * ns + (out offset - in offset)
+  const int first = out_info.first_offset - in_info.first_offset;
+  if (first + context_.front() < 0 || first + context_.back() >= ns)
+    throw std::invalid_argument("SpliceComponent: context outside the input chunk");
+  splice_rows(S(), in.Data(), input_dim_, ns, rows, context_.data(), (int)context_.size(), first, const_dim_,
+              out->Data());
 }
-void SpliceComponent::Backprop(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &,
+void SpliceComponent::Backprop(const ChunkInfo &in_info, const ChunkInfo &out_info, const CuMatrixBase &,
                                const CuMatrixBase &, const CuMatrixBase &out_deriv, Component *,
-                               CuMatrixBase *in_deriv) const {
-  if (in_deriv && in_deriv->Data() != out_deriv.Data())
-    KCTC_HIP_CHECK(hipMemcpyAsync(in_deriv->Data(), out_deriv.Data(),
-                                  sizeof(float) * out_deriv.NumRows() * out_deriv.NumCols(),
-                                  hipMemcpyDeviceToDevice, S()));
+                               CuMatrixBase *in_deriv) const {  // :2691-2760
+  if (!in_deriv) return;
+  if (IsIdentityForward()) {
+    if (in_deriv->Data() != out_deriv.Data())
+      KCTC_HIP_CHECK(hipMemcpyAsync(in_deriv->Data(), out_deriv.Data(),
+                                    sizeof(float) * out_deriv.NumRows() * out_deriv.NumCols(),
+                                    hipMemcpyDeviceToDevice, S()));
+    return;
+  }
+  const long rows = out_deriv.NumRows();
+  const int ns = (int)(in_deriv->NumRows() / rows);
+  splice_rows_backward(S(), out_deriv.Data(), input_dim_, ns, rows, context_.data(), (int)context_.size(),
+                       out_info.first_offset - in_info.first_offset, const_dim_, in_deriv->Data());
 }
-void SpliceComponent::Write(std::ostream &os, bool binary) const {
+void SpliceComponent::Write(std::ostream &os, bool binary) const {  // :2822-2833
   WriteToken(os, binary, "<SpliceComponent>");
   WriteToken(os, binary, "<InputDim>");
   kio::WriteInt(os, binary, input_dim_);
   WriteToken(os, binary, "<Context>");
   kio::WriteIntVector(os, binary, std::vector<int32_t>(context_.begin(), context_.end()));
   WriteToken(os, binary, "<ConstComponentDim>");
-  kio::WriteInt(os, binary, 0);
+  kio::WriteInt(os, binary, const_dim_);
   WriteToken(os, binary, "</SpliceComponent>");
-}// SpliceComponent::Read (nnet-component.cc:2797-2820), incl. the old
+}
+// SpliceComponent::Read (nnet-component.cc:2797-2820), incl. the old
 // <LeftContext>/<RightContext> form
 void SpliceComponent::Read(std::istream &is, bool binary) {
   ExpectToken(is, binary, "<InputDim>");
-  input_dim_ = kio::ReadInt(is, binary);
+  const int input_dim = kio::ReadInt(is, binary);
   const std::string t = kio::ReadToken(is, binary);
-  context_.clear();
+  std::vector<int> context;
   if (t == "<LeftContext>") {
     const int l = kio::ReadInt(is, binary);
     ExpectToken(is, binary, "<RightContext>");
     const int r = kio::ReadInt(is, binary);
-    for (int i = -l; i <= r; i++) context_.push_back(i);
+    for (int i = -l; i <= r; i++) context.push_back(i);
   } else if (t == "<Context>") {
-    for (int32_t c : kio::ReadIntVector(is, binary)) context_.push_back(c);
+    for (int32_t c : kio::ReadIntVector(is, binary)) context.push_back(c);
   } else {
     throw std::runtime_error("SpliceComponent: unknown token " + t);
   }
   ExpectToken(is, binary, "<ConstComponentDim>");
-  if (kio::ReadInt(is, binary) != 0) throw std::runtime_error("SpliceComponent: const_component_dim != 0 is not supported");
+  const int cdim = kio::ReadInt(is, binary);
   ExpectToken(is, binary, "</SpliceComponent>");
-  // as InitFromString: this path aliases the input (context {0}, the CTC
-  // recipe's splice); a spliced model would make OutputDim != InputDim
-  if (input_dim_ <= 0) throw std::runtime_error("SpliceComponent: bad <InputDim>");
-  if (context_ != std::vector<int>{0})
-    throw std::runtime_error("SpliceComponent: only context {0} (the CTC recipe's splice) is supported on this path");
+  if (input_dim <= 0) throw std::runtime_error("SpliceComponent: bad <InputDim>");
+  Init(input_dim, context, cdim);
 }
 // ---------------------------------------------------------------------------
 // CuDNNRecurrentComponent (nnet-cudnn-component.cc:56-772)
@@ -1017,6 +1044,17 @@ void Nnet::Init(const std::string &config, Rng &rng) {
   if (components_.empty()) throw std::invalid_argument("empty nnet config");
 }
 
+int Nnet::LeftContext() const {  // nnet-nnet.cc:52-64
+  int ans = 0;
+  for (const Component *c : components_) ans += c->Context().front();
+  return -ans;
+}
+int Nnet::RightContext() const {  // nnet-nnet.cc:66-73
+  int ans = 0;
+  for (const Component *c : components_) ans += c->Context().back();
+  return ans;
+}
+
 int Nnet::FirstUpdatableComponent() const {  // nnet-nnet.cc:838-845
   for (int i = 0; i < NumComponents(); i++)
     if (components_[i]->IsUpdatable()) return i;
@@ -1113,13 +1151,8 @@ const CuMatrixBase &NnetCtcUpdater::Forward(const float *feats, int T_max, int N
     if (auto *r = dynamic_cast<CuDNNRecurrentComponent *>(&nnet_->GetComponent(c)))
       r->SetErrorWord(static_cast<unsigned *>(err_word_.p));
   forward_data_.resize(C + 1);
-  chunk_info_.resize(C + 1);
-  for (int c = 0; c <= C; c++) {
-    chunk_info_[c].num_chunks = N;
-    chunk_info_[c].chunk_size = T_max;
-    chunk_info_[c].feat_dim = c == 0 ? nnet_->InputDim() : nnet_->GetComponent(c - 1).OutputDim();
-  }
-  forward_data_[0].SetView(const_cast<float *>(feats), (long)T_max * N, nnet_->InputDim());
+  SetupChunks(T_max, N);
+  forward_data_[0].SetView(const_cast<float *>(feats), (long)T_max * N * nnet_->NumSplice(), nnet_->InputDim());
   Propagate(T_max, N);
   unsigned herr = 0;
   KCTC_HIP_CHECK(hipMemcpyAsync(&herr, err_word_.p, sizeof(unsigned), hipMemcpyDeviceToHost, S()));
@@ -1149,13 +1182,8 @@ void NnetCtcUpdater::Enqueue(const float *feats, int T_max, int N, const int *nu
     if (auto *r = dynamic_cast<CuDNNRecurrentComponent *>(&nnet_->GetComponent(c)))
       r->SetErrorWord(static_cast<unsigned *>(err_word_.p));
   forward_data_.resize(C + 1);
-  chunk_info_.resize(C + 1);
-  for (int c = 0; c <= C; c++) {
-    chunk_info_[c].num_chunks = N;
-    chunk_info_[c].chunk_size = T_max;
-    chunk_info_[c].feat_dim = c == 0 ? nnet_->InputDim() : nnet_->GetComponent(c - 1).OutputDim();
-  }
-  forward_data_[0].SetView(const_cast<float *>(feats), rows, nnet_->InputDim());
+  SetupChunks(T_max, N);
+  forward_data_[0].SetView(const_cast<float *>(feats), rows * nnet_->NumSplice(), nnet_->InputDim());
   Propagate(T_max, N);
 
   // ---- ComputeObjfAndDeriv (:171-259) with the warp-ctc ABI ----
@@ -1282,6 +1310,30 @@ MinibatchStats NnetCtcUpdater::Finish() {
   }
   st.tot_accuracy = st.tot_weight - err;
   return st;
+}
+
+// Nnet::ComputeChunkInfo(num_splice, T*N) (nnet-nnet.cc:75-133) for the
+// contiguous case: the last component's output is frame offset L (the
+// network's left context), every component's input starts Context().front()
+// frames earlier.  Rows: T*N*num_splice before a splicing component (the
+// FormatNnetInput layout, ctc-nnet-update.cc:351-424), T*N after it; such a
+// component must come first (the nnet2 CTC recipe's Splice).
+void NnetCtcUpdater::SetupChunks(int T_max, int N) {
+  const int C = nnet_->NumComponents();
+  chunk_info_.resize(C + 1);
+  int off = nnet_->LeftContext();
+  for (int c = C; c >= 0; c--) {
+    chunk_info_[c].num_chunks = N;
+    chunk_info_[c].chunk_size = T_max;
+    chunk_info_[c].feat_dim = c == 0 ? nnet_->InputDim() : nnet_->GetComponent(c - 1).OutputDim();
+    chunk_info_[c].first_offset = off;
+    if (c > 0) {
+      const std::vector<int> ctx = nnet_->GetComponent(c - 1).Context();
+      if (c - 1 > 0 && ctx != std::vector<int>{0})
+        throw std::invalid_argument("a component with context other than {0} must come first (the recipe's Splice)");
+      off += ctx.front();
+    }
+  }
 }
 
 void NnetCtcUpdater::Propagate(int T, int N) {  // :136-169

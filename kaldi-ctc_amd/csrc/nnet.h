@@ -85,6 +85,7 @@ class CuMatrix : public CuMatrixBase {
 
 struct ChunkInfo {  // src/nnet2/nnet-component.h:72-146 (contiguous case)
   int feat_dim = 0, num_chunks = 0, chunk_size = 0;
+  int first_offset = 0;  // frame offset of a chunk's first row (Nnet::ComputeChunkInfo)
   long NumRows() const { return (long)num_chunks * chunk_size; }
   int NumCols() const { return feat_dim; }
   int NumChunks() const { return num_chunks; }
@@ -147,6 +148,9 @@ class Component {
   virtual void Write(std::ostream &os, bool binary) const = 0;
   virtual void Read(std::istream &is, bool binary) = 0;
   virtual void ZeroStats() {}
+  // frame offsets this component reads relative to each output frame
+  // (nnet-component.h:188; only SpliceComponent has more than {0})
+  virtual std::vector<int> Context() const { return std::vector<int>(1, 0); }
   static Component *NewComponentOfType(const std::string &type);
 };
 
@@ -181,13 +185,22 @@ class UpdatableComponent : public Component {
   DevBuf delta_;
 };
 
+// SpliceComponent (nnet-component.cc:2504-2820).  Its input is the
+// FormatNnetInput layout for num_splice = 1 + LeftContext + RightContext:
+// output frame j (= t*N + n) owns input rows j*num_splice .. +num_splice-1
+// (frames t .. t+num_splice-1 of utterance n), and output block c copies row
+// j*num_splice + L + context[c] (L = the network's left context; the
+// reference's CopyRows with ChunkInfo(num_splice, T*N), :2606-2689); the last
+// const-component-dim columns come from the chunk's first row.  Context {0}
+// without a const part (the CTC recipe's) aliases its input.
 class SpliceComponent : public Component {
  public:
   std::string Type() const override { return "SpliceComponent"; }
   int InputDim() const override { return input_dim_; }
-  int OutputDim() const override { return input_dim_ * (int)context_.size(); }
+  int OutputDim() const override { return (input_dim_ - const_dim_) * (int)context_.size() + const_dim_; }
   void InitFromString(std::string args, Rng &rng) override;
-  bool IsIdentityForward() const override { return true; }
+  bool IsIdentityForward() const override { return context_ == std::vector<int>{0} && const_dim_ == 0; }
+  std::vector<int> Context() const override { return context_; }
   bool BackpropNeedsInput() const override { return false; }
   bool BackpropNeedsOutput() const override { return false; }
   void Propagate(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &in,
@@ -198,7 +211,8 @@ class SpliceComponent : public Component {
   void Read(std::istream &is, bool binary) override;
 
  private:
-  int input_dim_ = 0;
+  void Init(int input_dim, std::vector<int> context, int const_dim);
+  int input_dim_ = 0, const_dim_ = 0;
   std::vector<int> context_{0};
 };
 
@@ -370,6 +384,11 @@ class Nnet {
   Component &GetComponent(int c) { return *components_[c]; }
   const Component &GetComponent(int c) const { return *components_[c]; }
   int FirstUpdatableComponent() const;
+  // Nnet::LeftContext / RightContext (nnet-nnet.cc:52-73): the sums of the
+  // components' first (negated) and last context offsets
+  int LeftContext() const;
+  int RightContext() const;
+  int NumSplice() const { return 1 + LeftContext() + RightContext(); }
   int InputDim() const { return components_.front()->InputDim(); }
   int OutputDim() const { return components_.back()->OutputDim(); }
   void ZeroStats();
@@ -437,6 +456,7 @@ class NnetCtcUpdater {
   void InjectStepError(unsigned word) { inject_err_ = word; }
 
  private:
+  void SetupChunks(int T_max, int N);
   void Propagate(int T, int N);
   void Backprop(int T, int N);
   Nnet *nnet_;

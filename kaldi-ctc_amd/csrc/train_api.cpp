@@ -339,6 +339,14 @@ int kctc_nnet_destroy(kctcNnet_t n) {
 
 int kctc_nnet_num_components(kctcNnet_t n) { return n ? n->nnet.NumComponents() : -1; }
 
+int kctc_nnet_context(kctcNnet_t n, int *left, int *right) {
+  return guarded([&] {
+    KCTC_REQUIRE(n && left && right, "kctc_nnet_context: null argument");
+    *left = n->nnet.LeftContext();
+    *right = n->nnet.RightContext();
+  });
+}
+
 int kctc_nnet_component_info(kctcNnet_t n, int c, char *buf, size_t len) {
   return guarded([&] {
     n->activate();
@@ -771,7 +779,10 @@ int kctc_nnet_train_simple(kctcNnet_t n, struct kctcEgsReader_ *r, long max_mini
       if (mb->InputDim() != n->nnet.InputDim())
         throw std::invalid_argument("egs input dim " + std::to_string(mb->InputDim()) + " != nnet input dim " +
                                     std::to_string(n->nnet.InputDim()));
-      n->egs_feats.ensure(sizeof(float) * (size_t)mb->T_max * mb->N * mb->InputDim());
+      if (mb->num_splice != n->nnet.NumSplice())
+        throw std::invalid_argument("the egs reader was opened with a context other than the network's "
+                                    "(kctc_nnet_context)");
+      n->egs_feats.ensure(sizeof(float) * (size_t)mb->T_max * mb->N * mb->num_splice * mb->InputDim());
       n->egs_scratch.ensure(kctc::egs::format_scratch_bytes(*mb));
       kctc::egs::format_on_device(*mb, n->egs_feats.f(), n->egs_scratch.p, n->egs_scratch.bytes, n->stream);
       const auto st = n->trainer.ComputeForMinibatch(n->egs_feats.f(), mb->T_max, mb->N, mb->num_frames.data(),
@@ -867,11 +878,12 @@ int kctc_nnet_compute_prob(kctcNnet_t n, const char *rspecifier, long *num_examp
     long ne = 0;
     double like = 0, acc = 0, w = 0;
     auto run = [&]() {  // ComputeNnetObjf on one batch (ctc-nnet-update.cc:426-431)
-      std::unique_ptr<kctc::egs::Minibatch> mb = kctc::egs::pack_minibatch(batch, 0, 0);
+      std::unique_ptr<kctc::egs::Minibatch> mb =
+          kctc::egs::pack_minibatch(batch, n->nnet.LeftContext(), n->nnet.RightContext());
       if (mb->InputDim() != n->nnet.InputDim())
         throw std::invalid_argument("egs input dim " + std::to_string(mb->InputDim()) + " != nnet input dim " +
                                     std::to_string(n->nnet.InputDim()));
-      n->egs_feats.ensure(sizeof(float) * (size_t)mb->T_max * mb->N * mb->InputDim());
+      n->egs_feats.ensure(sizeof(float) * (size_t)mb->T_max * mb->N * mb->num_splice * mb->InputDim());
       n->egs_scratch.ensure(kctc::egs::format_scratch_bytes(*mb));
       kctc::egs::format_on_device(*mb, n->egs_feats.f(), n->egs_scratch.p, n->egs_scratch.bytes, n->stream);
       const auto st = n->evaluator.ComputeForMinibatch(n->egs_feats.f(), mb->T_max, mb->N, mb->num_frames.data(),
