@@ -166,6 +166,9 @@ def test_spliced_model_round_trip(kctc, gpu, tmp_path, binary):
     assert back.info(0) == net.info(0) and "output-dim=24" in back.info(0)
     for c in range(net.num_components):
         if net.num_params(c):
-            np.testing.assert_array_equal(back.get_params(c), net.get_params(c))
+            if binary:
+                np.testing.assert_array_equal(back.get_params(c), net.get_params(c))
+            else:  # Kaldi text mode writes 7 significant digits
+                np.testing.assert_allclose(back.get_params(c), net.get_params(c), rtol=1e-6, atol=1e-9)
     back.close()
     net.close()
