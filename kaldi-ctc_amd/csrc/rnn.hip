@@ -1416,12 +1416,12 @@ __device__ __forceinline__ bool wave_wait_prod(const unsigned *f0, int prod, uns
 // Placement probe of a v6 launch in XCD-slot mapping: 1 iff every workgroup of
 // direction d reads the same HW_REG_XCC_ID (then the hand-off may stay in that
 // XCD's L2: plain payload and flag stores, sc1 loads).  Publishes epoch 1.
-__device__ int probe6(const RecParams &p, int d, int g, int nwg, int &bad, int *bad_lds, int *loc_lds) {
-  unsigned *ids = p.flags + 512 + d * nwg;
+__device__ int probe6(const RecParams &p, int grp, int d, int g, int nwg, int &bad, int *bad_lds, int *loc_lds) {
+  unsigned *ids = p.flags + 512 + (grp * p.dirs + d) * nwg;
   const unsigned me = xcc_id() + 1u;
   if (threadIdx.x == 0) __hip_atomic_store(ids + g, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  signal_epoch(flag6(p, 0, d, g, nwg), 1u, 0);
-  wait_flags6(flag6(p, 0, d, 0, nwg), nwg, 1u, p.err, bad, bad_lds);
+  signal_epoch(flag6(p, grp, d, g, nwg), 1u, 0);
+  wait_flags6(flag6(p, grp, d, 0, nwg), nwg, 1u, p.err, bad, bad_lds);
   if (threadIdx.x < 64) {
     bool ok = true;
     for (int i = threadIdx.x; i < nwg; i += 64)
@@ -1477,9 +1477,9 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   // workgroups share one XCD under round-robin dispatch; checked by probe6;
   // one row group only); else block b -> (group, workgroup, direction)
   const int dirs = p.dirs;
-  const int d = p.xpd ? (blockIdx.x & 7) : blockIdx.x % dirs;
+  const int d = p.xpd ? (blockIdx.x & 7) % dirs : blockIdx.x % dirs;
   const int g = p.xpd ? (blockIdx.x >> 3) : (blockIdx.x / dirs) % NWG;
-  const int grp = p.xpd ? 0 : blockIdx.x / (dirs * NWG);
+  const int grp = p.xpd ? (blockIdx.x & 7) / dirs : blockIdx.x / (dirs * NWG);
   if (d >= dirs || g >= NWG || grp >= p.rg) return;
   // rows n0 .. nend-1 of the batch (p.gs <= 16 of the 16 MFMA rows)
   const int N = p.N, T = p.T, n0 = grp * p.gs, nend = min(N, n0 + p.gs);
@@ -1615,7 +1615,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   int bad = 0;
   unsigned *myflag = flag6(p, grp, d, g, NWG);
   if (tid == 0) loc_lds = 0;
-  const int local = (p.xpd && p.allow_local) ? probe6(p, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
+  const int local = (p.xpd && p.allow_local) ? probe6(p, grp, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
   if (p.trace && tid == 0) p.trace[(long)blockIdx.x * 16 + 9] = (unsigned long long)(local + 1);  // step 0, slot 9
   int t_prev = -1;
   for (int k = T - 1; k >= 0 && !bad; k--) {
@@ -2914,7 +2914,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
       // (measured slower, 37.2 vs 33.6 ms/step of backward recurrence: the 32
       // workgroups of a direction then load 1 MB per step through ONE XCD's
       // fabric port; spread over the XCDs they use four)
-      p.xpd = (p.nwg == kCusPerXcd && dirs <= 8 && p.rg == 1 && env_int("KCTC_XCD6", 0)) ? 1 : 0;
+      p.xpd = (p.nwg == kCusPerXcd && dirs * p.rg <= 8 && env_int("KCTC_XCD6", 0)) ? 1 : 0;
       p.allow_local = env_int("KCTC_LOCAL", 1);
       p.poll_sleep = env_int("KCTC_POLL_SLEEP", 1);
       p.nopf = env_int("KCTC_DIAG_NOPF", 0);
