@@ -124,6 +124,11 @@ struct X3PBwdStream {
   unsigned *err = nullptr;
   int blocks = 0;                      // persistent blocks (each takes a CU: 96 KB LDS)
   bool bf16 = false;                   // rows packed as bf16 ([M][KB][64], KB 64-k blocks), B bf16, no exponents
+  // XCD-pinned producer (rnn.hip bwd_xcd_mask): its workgroups OR
+  // 1 << XCC_ID into *xcd_word as they start; a block waits until
+  // xcd_count XCDs are registered and exits if it is on one of them
+  const unsigned *xcd_word = nullptr;
+  int xcd_count = 0;
 };
 size_t x3p_bwd_stream_ints(int M, int N);
 void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a);

@@ -64,6 +64,8 @@ struct PParams {
                            // 32 register-A k loop without the two-deep prefetch
   unsigned *serr;          // producer's error word (wait timeout)
   int p256v;               // 256-tile k loop (KCTC_P256): 2 DMA spread over the MFMAs, 1 DMA block per stage, 0 auto
+  const unsigned *xcd_word;  // XCDs of a pinned producer (X3PBwdStream::xcd_word), xcd_count of them
+  int xcd_count;
   // backward stream (x3p_bwd_stream_kernel)
   const float *E;          // source rows of direction d: E + row * lde + d * edoff (KB * 32 floats)
   long lde, edoff;
@@ -72,6 +74,7 @@ struct PParams {
   int *arrive;             // [nrt][gx] direction partials arrived (+1) / partial published (+2)
   float *part;             // [M][N] the first direction's partial
 };
+
 
 template <int AUX = 0>
 __device__ __forceinline__ void issue_tile(const _Float16 *__restrict__ P, int rows, int r0, int KB, int kb,
@@ -254,6 +257,34 @@ __device__ __forceinline__ void wait_count(const int *a, int v, unsigned *err) {
     if (failed) wave_fail(err);
   }
   __syncthreads();
+}
+
+// true when this block runs on an XCD that an XCD-pinned producer occupies
+// (block-uniform): wave 0 waits until the producer's workgroups registered
+// p.xcd_count XCDs in *p.xcd_word (bounded, as the other waits), then looks
+// up its own.  Such blocks leave before taking work -- spinning on the
+// producer's flags there they would keep its workgroups off their CUs.
+__device__ bool on_pinned_xcd(const PParams &p, int *bc) {
+  if (!p.xcd_word) return false;
+  if (wave_id() == 0) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned m = 0;
+    bool failed = false;
+    int i = 0;
+    while (true) {
+      m = __builtin_amdgcn_readfirstlane(__hip_atomic_load(p.xcd_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if (__builtin_popcount(m) >= p.xcd_count) break;
+      failed = wave_timed_out(p.serr, i++, t0);
+      if (failed) break;
+      __builtin_amdgcn_s_sleep(4);
+    }
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    if (threadIdx.x == 0) *bc = failed ? 1 : (int)((m >> (x & 0xfu)) & 1u);
+    if (failed) wave_fail(p.serr);
+  }
+  __syncthreads();
+  return __builtin_amdgcn_readfirstlane(*bc) != 0;
 }
 
 // wait until every workgroup of producer direction d has published epoch
@@ -1100,6 +1131,7 @@ __global__ __launch_bounds__(NTH, 2) void x3p_bwd_stream_kernel(PParams p) {
   int *bc = next + 3;    // combine broadcast
   if (threadIdx.x == 0) { seen[0] = 0; seen[1] = 0; }
   const int J = p.P + p.gx, total = 2 * p.nrt * J, rows_per = TB / p.P;
+  if (on_pinned_xcd(p, bc)) return;  // before taking any job
   while (true) {
     if (threadIdx.x == 0) *next = atomicAdd(p.counter, 1);
     __syncthreads();
@@ -1458,6 +1490,7 @@ void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a) {
   p.counter = a.cnt; p.done = a.cnt + 1; p.arrive = a.cnt + 1 + 2 * p.nrt;
   p.part = a.part;
   p.sflags = a.flags; p.snwg = a.nwg; p.sT = a.T; p.sN = a.Nf; p.serr = a.err; p.srg = a.rg;
+  p.xcd_word = a.xcd_word; p.xcd_count = a.xcd_count;
   p.backoff = env_backoff();
   p.dbg = getenv("KCTC_STREAM_DBG") ? atoi(getenv("KCTC_STREAM_DBG")) : 0;
   KCTC_HIP_CHECK(hipMemsetAsync(a.cnt, 0, sizeof(int) * x3p_bwd_stream_ints(a.M, a.N), s));

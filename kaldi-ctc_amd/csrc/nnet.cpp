@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <iomanip>
 #include <iostream>
@@ -1276,9 +1277,13 @@ MinibatchStats NnetCtcUpdater::Finish() {
   last_ids_.assign(hids, hids + rows);
   last_costs_.assign(hcost, hcost + N);
   for (int i = 0; i < sl.nerr; i++) {
-    if (herr[i] & ~kErrPeerFailed)
-      throw std::runtime_error("recurrence hand-off timed out (device error word set); this minibatch's "
-                               "updates were skipped, the parameters are those before it");
+    if (herr[i] & ~kErrPeerFailed) {
+      // bits: 1 a recurrence's spin, 2 a streamed GEMM's wait, 8 a weight-gradient gate
+      char what[64];
+      snprintf(what, sizeof what, " (error word %d = 0x%x)", i, herr[i]);
+      throw std::runtime_error(std::string("recurrence hand-off timed out") + what +
+                               "; this minibatch's updates were skipped, the parameters are those before it");
+    }
     if (herr[i])
       throw std::runtime_error("the step failed on another data-parallel rank; every rank skipped this "
                                "minibatch's updates, the parameters are those before it");

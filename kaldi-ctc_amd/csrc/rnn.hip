@@ -253,6 +253,7 @@ struct RecParams {
   unsigned long long *trace;  // optional: [kTraceSteps][grid][8] s_memrealtime stamps
   int allow_local;  // v4: hand off through the shared L2 when placement allows it
   int xpd;          // v4: XCD slots per direction (nwg = 32 * xpd workgroups)
+  int ring;         // v6 backward: partial-dh images reused every `ring` steps (0: one image per step)
   float *xch;       // v4: per-step exchange images [T][dirs][KG][Npad][16] (workspace)
   int poll_sleep;   // v6: s_sleep between flag polls
   int nopf;         // diagnostic (KCTC_DIAG_NOPF): skip the operand prefetch (wrong results)
@@ -1367,6 +1368,9 @@ __device__ __forceinline__ float group_maxU(float v, int U) {
 // producers' flag stores and the consumers' polls spread over L2 / memory
 // channels instead of hammering one line.
 constexpr int kFlagStride = 32;  // words
+// word of the flag area where an XCD-pinned backward recurrence's workgroups
+// OR in 1 << XCC_ID (words 1008 / 1009: weight-gradient tile counters)
+constexpr int kXcdWord = 1016;
 __device__ __forceinline__ unsigned *flag6(const RecParams &p, int grp, int d, int g, int nwg) {
   return p.flags + 1024 + (((long)grp * p.dirs + d) * nwg + g) * kFlagStride;
 }
@@ -1614,6 +1618,12 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   rotate();
   int bad = 0;
   unsigned *myflag = flag6(p, grp, d, g, NWG);
+  // XCD-slot launches keep the hand-off in the XCD's L2 (plain flag stores
+  // other XCDs do not see): a second, sc1 copy of every epoch 256 lines on,
+  // for the streamed dx GEMM running on the other XCDs
+  unsigned *gflag = p.xpd ? myflag + 256 * kFlagStride : nullptr;
+  // and where it runs, for the streamed GEMM's blocks (on_pinned_xcd)
+  if (p.xpd && tid == 0) atomicOr(p.flags + kXcdWord, 1u << xcc_id());
   if (tid == 0) loc_lds = 0;
   const int local = (p.xpd && p.allow_local) ? probe6(p, grp, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
   if (p.trace && tid == 0) p.trace[(long)blockIdx.x * 16 + 9] = (unsigned long long)(local + 1);  // step 0, slot 9
@@ -1629,7 +1639,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
         wait_flags6(flag6(p, grp, d, 0, NWG), NWG, (unsigned)(ks + 1), p.err, bad, &bad_lds, p.poll_sleep);
       }
       REC_TRACE(ks, 1);
-      const auto rs = rsrc(p.xch + (long)(ks - 1) * xstep, (unsigned)(xstep * 4));
+      const auto rs = rsrc(p.xch + (long)(p.ring ? (ks - 1) % p.ring : ks - 1) * xstep, (unsigned)(xstep * 4));
       floatx4 sm = floatx4{0.f, 0.f, 0.f, 0.f};
       if (bfp) {
         typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
@@ -1748,7 +1758,11 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
 #pragma unroll
         for (int i = 0; i < 4; i++) ex[i] = -rowexp[fq * 4 + i];
       }
-      const auto ro = rsrc(p.xch + (long)ks * xstep, (unsigned)(xstep * 4));
+      // a ring of >= 2 images is safe: every workgroup is a consumer of every
+      // producer, so before a producer writes slot ks % ring at step ks it saw
+      // all flags of step ks - 1, i.e. every consumer had finished reading
+      // that slot's previous contents (step ks - ring, read during ks - ring + 1)
+      const auto ro = rsrc(p.xch + (long)(p.ring ? ks % p.ring : ks) * xstep, (unsigned)(xstep * 4));
       const long obase = (long)grp * xgrp + (long)(d * NWG + g) * PSTR;
 #pragma unroll
       for (int c = 0; c < CTW; c++) {
@@ -1775,6 +1789,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
     }
     REC_TRACE(ks, 7);
     signal_epoch(myflag, (unsigned)(ks + 2), local);
+    if (gflag && tid == 0) __hip_atomic_store(gflag, (unsigned)(ks + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     REC_TRACE(ks, 4);
     if (p.e_sc1) {
       // this step's DX rows for a streaming consumer on other XCDs: written
@@ -1795,7 +1810,10 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
     REC_TRACE(ks, 5);
   }
   if (t_prev >= 0 && !bad) e_store(t_prev);
-  if (!bad) signal_epoch(myflag, (unsigned)(T + 2), 0);  // the last step's rows are out
+  if (!bad) {
+    signal_epoch(myflag, (unsigned)(T + 2), 0);  // the last step's rows are out
+    if (gflag && tid == 0) __hip_atomic_store(gflag, (unsigned)(T + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   // bias partial sums of this row group: reduce over its rows in a fixed
   // order through LDS; the host adds the groups in order
   float *bs = red;  // [2][16][U][NW] floats
@@ -2455,6 +2473,25 @@ namespace {
 // recurrence instead of blocking it (its blocks only wait for recurrence flags).
 int g_usable_cus = 0, g_comm_cus = 0;
 
+// XCDs an XCD-pinned v6 backward recurrence of (d, N) occupies (bit x: XCD
+// x), 0 when it is not pinned: every (row group, direction) needs one XCD of
+// kCusPerXcd workgroups (H / U == 32), and the whole chip's CUs must be usable
+// (no CU partition).  KCTC_XCD6=0 switches it off.
+unsigned bwd_xcd_mask(const RnnDesc &d, int N) {
+  const V6Cfg c6 = pick6(d, N, false);
+  if (!c6 || d.H / c6.U != kCusPerXcd || d.dirs * c6.rg > 8 || !env_int("KCTC_XCD6", 1)) return 0;
+  int dev = 0, cus = 0;
+  KCTC_HIP_CHECK(hipGetDevice(&dev));
+  KCTC_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  if (rnn_usable_cus() != cus || cus != 8 * kCusPerXcd) return 0;
+  // an exchange's kernels (comm stream) landing on a pinned XCD would hold
+  // the recurrence's CUs there until the all-reduce ends, and a stream CU
+  // mask cannot keep them off an XCD (scripts/cumask_probe.hip: each mask
+  // bit selects one CU in every XCD): pinned only without an exchange
+  if (rnn_comm_cus() > 0) return 0;
+  return (1u << (d.dirs * c6.rg)) - 1u;
+}
+
 // persistent blocks a streamed GEMM may run beside a recurrence of `rec_wgs`
 // workgroups (rnn.h, CU budget); 0: too few to stream
 int stream_block_budget(int rec_wgs, bool backward) {
@@ -2723,10 +2760,17 @@ void launch_bwd_stream(const RnnDesc &d, const RecParams &p, int l, const float 
   a.C = dxl; a.ldc = Din;
   a.part = pk<float>(workspace, d, T, N, pl.part);
   a.cnt = pk<int>(workspace, d, T, N, pl.cnt);
-  a.flags = p.flags + 1024; a.nwg = p.nwg; a.T = T; a.Nf = N; a.err = err; a.rg = p.rg;
+  // XCD-pinned recurrence: its epochs' sc1 copies (the L2 flags are not
+  // visible here), and no block on the recurrence's XCDs
+  a.flags = p.flags + 1024 + (p.xpd ? 256 * kFlagStride : 0);
+  a.nwg = p.nwg; a.T = T; a.Nf = N; a.err = err; a.rg = p.rg;
+  const int pinned = p.xpd ? d.dirs * p.rg : 0;
+  if (pinned) { a.xcd_word = p.flags + kXcdWord; a.xcd_count = pinned; }
   // 96 measured best at configs[1]; never more than the CU budget leaves
-  // beside the recurrence and the exchange's kernels (rnn.h)
-  a.blocks = env_int("KCTC_BWD_STREAM_BLOCKS", std::min(96, stream_block_budget(d.dirs * p.nwg * p.rg, true)));
+  // beside the recurrence and the exchange's kernels (rnn.h).  Blocks landing
+  // on the pinned XCDs exit at once: launch enough that ~96 stay
+  const int nb = std::min(96, stream_block_budget(d.dirs * p.nwg * p.rg, true));
+  a.blocks = env_int("KCTC_BWD_STREAM_BLOCKS", pinned ? nb * 8 / (8 - pinned) : nb);
   ProfSpan ps(ov, "bwd_data_stream");
   gemm_x3p_bwd_stream(ov, a);
 }
@@ -2910,11 +2954,13 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     p.rg = ver == 6 ? c6.rg : 1;
     p.gs = ver == 6 ? c6.gs : 16;
     if (ver == 6) {
-      // XCD-slot mapping when a direction's workgroups fit one XCD
-      // (measured slower, 37.2 vs 33.6 ms/step of backward recurrence: the 32
-      // workgroups of a direction then load 1 MB per step through ONE XCD's
-      // fabric port; spread over the XCDs they use four)
-      p.xpd = (p.nwg == kCusPerXcd && dirs * p.rg <= 8 && env_int("KCTC_XCD6", 0)) ? 1 : 0;
+      // XCD-pinned backward (bwd_xcd_mask): each (row group, direction) on one
+      // XCD, the partial-dh hand-off in that XCD's L2, through a ring of two
+      // step images (L2-resident).  configs[1]: 3.36 -> 2.70 us per step with
+      // the streamed dx GEMM beside it (2.41 without), 468k -> 511k frames/s
+      p.xpd = bwd_xcd_mask(d, N) ? 1 : 0;
+      p.ring = std::max(0, env_int("KCTC_BWD_RING", p.xpd ? 2 : 0));
+      if (p.ring == 1) p.ring = 2;
       p.allow_local = env_int("KCTC_LOCAL", 1);
       p.poll_sleep = env_int("KCTC_POLL_SLEEP", 1);
       p.nopf = env_int("KCTC_DIAG_NOPF", 0);
@@ -2933,11 +2979,11 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     // dx_l = sum_dir DX_dir W_dir   (lower layer's dy, or the caller's dx)
     float *dxl = (l == 0) ? dx : res + lay.per_layer * (l - 1) + lay.dout;
     // streamed: computed on `overlap` while the recurrence runs, from its rows as they appear
-    const bool streamed = dxl && overlap && ver == 6 && dirs == 2 && !p.xpd &&
+    const bool streamed = dxl && overlap && ver == 6 && dirs == 2 &&
                           ((d.prec == kPrecX3 && N <= 16) || env_int("KCTC_STREAM_ALL", 0)) && use_x3(NW * H) &&
                           NW * H <= 4096 &&
                           (d.prec == kPrecX3 || (NW * H) % 64 == 0) && (long)TN * Din * 4 < (1L << 31) &&
-                          stream_block_budget((int)grid.x, true) && env_int("KCTC_BWD_STREAM", 1);
+                          stream_block_budget(dirs * p.nwg * p.rg, true) && env_int("KCTC_BWD_STREAM", 1);
     // weight gradients streamed off this recurrence (the bottom component):
     // its dGates rows must be written through too
     const bool wstream = wgrad && wgrad->side && !dxl && ver == 6 && !p.xpd && d.layers == 1 &&

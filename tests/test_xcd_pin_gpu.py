@@ -1,0 +1,49 @@
+"""XCD-pinned backward recurrence (rnn.hip bwd_xcd_mask).
+
+At H = 512 (32 workgroups of 16 units per direction) and N <= 16 every
+(row group, direction) of the v6 backward recurrence fits one XCD: the launch
+puts it there, exchanges the per-step partial dh through that XCD's L2 (a
+ring of two step images), and the streamed dx GEMM keeps off those XCDs and
+follows sc1 copies of the recurrence's flags.  Only where the bytes travel
+changes, not the arithmetic: the trained parameters must equal the
+unpinned run's (KCTC_XCD6=0) bit for bit, for LSTM and GRU, BLSTM with one
+and two row groups, and a ragged minibatch."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
+
+
+def _train(kctc, gpu, cfg, batch, pinned, steps=2):
+    import torch
+    feats, nf, fl, ll, T, N = batch
+    old = os.environ.get("KCTC_XCD6")
+    os.environ["KCTC_XCD6"] = "1" if pinned else "0"
+    try:
+        net = kctc.Nnet(cfg, seed=11)
+        f = torch.from_numpy(feats).to(gpu)
+        stats = [net.train_step(f, T, N, nf, fl, ll) for _ in range(steps)]
+        params = [net.get_params(c) for c in range(net.num_components) if net.num_params(c)]
+        net.close()
+    finally:
+        if old is None:
+            os.environ.pop("KCTC_XCD6", None)
+        else:
+            os.environ["KCTC_XCD6"] = old
+    return stats, params
+
+
+@pytest.mark.parametrize("mode,N,T", [(2, 16, 400), (2, 8, 300), (3, 16, 300), (2, 13, 350)])
+def test_pinned_backward_bit_identical(kctc, gpu, mode, N, T):
+    D, H, A, R = 40, 512, 41, 2
+    cfg = kctc.recipe_config(num_rnn=R, input_dim=D, hidden=H, num_targets=A, learning_rate=5e-4,
+                             max_seq_length=T, rnn_mode=mode)
+    feats, nf, fl, ll = kctc.synth_minibatch(7 + N, T, N, D, A, 0.125)
+    batch = (feats, nf, fl, ll, T, N)
+    a = _train(kctc, gpu, cfg, batch, pinned=False)
+    b = _train(kctc, gpu, cfg, batch, pinned=True)
+    assert a[0] == b[0]
+    for x, y in zip(a[1], b[1]):
+        np.testing.assert_array_equal(x, y)
