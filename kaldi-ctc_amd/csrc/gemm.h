@@ -78,6 +78,10 @@ struct X3PArgs {
   float *stream_part = nullptr;         // [row tiles][batch][col tiles][128 x 128] half-K partials
   long stream_group_step = 0;         // halves per row group's part of a step image
   unsigned *stream_err = nullptr;    // set (bit 2) if the producer stops publishing
+  // XCD-pinned producer (rnn.hip xcd_mask): blocks on its XCDs exit before
+  // taking work, as in X3PBwdStream
+  const unsigned *stream_xcd_word = nullptr;
+  int stream_xcd_count = 0;
   // bf16 operands (bf16_pack_rows / _cols: [rows][KB][64] bf16, KB = 64-k
   // blocks, no exponents): two v_mfma_f32_16x16x32_bf16 per stage, fp32
   // accumulation; streaming: A = a bf16 v6 forward's h images (eA0 = 0)
@@ -124,7 +128,7 @@ struct X3PBwdStream {
   unsigned *err = nullptr;
   int blocks = 0;                      // persistent blocks (each takes a CU: 96 KB LDS)
   bool bf16 = false;                   // rows packed as bf16 ([M][KB][64], KB 64-k blocks), B bf16, no exponents
-  // XCD-pinned producer (rnn.hip bwd_xcd_mask): its workgroups OR
+  // XCD-pinned producer (rnn.hip xcd_mask): its workgroups OR
   // 1 << XCC_ID into *xcd_word as they start; a block waits until
   // xcd_count XCDs are registered and exits if it is on one of them
   const unsigned *xcd_word = nullptr;

@@ -704,6 +704,7 @@ __global__ __launch_bounds__(NTH, 2) void gemm_x3p_kernel(PParams p) {
   int *prog = next + 1;
   const int total = STREAM ? stream_total(p) : p.tiles * p.batch * p.split;
   if (STREAM && threadIdx.x == 0) { prog[0] = -1; prog[1] = -1; }
+  if (STREAM && on_pinned_xcd(p, prog + 2)) return;  // before taking any job
   if (p.counter) {
     while (true) {
       if (threadIdx.x == 0) *next = atomicAdd(p.counter, 1);
@@ -1408,6 +1409,7 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
   p.backoff = env_backoff();
   p.nrt = ceil_div(g.M, TB);
   p.sxs = g.stream_step; p.serr = g.stream_err;
+  p.xcd_word = g.stream_xcd_word; p.xcd_count = g.stream_xcd_count;
   p.sdir = 0;
   p.arrive = nullptr;
   p.dbg = getenv("KCTC_STREAM_DBG") ? atoi(getenv("KCTC_STREAM_DBG")) : 0;

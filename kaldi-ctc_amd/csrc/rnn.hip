@@ -126,7 +126,12 @@ constexpr size_t kFlagBytes = 4096 + 512 * 128;  // v6: up to 4 row groups x 2 d
 static size_t xch_offset(const RnnDesc &d, int T, int N) { return flags_offset(d, T, N) + kFlagBytes; }
 static size_t xch_bytes(const RnnDesc &d, int T, int N) {
   const long Npad = (N + 15) / 16 * 16;
-  return sizeof(float) * (size_t)T * d.dirs * d.nw() * d.H * Npad;
+  // v4 images: 4 B x dirs x nW x H x Npad per step; the v6 forward's
+  // [2 dirs][H/32][hi, lo][16][32] halves per row group of <= 16 rows (at most
+  // 2 Npad / 16 groups): 16 B x H x Npad.  + 2 steps: the v6 forward's ring of
+  // hand-off images after its T step images
+  const size_t per = std::max<size_t>(sizeof(float) * d.dirs * d.nw(), 16);
+  return per * (size_t)(T + 2) * d.H * Npad;
 }
 // then the packed split-fp16 GEMM operands of one layer at a time (forward,
 // backward-data and the weight GEMMs of a component never overlap):
@@ -253,7 +258,8 @@ struct RecParams {
   unsigned long long *trace;  // optional: [kTraceSteps][grid][8] s_memrealtime stamps
   int allow_local;  // v4: hand off through the shared L2 when placement allows it
   int xpd;          // v4: XCD slots per direction (nwg = 32 * xpd workgroups)
-  int ring;         // v6 backward: partial-dh images reused every `ring` steps (0: one image per step)
+  int ring;         // v6: hand-off images reused every `ring` steps (0: one image per step; forward: ring after the T step images)
+  int fcopy;        // v6 forward, XCD-pinned: h images also written through (sc1) per step for a streamed projection
   float *xch;       // v4: per-step exchange images [T][dirs][KG][Npad][16] (workspace)
   int poll_sleep;   // v6: s_sleep between flag polls
   int nopf;         // diagnostic (KCTC_DIAG_NOPF): skip the operand prefetch (wrong results)
@@ -1889,11 +1895,15 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   using AT = typename std::conditional<BF, __bf16, _Float16>::type;
   using AV = typename std::conditional<BF, bf16x8, halfx8>::type;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ int bad_lds;
+  __shared__ int bad_lds, loc_lds;
   __shared__ float wmax[NWV];
   const int dirs = p.dirs;
-  const int d = blockIdx.x % dirs, g = (blockIdx.x / dirs) % NWG, grp = blockIdx.x / (dirs * NWG);
-  if (grp >= p.rg) return;
+  // xpd = 1: XCD-slot mapping as rnn_bwd_rec6 (block b -> (row group, direction)
+  // slot b & 7, workgroup b >> 3: one XCD per slot under round-robin dispatch)
+  const int d = p.xpd ? (blockIdx.x & 7) % dirs : blockIdx.x % dirs;
+  const int g = p.xpd ? (blockIdx.x >> 3) : (blockIdx.x / dirs) % NWG;
+  const int grp = p.xpd ? (blockIdx.x & 7) / dirs : blockIdx.x / (dirs * NWG);
+  if (g >= NWG || grp >= p.rg) return;
   const int N = p.N, T = p.T, n0 = grp * p.gs, nend = min(N, n0 + p.gs);
   const int u0 = g * U;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
@@ -1989,6 +1999,19 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   gin_load(d == 0 ? 0 : T - 1, gin);
   int bad = 0;
   unsigned *myflag = flag6(p, grp, d, g, NWG);
+  // XCD-pinned (p.xpd): the hand-off goes through a ring of p.ring step images
+  // after the T per-step images, kept in the XCD's L2 (plain stores, workgroup-
+  // scope flags) when probe6 finds the direction's workgroups on one XCD; a
+  // streamed projection on the other XCDs reads the per-step images, written
+  // through (sc1) after each step's signal, and follows sc1 copies of the
+  // epochs 256 lines on: gflag = k + 1 at step k's signal (whose drain
+  // completed step k - 1's copy), T + 1 at exit -- "epoch - 2 = last step out"
+  // as the unpinned flags
+  unsigned *gflag = (p.xpd && p.fcopy) ? myflag + 256 * kFlagStride : nullptr;
+  if (p.xpd && tid == 0) atomicOr(p.flags + kXcdWord, 1u << xcc_id());
+  if (tid == 0) loc_lds = 0;
+  const int local = (p.xpd && p.allow_local) ? probe6(p, grp, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
+  const long rbase = (long)T * XS;  // ring slots (p.ring > 0)
   // publish geometry: store thread s < NP * 16 * CH: part = s / (16 CH), row, chunk
   const int sp = tid / (16 * CH), sn = (tid / CH) % 16, sch = tid % CH;
   const int kb0 = u0 >> 5, koff = (u0 & 31) + sch * 8;
@@ -2016,7 +2039,8 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
         wait_flags6(flag6(p, grp, d, 0, NWG), NWG, (unsigned)(k + 1), p.err, bad, &bad_lds, p.poll_sleep);
       }
       REC_TRACE(k, 1);
-      const auto rs = rsrc(xch + (long)tp * XS, (unsigned)(XS * sizeof(AT)));
+      const auto rs = rsrc(xch + (p.ring ? rbase + (long)((k - 1) % p.ring) * XS : (long)tp * XS),
+                           (unsigned)(XS * sizeof(AT)));
       u32x4 ah[KBW], al[KBW];
 #pragma unroll
       for (int i = 0; i < KBW; i++) {
@@ -2098,14 +2122,22 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
       }
     }
     __syncthreads();
-    if (tid < NP * 16 * CH && n0 + sn < nend) {
-      const u32x4 v = *reinterpret_cast<const u32x4 *>(stg + (sp * 16 + sn) * U + sch * 8);
-      const long o = gimg + ((((long)d * KB + kb0) * NP + sp) * 16 + sn) * 32 + koff;
-      __builtin_amdgcn_raw_buffer_store_b128(v, rsrc(xch + (long)t * XS, (unsigned)(XS * sizeof(AT))),
-                                             (int)(o * sizeof(AT)), 0, 16);
+    const bool pub = tid < NP * 16 * CH && n0 + sn < nend;
+    const long po = gimg + ((((long)d * KB + kb0) * NP + sp) * 16 + sn) * 32 + koff;
+    u32x4 pv = u32x4{0u, 0u, 0u, 0u};
+    if (pub) {
+      pv = *reinterpret_cast<const u32x4 *>(stg + (sp * 16 + sn) * U + sch * 8);
+      const auto ro = rsrc(xch + (p.ring ? rbase + (long)(k % p.ring) * XS : (long)t * XS), (unsigned)(XS * sizeof(AT)));
+      // local: plain stores stay in the XCD's L2 for the consumers' sc1 loads
+      if (local) __builtin_amdgcn_raw_buffer_store_b128(pv, ro, (int)(po * sizeof(AT)), 0, 0);
+      else __builtin_amdgcn_raw_buffer_store_b128(pv, ro, (int)(po * sizeof(AT)), 0, 16);
     }
     REC_TRACE(k, 7);
-    signal_epoch(myflag, (unsigned)(k + 2), 0);
+    signal_epoch(myflag, (unsigned)(k + 2), local);
+    if (gflag && tid == 0) __hip_atomic_store(gflag, (unsigned)(k + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (gflag && pub)  // the streamed projection's copy, drained by the next signal
+      __builtin_amdgcn_raw_buffer_store_b128(pv, rsrc(xch + (long)t * XS, (unsigned)(XS * sizeof(AT))),
+                                             (int)(po * sizeof(AT)), 0, 16);
     REC_TRACE(k, 4);
 #pragma unroll
     for (int q = 0; q < NW; q++) gin[q] = gnx[q];
@@ -2113,6 +2145,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     REC_TRACE(k, 5);
   }
   if (t_prev >= 0 && !bad) out_store(t_prev);
+  if (gflag && !bad) signal_epoch(gflag, (unsigned)(T + 1), 0);  // the last step's copy is out
   if (bad && tid == 0) atomicOr(p.err, 1u);
 }
 
@@ -2477,18 +2510,21 @@ int g_usable_cus = 0, g_comm_cus = 0;
 // x), 0 when it is not pinned: every (row group, direction) needs one XCD of
 // kCusPerXcd workgroups (H / U == 32), and the whole chip's CUs must be usable
 // (no CU partition).  KCTC_XCD6=0 switches it off.
-unsigned bwd_xcd_mask(const RnnDesc &d, int N) {
-  const V6Cfg c6 = pick6(d, N, false);
-  if (!c6 || d.H / c6.U != kCusPerXcd || d.dirs * c6.rg > 8 || !env_int("KCTC_XCD6", 1)) return 0;
+unsigned xcd_mask(const RnnDesc &d, int N, bool fwd) {
+  const V6Cfg c6 = pick6(d, N, fwd);
+  if (!c6 || d.H / c6.U != kCusPerXcd || d.dirs * c6.rg > 8) return 0;
+  if (!env_int(fwd ? "KCTC_XCD6F" : "KCTC_XCD6", 1)) return 0;
   int dev = 0, cus = 0;
   KCTC_HIP_CHECK(hipGetDevice(&dev));
   KCTC_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   if (rnn_usable_cus() != cus || cus != 8 * kCusPerXcd) return 0;
-  // an exchange's kernels (comm stream) landing on a pinned XCD would hold
-  // the recurrence's CUs there until the all-reduce ends, and a stream CU
-  // mask cannot keep them off an XCD (scripts/cumask_probe.hip: each mask
-  // bit selects one CU in every XCD): pinned only without an exchange
-  if (rnn_comm_cus() > 0) return 0;
+  // backward: an exchange's kernels (comm stream) landing on a pinned XCD
+  // would hold the recurrence's CUs there until the all-reduce ends, and a
+  // stream CU mask cannot keep them off an XCD (scripts/cumask_probe.hip:
+  // each mask bit selects one CU in every XCD): pinned only without an
+  // exchange.  No exchange kernel runs during a forward pass (the previous
+  // step's updates waited for every bucket), so the forward stays pinned.
+  if (!fwd && rnn_comm_cus() > 0) return 0;
   return (1u << (d.dirs * c6.rg)) - 1u;
 }
 
@@ -2563,7 +2599,11 @@ void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
   x.bias2 = n.mode == kGru ? nullptr : wl + (n.lin_offset(0, NW, true) - pl0);
   x.batch = n.dirs; x.sB = (long)G * KB * 64; x.seB = bf ? 0 : G; x.sC = G; x.sBias = pls;
   x.tile_counter = reinterpret_cast<int *>(static_cast<char *>(c.workspace) + flags_offset(n, T, N));
-  x.stream_flags = p.flags + 1024; x.stream_nwg = p.nwg; x.stream_T = T; x.stream_N = N;
+  // XCD-pinned producer: the sc1 copies of its epochs, no block on its XCDs
+  x.stream_flags = p.flags + 1024 + (p.xpd ? 256 * kFlagStride : 0);
+  x.stream_nwg = p.nwg; x.stream_T = T; x.stream_N = N;
+  const int pinned = p.xpd ? d.dirs * p.rg : 0;
+  if (pinned) { x.stream_xcd_word = p.flags + kXcdWord; x.stream_xcd_count = pinned; }
   x.stream_group_step = 2L * (d.H / 32) * (bf ? 1 : 2) * 16 * 32;  // rnn_fwd_rec6's XG
   x.stream_rg = p.rg; x.stream_gs = p.gs; x.stream_step = x.stream_group_step * p.rg; x.stream_err = err;
   // K split by producer direction: the work is ready from the first steps
@@ -2576,7 +2616,9 @@ void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
   // persistent blocks (96 KB each) take the rest minus a margin (chain_ok
   // checked that at least 8 fit).  No gradient exchange runs during a
   // forward pass: the updates of the previous step waited for it.
-  x.max_blocks = env_int("KCTC_STREAM_BLOCKS", stream_block_budget(d.dirs * p.nwg * p.rg, false));
+  // (blocks landing on a pinned producer's XCDs exit at once: launch enough that the budget stays)
+  const int nb = stream_block_budget(d.dirs * p.nwg * p.rg, false);
+  x.max_blocks = env_int("KCTC_STREAM_BLOCKS", pinned ? nb * 8 / (8 - pinned) : nb);
   {
     ProfSpan ps(c.side, "fwd_proj_stream");
     gemm_x3p(c.side, x);
@@ -2702,10 +2744,19 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.poll_sleep = env_int("KCTC_POLL_SLEEP", 1);
     p.nopf = env_int("KCTC_DIAG_NOPF", 0);
     p.wwait = env_int("KCTC_FWD_WWAIT", 1);  // measured: forward recurrence 29.7 -> 28.6 ms/step
-    const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : dirs * p.nwg * p.rg);
+    const bool chained = l == d.layers - 1 && chain_ok(d, ver, T, N, chain);
+    if (ver == 6) {
+      // XCD-pinned forward (xcd_mask): each (row group, direction) on one XCD,
+      // the h hand-off in its L2 through a ring of two step images; a
+      // streamed projection gets sc1 copies of the step images and flags
+      p.xpd = xcd_mask(d, N, true) ? 1 : 0;
+      p.ring = p.xpd ? 2 : 0;
+      p.fcopy = p.xpd && chained;
+      p.allow_local = p.xpd ? env_int("KCTC_LOCAL", 1) : 0;
+    }
+    const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : ver == 6 && p.xpd ? 8 * p.nwg : dirs * p.nwg * p.rg);
     RecTrace tr;
     if (tr.arm("fwd", grid.x)) p.trace = tr.dev;
-    const bool chained = l == d.layers - 1 && chain_ok(d, ver, T, N, chain);
     const hipEvent_t fork = chained ? fork_event(s) : nullptr;
     {
       ProfSpan ps(s, "rnn_fwd_rec");
@@ -2717,7 +2768,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       launch_chain_proj(d, p, fork, T, N, *chain, err);
       join_stream(s, chain->side);
     }
-    tr.dump("fwd", s, grid.x, p.nwg, T, dirs, ver, ver == 6 ? 0 : p.xpd);
+    tr.dump("fwd", s, grid.x, p.nwg, T, dirs, ver, ver == 6 ? (p.xpd ? 1 : 0) : p.xpd);
     in = out;
   }
   return KRNN_OK;
@@ -2954,11 +3005,11 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     p.rg = ver == 6 ? c6.rg : 1;
     p.gs = ver == 6 ? c6.gs : 16;
     if (ver == 6) {
-      // XCD-pinned backward (bwd_xcd_mask): each (row group, direction) on one
+      // XCD-pinned backward (xcd_mask): each (row group, direction) on one
       // XCD, the partial-dh hand-off in that XCD's L2, through a ring of two
       // step images (L2-resident).  configs[1]: 3.36 -> 2.70 us per step with
       // the streamed dx GEMM beside it (2.41 without), 468k -> 511k frames/s
-      p.xpd = bwd_xcd_mask(d, N) ? 1 : 0;
+      p.xpd = xcd_mask(d, N, false) ? 1 : 0;
       p.ring = std::max(0, env_int("KCTC_BWD_RING", p.xpd ? 2 : 0));
       if (p.ring == 1) p.ring = 2;
       p.allow_local = env_int("KCTC_LOCAL", 1);
