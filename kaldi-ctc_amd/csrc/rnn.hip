@@ -1633,6 +1633,20 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   if (tid == 0) loc_lds = 0;
   const int local = (p.xpd && p.allow_local) ? probe6(p, grp, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
   if (p.trace && tid == 0) p.trace[(long)blockIdx.x * 16 + 9] = (unsigned long long)(local + 1);  // step 0, slot 9
+  // step t's DX rows for a streaming consumer on other XCDs, from the LDS
+  // stage: written through (sc1) as whole 16-B chunks, 4 lanes per
+  // contiguous 64-B run (4-B write-through stores per element cost ~8 us per
+  // step); the next signal drains them, so they are complete at epoch t + 3
+  auto e_sc1_store = [&](int tt) {
+    constexpr int CPR = NW * U / 4;  // chunks per row
+    const int rn = tid / CPR, c = tid - rn * CPR;
+    if (rn < 16 && n0 + rn < nend) {
+      const int q = (c * 4) / U, u = (c * 4) % U;
+      const u32x4 v = *reinterpret_cast<const u32x4 *>(estg + rn * NW * U + c * 4);
+      const int off = (int)(((long)(n0 + rn) * ldg + (long)d * NW * H + q * H + u0 + u) * 4);
+      __builtin_amdgcn_raw_buffer_store_b128(v, rsrc(p.DX + (long)tt * N * ldg, (unsigned)(N * ldg * 4)), off, 0, 16);
+    }
+  };
   int t_prev = -1;
   for (int k = T - 1; k >= 0 && !bad; k--) {
     const int t = d == 0 ? k : T - 1 - k;
@@ -1672,6 +1686,13 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
       }
       st4(red + (long)(pg * POS + pos) * 4, sm);
       REC_TRACE(ks, 2);
+      // behind this step's hand-off loads: the write-through copies for the
+      // streamed dx GEMM -- the previous step's dGates rows (staged in LDS)
+      // and the epoch the last signal drained (step ks - 2's rows).  Issued
+      // after the signal instead, they were still in flight at the next flag
+      // poll, which waits for every older store (one vmcnt for loads and stores)
+      if (p.e_sc1) e_sc1_store(t_prev);
+      if (gflag && tid == 0) __hip_atomic_store(gflag, (unsigned)(ks + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("" ::: "memory");
     // behind the hand-off loads: next step's operands, last step's row-major dGates
@@ -1795,28 +1816,14 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
     }
     REC_TRACE(ks, 7);
     signal_epoch(myflag, (unsigned)(ks + 2), local);
-    if (gflag && tid == 0) __hip_atomic_store(gflag, (unsigned)(ks + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     REC_TRACE(ks, 4);
-    if (p.e_sc1) {
-      // this step's DX rows for a streaming consumer on other XCDs: written
-      // through (sc1) as whole 16-B chunks, 4 lanes per contiguous 64-B run;
-      // issued after the signal, so only the NEXT signal (epoch ks + 3) waits
-      // for them (4-B write-through stores per element cost ~8 us per step)
-      constexpr int CPR = NW * U / 4;  // chunks per row
-      const int rn = tid / CPR, c = tid - rn * CPR;
-      if (rn < 16 && n0 + rn < nend) {
-        const int q = (c * 4) / U, u = (c * 4) % U;
-        const u32x4 v = *reinterpret_cast<const u32x4 *>(estg + rn * NW * U + c * 4);
-        const int off = (int)(((long)(n0 + rn) * ldg + (long)d * NW * H + q * H + u0 + u) * 4);
-        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc(p.DX + (long)t * N * ldg, (unsigned)(N * ldg * 4)), off, 0, 16);
-      }
-    }
     rotate();
     t_prev = t;
     REC_TRACE(ks, 5);
   }
   if (t_prev >= 0 && !bad) e_store(t_prev);
   if (!bad) {
+    if (p.e_sc1 && t_prev >= 0) e_sc1_store(t_prev);
     signal_epoch(myflag, (unsigned)(T + 2), 0);  // the last step's rows are out
     if (gflag && tid == 0) __hip_atomic_store(gflag, (unsigned)(T + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -1911,8 +1918,12 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   constexpr long XG = 2L * KB * NP * 16 * 32;  // halves per row group's image of a step (dirs <= 2)
   const long XS = XG * p.rg;                    // halves per step image
   float *red = smem;                                                       // [NWV][16][RP]
-  AT *stg = reinterpret_cast<AT *>(smem + NWV * 16 * RP + 3);              // [NP][16][U], 16-B aligned below
-  stg = reinterpret_cast<AT *>((reinterpret_cast<uintptr_t>(stg) + 15) & ~uintptr_t(15));
+  // [NP][16][U], 16-B aligned.  Offset arithmetic on smem only: a pointer
+  // rounded through an integer loses the LDS address space, and the staging
+  // reads and writes became FLAT instructions (counted in vmcnt, so the
+  // publish waited for every store of the step still in flight)
+  constexpr int kStgOff = (NWV * 16 * RP + 3 + 3) / 4 * 4;
+  AT *stg = reinterpret_cast<AT *>(smem + kStgOff);
   const float *Wd = p.w + d * p.pl_stride;
   const float *R = Wd + p.r_off;
   AT *xch = reinterpret_cast<AT *>(p.xch);
@@ -2003,15 +2014,23 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // after the T per-step images, kept in the XCD's L2 (plain stores, workgroup-
   // scope flags) when probe6 finds the direction's workgroups on one XCD; a
   // streamed projection on the other XCDs reads the per-step images, written
-  // through (sc1) after each step's signal, and follows sc1 copies of the
-  // epochs 256 lines on: gflag = k + 1 at step k's signal (whose drain
-  // completed step k - 1's copy), T + 1 at exit -- "epoch - 2 = last step out"
-  // as the unpinned flags
+  // through (sc1) behind the next step's hand-off loads, and follows sc1
+  // copies of the epochs 256 lines on: gflag = k in step k's load phase
+  // (step k - 1's signal drained step k - 2's copy), T + 1 at exit -- "epoch
+  // - 2 = last step out" as the unpinned flags
   unsigned *gflag = (p.xpd && p.fcopy) ? myflag + 256 * kFlagStride : nullptr;
   if (p.xpd && tid == 0) atomicOr(p.flags + kXcdWord, 1u << xcc_id());
   if (tid == 0) loc_lds = 0;
   const int local = (p.xpd && p.allow_local) ? probe6(p, grp, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
+  if (p.trace && tid == 0) p.trace[(long)blockIdx.x * 16 + 9] = (unsigned long long)(local + 1);  // step 0, slot 9
   const long rbase = (long)T * XS;  // ring slots (p.ring > 0)
+  // the published 16 B of h: live across the whole loop (used after it), so
+  // that no other value of the step is allocated to the data registers of the
+  // write-through copy still in flight (gfx9 waits for a store's completion
+  // before its data VGPRs are overwritten)
+  u32x4 pv = u32x4{0u, 0u, 0u, 0u};
+  // the per-step images as one loop-invariant buffer (chain_ok: T XS halves < 2 GB)
+  const auto crs = rsrc(xch, gflag ? (unsigned)(T * XS * sizeof(AT)) : 0u);
   // publish geometry: store thread s < NP * 16 * CH: part = s / (16 CH), row, chunk
   const int sp = tid / (16 * CH), sn = (tid / CH) % 16, sch = tid % CH;
   const int kb0 = u0 >> 5, koff = (u0 & 31) + sch * 8;
@@ -2025,6 +2044,8 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     if (i < KBW && kb < KB) wprod = kb * PPK + lane % PPK;
   }
   const long gimg = (long)grp * XG;
+  const bool pub = tid < NP * 16 * CH && n0 + sn < nend;  // a publishing thread: 16 B of h
+  const long po = gimg + ((((long)d * KB + kb0) * NP + sp) * 16 + sn) * 32 + koff;
   int t_prev = -1;
   for (int k = 0; k < T && !bad; k++) {
     const int t = d == 0 ? k : T - 1 - k, tp = d == 0 ? t - 1 : t + 1;
@@ -2042,17 +2063,33 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
       const auto rs = rsrc(xch + (p.ring ? rbase + (long)((k - 1) % p.ring) * XS : (long)tp * XS),
                            (unsigned)(XS * sizeof(AT)));
       u32x4 ah[KBW], al[KBW];
+      // unconditional loads (rows past N and k blocks past KB at an offset
+      // past the buffer: the hardware returns zeros), so that the compiler
+      // counts them exactly and the first MFMAs wait for their own loads only
 #pragma unroll
       for (int i = 0; i < KBW; i++) {
         const int kb = w + NWV * i;
-        if (kb < KB && arow_live) {
-          const long o = gimg + ((((long)d * KB + kb) * NP) * 16 + fr) * 32 + fq * 8;
-          ah[i] = ld_sc1(rs, (unsigned)(o * sizeof(AT)));
-          if constexpr (!BF) al[i] = ld_sc1(rs, (unsigned)((o + 16 * 32) * sizeof(AT)));
-        } else {
-          ah[i] = al[i] = u32x4{0u, 0u, 0u, 0u};
-        }
+        const long o = gimg + ((((long)d * KB + kb) * NP) * 16 + fr) * 32 + fq * 8;
+        const unsigned off = (kb < KB && arow_live) ? (unsigned)(o * sizeof(AT)) : 0x7fff0000u;
+        ah[i] = ld_sc1(rs, off);
+        if constexpr (!BF) al[i] = ld_sc1(rs, off + 16 * 32 * sizeof(AT));
       }
+      // the streamed projection's write-through copy of the previous step's
+      // image (pv still holds it), issued behind this step's hand-off loads:
+      // gfx9 counts stores and loads in one vmcnt, so a write-through store
+      // in flight at the next flag poll would hold up that poll; here the
+      // waits for the loads ahead of it do not cover it, and this step's
+      // signal drains it (the next step publishes its epoch)
+      // (every lane of every wave issues it -- non-publishing lanes at an
+      // offset past the buffer, which the hardware drops -- so that no
+      // branch makes the compiler's wait counts conservative)
+      // (unconditional: without a consumer crs covers 0 bytes and the store is dropped)
+      __builtin_amdgcn_raw_buffer_store_b128(pv, crs, pub ? (int)(po * sizeof(AT)) : 0x7ffffff0,
+                                             gflag ? (int)(tp * XS * sizeof(AT)) : 0, 16);
+      // and the epoch of the copy the last signal drained (step k - 2's):
+      // a write-through flag store left in flight at the signal would hold
+      // up the next step's first flag poll (one vmcnt for loads and stores)
+      if (gflag && tid == 0) __hip_atomic_store(gflag, (unsigned)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
       for (int i = 0; i < KBW; i++) {
         if (w + NWV * i < KB) {
@@ -2112,6 +2149,11 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
       }
       if (!live) h = 0.f;
       hval = h;
+      // the next step's input projection (loaded behind this step's hand-off
+      // loads) moves in here, before any write-through store is in flight:
+      // the wait for it must not cover the sc1 stores issued after the signal
+#pragma unroll
+      for (int q = 0; q < NW; q++) gin[q] = gnx[q];
       if constexpr (BF) {
         stg[en * U + eu] = (__bf16)h;
       } else {
@@ -2122,9 +2164,6 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
       }
     }
     __syncthreads();
-    const bool pub = tid < NP * 16 * CH && n0 + sn < nend;
-    const long po = gimg + ((((long)d * KB + kb0) * NP + sp) * 16 + sn) * 32 + koff;
-    u32x4 pv = u32x4{0u, 0u, 0u, 0u};
     if (pub) {
       pv = *reinterpret_cast<const u32x4 *>(stg + (sp * 16 + sn) * U + sch * 8);
       const auto ro = rsrc(xch + (p.ring ? rbase + (long)(k % p.ring) * XS : (long)t * XS), (unsigned)(XS * sizeof(AT)));
@@ -2134,18 +2173,17 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     }
     REC_TRACE(k, 7);
     signal_epoch(myflag, (unsigned)(k + 2), local);
-    if (gflag && tid == 0) __hip_atomic_store(gflag, (unsigned)(k + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (gflag && pub)  // the streamed projection's copy, drained by the next signal
-      __builtin_amdgcn_raw_buffer_store_b128(pv, rsrc(xch + (long)t * XS, (unsigned)(XS * sizeof(AT))),
-                                             (int)(po * sizeof(AT)), 0, 16);
     REC_TRACE(k, 4);
-#pragma unroll
-    for (int q = 0; q < NW; q++) gin[q] = gnx[q];
     t_prev = t;
     REC_TRACE(k, 5);
   }
   if (t_prev >= 0 && !bad) out_store(t_prev);
-  if (gflag && !bad) signal_epoch(gflag, (unsigned)(T + 1), 0);  // the last step's copy is out
+  if (gflag && !bad) {  // the last step's copy, then its epoch
+    if (pub) __builtin_amdgcn_raw_buffer_store_b128(pv, rsrc(xch + (long)t_prev * XS, (unsigned)(XS * sizeof(AT))),
+                                                    (int)(po * sizeof(AT)), 0, 16);
+    signal_epoch(gflag, (unsigned)(T + 1), 0);
+  }
+  asm volatile("" ::"v"(pv));
   if (bad && tid == 0) atomicOr(p.err, 1u);
 }
 
