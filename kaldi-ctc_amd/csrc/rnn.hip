@@ -1922,7 +1922,8 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // rounded through an integer loses the LDS address space, and the staging
   // reads and writes became FLAT instructions (counted in vmcnt, so the
   // publish waited for every store of the step still in flight)
-  constexpr int kStgOff = (NWV * 16 * RP + 3 + 3) / 4 * 4;
+  constexpr int RPR = (U % 16 == 0 && NW <= 4 && 4 * U > RP) ? 4 * U : RP;  // red floats per (wave, row)
+  constexpr int kStgOff = (NWV * 16 * RPR + 3 + 3) / 4 * 4;
   AT *stg = reinterpret_cast<AT *>(smem + kStgOff);
   const float *Wd = p.w + d * p.pl_stride;
   const float *R = Wd + p.r_off;
@@ -2113,22 +2114,49 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     // behind the hand-off loads: last step's row-major outputs, next step's input projection
     if (t_prev >= 0 && !(p.nopf & 2)) out_store(t_prev);
     if (k + 1 < T && !(p.nopf & 1)) gin_load(d == 0 ? t + 1 : t - 1, gnx);
+    // K partials through LDS.  U % 16 == 0: column ct * 16 + fr of the
+    // tile is gate ct / (U / 16) of unit (ct % (U / 16)) * 16 + fr, so a lane
+    // holds every gate of its (row, unit) elements: one float4 per (wave,
+    // row, unit) [NWV][16][U][4], and a cell thread sums NWV float4 reads
+    // (4x fewer LDS instructions than one float per gate)
+    constexpr bool RED4 = U % 16 == 0 && NW <= 4;
+    if constexpr (RED4) {
+      constexpr int SU = U / 16;
 #pragma unroll
-    for (int ct = 0; ct < CT; ct++)
+      for (int su = 0; su < SU; su++)
 #pragma unroll
-      for (int i = 0; i < 4; i++) red[(w * 16 + fq * 4 + i) * RP + ct * 16 + fr] = acc[ct][i];
+        for (int i = 0; i < 4; i++) {
+          floatx4 v4 = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int q = 0; q < NW; q++) v4[q] = acc[q * SU + su][i];
+          st4(red + (((long)(w * 16 + fq * 4 + i) * U + su * 16 + fr) << 2), v4);
+        }
+    } else {
+#pragma unroll
+      for (int ct = 0; ct < CT; ct++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) red[(w * 16 + fq * 4 + i) * RP + ct * 16 + fr] = acc[ct][i];
+    }
     __syncthreads();
     if (bad_lds) bad = 1;
     REC_TRACE(k, 3);
     if (has_e) {
       float rh[NW];
+      if constexpr (RED4) {
+        floatx4 sm = *reinterpret_cast<const floatx4 *>(red + (((long)en * U + eu) << 2));  // fixed order
 #pragma unroll
-      for (int q = 0; q < NW; q++) {
-        const int c = q * U + eu;
-        float sm = red[(0 * 16 + en) * RP + c];  // the waves' K partials in a fixed order
+        for (int v = 1; v < NWV; v++) sm += *reinterpret_cast<const floatx4 *>(red + (((long)(v * 16 + en) * U + eu) << 2));
 #pragma unroll
-        for (int v = 1; v < NWV; v++) sm += red[(v * 16 + en) * RP + c];
-        rh[q] = BF ? sm : ldexpf(sm, sOut);
+        for (int q = 0; q < NW; q++) rh[q] = BF ? sm[q] : ldexpf(sm[q], sOut);
+      } else {
+#pragma unroll
+        for (int q = 0; q < NW; q++) {
+          const int c = q * U + eu;
+          float sm = red[(0 * 16 + en) * RP + c];  // the waves' K partials in a fixed order
+#pragma unroll
+          for (int v = 1; v < NWV; v++) sm += red[(v * 16 + en) * RP + c];
+          rh[q] = BF ? sm : ldexpf(sm, sOut);
+        }
       }
       float h;
       if (MODE == kLstm) {
@@ -2172,7 +2200,23 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
       else __builtin_amdgcn_raw_buffer_store_b128(pv, ro, (int)(po * sizeof(AT)), 0, 16);
     }
     REC_TRACE(k, 7);
-    signal_epoch(myflag, (unsigned)(k + 2), local);
+    if constexpr (NP * 16 * CH <= 64) {
+      // one publishing wave (wave 0 stores the whole h part): it drains its
+      // own stores and raises the flag, no workgroup barrier.  The other
+      // waves go on to the next step's wait: their reads of red and stg this
+      // step all came before the barrier above, and the next writes of either
+      // follow the next K-reduction barrier, which wave 0 reaches only after
+      // its stg read
+      if (w == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) {
+          if (local) __hip_atomic_store(myflag, (unsigned)(k + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          else __hip_atomic_store(myflag, (unsigned)(k + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    } else {
+      signal_epoch(myflag, (unsigned)(k + 2), local);
+    }
     REC_TRACE(k, 4);
     t_prev = t;
     REC_TRACE(k, 5);
@@ -2461,7 +2505,8 @@ static int pick_bwd_u6(const RnnDesc &d, int N) { return pick6(d, N, false).U; }
 
 static size_t fwd6_lds_bytes(const RnnDesc &d, const V6Cfg &c) {
   const int CT = (d.nw() * c.U + 15) / 16, nwv = c.nth / 64, np = d.prec == kPrecBf16 ? 1 : 2;
-  const size_t b = sizeof(float) * (nwv * 16 * (size_t)(CT * 16 + 1) + 8) + np * 16 * (size_t)c.U * 2 + 16;
+  const size_t rp = std::max(CT * 16 + 1, 4 * c.U);  // rnn_fwd_rec6's RPR (float4 K partials)
+  const size_t b = sizeof(float) * (nwv * 16 * rp + 8) + np * 16 * (size_t)c.U * 2 + 16;
   return std::max(b, (size_t)96 * 1024);  // one recurrence workgroup per CU
 }
 static size_t bwd6_lds_bytes(const RnnDesc &d, const V6Cfg &c) {
