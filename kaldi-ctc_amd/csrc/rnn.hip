@@ -1361,7 +1361,19 @@ typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 // products of the v6 recurrences: split-fp16 (fp32-class) or bf16
-enum { kPrecX3 = 0, kPrecBf16 = 1 };
+enum { kPrecX3 = 0, kPrecBf16 = 1, kPrecX3S = 2 };
+// kPrecX3S: split-fp16 with the hi and lo parts stacked in ONE 16-row MFMA
+// operand -- for row groups of <= 8 sequences, whose tiles leave rows 8..15
+// empty: A = [hi rows 0..7; lo rows 0..7], acc += A B_hi + A B_lo, then row r
+// + row r + 8 = hi B_hi + hi B_lo + lo B_hi + lo B_lo (all four terms: 2 MFMAs
+// per block instead of 3, and the lo x lo term the 3-MFMA form drops)
+
+// rows r + 8 of a 16 x 16 C fragment (lanes 32..63) added into rows r (lanes
+// 0..31); lanes 32..63 are left with garbage
+__device__ __forceinline__ float fold_rows8(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return x + __uint_as_float(r[1]);
+}
 // max over each aligned group of U (8, 16, 32) lanes, all lanes active
 __device__ __forceinline__ float group_maxU(float v, int U) {
   v = U > 8 ? group_max16(v) : group_max8(v);
@@ -1477,6 +1489,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   constexpr int PER = NWG / NGRP;  // producers summed per group
   static_assert(NWG % NGRP == 0, "producer groups");
   constexpr bool BF = P == kPrecBf16;
+  constexpr bool STK = P == kPrecX3S;  // dGates hi / lo stacked in one 16-row A image (groups of <= 8 rows)
   using AT = typename std::conditional<BF, __bf16, _Float16>::type;
   using AV = typename std::conditional<BF, bf16x8, halfx8>::type;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1744,12 +1757,24 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
         for (int q = 0; q < NW; q++) Ahi[en * AP + q * U + eu] = (__bf16)eg[q];
       } else {
         const int se = split_exp(group_maxU(m, U));
+        if constexpr (STK) {  // rows en < 8 only: lo parts go to rows en + 8
+          if (en < 8) {
 #pragma unroll
-        for (int q = 0; q < NW; q++) {
-          _Float16 h, l;
-          split16(ldexpf(eg[q], se), h, l);
-          Ahi[en * AP + q * U + eu] = h;
-          Alo[en * AP + q * U + eu] = l;
+            for (int q = 0; q < NW; q++) {
+              _Float16 h, l;
+              split16(ldexpf(eg[q], se), h, l);
+              Ahi[en * AP + q * U + eu] = h;
+              Ahi[(en + 8) * AP + q * U + eu] = l;
+            }
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < NW; q++) {
+            _Float16 h, l;
+            split16(ldexpf(eg[q], se), h, l);
+            Ahi[en * AP + q * U + eu] = h;
+            Alo[en * AP + q * U + eu] = l;
+          }
         }
         if (eu == 0) rowexp[en] = se + sB;
       }
@@ -1770,6 +1795,11 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
         if constexpr (BF) {
 #pragma unroll
           for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bhi[c][kb], acc[c], 0, 0, 0);
+        } else if constexpr (STK) {
+#pragma unroll
+          for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bhi[c][kb], acc[c], 0, 0, 0);
+#pragma unroll
+          for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, blo[c][kb], acc[c], 0, 0, 0);
         } else {
           const AV al = *reinterpret_cast<const AV *>(Alo + fr * AP + kb * 32 + fq * 8);
 #pragma unroll
@@ -1780,10 +1810,16 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
           for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bhi[c][kb], acc[c], 0, 0, 0);
         }
       }
+      if constexpr (STK) {  // rows 8..15 hold the lo parts' products: fold them into rows 0..7
+#pragma unroll
+        for (int c = 0; c < CTW; c++)
+#pragma unroll
+          for (int i = 0; i < 4; i++) acc[c][i] = fold_rows8(acc[c][i]);
+      }
       int ex[4] = {0, 0, 0, 0};
       if constexpr (!BF) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) ex[i] = -rowexp[fq * 4 + i];
+        for (int i = 0; i < 4; i++) ex[i] = -rowexp[(fq & (STK ? 1 : 3)) * 4 + i];
       }
       // a ring of >= 2 images is safe: every workgroup is a consumer of every
       // producer, so before a producer writes slot ks % ring at step ks it saw
@@ -1897,6 +1933,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   constexpr int KB = H / 32, KBW = (KB + NWV - 1) / NWV, NWG = H / U;
   constexpr int CH = U / 8;  // 16-B chunks of a published row part
   constexpr bool BF = P == kPrecBf16;
+  constexpr bool STK = P == kPrecX3S;  // hi / lo stacked in one 16-row A operand (groups of <= 8 rows)
   constexpr int NP = BF ? 1 : 2;  // parts of an exchanged h: hi (+ lo)
   static_assert(16 * U <= NTH, "one (row, unit) element per thread");
   using AT = typename std::conditional<BF, __bf16, _Float16>::type;
@@ -2036,7 +2073,8 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   const int sp = tid / (16 * CH), sn = (tid / CH) % 16, sch = tid % CH;
   const int kb0 = u0 >> 5, koff = (u0 & 31) + sch * 8;
   // rows past N (a group of fewer than 16 sequences) are neither loaded nor stored
-  const bool arow_live = n0 + fr < nend;
+  // (STK: lanes fr >= 8 load the lo part of row fr - 8)
+  const bool arow_live = n0 + (STK ? (fr & 7) : fr) < nend;
   // per-wave wait: the producers of the k blocks this wave loads (32 / U per block)
   int wprod = -1;
   {
@@ -2070,10 +2108,11 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
 #pragma unroll
       for (int i = 0; i < KBW; i++) {
         const int kb = w + NWV * i;
-        const long o = gimg + ((((long)d * KB + kb) * NP) * 16 + fr) * 32 + fq * 8;
+        const long o = STK ? gimg + ((((long)d * KB + kb) * NP + (fr >> 3)) * 16 + (fr & 7)) * 32 + fq * 8
+                           : gimg + ((((long)d * KB + kb) * NP) * 16 + fr) * 32 + fq * 8;
         const unsigned off = (kb < KB && arow_live) ? (unsigned)(o * sizeof(AT)) : 0x7fff0000u;
         ah[i] = ld_sc1(rs, off);
-        if constexpr (!BF) al[i] = ld_sc1(rs, off + 16 * 32 * sizeof(AT));
+        if constexpr (!BF && !STK) al[i] = ld_sc1(rs, off + 16 * 32 * sizeof(AT));
       }
       // the streamed projection's write-through copy of the previous step's
       // image (pv still holds it), issued behind this step's hand-off loads:
@@ -2098,6 +2137,11 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
           if constexpr (BF) {
 #pragma unroll
             for (int ct = 0; ct < CT; ct++) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bhi[ct][i], acc[ct], 0, 0, 0);
+          } else if constexpr (STK) {
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bhi[ct][i], acc[ct], 0, 0, 0);
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, blo[ct][i], acc[ct], 0, 0, 0);
           } else {
             const AV a1 = __builtin_bit_cast(AV, al[i]);
 #pragma unroll
@@ -2120,6 +2164,12 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     // row, unit) [NWV][16][U][4], and a cell thread sums NWV float4 reads
     // (4x fewer LDS instructions than one float per gate)
     constexpr bool RED4 = U % 16 == 0 && NW <= 4;
+    if constexpr (STK) {  // rows 8..15 hold the lo parts' products: fold them into rows 0..7
+#pragma unroll
+      for (int ct = 0; ct < CT; ct++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) acc[ct][i] = fold_rows8(acc[ct][i]);
+    }
     if constexpr (RED4) {
       constexpr int SU = U / 16;
 #pragma unroll
@@ -2300,14 +2350,30 @@ static void launch6_h(bool fwd, const RecParams &p, dim3 grid, size_t lds, hipSt
     default: throw std::logic_error("v6 recurrence: H not compiled");
   }
 }
+static int env_int(const char *name, int dflt);
 template <int MODE, int P>
 static void launch6_u(bool fwd, int nth, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
   switch (p.U) {
     case 8: launch6_h<MODE, 8, 256, P>(fwd, p, grid, lds, s); break;
     case 16:
       if (nth == 1024) launch6_h<MODE, 16, 1024, P>(fwd, p, grid, lds, s);
-      else if (nth == 512) launch6_h<MODE, 16, 512, P>(fwd, p, grid, lds, s);
-      else launch6_h<MODE, 16, 256, P>(fwd, p, grid, lds, s);
+      else if (nth == 512) {
+        // row groups of <= 8 sequences: hi / lo stacked in one MFMA operand
+        // (KCTC_STK=1, off by default: equally accurate or better -- all four
+        // products -- but not faster at configs[1]: forward 2.31 vs 2.32,
+        // backward 2.54 vs 2.49 us/step; the steps are bound by the hand-off
+        // latencies, and the fold adds a cross-lane exchange)
+        const int stk = env_int("KCTC_STK", 0);  // read per launch (tests toggle it)
+        if constexpr (P == kPrecX3) {
+          if (p.gs <= 8 && stk) {
+            launch6_h<MODE, 16, 512, kPrecX3S>(fwd, p, grid, lds, s);
+            break;
+          }
+        }
+        launch6_h<MODE, 16, 512, P>(fwd, p, grid, lds, s);
+      } else {
+        launch6_h<MODE, 16, 256, P>(fwd, p, grid, lds, s);
+      }
       break;
     default: launch6_h<MODE, 32, 512, P>(fwd, p, grid, lds, s); break;
   }

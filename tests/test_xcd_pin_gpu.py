@@ -51,3 +51,21 @@ def test_pinned_bit_identical(kctc, gpu, mode, N, T, var):
     assert a[0] == b[0]
     for x, y in zip(a[1], b[1]):
         np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("mode", [2, 3])
+def test_stacked_hilo_matches_oracle_grade(kctc, gpu, mode):
+    """KCTC_STK=1 (rnn.hip kPrecX3S: hi / lo of a <= 8-row group stacked in one
+    MFMA operand, all four split products) against the default 3-MFMA form:
+    not bit-identical (different products and order), but the two agree to
+    fp32-class accuracy after two training steps."""
+    D, H, A, R, N, T = 40, 512, 41, 2, 16, 300
+    cfg = kctc.recipe_config(num_rnn=R, input_dim=D, hidden=H, num_targets=A, learning_rate=5e-4,
+                             max_seq_length=T, rnn_mode=mode)
+    feats, nf, fl, ll = kctc.synth_minibatch(5, T, N, D, A, 0.125)
+    batch = (feats, nf, fl, ll, T, N)
+    a = _train(kctc, gpu, cfg, batch, pinned=False, var="KCTC_STK")
+    b = _train(kctc, gpu, cfg, batch, pinned=True, var="KCTC_STK")
+    for x, y in zip(a[1], b[1]):
+        err = np.linalg.norm(x - y) / max(np.linalg.norm(x), 1e-30)
+        assert err < 1e-5, err
