@@ -1392,6 +1392,11 @@ constexpr int kXcdWord = 1016;
 __device__ __forceinline__ unsigned *flag6(const RecParams &p, int grp, int d, int g, int nwg) {
   return p.flags + 1024 + (((long)grp * p.dirs + d) * nwg + g) * kFlagStride;
 }
+// aggregated epoch of (row group, direction) for the streamed GEMMs of an
+// XCD-pinned recurrence: one line each, 256 lines past the flag lines
+__device__ __forceinline__ unsigned *agg_flag6(const RecParams &p, int grp, int d) {
+  return p.flags + 1024 + (256 + (long)grp * p.dirs + d) * kFlagStride;
+}
 __device__ __forceinline__ void wait_flags6(const unsigned *f0, int nwg, unsigned epoch, unsigned *err, int &bad,
                                             int *bad_lds, int sleep = 1) {
   if (threadIdx.x < 64) {
@@ -1453,6 +1458,32 @@ __device__ int probe6(const RecParams &p, int grp, int d, int g, int nwg, int &b
   }
   __syncthreads();
   return *loc_lds;
+}
+
+// 4-byte LDS-DMA (global_load_lds_dword): lane l's dword to LDS byte address
+// lds + 4 l.  Inline asm, so that the compiler's wait-count pass does not see
+// it: a pending LDS-DMA there merges into the other waves' code paths of
+// the same kernel and turns their exact vmcnt waits into vmcnt(0).  The
+// issuing wave waits for it with explicit s_waitcnt and reads none of it.
+__device__ __forceinline__ void dma_lds_dword(const float *g, unsigned lds) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(lds) : "memory", "m0");
+}
+
+// Workgroup barrier for LDS hand-offs.  RAW = true: the LDS writes drained
+// and s_barrier, without __syncthreads' fence -- with LDS-DMA in flight the
+// fence waits for every outstanding vector memory operation (vmcnt(0)),
+// which would turn the IO waves' G fetch three steps ahead into one step and
+// hold the hand-off waves on their own stores.  Only for barriers that order
+// LDS traffic alone.
+template <bool RAW>
+__device__ __forceinline__ void lds_barrier() {
+  if constexpr (RAW) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  } else {
+    __syncthreads();
+  }
 }
 
 // exponent s with max * 2^s in [2^13, 2^14) (s = 14 for max == 0)
@@ -1638,9 +1669,13 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   int bad = 0;
   unsigned *myflag = flag6(p, grp, d, g, NWG);
   // XCD-slot launches keep the hand-off in the XCD's L2 (plain flag stores
-  // other XCDs do not see): a second, sc1 copy of every epoch 256 lines on,
-  // for the streamed dx GEMM running on the other XCDs
-  unsigned *gflag = p.xpd ? myflag + 256 * kFlagStride : nullptr;
+  // other XCDs do not see).  For the streamed dx GEMM running on the other
+  // XCDs, workgroup 0 of each (row group, direction) publishes ONE aggregated
+  // sc1 epoch (agg_flag6): after the first barrier of step ks it has seen every
+  // producer's epoch ks + 1, whose signals drained their rows of step ks - 2,
+  // so it stores ks + 1 ("rows of step k complete at epoch k + 3").  One line
+  // per direction instead of 32 for up to ~100 polling GEMM blocks.
+  unsigned *gflag = (p.xpd && p.e_sc1 && g == 0) ? agg_flag6(p, grp, d) : nullptr;
   // and where it runs, for the streamed GEMM's blocks (on_pinned_xcd)
   if (p.xpd && tid == 0) atomicOr(p.flags + kXcdWord, 1u << xcc_id());
   if (tid == 0) loc_lds = 0;
@@ -1705,7 +1740,6 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
       // after the signal instead, they were still in flight at the next flag
       // poll, which waits for every older store (one vmcnt for loads and stores)
       if (p.e_sc1) e_sc1_store(t_prev);
-      if (gflag && tid == 0) __hip_atomic_store(gflag, (unsigned)(ks + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("" ::: "memory");
     // behind the hand-off loads: next step's operands, last step's row-major dGates
@@ -1713,6 +1747,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
     if (k > 0 && !(p.nopf & 1)) prefetch(k - 1);
     __syncthreads();
     if (bad_lds) bad = 1;
+    if (gflag && ks > 0 && tid == 0) __hip_atomic_store(gflag, (unsigned)(ks + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (has_e) {
       float dhr = 0.f;
       if (ks > 0) {
@@ -1861,7 +1896,10 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   if (!bad) {
     if (p.e_sc1 && t_prev >= 0) e_sc1_store(t_prev);
     signal_epoch(myflag, (unsigned)(T + 2), 0);  // the last step's rows are out
-    if (gflag && tid == 0) __hip_atomic_store(gflag, (unsigned)(T + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (gflag) {  // every producer's last rows are out
+      wait_flags6(flag6(p, grp, d, 0, NWG), NWG, (unsigned)(T + 2), p.err, bad, &bad_lds, p.poll_sleep);
+      if (!bad && tid == 0) __hip_atomic_store(gflag, (unsigned)(T + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   // bias partial sums of this row group: reduce over its rows in a fixed
   // order through LDS; the host adds the groups in order
@@ -1929,13 +1967,27 @@ template <int MODE, int U, int H, int NTH, int P>
 __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   constexpr int NW = MODE == kLstm ? 4 : 3;
   constexpr int NWV = NTH / 64;
+  // P & 4: IO waves.  The upper half of the waves neither waits for the
+  // hand-off nor multiplies: they load the input projection rows (G) of the
+  // coming steps and pass them through LDS.  A wave's vmcnt counts its loads
+  // and stores in order, so a G load (HBM latency) issued by a hand-off wave
+  // held up that wave's next flag poll / hand-off loads / publish drain
+  // (measured: forward 2.38 -> 1.89 us/step with the G loads left out)
+  constexpr bool IOW = (P & 4) != 0;
+  // the row-major outputs through the IO waves too: measured slower (forward
+  // 2.46 -> 2.52 us/step; the IO waves' waits then delay the post-cell barrier)
+  constexpr bool IO_OUT = false;
+  constexpr int PR = P & 3;
+  constexpr int CW = IOW ? NWV / 2 : NWV;  // hand-off (compute) waves
   constexpr int NC = NW * U, CT = (NC + 15) / 16, RP = CT * 16 + 1;  // red row pitch (floats)
-  constexpr int KB = H / 32, KBW = (KB + NWV - 1) / NWV, NWG = H / U;
+  constexpr int KB = H / 32, KBW = (KB + CW - 1) / CW, NWG = H / U;
   constexpr int CH = U / 8;  // 16-B chunks of a published row part
-  constexpr bool BF = P == kPrecBf16;
-  constexpr bool STK = P == kPrecX3S;  // hi / lo stacked in one 16-row A operand (groups of <= 8 rows)
+  constexpr bool BF = PR == kPrecBf16;
+  constexpr bool STK = PR == kPrecX3S;  // hi / lo stacked in one 16-row A operand (groups of <= 8 rows)
   constexpr int NP = BF ? 1 : 2;  // parts of an exchanged h: hi (+ lo)
   static_assert(16 * U <= NTH, "one (row, unit) element per thread");
+  static_assert(!IOW || (16 * U == CW * 64 && NW <= 4 && NP * 16 * U / 8 <= 64),
+                "IO waves: the elements fill the compute waves, one publishing wave");
   using AT = typename std::conditional<BF, __bf16, _Float16>::type;
   using AV = typename std::conditional<BF, bf16x8, halfx8>::type;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1962,6 +2014,10 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   constexpr int RPR = (U % 16 == 0 && NW <= 4 && 4 * U > RP) ? 4 * U : RP;  // red floats per (wave, row)
   constexpr int kStgOff = (NWV * 16 * RPR + 3 + 3) / 4 * 4;
   AT *stg = reinterpret_cast<AT *>(smem + kStgOff);
+  // IO waves: the G rows of step k in slot k & 3, [4][NW][16 U] floats,
+  // filled by LDS-DMA three steps ahead
+  float *ginl = smem + kStgOff + (NP * 16 * U + 7) / 8 * 4;  // 16-B aligned
+  float *outl = ginl + 4 * NW * 16 * U;  // (IO_OUT) [2][NW + 2][16 U]
   const float *Wd = p.w + d * p.pl_stride;
   const float *R = Wd + p.r_off;
   AT *xch = reinterpret_cast<AT *>(p.xch);
@@ -1981,7 +2037,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
         const float *rr = rrow(c);
 #pragma unroll
         for (int i = 0; i < KBW; i++) {
-          const int kb = w + NWV * i;
+          const int kb = w < CW ? w + CW * i : KB;
           if (kb < KB) {
 #pragma unroll
             for (int j = 0; j < 8; j++) mx = fmaxf(mx, fabsf(rr[kb * 32 + fq * 8 + j]));
@@ -2005,7 +2061,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     const int c = ct * 16 + fr;
 #pragma unroll
     for (int i = 0; i < KBW; i++) {
-      const int kb = w + NWV * i;
+      const int kb = w < CW ? w + CW * i : KB;
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         const float v = (c < NC && kb < KB) ? rrow(c)[kb * 32 + fq * 8 + j] : 0.f;
@@ -2045,7 +2101,47 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     for (int q = 0; q < NW; q++) p.G[grow + q * H] = act[q];
     p.aux[((long)t * N + n) * ldy + (long)d * H + u0 + eu] = cnew;
   };
-  gin_load(d == 0 ? 0 : T - 1, gin);
+  // IO waves: thread tid - 64 CW <-> element (ion, iou); G of step k into
+  // ginl[k & 1] before step k's K-reduction barrier
+  const int iot = tid - 64 * CW, ion = iot / U, iou = iot - ion * U;
+  const bool io_live = IOW && w >= CW && n0 + ion < nend;
+  // G row of forward-order step kk of this lane's element into slot kk & 3
+  // by LDS-DMA (lane l of IO wave v writes element 64 v + l); NW DMAs per
+  // call whatever kk, so that the waits can count them (rows past N and
+  // steps past T read a valid row and are never used)
+  auto io_dma = [&](int kk) {
+    const int tt = d == 0 ? min(kk, T - 1) : max(T - 1 - kk, 0);
+    const long gr = ((long)tt * N + n0 + (io_live ? ion : 0)) * ldg + (long)d * NW * H + u0 + iou;
+#pragma unroll
+    for (int q = 0; q < NW; q++) {
+      const unsigned dst = __builtin_amdgcn_readfirstlane(
+          (unsigned)reinterpret_cast<uintptr_t>(ginl + ((kk & 3) * NW + q) * 16 * U + (w - CW) * 64));
+      dma_lds_dword(p.G + gr + q * H, dst);
+    }
+  };
+  auto io_out = [&](int kk) {  // row-major outputs of step kk from outl[kk & 1]
+    if (!io_live) return;
+    const int tt = d == 0 ? kk : T - 1 - kk;
+    const float *o = outl + (long)(kk & 1) * (NW + 2) * 16 * U + iot;
+    const long yrow = ((long)tt * N + n0 + ion) * ldy + (long)d * H + u0 + iou;
+    const long grow = ((long)tt * N + n0 + ion) * ldg + (long)d * NW * H + u0 + iou;
+    p.y[yrow] = o[0];
+#pragma unroll
+    for (int q = 0; q < NW; q++) p.G[grow + q * H] = o[(1 + q) * 16 * U];
+    p.aux[yrow] = o[(NW + 1) * 16 * U];
+  };
+  if constexpr (IOW) {
+    if (w >= CW) {  // steps 0..2; step 0's in place before the loop's first barrier
+      io_dma(0);
+      io_dma(1);
+      io_dma(2);
+      if constexpr (NW == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    }
+    __syncthreads();
+  } else {
+    gin_load(d == 0 ? 0 : T - 1, gin);
+  }
   int bad = 0;
   unsigned *myflag = flag6(p, grp, d, g, NWG);
   // XCD-pinned (p.xpd): the hand-off goes through a ring of p.ring step images
@@ -2056,7 +2152,11 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // copies of the epochs 256 lines on: gflag = k in step k's load phase
   // (step k - 1's signal drained step k - 2's copy), T + 1 at exit -- "epoch
   // - 2 = last step out" as the unpinned flags
-  unsigned *gflag = (p.xpd && p.fcopy) ? myflag + 256 * kFlagStride : nullptr;
+  // (aggregated over the direction's workgroups by workgroup 0, as in
+  // rnn_bwd_rec6: agg_flag6 = k after the K-reduction barrier of step k, by
+  // which every producer's signal of step k - 1 drained its copy of step k - 2)
+  const bool fcopy = p.xpd && p.fcopy;
+  unsigned *gflag = (fcopy && g == 0) ? agg_flag6(p, grp, d) : nullptr;
   if (p.xpd && tid == 0) atomicOr(p.flags + kXcdWord, 1u << xcc_id());
   if (tid == 0) loc_lds = 0;
   const int local = (p.xpd && p.allow_local) ? probe6(p, grp, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
@@ -2068,7 +2168,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // before its data VGPRs are overwritten)
   u32x4 pv = u32x4{0u, 0u, 0u, 0u};
   // the per-step images as one loop-invariant buffer (chain_ok: T XS halves < 2 GB)
-  const auto crs = rsrc(xch, gflag ? (unsigned)(T * XS * sizeof(AT)) : 0u);
+  const auto crs = rsrc(xch, fcopy ? (unsigned)(T * XS * sizeof(AT)) : 0u);
   // publish geometry: store thread s < NP * 16 * CH: part = s / (16 CH), row, chunk
   const int sp = tid / (16 * CH), sn = (tid / CH) % 16, sch = tid % CH;
   const int kb0 = u0 >> 5, koff = (u0 & 31) + sch * 8;
@@ -2079,7 +2179,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   int wprod = -1;
   {
     constexpr int PPK = 32 / U;
-    const int i = lane / PPK, kb = w + NWV * i;
+    const int i = lane / PPK, kb = w < CW ? w + CW * i : KB;
     if (i < KBW && kb < KB) wprod = kb * PPK + lane % PPK;
   }
   const long gimg = (long)grp * XG;
@@ -2092,8 +2192,8 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
 #pragma unroll
     for (int ct = 0; ct < CT; ct++) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
     REC_TRACE(k, 0);
-    if (k > 0) {
-      if (p.wwait) {
+    if (k > 0 && (!IOW || w < CW)) {
+      if (p.wwait || IOW) {
         if (!wave_wait_prod(flag6(p, grp, d, 0, NWG), wprod, (unsigned)(k + 1), p.err, &bad_lds, p.poll_sleep)) bad = 1;
       } else {
         wait_flags6(flag6(p, grp, d, 0, NWG), NWG, (unsigned)(k + 1), p.err, bad, &bad_lds, p.poll_sleep);
@@ -2107,7 +2207,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
       // counts them exactly and the first MFMAs wait for their own loads only
 #pragma unroll
       for (int i = 0; i < KBW; i++) {
-        const int kb = w + NWV * i;
+        const int kb = w + CW * i;
         const long o = STK ? gimg + ((((long)d * KB + kb) * NP + (fr >> 3)) * 16 + (fr & 7)) * 32 + fq * 8
                            : gimg + ((((long)d * KB + kb) * NP) * 16 + fr) * 32 + fq * 8;
         const unsigned off = (kb < KB && arow_live) ? (unsigned)(o * sizeof(AT)) : 0x7fff0000u;
@@ -2125,14 +2225,11 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
       // branch makes the compiler's wait counts conservative)
       // (unconditional: without a consumer crs covers 0 bytes and the store is dropped)
       __builtin_amdgcn_raw_buffer_store_b128(pv, crs, pub ? (int)(po * sizeof(AT)) : 0x7ffffff0,
-                                             gflag ? (int)(tp * XS * sizeof(AT)) : 0, 16);
-      // and the epoch of the copy the last signal drained (step k - 2's):
-      // a write-through flag store left in flight at the signal would hold
-      // up the next step's first flag poll (one vmcnt for loads and stores)
-      if (gflag && tid == 0) __hip_atomic_store(gflag, (unsigned)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                             fcopy ? (int)(tp * XS * sizeof(AT)) : 0, 16);
+
 #pragma unroll
       for (int i = 0; i < KBW; i++) {
-        if (w + NWV * i < KB) {
+        if (w + CW * i < KB) {
           const AV a0 = __builtin_bit_cast(AV, ah[i]);
           if constexpr (BF) {
 #pragma unroll
@@ -2156,8 +2253,8 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     }
     asm volatile("" ::: "memory");
     // behind the hand-off loads: last step's row-major outputs, next step's input projection
-    if (t_prev >= 0 && !(p.nopf & 2)) out_store(t_prev);
-    if (k + 1 < T && !(p.nopf & 1)) gin_load(d == 0 ? t + 1 : t - 1, gnx);
+    if (!IO_OUT && t_prev >= 0 && !(p.nopf & 2)) out_store(t_prev);
+    if (!IOW && k + 1 < T && !(p.nopf & 1)) gin_load(d == 0 ? t + 1 : t - 1, gnx);
     // K partials through LDS.  U % 16 == 0: column ct * 16 + fr of the
     // tile is gate ct / (U / 16) of unit (ct % (U / 16)) * 16 + fr, so a lane
     // holds every gate of its (row, unit) elements: one float4 per (wave,
@@ -2172,30 +2269,39 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     }
     if constexpr (RED4) {
       constexpr int SU = U / 16;
+      if (w < CW) {
 #pragma unroll
-      for (int su = 0; su < SU; su++)
+        for (int su = 0; su < SU; su++)
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-          floatx4 v4 = floatx4{0.f, 0.f, 0.f, 0.f};
+          for (int i = 0; i < 4; i++) {
+            floatx4 v4 = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int q = 0; q < NW; q++) v4[q] = acc[q * SU + su][i];
-          st4(red + (((long)(w * 16 + fq * 4 + i) * U + su * 16 + fr) << 2), v4);
-        }
+            for (int q = 0; q < NW; q++) v4[q] = acc[q * SU + su][i];
+            st4(red + (((long)(w * 16 + fq * 4 + i) * U + su * 16 + fr) << 2), v4);
+          }
+      }
     } else {
 #pragma unroll
       for (int ct = 0; ct < CT; ct++)
 #pragma unroll
         for (int i = 0; i < 4; i++) red[(w * 16 + fq * 4 + i) * RP + ct * 16 + fr] = acc[ct][i];
     }
-    __syncthreads();
+    lds_barrier<IOW>();
     if (bad_lds) bad = 1;
+    // the aggregated epoch (before the signal: a write-through flag store
+    // left in flight there would hold up the next step's first flag poll)
+    if (gflag && k > 0 && tid == 0) __hip_atomic_store(gflag, (unsigned)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     REC_TRACE(k, 3);
     if (has_e) {
       float rh[NW];
       if constexpr (RED4) {
         floatx4 sm = *reinterpret_cast<const floatx4 *>(red + (((long)en * U + eu) << 2));  // fixed order
 #pragma unroll
-        for (int v = 1; v < NWV; v++) sm += *reinterpret_cast<const floatx4 *>(red + (((long)(v * 16 + en) * U + eu) << 2));
+        for (int v = 1; v < CW; v++) sm += *reinterpret_cast<const floatx4 *>(red + (((long)(v * 16 + en) * U + eu) << 2));
+        if constexpr (IOW) {  // this step's G row, put there by the IO waves
+#pragma unroll
+          for (int q = 0; q < NW; q++) gin[q] = ginl[((k & 3) * NW + q) * 16 * U + tid];
+        }
 #pragma unroll
         for (int q = 0; q < NW; q++) rh[q] = BF ? sm[q] : ldexpf(sm[q], sOut);
       } else {
@@ -2227,11 +2333,20 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
       }
       if (!live) h = 0.f;
       hval = h;
+      if constexpr (IO_OUT) {  // outputs for the IO waves (stored during the next step)
+        float *o = outl + (long)(k & 1) * (NW + 2) * 16 * U + tid;
+        o[0] = h;
+#pragma unroll
+        for (int q = 0; q < NW; q++) o[(1 + q) * 16 * U] = act[q];
+        o[(NW + 1) * 16 * U] = cnew;
+      }
       // the next step's input projection (loaded behind this step's hand-off
       // loads) moves in here, before any write-through store is in flight:
       // the wait for it must not cover the sc1 stores issued after the signal
+      if constexpr (!IOW) {
 #pragma unroll
-      for (int q = 0; q < NW; q++) gin[q] = gnx[q];
+        for (int q = 0; q < NW; q++) gin[q] = gnx[q];
+      }
       if constexpr (BF) {
         stg[en * U + eu] = (__bf16)h;
       } else {
@@ -2241,7 +2356,36 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
         stg[(16 + en) * U + eu] = hl;
       }
     }
-    __syncthreads();
+    if (IOW && w >= CW) {
+      // IO waves, while the cell threads work: step k + 1's G (loaded during
+      // step k - 1) into its slot -- read by the cell threads after the next
+      // K-reduction barrier; the slot's step k - 1 readers passed the
+      // barrier below last step -- then step k + 2's loads, then the
+      // row-major outputs of step k - 1 (written before the last barrier;
+      // their slot is rewritten after the next K-reduction barrier)
+      if (!(p.nopf & 1)) {
+        // step k + 3's G into slot (k + 3) & 3 (last read by the cell threads
+        // of step k - 1, before the last barrier), then wait for the DMAs
+        // issued up to step k - 2: step k + 1's G is in place before the
+        // barrier below, two steps after it was asked for
+        io_dma(k + 3);
+        if constexpr (NW == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      }
+      if ((p.nopf & 4) && io_live && k + 2 < T) {
+        // diagnostic (KCTC_DIAG_NOPF=5): the same G loads, never waited for
+        // (inline asm: the compiler does not count them) -- timing only
+        const int tt = d == 0 ? k + 2 : T - 3 - k;
+        const float *gp = p.G + ((long)tt * N + n0 + ion) * ldg + (long)d * NW * H + u0 + iou;
+#pragma unroll
+        for (int q = 0; q < NW; q++) {
+          float dummy;
+          asm volatile("global_load_dword %0, %1, off" : "=v"(dummy) : "v"(gp + q * H) : "memory");
+        }
+      }
+      if (IO_OUT && k > 0 && !(p.nopf & 2)) io_out(k - 1);
+    }
+    lds_barrier<IOW>();
     if (pub) {
       pv = *reinterpret_cast<const u32x4 *>(stg + (sp * 16 + sn) * U + sch * 8);
       const auto ro = rsrc(xch + (p.ring ? rbase + (long)(k % p.ring) * XS : (long)t * XS), (unsigned)(XS * sizeof(AT)));
@@ -2271,11 +2415,22 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     t_prev = t;
     REC_TRACE(k, 5);
   }
-  if (t_prev >= 0 && !bad) out_store(t_prev);
-  if (gflag && !bad) {  // the last step's copy, then its epoch
+  if (IOW && w >= CW) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the IO waves' DMAs (ahead of T) land
+  if (t_prev >= 0 && !bad) {
+    if constexpr (IO_OUT) {
+      if (w >= CW) io_out(T - 1);  // outl of the last step: written before the loop's last barrier
+    } else {
+      out_store(t_prev);
+    }
+  }
+  if (fcopy && !bad) {  // the last step's copy, then (workgroup 0) every producer's, then the epoch
     if (pub) __builtin_amdgcn_raw_buffer_store_b128(pv, rsrc(xch + (long)t_prev * XS, (unsigned)(XS * sizeof(AT))),
                                                     (int)(po * sizeof(AT)), 0, 16);
-    signal_epoch(gflag, (unsigned)(T + 1), 0);
+    signal_epoch(myflag, (unsigned)(T + 2), local);
+    if (gflag) {
+      wait_flags6(flag6(p, grp, d, 0, NWG), NWG, (unsigned)(T + 2), p.err, bad, &bad_lds, p.poll_sleep);
+      if (!bad && tid == 0) __hip_atomic_store(gflag, (unsigned)(T + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   asm volatile("" ::"v"(pv));
   if (bad && tid == 0) atomicOr(p.err, 1u);
@@ -2332,9 +2487,11 @@ static void launch6_shape(bool fwd, const RecParams &p, dim3 grid, size_t lds, h
     if (fwd) {
       set_lds(rnn_fwd_rec6<MODE, U, H, NTH, P>, lds);
       hipLaunchKernelGGL((rnn_fwd_rec6<MODE, U, H, NTH, P>), grid, dim3(NTH), lds, s, p);
-    } else {
+    } else if constexpr ((P & 4) == 0) {
       set_lds(rnn_bwd_rec6<MODE, U, H, NTH, P>, lds);
       hipLaunchKernelGGL((rnn_bwd_rec6<MODE, U, H, NTH, P>), grid, dim3(NTH), lds, s, p);
+    } else {
+      throw std::logic_error("v6 recurrence: IO waves are a forward variant");
     }
   } else {
     throw std::logic_error("v6 recurrence: shape not compiled");
@@ -2367,6 +2524,13 @@ static void launch6_u(bool fwd, int nth, const RecParams &p, dim3 grid, size_t l
         if constexpr (P == kPrecX3) {
           if (p.gs <= 8 && stk) {
             launch6_h<MODE, 16, 512, kPrecX3S>(fwd, p, grid, lds, s);
+            break;
+          }
+        }
+        // forward with IO waves (the G loads off the hand-off waves; KCTC_FWD_IOW=0: all waves hand off)
+        if constexpr (MODE == kLstm || MODE == kGru) {
+          if (fwd && env_int("KCTC_FWD_IOW", 1)) {
+            launch6_h<MODE, 16, 512, P | 4>(fwd, p, grid, lds, s);
             break;
           }
         }
@@ -2572,7 +2736,8 @@ static int pick_bwd_u6(const RnnDesc &d, int N) { return pick6(d, N, false).U; }
 static size_t fwd6_lds_bytes(const RnnDesc &d, const V6Cfg &c) {
   const int CT = (d.nw() * c.U + 15) / 16, nwv = c.nth / 64, np = d.prec == kPrecBf16 ? 1 : 2;
   const size_t rp = std::max(CT * 16 + 1, 4 * c.U);  // rnn_fwd_rec6's RPR (float4 K partials)
-  const size_t b = sizeof(float) * (nwv * 16 * rp + 8) + np * 16 * (size_t)c.U * 2 + 16;
+  const size_t b = sizeof(float) * (nwv * 16 * rp + 8) + np * 16 * (size_t)c.U * 2 + 16 +
+                   sizeof(float) * 16 * c.U * (4 * d.nw() + 2 * (d.nw() + 2)) + 16;  // + the IO waves' G and output slots
   return std::max(b, (size_t)96 * 1024);  // one recurrence workgroup per CU
 }
 static size_t bwd6_lds_bytes(const RnnDesc &d, const V6Cfg &c) {
@@ -2710,6 +2875,11 @@ bool chain_ok(const RnnDesc &d, int ver, int T, int N, const RnnFwdChain *c) {
   // the CUs left beside the 128-workgroup recurrence outlasts it (990k ->
   // 728k and 560k -> 389k frames/s measured), the 256-tile GEMM after it wins
   if ((N > 16 || d.prec == kPrecBf16) && !env_int("KCTC_STREAM_ALL", 0)) return false;
+  // an XCD-pinned producer runs faster alone: beside the streamed projection
+  // (HBM traffic on the other XCDs) its steps took 0.17-0.3 us longer, more
+  // than the 256-tile GEMM after it costs (configs[1]: 555.9k vs 564.8k
+  // frames/s same box); KCTC_FWD_STREAM_PINNED=1 streams anyway
+  if (xcd_mask(d, N, true) && !env_int("KCTC_FWD_STREAM_PINNED", 0)) return false;
   const V6Cfg c6 = pick6(d, N, true);
   if (!c6 || !stream_block_budget(d.dirs * (d.H / c6.U) * c6.rg, false)) return false;
   const long xs = 2L * (d.H / 32) * (d.prec == kPrecBf16 ? 1 : 2) * 16 * 32 * pick6(d, N, true).rg;  // halves per step image
@@ -2749,8 +2919,8 @@ void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
   x.batch = n.dirs; x.sB = (long)G * KB * 64; x.seB = bf ? 0 : G; x.sC = G; x.sBias = pls;
   x.tile_counter = reinterpret_cast<int *>(static_cast<char *>(c.workspace) + flags_offset(n, T, N));
   // XCD-pinned producer: the sc1 copies of its epochs, no block on its XCDs
-  x.stream_flags = p.flags + 1024 + (p.xpd ? 256 * kFlagStride : 0);
-  x.stream_nwg = p.nwg; x.stream_T = T; x.stream_N = N;
+  x.stream_flags = p.flags + 1024 + (p.xpd ? 256 * kFlagStride : 0);  // pinned: agg_flag6 lines
+  x.stream_nwg = p.xpd ? 1 : p.nwg; x.stream_T = T; x.stream_N = N;
   const int pinned = p.xpd ? d.dirs * p.rg : 0;
   if (pinned) { x.stream_xcd_word = p.flags + kXcdWord; x.stream_xcd_count = pinned; }
   x.stream_group_step = 2L * (d.H / 32) * (bf ? 1 : 2) * 16 * 32;  // rnn_fwd_rec6's XG
@@ -2962,8 +3132,8 @@ void launch_bwd_stream(const RnnDesc &d, const RecParams &p, int l, const float 
   a.cnt = pk<int>(workspace, d, T, N, pl.cnt);
   // XCD-pinned recurrence: its epochs' sc1 copies (the L2 flags are not
   // visible here), and no block on the recurrence's XCDs
-  a.flags = p.flags + 1024 + (p.xpd ? 256 * kFlagStride : 0);
-  a.nwg = p.nwg; a.T = T; a.Nf = N; a.err = err; a.rg = p.rg;
+  a.flags = p.flags + 1024 + (p.xpd ? 256 * kFlagStride : 0);  // pinned: agg_flag6 lines
+  a.nwg = p.xpd ? 1 : p.nwg; a.T = T; a.Nf = N; a.err = err; a.rg = p.rg;
   const int pinned = p.xpd ? d.dirs * p.rg : 0;
   if (pinned) { a.xcd_word = p.flags + kXcdWord; a.xcd_count = pinned; }
   // 96 measured best at configs[1]; never more than the CU budget leaves

@@ -46,8 +46,18 @@ def test_pinned_bit_identical(kctc, gpu, mode, N, T, var):
                              max_seq_length=T, rnn_mode=mode)
     feats, nf, fl, ll = kctc.synth_minibatch(7 + N, T, N, D, A, 0.125)
     batch = (feats, nf, fl, ll, T, N)
-    a = _train(kctc, gpu, cfg, batch, pinned=False, var=var)
-    b = _train(kctc, gpu, cfg, batch, pinned=True, var=var)
+    # the pinned forward's streamed projection (off by default, rnn.hip
+    # chain_ok) is part of what the forward case checks
+    old = os.environ.get("KCTC_FWD_STREAM_PINNED")
+    os.environ["KCTC_FWD_STREAM_PINNED"] = "1"
+    try:
+        a = _train(kctc, gpu, cfg, batch, pinned=False, var=var)
+        b = _train(kctc, gpu, cfg, batch, pinned=True, var=var)
+    finally:
+        if old is None:
+            os.environ.pop("KCTC_FWD_STREAM_PINNED", None)
+        else:
+            os.environ["KCTC_FWD_STREAM_PINNED"] = old
     assert a[0] == b[0]
     for x, y in zip(a[1], b[1]):
         np.testing.assert_array_equal(x, y)
