@@ -1465,8 +1465,14 @@ __device__ int probe6(const RecParams &p, int grp, int d, int g, int nwg, int &b
 // it: a pending LDS-DMA there merges into the other waves' code paths of
 // the same kernel and turns their exact vmcnt waits into vmcnt(0).  The
 // issuing wave waits for it with explicit s_waitcnt and reads none of it.
+// M0 (a reserved register) is saved and restored inside the statement.
 __device__ __forceinline__ void dma_lds_dword(const float *g, unsigned lds) {
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(lds) : "memory", "m0");
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g), "s"(lds)
+      : "memory");
 }
 
 // Workgroup barrier for LDS hand-offs.  RAW = true: the LDS writes drained
@@ -2214,6 +2220,10 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
         ah[i] = ld_sc1(rs, off);
         if constexpr (!BF && !STK) al[i] = ld_sc1(rs, off + 16 * 32 * sizeof(AT));
       }
+      // all hand-off loads in flight before the first MFMA waits: without
+      // this the scheduler (U = 32) issued the second k block's loads only
+      // after the first block's MFMAs, one more L2 round trip per step
+      __builtin_amdgcn_sched_barrier(0);
       // the streamed projection's write-through copy of the previous step's
       // image (pv still holds it), issued behind this step's hand-off loads:
       // gfx9 counts stores and loads in one vmcnt, so a write-through store
@@ -2736,8 +2746,10 @@ static int pick_bwd_u6(const RnnDesc &d, int N) { return pick6(d, N, false).U; }
 static size_t fwd6_lds_bytes(const RnnDesc &d, const V6Cfg &c) {
   const int CT = (d.nw() * c.U + 15) / 16, nwv = c.nth / 64, np = d.prec == kPrecBf16 ? 1 : 2;
   const size_t rp = std::max(CT * 16 + 1, 4 * c.U);  // rnn_fwd_rec6's RPR (float4 K partials)
+  // + the IO waves' G (and output) slots, for the shape that runs them (launch6_u)
+  const bool iow = c.U == 16 && c.nth == 512;
   const size_t b = sizeof(float) * (nwv * 16 * rp + 8) + np * 16 * (size_t)c.U * 2 + 16 +
-                   sizeof(float) * 16 * c.U * (4 * d.nw() + 2 * (d.nw() + 2)) + 16;  // + the IO waves' G and output slots
+                   (iow ? sizeof(float) * 16 * c.U * (4 * d.nw() + 2 * (d.nw() + 2)) + 16 : 0);
   return std::max(b, (size_t)96 * 1024);  // one recurrence workgroup per CU
 }
 static size_t bwd6_lds_bytes(const RnnDesc &d, const V6Cfg &c) {
