@@ -2043,7 +2043,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
         const float *rr = rrow(c);
 #pragma unroll
         for (int i = 0; i < KBW; i++) {
-          const int kb = w < CW ? w + CW * i : KB;
+          const int kb = (!IOW || w < CW) ? w + CW * i : KB;
           if (kb < KB) {
 #pragma unroll
             for (int j = 0; j < 8; j++) mx = fmaxf(mx, fabsf(rr[kb * 32 + fq * 8 + j]));
@@ -2067,7 +2067,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     const int c = ct * 16 + fr;
 #pragma unroll
     for (int i = 0; i < KBW; i++) {
-      const int kb = w < CW ? w + CW * i : KB;
+      const int kb = (!IOW || w < CW) ? w + CW * i : KB;
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         const float v = (c < NC && kb < KB) ? rrow(c)[kb * 32 + fq * 8 + j] : 0.f;
@@ -2161,7 +2161,10 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // (aggregated over the direction's workgroups by workgroup 0, as in
   // rnn_bwd_rec6: agg_flag6 = k after the K-reduction barrier of step k, by
   // which every producer's signal of step k - 1 drained its copy of step k - 2)
-  const bool fcopy = p.xpd && p.fcopy;
+  // (compiled into the IO-wave variant only, the one chain_ok lets stream
+  // off a pinned producer: the dead code of it in the other variants changed
+  // their schedules -- U = 32 forward 3.19 -> 4.0 us/step at configs[2])
+  const bool fcopy = IOW && p.xpd && p.fcopy;
   unsigned *gflag = (fcopy && g == 0) ? agg_flag6(p, grp, d) : nullptr;
   if (p.xpd && tid == 0) atomicOr(p.flags + kXcdWord, 1u << xcc_id());
   if (tid == 0) loc_lds = 0;
@@ -2185,7 +2188,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   int wprod = -1;
   {
     constexpr int PPK = 32 / U;
-    const int i = lane / PPK, kb = w < CW ? w + CW * i : KB;
+    const int i = lane / PPK, kb = (!IOW || w < CW) ? w + CW * i : KB;
     if (i < KBW && kb < KB) wprod = kb * PPK + lane % PPK;
   }
   const long gimg = (long)grp * XG;
@@ -2279,7 +2282,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     }
     if constexpr (RED4) {
       constexpr int SU = U / 16;
-      if (w < CW) {
+      if (!IOW || w < CW) {
 #pragma unroll
         for (int su = 0; su < SU; su++)
 #pragma unroll
@@ -2343,6 +2346,12 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
       }
       if (!live) h = 0.f;
       hval = h;
+      if constexpr (!IOW) {
+        // the next step's input projection (loaded behind this step's
+        // hand-off loads) moves in here
+#pragma unroll
+        for (int q = 0; q < NW; q++) gin[q] = gnx[q];
+      }
       if constexpr (IO_OUT) {  // outputs for the IO waves (stored during the next step)
         float *o = outl + (long)(k & 1) * (NW + 2) * 16 * U + tid;
         o[0] = h;
@@ -2350,13 +2359,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
         for (int q = 0; q < NW; q++) o[(1 + q) * 16 * U] = act[q];
         o[(NW + 1) * 16 * U] = cnew;
       }
-      // the next step's input projection (loaded behind this step's hand-off
-      // loads) moves in here, before any write-through store is in flight:
-      // the wait for it must not cover the sc1 stores issued after the signal
-      if constexpr (!IOW) {
-#pragma unroll
-        for (int q = 0; q < NW; q++) gin[q] = gnx[q];
-      }
+
       if constexpr (BF) {
         stg[en * U + eu] = (__bf16)h;
       } else {
@@ -2892,6 +2895,11 @@ bool chain_ok(const RnnDesc &d, int ver, int T, int N, const RnnFwdChain *c) {
   // than the 256-tile GEMM after it costs (configs[1]: 555.9k vs 564.8k
   // frames/s same box); KCTC_FWD_STREAM_PINNED=1 streams anyway
   if (xcd_mask(d, N, true) && !env_int("KCTC_FWD_STREAM_PINNED", 0)) return false;
+  // and only the IO-wave variant (U = 16, 512 threads) carries the copies
+  // (launch6_u: U = 16 / 512 threads, KCTC_FWD_IOW, not the stacked variant)
+  if (xcd_mask(d, N, true) && !(pick6(d, N, true).U == 16 && pick6(d, N, true).nth == 512 &&
+                                env_int("KCTC_FWD_IOW", 1) && !env_int("KCTC_STK", 0)))
+    return false;
   const V6Cfg c6 = pick6(d, N, true);
   if (!c6 || !stream_block_budget(d.dirs * (d.H / c6.U) * c6.rg, false)) return false;
   const long xs = 2L * (d.H / 32) * (d.prec == kPrecBf16 ? 1 : 2) * 16 * 32 * pick6(d, N, true).rg;  // halves per step image
