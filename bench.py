@@ -20,8 +20,16 @@ CU-masked share of it (kctc_set_cu_partition) -- a rehearsal of the N-rank
 path on a one-GPU box, not a throughput configuration.
 
 Before the timed region the bench checks the loss: one train step of the
-committed full-size fixture (tests/golden/sketch_step.npz, fp64 oracle, same
-parameters and minibatch) must match at 1e-4 (`loss_match`).
+committed full-size fixture of the measured config (tests/golden/
+sketch_step*.npz, fp64 oracle, same parameters and minibatch) must match at
+1e-4 -- configs[4] (bf16 operands) at its error model's per-output bar
+(tests/sketch_common.py) -- (`loss_match`).
+
+`value` is the HBM-resident pass (the measurement contract: inputs resident
+when the timed region starts; the trainer's boundary takes device features).
+`h2d_inclusive` repeats the K steps with the features copied from pinned host
+memory inside every step -- SURVEY §8d's timed region, which starts at the
+H2D copy -- and is reported beside it.
 
 Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (HIP
 events on the trainer's stream over the timed region) and a CPU baseline
@@ -210,24 +218,29 @@ def pmc_traffic(kernel):
 
 
 # ---- checks and baselines ---------------------------------------------------------
-def loss_match(k, dev):
-    """One train step of the committed full-size fixture (tests/golden/
-    sketch_step.npz, generated by tests/golden/make_sketch.py with the fp64
-    oracle): 5 x BLSTM-512, N=16, T_max=2000, the fixture's parameters and
+def loss_match(k, dev, case="cfg1"):
+    """One train step of the committed full-size fixture of `case` (tests/golden/
+    sketch_step*.npz, generated by tests/golden/make_sketch.py with the fp64
+    oracle): configs[1] / [2] / [4] at their shapes, the fixture's parameters and
     bench.py's first minibatch.  Reports the per-utterance cost error, the
     network output's and every applied gradient's sketch error (norm-wise
     relative, tests/sketch_common.py) and the best-path flips against the
-    fp64 output, with the 1e-4 bar."""
+    fp64 output, each with its bar: 1e-4, or for configs[4] (bf16 operands)
+    the error model's tolerance of that output (sketch_common.bf16_tol)."""
     import torch
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import sketch_common as S
-    g = np.load(os.path.join(ROOT, "tests", "golden", "sketch_step.npz"))
-    s = S.STEP
+    s = S.STEPS[case]
+    g = np.load(os.path.join(ROOT, "tests", "golden", s["file"] + ".npz"))
     T, N, D, H, A, R = s["T"], s["N"], s["D"], s["H"], s["A"], s["R"]
-    rnn, Wa, ba = S.step_params(S.ProductLayout(k))
-    feats, nf, fl, ll = S.step_inputs(k)
+    bf16 = s.get("prec") == "bf16"
+    tol = (lambda what, c=0: float(S.bf16_tol(S.step_stages(R, what, c)))) if bf16 else (lambda what, c=0: LOSS_BAR)
+    rnn, Wa, ba = S.step_params(S.ProductLayout(k), case)
+    feats, nf, fl, ll = S.step_inputs(k, case)
     net = k.Nnet(k.recipe_config(num_rnn=R, input_dim=D, hidden=H, num_targets=A, learning_rate=s["lr"],
-                                 max_seq_length=T), seed=1, device=dev.index)
+                                 max_seq_length=T, rnn_mode=s["mode"]), seed=1, device=dev.index)
+    if bf16:
+        net.set_precision("bf16")
     rnn_idx = [1 + 2 * c for c in range(R)]
     aff_idx = 2 * R + 1
     for c, i in enumerate(rnn_idx):
@@ -238,23 +251,29 @@ def loss_match(k, dev):
     costs = net.last_costs(N)
     rc = np.abs(costs - g["costs"]) / np.abs(g["costs"])
     logits = net.last_output(T, N, A)
-    e_log = S.compare(logits, S.load(g, "logits"), 500, LOSS_BAR)
-    errs = [S.compare(np.clip(net.get_grad(i).astype(np.float64), -5.0, 5.0), S.load(g, f"g{c}"), 600 + c,
-                      LOSS_BAR) for c, i in enumerate(rnn_idx)]
-    errs.append(S.compare(net.get_grad(aff_idx).astype(np.float64), S.load(g, "gaff"), 700, LOSS_BAR))
+    table = {"costs": (float(rc.max()), tol("costs")),
+             "tot_objf": (abs(objf - float(g["tot_objf"])) / abs(float(g["tot_objf"])), tol("costs"))}
+    e = S.compare(logits, S.load(g, "logits"), 500, tol("logits"))
+    table["logits"] = (max(e["norm"], e["proj"]), tol("logits"))
+    for c, i in enumerate(rnn_idx):
+        e = S.compare(np.clip(net.get_grad(i).astype(np.float64), -5.0, 5.0), S.load(g, f"g{c}"), 600 + c,
+                      tol("grad", c))
+        table[f"grad_rnn{c}"] = (max(e["norm"], e["proj"]), tol("grad", c))
+    e = S.compare(net.get_grad(aff_idx).astype(np.float64), S.load(g, "gaff"), 700, tol("affine"))
+    table["grad_affine"] = (max(e["norm"], e["proj"]), tol("affine"))
     ids = net.last_best_path(T, N)
     net.close()
-    out = {"fixture": "tests/golden/sketch_step.npz (fp64 oracle, configs[1] step, params pseed 77, "
-                      "minibatch seed 20161015)",
-           "max_rel_cost": float(rc.max()),
-           "tot_objf_rel": abs(objf - float(g["tot_objf"])) / abs(float(g["tot_objf"])),
-           "logits_sketch_err": max(e_log["norm"], e_log["proj"]),
-           "grad_sketch_err": max(max(e["norm"], e["proj"]) for e in errs),
+    grads = [v[0] for key, v in table.items() if key.startswith("grad_")]
+    out = {"fixture": f"tests/golden/{s['file']}.npz (fp64 oracle, {case} step, params pseed {s['pseed']}, "
+                      f"minibatch seed {s['seed']})",
+           "max_rel_cost": table["costs"][0], "tot_objf_rel": table["tot_objf"][0],
+           "logits_sketch_err": table["logits"][0], "grad_sketch_err": max(grads),
            "best_path_flips": int(np.sum(ids != g["ids"])), "frames": int(ids.size),
-           "objf_per_label": objf / wt, "bar": LOSS_BAR}
-    out["pass"] = bool(out["max_rel_cost"] < LOSS_BAR and out["tot_objf_rel"] < LOSS_BAR and
-                       out["logits_sketch_err"] < LOSS_BAR and out["grad_sketch_err"] < LOSS_BAR and
-                       wt == float(g["tot_weight"]))
+           "objf_per_label": objf / wt,
+           "bar": "bf16 error model per output (tests/sketch_common.bf16_tol)" if bf16 else LOSS_BAR,
+           "errors_vs_bar": {key: {"err": float("%.3g" % v[0]), "bar": float("%.3g" % v[1])}
+                             for key, v in table.items()}}
+    out["pass"] = bool(all(v[0] < v[1] for v in table.values()) and wt == float(g["tot_weight"]))
     return out
 
 
@@ -343,8 +362,8 @@ def main():
                    else "gradient sum every step"}
 
     lm = None
-    if rank == 0 and not args.no_loss_match and args.config == 1 and (T, N, H, L) == (2000, 16, 512, 5):
-        lm = loss_match(k, dev)
+    if rank == 0 and not args.no_loss_match and (T, N, H, L) == (cf["T"], cf["N"], cf["H"], 5):
+        lm = loss_match(k, dev, {1: "cfg1", 2: "cfg2", 4: "cfg4"}[args.config])
 
     total = args.warmup + args.steps
     batches, host_batches = [], []
@@ -457,10 +476,26 @@ def main():
     engine = "bf16 MFMA (dense 2.5 PF)" if bf16 else "split-fp16 x3 on the f16 MFMA (2.5 PF / 3)"
     roof = None
     if prof:
-        dom = max((f for f in prof if f in fam_flops), key=lambda f: prof[f][0])
-        ms, n = prof[dom]
+        # the dominant KERNEL: the four GEMM families all run the packed GEMM
+        # kernel (gemm_p256 / gemm_x3p), so they are priced together against
+        # each recurrence kernel
+        kernels = {"rnn_fwd_rec": ["rnn_fwd_rec"], "rnn_bwd_rec": ["rnn_bwd_rec"],
+                   "gemm_p256 (gate GEMMs: fwd_proj, bwd_data, bwd_w, bwd_r)":
+                       ["gemm_fwd_proj", "gemm_bwd_data", "gemm_bwd_w", "gemm_bwd_r"]}
+        # a family some of whose layers ran as a streamed GEMM (its own span
+        # family) has fewer launches than layers: count that share of its FLOPs
+        per_step = {"gemm_fwd_proj": L, "gemm_bwd_data": L - 1, "gemm_bwd_w": L, "gemm_bwd_r": L,
+                    "rnn_fwd_rec": L, "rnn_bwd_rec": L}
+
+        def fam_share(f):
+            return min(1.0, prof[f][1] / args.steps / max(per_step[f], 1))
+        ktime = {kn: (sum(prof[f][0] for f in fams if f in prof), sum(prof[f][1] for f in fams if f in prof),
+                      sum(fam_flops[f] * fam_share(f) for f in fams if f in prof) * args.steps)
+                 for kn, fams in kernels.items()}
+        dom = max((kn for kn in ktime if ktime[kn][1]), key=lambda kn: ktime[kn][0])
+        ms, n, flops_total = ktime[dom]
         avg_s = ms / n / 1e3
-        flops_per_launch = fam_flops[dom] / (n / args.steps)
+        flops_per_launch = flops_total / n
         achieved = flops_per_launch / avg_s / 1e12
         traffic, tsrc = pmc_traffic(dom) if args.config == 1 else (None, None)
         roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak_mfma, "unit": "TFLOP/s",
@@ -468,7 +503,8 @@ def main():
                 "kernel": dom, "avg_launch_ms": round(ms / n, 4), "flops_per_launch": flops_per_launch,
                 "engine": {"name": engine, "peak": round(peak_engine, 1),
                            "frac": round(achieved / peak_engine, 4)},
-                "families_ms_per_step": {f: round(prof[f][0] / args.steps, 3) for f in prof}}
+                "families_ms_per_step": {f: round(prof[f][0] / args.steps, 3) for f in prof},
+                "families_launches_per_step": {f: round(prof[f][1] / args.steps, 2) for f in prof}}
         aux = {}
         # the recurrences are serial over T: their step latency is the figure
         # that bounds them

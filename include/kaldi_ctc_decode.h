@@ -47,14 +47,19 @@ int kctc_ctc_decodable(struct ihipStream_t *stream, const float *probs, int T, i
                        float prob_scale, float blank_threshold, float floor_value, float *out, void *scratch,
                        int *num_kept);
 
-/* forward pass of the whole network: feats_dev [T_max*N][input_dim] ->
+/* forward pass of the whole network: feats_dev [T_max*N*num_splice][input_dim]
+ * (FormatNnetInput layout, num_splice = 1 + left + right context,
+ * kctc_nnet_context; the caller's buffer must hold that many rows) ->
  * out_dev [T_max*N][output_dim] (device), len = T_max*N*output_dim */
 int kctc_nnet_propagate(kctcNnet_t nnet, const float *feats_dev, int T_max, int N, float *out_dev, long len);
 
-/* CtcDecodableAmNnet for one utterance feats_dev [T][input_dim] with the
- * model's priors (an nnet2-ctc model file read by kctc_am_nnet_read): writes
- * the kept rows of the [T][A] log-likelihood matrix to out_host (capacity
- * T*A floats), *num_rows = rows kept. */
+/* CtcDecodableAmNnet for one utterance feats_dev [T][input_dim] (plain
+ * feature rows) with the model's priors (an nnet2-ctc model file read by
+ * kctc_am_nnet_read), pad_input = true (the reference's default): a network
+ * with frame context sees the first / last frame repeated LeftContext /
+ * RightContext times (NnetComputer, src/nnet2/nnet-compute.cc:64-90), so T
+ * frames give T rows.  Writes the kept rows of the [T][A] log-likelihood
+ * matrix to out_host (capacity T*A floats), *num_rows = rows kept. */
 int kctc_am_nnet_decodable(kctcNnet_t nnet, const float *feats_dev, int T, float prob_scale,
                            float blank_threshold, float *out_host, int *num_rows);
 

@@ -23,8 +23,9 @@
  *   kctc_nnet_enable_dp     <- (new) data parallelism: RCCL all-reduce of the
  *                              weight gradients over xGMI; replaces the recipe's
  *                              per-iteration model averaging (nnet-am-average)
- * Features are device pointers in the time-major [T_max*N][dim] layout of
- * FormatNnetInput; labels/lengths are host arrays.  Return 0 on success,
+ * Features are device pointers in the time-major [T_max*N*num_splice][dim]
+ * layout of FormatNnetInput (num_splice = 1 for context-free networks);
+ * labels/lengths are host arrays.  Return 0 on success,
  * non-zero on error (kctc_last_error() describes it).
  */
 #ifndef KALDI_CTC_AMD_KALDI_CTC_TRAIN_H_
@@ -83,8 +84,12 @@ int kctc_nnet_last_best_path(kctcNnet_t nnet, int *ids, long len);
 int kctc_nnet_last_costs(kctcNnet_t nnet, double *costs, int N);
 int kctc_nnet_last_output(kctcNnet_t nnet, float *host, long len);
 
-/* One SGD minibatch.  feats_dev [T_max*N][input_dim] (device, zero padded).
- * Outputs: sum of CTC costs, accuracy numerator (sum L - edits), weight (sum L). */
+/* One SGD minibatch.  feats_dev [T_max*N*num_splice][input_dim] (device,
+ * zero padded; num_splice = 1 + left + right context of kctc_nnet_context,
+ * 1 for the recipe's networks): the call reads exactly that many rows, so a
+ * buffer laid out for another context is an out-of-bounds read, not an error
+ * the library can see.  Outputs: sum of CTC costs, accuracy numerator
+ * (sum L - edits), weight (sum L). */
 int kctc_nnet_train_step(kctcNnet_t nnet, const float *feats_dev, int T_max, int N,
                          const int *num_frames, const int *flat_labels, const int *label_lengths,
                          double *tot_objf, double *tot_accuracy, double *tot_weight);
@@ -101,6 +106,7 @@ int kctc_nnet_train_step_async(kctcNnet_t nnet, const float *feats_dev, int T_ma
 int kctc_nnet_train_flush(kctcNnet_t nnet, int *have_stats, double *tot_objf, double *tot_accuracy,
                           double *tot_weight);
 
+/* ComputeNnetObjf: the same input layout as kctc_nnet_train_step, no update */
 int kctc_nnet_compute_objf(kctcNnet_t nnet, const float *feats_dev, int T_max, int N,
                            const int *num_frames, const int *flat_labels,
                            const int *label_lengths, double *tot_objf, double *tot_accuracy,

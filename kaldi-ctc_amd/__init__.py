@@ -426,7 +426,19 @@ class Nnet:
         _tcheck(lib().kctc_nnet_last_output(self.h, out.ctypes.data, out.size), "last_output")
         return out
 
+    def _check_feats(self, feats, T, N):
+        """feats must hold the FormatNnetInput rows of this network's context:
+        T*N*(1 + left + right) rows of input_dim (the C ABI reads exactly that)."""
+        l, r = self.context
+        rows = T * N * (1 + l + r)
+        if feats.dim() != 2 or feats.shape[0] != rows:
+            raise KctcError(f"feats has shape {tuple(feats.shape)}; this network (context -{l}..+{r}) reads "
+                            f"[T*N*{1 + l + r} = {rows}, input_dim] rows")
+        if not feats.is_contiguous():
+            raise KctcError("feats must be contiguous")
+
     def _step(self, fn, feats, T, N, num_frames, flat_labels, label_lengths):
+        self._check_feats(feats, T, N)
         nf = np.ascontiguousarray(num_frames, dtype=np.int32)
         fl = np.ascontiguousarray(flat_labels, dtype=np.int32)
         if fl.size == 0:
@@ -446,13 +458,17 @@ class Nnet:
         return l.value, r.value
 
     def train_step(self, feats, T, N, num_frames, flat_labels, label_lengths):
-        """DoBackprop on one minibatch; feats: device [T*N, D]. -> (objf, accuracy, weight)"""
+        """DoBackprop on one minibatch; feats: device [T*N*num_splice, D] (the
+        FormatNnetInput layout, num_splice = 1 + left + right of `context`).
+        -> (objf, accuracy, weight)"""
         return self._step(lib().kctc_nnet_train_step, feats, T, N, num_frames, flat_labels, label_lengths)
 
     def train_step_async(self, feats, T, N, num_frames, flat_labels, label_lengths):
         """Queue a training step (feats must stay alive until its stats come
         back); returns the stats of the minibatch queued before the previous
-        one once two are in flight, else None (kctc_nnet_train_step_async)."""
+        one once two are in flight, else None (kctc_nnet_train_step_async).
+        feats: device [T*N*num_splice, D] as for train_step."""
+        self._check_feats(feats, T, N)
         nf = np.ascontiguousarray(num_frames, dtype=np.int32)
         fl = np.ascontiguousarray(flat_labels, dtype=np.int32)
         if fl.size == 0:
@@ -476,6 +492,7 @@ class Nnet:
             out.append((o.value, a.value, w.value))
 
     def compute_objf(self, feats, T, N, num_frames, flat_labels, label_lengths):
+        """ComputeNnetObjf (no update); feats as for train_step."""
         return self._step(lib().kctc_nnet_compute_objf, feats, T, N, num_frames, flat_labels, label_lengths)
 
     @property
@@ -491,8 +508,10 @@ class Nnet:
         return ms.value, n.value
 
     def propagate(self, feats, T, N, out=None):
-        """NnetComputation: network output [T*N, output_dim] (torch CUDA tensor)."""
+        """NnetComputation: network output [T*N, output_dim] (torch CUDA tensor)
+        of feats [T*N*num_splice, D] (FormatNnetInput layout)."""
         import torch
+        self._check_feats(feats, T, N)
         A = int(self.info(self.num_components - 1).split("output-dim=")[1].split(",")[0])
         if out is None:
             out = torch.empty((T * N, A), dtype=torch.float32, device=feats.device)
@@ -500,7 +519,10 @@ class Nnet:
         return out
 
     def decodable(self, feats, T, prob_scale=1.0, blank_threshold=1.0):
-        """CtcDecodableAmNnet of one utterance -> np [kept, A] log-likelihoods."""
+        """CtcDecodableAmNnet of one utterance feats [T, D] (plain rows; padded
+        for the network's context as pad_input = true) -> np [kept, A]."""
+        if feats.dim() != 2 or feats.shape[0] != T or not feats.is_contiguous():
+            raise KctcError(f"feats must be a contiguous [T={T}, input_dim] tensor, got {tuple(feats.shape)}")
         A = int(self.info(self.num_components - 1).split("output-dim=")[1].split(",")[0])
         out = np.empty((T, A), np.float32)
         k = ctypes.c_int()
@@ -559,6 +581,22 @@ class Nnet:
         data-parallel rank -- and the step raises."""
         _tcheck(lib().kctc_nnet_inject_step_error(self.h, int(word)), "inject_step_error")
 
+    def get_component(self, c):
+        """A copy of component c (Nnet::GetComponent(c).Copy())."""
+        h = ctypes.c_void_p()
+        _tcheck(lib().kctc_nnet_get_component(self.h, int(c), ctypes.byref(h)), "kctc_nnet_get_component")
+        return Component(_handle=h)
+
+    def set_component(self, c, component):
+        """Nnet::SetComponent(c, component.Copy())."""
+        _tcheck(lib().kctc_nnet_set_component(self.h, int(c), component.h), "kctc_nnet_set_component")
+
+    def scale_params(self, scale, skip_last_layer=False):
+        _tcheck(lib().kctc_nnet_scale_params(self.h, float(scale), int(bool(skip_last_layer))), "scale_params")
+
+    def add_params(self, alpha, other, skip_last_layer=False):
+        _tcheck(lib().kctc_nnet_add_params(self.h, float(alpha), other.h, int(bool(skip_last_layer))), "add_params")
+
     def enable_cu_probe(self, blocks, usec):
         """CU-budget probe: every gradient bucket launches a kernel holding
         `blocks` whole CUs for `usec` us on a comm stream (blocks 0: off)."""
@@ -566,6 +604,184 @@ class Nnet:
 
 
 _HOST_ALLREDUCE = ctypes.CFUNCTYPE(None, ctypes.POINTER(ctypes.c_float), ctypes.c_long, ctypes.c_void_p)
+
+
+# ---------------------------------------------------------------------------
+# nnet2 Component plug-in point (include/kaldi_nnet2_component.h)
+# ---------------------------------------------------------------------------
+def _torch_sync():
+    """The component ABI runs on its own stream: wait for torch's first."""
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.current_stream().synchronize()
+
+
+class Component:
+    """One nnet2 component on the GPU, with the reference's member names
+    (src/nnet2/nnet-component.h:157-348): Propagate / Backprop / Copy /
+    Write / ReadNew and, for UpdatableComponents, SetZero / DotProduct /
+    PerturbParams / Scale / Add / Vectorize / UnVectorize.  Matrices are torch
+    CUDA float32 tensors in the time-major [T*N(*num_splice), dim] layout;
+    Backprop with a to_update component updates it at once, as the
+    reference does (a SetZero(True) copy then holds the gradient)."""
+
+    def __init__(self, config_line=None, seed=0, device=0, _handle=None):
+        if _handle is not None:
+            self.h = _handle
+            return
+        h = ctypes.c_void_p()
+        _tcheck(lib().kctc_component_init(ctypes.byref(h), config_line.encode(), int(seed), int(device)),
+                "kctc_component_init")
+        self.h = h
+
+    @classmethod
+    def ReadNew(cls, path, device=0):
+        h = ctypes.c_void_p()
+        _tcheck(lib().kctc_component_read(ctypes.byref(h), str(path).encode(), int(device)), "kctc_component_read")
+        return cls(_handle=h)
+
+    def Write(self, path, binary=True):
+        _tcheck(lib().kctc_component_write(self.h, str(path).encode(), int(bool(binary))), "kctc_component_write")
+
+    def Copy(self):
+        h = ctypes.c_void_p()
+        _tcheck(lib().kctc_component_copy(self.h, ctypes.byref(h)), "kctc_component_copy")
+        return Component(_handle=h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().kctc_component_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def Type(self):
+        buf = ctypes.create_string_buffer(256)
+        _tcheck(lib().kctc_component_type(self.h, buf, 256), "kctc_component_type")
+        return buf.value.decode()
+
+    def Info(self):
+        buf = ctypes.create_string_buffer(1024)
+        _tcheck(lib().kctc_component_info(self.h, buf, 1024), "kctc_component_info")
+        return buf.value.decode()
+
+    def _dims(self):
+        i, o = ctypes.c_int(), ctypes.c_int()
+        _tcheck(lib().kctc_component_dims(self.h, ctypes.byref(i), ctypes.byref(o)), "kctc_component_dims")
+        return i.value, o.value
+
+    def InputDim(self):
+        return self._dims()[0]
+
+    def OutputDim(self):
+        return self._dims()[1]
+
+    def Context(self):
+        buf = (ctypes.c_int * 64)()
+        n = ctypes.c_int()
+        _tcheck(lib().kctc_component_context(self.h, buf, 64, ctypes.byref(n)), "kctc_component_context")
+        return list(buf[:n.value])
+
+    def NumSplice(self):
+        ctx = self.Context()
+        return ctx[-1] - ctx[0] + 1
+
+    def _needs(self):
+        i, o = ctypes.c_int(), ctypes.c_int()
+        _tcheck(lib().kctc_component_backprop_needs(self.h, ctypes.byref(i), ctypes.byref(o)), "backprop_needs")
+        return bool(i.value), bool(o.value)
+
+    def BackpropNeedsInput(self):
+        return self._needs()[0]
+
+    def BackpropNeedsOutput(self):
+        return self._needs()[1]
+
+    def IsUpdatable(self):
+        return bool(lib().kctc_component_is_updatable(self.h))
+
+    def Propagate(self, T, N, inp, out=None):
+        """out [T*N, OutputDim] = component(inp [T*N*NumSplice, InputDim])."""
+        import torch
+        if out is None:
+            out = torch.empty((T * N, self.OutputDim()), dtype=torch.float32, device=inp.device)
+        _torch_sync()
+        _tcheck(lib().kctc_component_propagate(self.h, T, N, _ptr(inp), inp.numel(), _ptr(out), out.numel()),
+                "kctc_component_propagate")
+        return out
+
+    def Backprop(self, T, N, in_value, out_value, out_deriv, to_update=None, in_deriv=None):
+        """Backprop(in_info, out_info, in_value, out_value, out_deriv, to_update,
+        in_deriv); in_deriv (a tensor to fill, or None) is returned."""
+        _torch_sync()
+        _tcheck(lib().kctc_component_backprop(
+            self.h, T, N, _ptr(in_value), 0 if in_value is None else in_value.numel(),
+            _ptr(out_value), 0 if out_value is None else out_value.numel(), _ptr(out_deriv), out_deriv.numel(),
+            None if to_update is None else to_update.h, _ptr(in_deriv),
+            0 if in_deriv is None else in_deriv.numel()), "kctc_component_backprop")
+        return in_deriv
+
+    # ---- UpdatableComponent ----
+    def NumParameters(self):
+        return lib().kctc_component_num_params(self.h)
+
+    def Vectorize(self):
+        out = np.zeros(self.NumParameters(), np.float32)
+        _tcheck(lib().kctc_component_get_params(self.h, out.ctypes.data, out.size), "kctc_component_get_params")
+        return out
+
+    def UnVectorize(self, params):
+        a = np.ascontiguousarray(params, dtype=np.float32)
+        _tcheck(lib().kctc_component_set_params(self.h, a.ctypes.data, a.size), "kctc_component_set_params")
+
+    def LearningRate(self):
+        lr = ctypes.c_float()
+        _tcheck(lib().kctc_component_learning_rate(self.h, ctypes.byref(lr)), "kctc_component_learning_rate")
+        return lr.value
+
+    def SetLearningRate(self, lr):
+        _tcheck(lib().kctc_component_set_learning_rate(self.h, float(lr)), "kctc_component_set_learning_rate")
+
+    def IsGradient(self):
+        return bool(lib().kctc_component_is_gradient(self.h))
+
+    def SetZero(self, treat_as_gradient):
+        _tcheck(lib().kctc_component_set_zero(self.h, int(bool(treat_as_gradient))), "kctc_component_set_zero")
+
+    def DotProduct(self, other):
+        d = ctypes.c_double()
+        _tcheck(lib().kctc_component_dot_product(self.h, other.h, ctypes.byref(d)), "kctc_component_dot_product")
+        return d.value
+
+    def PerturbParams(self, stddev):
+        _tcheck(lib().kctc_component_perturb_params(self.h, float(stddev)), "kctc_component_perturb_params")
+
+    def Scale(self, scale):
+        _tcheck(lib().kctc_component_scale(self.h, float(scale)), "kctc_component_scale")
+
+    def Add(self, alpha, other):
+        _tcheck(lib().kctc_component_add(self.h, float(alpha), other.h), "kctc_component_add")
+
+    def srand(self, seed):
+        _tcheck(lib().kctc_component_srand(self.h, int(seed)), "kctc_component_srand")
+
+
+def set_perturb_seed(seed):
+    """Seed of PerturbParams' noise stream (kctc_set_perturb_seed)."""
+    _tcheck(lib().kctc_set_perturb_seed(int(seed)), "kctc_set_perturb_seed")
+
+
+def average_models(nnets, weights=None, skip_last_layer=False):
+    """nnet-am-average in process: nnets[0] = sum_i weights[i] * nnets[i]
+    (default weights 1/len(nnets)) through the components' Scale / Add."""
+    arr = (ctypes.c_void_p * len(nnets))(*[n.h.value if hasattr(n.h, "value") else n.h for n in nnets])
+    w = None if weights is None else np.ascontiguousarray(weights, dtype=np.float32)
+    _tcheck(lib().kctc_nnet_average_models(arr, None if w is None else w.ctypes.data, len(nnets),
+                                           int(bool(skip_last_layer))), "kctc_nnet_average_models")
 
 
 def set_cu_partition(part, nparts):

@@ -9,6 +9,8 @@ namespace kctc {
 
 // out = softmax of each row of in (max-subtracted), floored at 1e-20
 void softmax_rows(hipStream_t s, const float *in, long rows, int cols, float *out);
+// SoftmaxComponent::Backprop: out = value * (deriv - rowdot(value, deriv))
+void diff_softmax_rows(hipStream_t s, const float *value, const float *deriv, long rows, int cols, float *out);
 // probs [T][A] -> out [kept][A] (see decodable.hip); priors: linear, device,
 // nullable; scratch >= ctc_decodable_scratch_bytes(T); *kept_dev (device int)
 size_t ctc_decodable_scratch_bytes(int T);

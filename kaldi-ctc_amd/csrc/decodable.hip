@@ -92,7 +92,27 @@ __global__ __launch_bounds__(256) void k_decodable_rows(const float *__restrict_
   }
 }
 
+// DiffSoftmaxPerRow (SoftmaxComponent::Backprop, nnet-component.cc:948-976):
+// d_i = p_i e_i - p_i (p . e), one wave per row
+__global__ __launch_bounds__(256) void k_diff_softmax_rows(const float *__restrict__ p, const float *__restrict__ e,
+                                                           long rows, int cols, float *__restrict__ d) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float *pr = p + row * cols, *er = e + row * cols;
+  float s = 0.f;
+  for (int j = lane; j < cols; j += 64) s += pr[j] * er[j];
+  s = wave_sum(s);
+  float *dr = d + row * cols;
+  for (int j = lane; j < cols; j += 64) dr[j] = pr[j] * (er[j] - s);
+}
+
 }  // namespace
+
+void diff_softmax_rows(hipStream_t s, const float *value, const float *deriv, long rows, int cols, float *out) {
+  if (rows <= 0 || cols <= 0) return;
+  hipLaunchKernelGGL(k_diff_softmax_rows, dim3(ceil_div(rows, 4)), dim3(256), 0, s, value, deriv, rows, cols, out);
+}
 
 void softmax_rows(hipStream_t s, const float *in, long rows, int cols, float *out) {
   if (rows <= 0 || cols <= 0) return;

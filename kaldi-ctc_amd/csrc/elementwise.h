@@ -25,6 +25,16 @@ void sum_rows(hipStream_t s, const float *X, long rows, int cols, float alpha, f
               float *out, float *ws);
 void fill(hipStream_t s, float *p, long n, float v);
 void scale_inplace(hipStream_t s, float *p, long n, float alpha);
+// y += alpha * x (CuVector::AddVec)
+void axpy(hipStream_t s, float *y, const float *x, long n, float alpha);
+// x += stddev * N(0,1) (PerturbParams: a temporary SetRandn() then AddVec);
+// element i draws from a counter-based splitmix64 + Box-Muller stream of
+// (seed, i), so the noise does not depend on the launch shape
+void add_randn(hipStream_t s, float *x, long n, float stddev, unsigned long long seed);
+// *out (device double) = sum_i a[i] * b[i] (VecVec / TraceMatMat over the flat
+// parameters), fp64 accumulation in a fixed order: deterministic
+size_t dot_ws_bytes();
+void dot_f64(hipStream_t s, const float *a, const float *b, long n, double *out, void *ws);
 
 // SpliceComponent on the FormatNnetInput layout (nnet.h): output row j, block
 // c = input row j * ns + first + ctx[c] (dim - const_dim columns); the last
@@ -36,6 +46,12 @@ void splice_rows(hipStream_t s, const float *in, int dim, int ns, long rows, con
                  int const_dim, float *out);
 void splice_rows_backward(hipStream_t s, const float *out_deriv, int dim, int ns, long rows, const int *ctx, int nctx,
                           int first, int const_dim, float *in_deriv);
+
+// NnetComputer's padded input (nnet-compute.cc:64-90, pad = true) laid out
+// for this path's SpliceComponent (ns = 1 + left + right rows per output
+// frame): out row t*ns + s = feats row clamp(t + s - left, 0, T-1) (the first
+// and last frames repeated left / right times), feats [T][dim] -> out [T*ns][dim]
+void pad_splice_input(hipStream_t s, const float *feats, int T, int dim, int left, int ns, float *out);
 
 // Data-parallel agreement on a failed step: the step's device error word (set
 // by a recurrence's bounded-spin timeout) as a 0/1 float that the gradient

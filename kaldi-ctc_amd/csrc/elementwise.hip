@@ -222,6 +222,67 @@ void scale_inplace(hipStream_t s, float *p, long n, float alpha) {
   hipLaunchKernelGGL(k_scale, dim3(grid_for(n)), dim3(256), 0, s, p, n, alpha);
 }
 
+// ---- UpdatableComponent parameter arithmetic --------------------------------
+__global__ void k_axpy(float *__restrict__ y, const float *__restrict__ x, long n, float a) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) y[i] += a * x[i];
+}
+
+__device__ __forceinline__ unsigned long long splitmix(unsigned long long z) {
+  z += 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+__global__ void k_add_randn(float *__restrict__ x, long n, float stddev, unsigned long long seed) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const unsigned long long a = splitmix(seed ^ splitmix(2ull * (unsigned long long)i));
+    const unsigned long long b = splitmix(seed ^ splitmix(2ull * (unsigned long long)i + 1ull));
+    const double u1 = ((double)(a >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+    const double u2 = ((double)(b >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+    x[i] += stddev * (float)(sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
+  }
+}
+
+constexpr int kDotBlocks = 256;
+// fixed grid: block b sums elements b*256+tid, + kDotBlocks*256, ... in fp64,
+// then a fixed-order tree; the partials are summed in block order
+__global__ __launch_bounds__(256) void k_dot_partial(const float *__restrict__ a, const float *__restrict__ b,
+                                                     long n, double *__restrict__ part) {
+  __shared__ double w[4];
+  double s = 0.0;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)kDotBlocks * 256)
+    s += (double)a[i] * (double)b[i];
+  s = wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (w[0] + w[1]) + (w[2] + w[3]);
+}
+__global__ __launch_bounds__(64) void k_dot_final(const double *__restrict__ part, double *__restrict__ out) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < kDotBlocks; i += 64) s += part[i];
+  s = wave_sum_d(s);
+  if (threadIdx.x == 0) *out = s;
+}
+
+void axpy(hipStream_t s, float *y, const float *x, long n, float alpha) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_axpy, dim3(grid_for(n)), dim3(256), 0, s, y, x, n, alpha);
+}
+
+void add_randn(hipStream_t s, float *x, long n, float stddev, unsigned long long seed) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_add_randn, dim3(grid_for(n)), dim3(256), 0, s, x, n, stddev, seed);
+}
+
+size_t dot_ws_bytes() { return sizeof(double) * kDotBlocks; }
+
+void dot_f64(hipStream_t s, const float *a, const float *b, long n, double *out, void *ws) {
+  double *part = static_cast<double *>(ws);
+  hipLaunchKernelGGL(k_dot_partial, dim3(kDotBlocks), dim3(256), 0, s, a, b, n < 0 ? 0 : n, part);
+  hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(64), 0, s, part, out);
+}
+
 // ---- SpliceComponent --------------------------------------------------------
 struct SpliceArgs {
   int n, first, dim, const_dim, ns, out_dim;
@@ -283,6 +344,23 @@ void splice_rows_backward(hipStream_t s, const float *out_deriv, int dim, int ns
   if (rows <= 0) return;
   const SpliceArgs a = splice_args(dim, ns, ctx, nctx, first, const_dim);
   hipLaunchKernelGGL(k_splice_bwd, dim3(grid_for(rows * ns * dim)), dim3(256), 0, s, out_deriv, rows, a, in_deriv);
+}
+
+__global__ void k_pad_splice(const float *__restrict__ feats, int T, int dim, int left, int ns,
+                             float *__restrict__ out) {
+  const long total = (long)T * ns * dim;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long r = e / dim;
+    const int col = (int)(e - r * dim);
+    const int t = (int)(r / ns), sp = (int)(r - (long)t * ns);
+    const int src = min(max(t + sp - left, 0), T - 1);
+    out[e] = feats[(long)src * dim + col];
+  }
+}
+
+void pad_splice_input(hipStream_t s, const float *feats, int T, int dim, int left, int ns, float *out) {
+  if (T <= 0 || dim <= 0 || ns <= 0) return;
+  hipLaunchKernelGGL(k_pad_splice, dim3(grid_for((long)T * ns * dim)), dim3(256), 0, s, feats, T, dim, left, ns, out);
 }
 
 // ---- data-parallel step agreement ------------------------------------------

@@ -278,6 +278,20 @@ Component *Component::NewComponentOfType(const std::string &type) {
   return nullptr;
 }
 
+Component *Component::ReadNew(std::istream &is, bool binary) {
+  const std::string t = kio::ReadToken(is, binary);
+  if (t.size() < 3 || t.front() != '<' || t.back() != '>') throw std::runtime_error("bad component token " + t);
+  Component *c = NewComponentOfType(t.substr(1, t.size() - 2));
+  if (!c) throw std::runtime_error("Unknown component type " + t);
+  try {
+    c->Read(is, binary);
+  } catch (...) {
+    delete c;
+    throw;
+  }
+  return c;
+}
+
 // ---------------------------------------------------------------------------
 // SpliceComponent (nnet-component.cc:2504-2820)
 // ---------------------------------------------------------------------------
@@ -341,6 +355,13 @@ void SpliceComponent::Backprop(const ChunkInfo &in_info, const ChunkInfo &out_in
   const int ns = (int)(in_deriv->NumRows() / rows);
   splice_rows_backward(S(), out_deriv.Data(), input_dim_, ns, rows, context_.data(), (int)context_.size(),
                        out_info.first_offset - in_info.first_offset, const_dim_, in_deriv->Data());
+}
+Component *SpliceComponent::Copy() const {
+  auto *c = new SpliceComponent;
+  c->input_dim_ = input_dim_;
+  c->const_dim_ = const_dim_;
+  c->context_ = context_;
+  return c;
 }
 void SpliceComponent::Write(std::ostream &os, bool binary) const {  // :2822-2833
   WriteToken(os, binary, "<SpliceComponent>");
@@ -575,6 +596,60 @@ void UpdatableComponent::UpdateWith(float *params, const float *grad, float clip
     momentum_update(S(), params, delta_.f(), grad, NumParameters(), learning_rate_, clip, momentum_, skip);
 }
 
+// ---- UpdatableComponent parameter arithmetic (nnet-component.h:295-318) ----
+static unsigned long long g_perturb_seed = 20161015ull, g_perturb_calls = 0;
+void UpdatableComponent::SetPerturbSeed(unsigned long long seed) {
+  g_perturb_seed = seed;
+  g_perturb_calls = 0;
+}
+
+void UpdatableComponent::CopyUpdatableFrom(const UpdatableComponent &o) {
+  learning_rate_ = o.learning_rate_;
+  is_gradient_ = o.is_gradient_;
+}
+
+void UpdatableComponent::CheckSameKind(const UpdatableComponent &o, const char *what) const {
+  if (o.Type() != Type() || o.NumParameters() != NumParameters())
+    throw std::invalid_argument(std::string(what) + ": components of different type or size (" + Type() + " vs " +
+                                o.Type() + ")");
+}
+
+void UpdatableComponent::SetZero(bool treat_as_gradient) {
+  if (treat_as_gradient) {
+    SetLearningRate(1.0f);
+    is_gradient_ = true;
+  }
+  KCTC_HIP_CHECK(hipMemsetAsync(ParamData(), 0, sizeof(float) * NumParameters(), S()));
+}
+
+double UpdatableComponent::DotProduct(const UpdatableComponent &other) const {
+  CheckSameKind(other, "DotProduct");
+  auto *self = const_cast<UpdatableComponent *>(this);
+  auto *o = const_cast<UpdatableComponent *>(&other);
+  DevBuf ws;
+  ws.ensure(dot_ws_bytes() + sizeof(double));
+  double *out = reinterpret_cast<double *>(static_cast<char *>(ws.p) + dot_ws_bytes());
+  // the other component's parameters may still be written on its own stream
+  KCTC_HIP_CHECK(hipStreamSynchronize(o->GradStream()));
+  dot_f64(S(), self->ParamData(), o->ParamData(), NumParameters(), out, ws.p);
+  double h = 0;
+  KCTC_HIP_CHECK(hipMemcpyAsync(&h, out, sizeof(double), hipMemcpyDeviceToHost, S()));
+  KCTC_HIP_CHECK(hipStreamSynchronize(S()));
+  return h;
+}
+
+void UpdatableComponent::PerturbParams(float stddev) {
+  Rng r(g_perturb_seed + 0x51ED27ull * ++g_perturb_calls);
+  add_randn(S(), ParamData(), NumParameters(), stddev, r.next());
+}
+
+void UpdatableComponent::Scale(float scale) { scale_inplace(S(), ParamData(), NumParameters(), scale); }
+
+void UpdatableComponent::Add(float alpha, const UpdatableComponent &other) {
+  CheckSameKind(other, "Add");
+  axpy(S(), ParamData(), const_cast<UpdatableComponent &>(other).ParamData(), NumParameters(), alpha);
+}
+
 int CuDNNRecurrentComponent::side_gemm_blocks() const {
   const char *e = getenv("KCTC_SIDE_BLOCKS");
   if (e && *e) return atoi(e);
@@ -584,6 +659,29 @@ int CuDNNRecurrentComponent::side_gemm_blocks() const {
 void CuDNNRecurrentComponent::ApplyUpdate(const unsigned *skip) {
   // ApplyFloor(-clip) / ApplyCeiling(clip) then filter_params_ += lr * grad
   UpdateWith(params_.f(), grad_.f(), clip_gradient_, skip);
+}
+
+// CuDNNRecurrentComponent(const CuDNNRecurrentComponent &) (nnet-cudnn-component.cc:650-671):
+// configuration and filter_params_, no minibatch state (mini_batch_ = 0)
+Component *CuDNNRecurrentComponent::Copy() const {
+  auto *c = new CuDNNRecurrentComponent;
+  c->CopyUpdatableFrom(*this);
+  c->desc_ = desc_;
+  c->max_seq_length_ = max_seq_length_;
+  c->param_stddev_ = param_stddev_;
+  c->bias_stddev_ = bias_stddev_;
+  c->clip_gradient_ = clip_gradient_;
+  const long P = NumParameters();
+  c->params_.ensure(sizeof(float) * P);
+  c->grad_.ensure(sizeof(float) * P);
+  KCTC_HIP_CHECK(hipMemcpyAsync(c->params_.p, params_.p, sizeof(float) * P, hipMemcpyDeviceToDevice, S()));
+  return c;
+}
+
+// :723-730 (SetBufferZero: the reserve is rebuilt by the next Propagate here)
+void CuDNNRecurrentComponent::SetZero(bool treat_as_gradient) {
+  UpdatableComponent::SetZero(treat_as_gradient);
+  input_projected_ = false;
 }
 
 void CuDNNRecurrentComponent::Vectorize(float *host) const {
@@ -760,6 +858,50 @@ void ClipGradientComponent::Backprop(const ChunkInfo &, const ChunkInfo &, const
                     scratch_.p, dev_);
 }
 
+Component *ClipGradientComponent::Copy() const {
+  auto *c = new ClipGradientComponent;
+  c->dim_ = dim_;
+  c->clipping_threshold_ = clipping_threshold_;
+  c->norm_based_clipping_ = norm_based_clipping_;
+  c->self_repair_clipped_proportion_threshold_ = self_repair_clipped_proportion_threshold_;
+  c->self_repair_target_ = self_repair_target_;
+  c->self_repair_scale_ = self_repair_scale_;
+  SyncStats();
+  c->num_clipped_ = num_clipped_;
+  c->count_ = count_;
+  c->num_self_repaired_ = num_self_repaired_;
+  c->num_backpropped_ = num_backpropped_;
+  KCTC_HIP_CHECK(hipMemcpyAsync(c->dev_, dev_, sizeof(ClipState), hipMemcpyDeviceToDevice, S()));
+  return c;
+}
+
+// the device counters are the truth during training; scaled on the host and
+// written back (both are off the per-step path)
+void ClipGradientComponent::Scale(float scale) {  // :1064-1067
+  SyncStats();
+  count_ *= scale;
+  num_clipped_ *= scale;
+  ClipState h{};
+  h.num_clipped = num_clipped_;
+  h.count = count_;
+  h.num_self_repaired = num_self_repaired_;
+  KCTC_HIP_CHECK(hipMemcpyAsync(dev_, &h, sizeof(h), hipMemcpyHostToDevice, S()));
+  KCTC_HIP_CHECK(hipStreamSynchronize(S()));
+}
+
+void ClipGradientComponent::Add(float alpha, const ClipGradientComponent &other) {  // :1069-1073
+  SyncStats();
+  other.SyncStats();
+  count_ += alpha * other.count_;
+  num_clipped_ += alpha * other.num_clipped_;
+  ClipState h{};
+  h.num_clipped = num_clipped_;
+  h.count = count_;
+  h.num_self_repaired = num_self_repaired_;
+  KCTC_HIP_CHECK(hipMemcpyAsync(dev_, &h, sizeof(h), hipMemcpyHostToDevice, S()));
+  KCTC_HIP_CHECK(hipStreamSynchronize(S()));
+}
+
 void ClipGradientComponent::SyncStats() const {
   ClipState h;
   KCTC_HIP_CHECK(hipMemcpyAsync(&h, dev_, sizeof(h), hipMemcpyDeviceToHost, S()));
@@ -857,10 +999,41 @@ void SoftmaxComponent::Propagate(const ChunkInfo &, const ChunkInfo &, const CuM
   ProfScope ps("softmax");
   softmax_rows(S(), in.Data(), in.NumRows(), dim_, out->Data());  // ApplySoftMaxPerRow + ApplyFloor(1e-20)
 }
-void SoftmaxComponent::Backprop(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &, const CuMatrixBase &,
-                                const CuMatrixBase &, Component *, CuMatrixBase *) const {
-  throw std::logic_error("SoftmaxComponent::Backprop: not on the CTC training path (CTC trains on the "
-                         "un-normalised affine output; the softmax is appended for decoding)");
+void SoftmaxComponent::Backprop(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &,
+                                const CuMatrixBase &out_value, const CuMatrixBase &out_deriv, Component *to_update_in,
+                                CuMatrixBase *in_deriv) const {
+  const long rows = out_deriv.NumRows();
+  if (in_deriv) diff_softmax_rows(S(), out_value.Data(), out_deriv.Data(), rows, dim_, in_deriv->Data());
+  if (to_update_in) {  // NonlinearComponent::UpdateStats(out_value) (:337-363): value_sum_ += column sums, count_ += rows
+    auto *to_update = dynamic_cast<SoftmaxComponent *>(to_update_in);
+    if (!to_update) throw std::invalid_argument("SoftmaxComponent: bad to_update");
+    ws_.ensure(sizeof(float) * ((size_t)dim_ + sum_rows_ws_floats(rows, dim_)));
+    sum_rows(S(), out_value.Data(), rows, dim_, 1.f, 0.f, ws_.f(), ws_.f() + dim_);
+    auto v = d2h(ws_.f(), dim_);
+    if (to_update->value_sum_.empty()) to_update->value_sum_.assign(dim_, 0.0);
+    for (int j = 0; j < dim_; j++) to_update->value_sum_[j] += v[j];
+    to_update->count_ += (double)rows;
+  }
+}
+Component *SoftmaxComponent::Copy() const {
+  auto *c = new SoftmaxComponent;
+  c->dim_ = dim_;
+  c->value_sum_ = value_sum_;
+  c->deriv_sum_ = deriv_sum_;
+  c->count_ = count_;
+  return c;
+}
+void SoftmaxComponent::Scale(float scale) {  // NonlinearComponent::Scale (nnet-component.cc:365-369)
+  for (auto &v : value_sum_) v *= scale;
+  for (auto &v : deriv_sum_) v *= scale;
+  count_ *= scale;
+}
+void SoftmaxComponent::Add(float alpha, const SoftmaxComponent &other) {  // NonlinearComponent::Add (:371-382)
+  if (value_sum_.empty() && !other.value_sum_.empty()) value_sum_.assign(other.value_sum_.size(), 0.0);
+  if (deriv_sum_.empty() && !other.deriv_sum_.empty()) deriv_sum_.assign(other.deriv_sum_.size(), 0.0);
+  for (size_t j = 0; j < other.value_sum_.size() && j < value_sum_.size(); j++) value_sum_[j] += alpha * other.value_sum_[j];
+  for (size_t j = 0; j < other.deriv_sum_.size() && j < deriv_sum_.size(); j++) deriv_sum_[j] += alpha * other.deriv_sum_[j];
+  count_ += alpha * other.count_;
 }
 void SoftmaxComponent::Write(std::ostream &os, bool binary) const {
   WriteToken(os, binary, "<SoftmaxComponent>");
@@ -963,6 +1136,18 @@ void AffineComponent::Backprop(const ChunkInfo &, const ChunkInfo &, const CuMat
   }
 }
 
+Component *AffineComponent::Copy() const {  // AffineComponent(const AffineComponent &) (:1046-1050)
+  auto *c = new AffineComponent;
+  c->CopyUpdatableFrom(*this);
+  c->in_dim_ = in_dim_;
+  c->out_dim_ = out_dim_;
+  const long P = NumParameters();
+  c->params_.ensure(sizeof(float) * P);
+  c->grad_.ensure(sizeof(float) * P);
+  KCTC_HIP_CHECK(hipMemcpyAsync(c->params_.p, params_.p, sizeof(float) * P, hipMemcpyDeviceToDevice, S()));
+  return c;
+}
+
 void AffineComponent::ApplyUpdate(const unsigned *skip) {
   UpdateWith(params_.f(), grad_.f(), 0.f, skip);
 }
@@ -1062,6 +1247,27 @@ int Nnet::FirstUpdatableComponent() const {  // nnet-nnet.cc:838-845
   return NumComponents();
 }
 
+int Nnet::LastUpdatableComponent() const {
+  for (int i = NumComponents() - 1; i >= 0; i--)
+    if (components_[i]->IsUpdatable()) return i;
+  return -1;
+}
+
+void Nnet::SetComponent(int c, Component *component) {
+  if (c < 0 || c >= NumComponents() || !component) {
+    delete component;
+    throw std::out_of_range("Nnet::SetComponent: bad index");
+  }
+  const bool in_ok = c == 0 || components_[c - 1]->OutputDim() == component->InputDim();
+  const bool out_ok = c + 1 == NumComponents() || component->OutputDim() == components_[c + 1]->InputDim();
+  if (!in_ok || !out_ok || (c > 0 && component->Context() != std::vector<int>{0})) {
+    delete component;
+    throw std::invalid_argument("Nnet::SetComponent: dimensions or context do not match the neighbours");
+  }
+  delete components_[c];
+  components_[c] = component;
+}
+
 void Nnet::ZeroStats() {
   for (auto *c : components_) c->ZeroStats();
 }
@@ -1100,14 +1306,7 @@ void Nnet::Read(std::istream &is, bool binary) {
   const int n = kio::ReadInt(is, binary);
   if (n <= 0) throw std::runtime_error("Nnet::Read: <NumComponents> " + std::to_string(n));
   ExpectToken(is, binary, "<Components>");
-  for (int i = 0; i < n; i++) {
-    const std::string t = kio::ReadToken(is, binary);
-    if (t.size() < 3) throw std::runtime_error("bad component token " + t);
-    Component *c = Component::NewComponentOfType(t.substr(1, t.size() - 2));
-    if (!c) throw std::runtime_error("Unknown component " + t);
-    components_.push_back(c);
-    c->Read(is, binary);
-  }
+  for (int i = 0; i < n; i++) components_.push_back(Component::ReadNew(is, binary));
   ExpectToken(is, binary, "</Components>");
   ExpectToken(is, binary, "</Nnet>");
   // Nnet::Read -> Check (nnet-nnet.cc:197-198, 281-289): every component's output feeds the next

@@ -4,8 +4,10 @@
 // (src/nnet2/nnet-component.h:157-348, nnet-cudnn-component.h, nnet-nnet.h,
 // src/ctc/ctc-nnet-update.h), on device buffers and one HIP stream:
 //   Component / UpdatableComponent      Propagate / Backprop / InitFromString /
-//                                       Info / Read / Write / Vectorize ...
-//   SpliceComponent                     context 0 only (the CTC recipe)
+//                                       Info / Read / Write / Copy / Vectorize /
+//                                       SetZero / DotProduct / PerturbParams /
+//                                       Scale / Add
+//   SpliceComponent                     any sorted context, const-component-dim
 //   CuDNNRecurrentComponent             -> rnn.hip (cuDNN-shaped gfx950 kernels)
 //   ClipGradientComponent               -> elementwise.hip / clipgrad.hip
 //   AffineComponent                     -> gemm.hip
@@ -147,11 +149,17 @@ class Component {
                         CuMatrixBase *in_deriv) const = 0;
   virtual void Write(std::ostream &os, bool binary) const = 0;
   virtual void Read(std::istream &is, bool binary) = 0;
+  // a deep copy (device parameters and statistics copied on the stream); like
+  // the reference's copy constructors it carries no minibatch state, so a
+  // copied CuDNNRecurrentComponent must Propagate before it can Backprop
+  virtual Component *Copy() const = 0;
   virtual void ZeroStats() {}
   // frame offsets this component reads relative to each output frame
   // (nnet-component.h:188; only SpliceComponent has more than {0})
   virtual std::vector<int> Context() const { return std::vector<int>(1, 0); }
   static Component *NewComponentOfType(const std::string &type);
+  // "<Type>" token, then the body (nnet-component.cc:38-48)
+  static Component *ReadNew(std::istream &is, bool binary);
 };
 
 class UpdatableComponent : public Component {
@@ -159,6 +167,24 @@ class UpdatableComponent : public Component {
   bool IsUpdatable() const override { return true; }
   float LearningRate() const { return learning_rate_; }
   void SetLearningRate(float lr) { learning_rate_ = lr; }
+  // nnet-component.h:295-318.  Both updatable components on this path keep
+  // all their parameters in ParamData() (Vectorize order), so these are
+  // defined once on that flat vector; each equals the reference's per-class
+  // definition (AffineComponent: TraceMatMat(linear, other.linear, kTrans) +
+  // VecVec(bias, other.bias) == the flat dot, nnet-component.cc:1026-1123;
+  // CuDNNRecurrentComponent: filter_params_, nnet-cudnn-component.cc:723-772).
+  // SetZero(true): parameters 0, learning rate 1, is-gradient (then a Backprop
+  // with this as to_update followed by ApplyUpdate stores the gradient in it)
+  virtual void SetZero(bool treat_as_gradient);
+  // fp64 accumulation on the device (the reference: fp32 VecVec)
+  virtual double DotProduct(const UpdatableComponent &other) const;
+  // params += stddev * N(0,1), from the process's perturbation stream
+  // (SetPerturbSeed; each call draws fresh noise)
+  virtual void PerturbParams(float stddev);
+  virtual void Scale(float scale);
+  virtual void Add(float alpha, const UpdatableComponent &other);
+  bool IsGradient() const { return is_gradient_; }
+  static void SetPerturbSeed(unsigned long long seed);
   virtual long NumParameters() const = 0;
   virtual void Vectorize(float *host) const = 0;      // host copy of all params
   virtual void UnVectorize(const float *host) = 0;
@@ -179,7 +205,10 @@ class UpdatableComponent : public Component {
 
  protected:
   void UpdateWith(float *params, const float *grad, float clip, const unsigned *skip);
+  void CopyUpdatableFrom(const UpdatableComponent &o);  // learning rate, is-gradient
+  void CheckSameKind(const UpdatableComponent &o, const char *what) const;
   float learning_rate_ = 0.001f;
+  bool is_gradient_ = false;  // <IsGradient>, read and written back
   hipStream_t grad_stream_ = nullptr;  // nullptr: the device's compute stream
   float momentum_ = 0.f;
   DevBuf delta_;
@@ -209,6 +238,7 @@ class SpliceComponent : public Component {
                 const CuMatrixBase &, Component *, CuMatrixBase *) const override;
   void Write(std::ostream &os, bool binary) const override;
   void Read(std::istream &is, bool binary) override;
+  Component *Copy() const override;
 
  private:
   void Init(int input_dim, std::vector<int> context, int const_dim);
@@ -233,6 +263,8 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
                 CuMatrixBase *in_deriv) const override;
   void Write(std::ostream &os, bool binary) const override;
   void Read(std::istream &is, bool binary) override;
+  Component *Copy() const override;
+  void SetZero(bool treat_as_gradient) override;
   long NumParameters() const override { return desc_.params_size(); }
   void Vectorize(float *host) const override;
   void UnVectorize(const float *host) override;
@@ -255,6 +287,8 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
     desc_.prec = prec;
   }
   void SetMiniBatch(int n) const { mini_batch_ = n; }  // Init(mini_batch) on change
+  // whether the last Propagate ran on a T x N input (Backprop's reserve-space precondition)
+  bool PropagatedShape(int T, int N) const { return seq_length_ == T && mini_batch_ == N && reserve_.p; }
   // Propagate whose last recurrence also produces `next`'s layer-0 input
   // projection on the side stream (rnn.h RnnFwdChain), `next` being the
   // following RNN with only identity-forward components in between; `next`
@@ -266,7 +300,6 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   RnnDesc desc_;
   int max_seq_length_ = 2000;
   float param_stddev_ = 0.02f, bias_stddev_ = 0.2f, clip_gradient_ = 5.0f;
-  bool is_gradient_ = false;
   DevBuf params_, grad_;
   mutable DevBuf reserve_, workspace_;
   mutable int mini_batch_ = 0, seq_length_ = 0;
@@ -295,7 +328,11 @@ class ClipGradientComponent : public Component {
                 CuMatrixBase *in_deriv) const override;
   void Write(std::ostream &os, bool binary) const override;
   void Read(std::istream &is, bool binary) override;
+  Component *Copy() const override;
   void ZeroStats() override;
+  // the counters' Scale / Add (nnet-cudnn-component.cc:1064-1073)
+  void Scale(float scale);
+  void Add(float alpha, const ClipGradientComponent &other);
   // host view of the device counters (valid after a stream sync)
   void SyncStats() const;
   double NumClipped() const { return num_clipped_; }
@@ -335,13 +372,22 @@ class SoftmaxComponent : public Component {
   bool BackpropNeedsInput() const override { return false; }
   void Propagate(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &in,
                  CuMatrixBase *out) const override;
-  void Backprop(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &, const CuMatrixBase &,
-                const CuMatrixBase &, Component *, CuMatrixBase *) const override;
+  // DiffSoftmaxPerRow; to_update's statistics get UpdateStats(out_value)
+  // (nnet-component.cc:948-976, NonlinearComponent::UpdateStats)
+  void Backprop(const ChunkInfo &, const ChunkInfo &, const CuMatrixBase &, const CuMatrixBase &out_value,
+                const CuMatrixBase &out_deriv, Component *to_update, CuMatrixBase *in_deriv) const override;
   void Write(std::ostream &os, bool binary) const override;
   void Read(std::istream &is, bool binary) override;
+  Component *Copy() const override;
+  // NonlinearComponent::Scale / Add of the statistics (nnet-am-average)
+  void Scale(float scale);
+  void Add(float alpha, const SoftmaxComponent &other);
+  const std::vector<double> &ValueSum() const { return value_sum_; }
+  double Count() const { return count_; }
 
  private:
   int dim_ = 0;
+  mutable DevBuf ws_;
   std::vector<double> value_sum_, deriv_sum_;
   double count_ = 0;
 };
@@ -361,6 +407,7 @@ class AffineComponent : public UpdatableComponent {
                 CuMatrixBase *in_deriv) const override;
   void Write(std::ostream &os, bool binary) const override;
   void Read(std::istream &is, bool binary) override;
+  Component *Copy() const override;
   long NumParameters() const override { return (long)(in_dim_ + 1) * out_dim_; }
   void Vectorize(float *host) const override;  // linear (row-major) then bias
   void UnVectorize(const float *host) override;
@@ -370,7 +417,6 @@ class AffineComponent : public UpdatableComponent {
 
  private:
   int in_dim_ = 0, out_dim_ = 0;
-  bool is_gradient_ = false;  // <IsGradient>, read and written back
   DevBuf params_, grad_;  // [out][in] followed by [out]
   mutable DevBuf ws_;
 };
@@ -384,6 +430,9 @@ class Nnet {
   Component &GetComponent(int c) { return *components_[c]; }
   const Component &GetComponent(int c) const { return *components_[c]; }
   int FirstUpdatableComponent() const;
+  int LastUpdatableComponent() const;  // -1 when none (nnet-nnet.cc)
+  // takes ownership; dimensions must still chain (nnet-nnet.cc:659-665)
+  void SetComponent(int c, Component *component);
   // Nnet::LeftContext / RightContext (nnet-nnet.cc:52-73): the sums of the
   // components' first (negated) and last context offsets
   int LeftContext() const;

@@ -20,6 +20,7 @@
 #include "elementwise.h"
 #include "kaldi_io.h"
 #include "nnet.h"
+#include "nnet_handle.h"
 
 using kctc::nnet2::CuDevice;
 
@@ -214,72 +215,32 @@ int kctc_usable_cus_override() {
 
 void kctc_set_error(const char *msg) { g_err = msg ? msg : ""; }
 
-struct kctcNnetImpl {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  kctc::nnet2::Nnet nnet;
-  kctc::nnet2::NnetCtcUpdater trainer{&nnet, true};
-  kctc::nnet2::NnetCtcUpdater evaluator{&nnet, false};
-  hipStream_t side = nullptr, stream2 = nullptr;
-  kctc::nnet2::GradExchange *dp = nullptr;
-  bool dp_average = false;  // model averaging: no per-step gradient exchange
-  kctc::nnet2::DevBuf egs_feats, egs_scratch;  // TrainNnetSimple staging
-  // decodable (per utterance): device priors, uploaded again only when they
-  // change, and the output / scratch buffers, grown and kept
-  kctc::nnet2::DevBuf dec_priors, dec_out, dec_scratch;
-  std::vector<float> dec_priors_host;
-  // nnet2-ctc model file extras: the CtcTransitionModel exactly as read (opaque
-  // bytes, in the mode of the file it came from) and AmNnet's priors
-  std::string trans_model;
-  bool trans_model_binary = false;
-  std::vector<float> priors;
-  ~kctcNnetImpl() {
-    delete dp;
-    if (stream) (void)hipStreamSynchronize(stream);
-    if (side) (void)hipStreamSynchronize(side);
-    if (stream2) (void)hipStreamSynchronize(stream2);
-    auto &d = CuDevice::Instantiate();
-    if (d.stream == stream) d.stream = nullptr;
-    if (d.side == side) d.side = nullptr;
-    if (d.stream2 == stream2) d.stream2 = nullptr;
-    if (stream) (void)hipStreamDestroy(stream);
-    if (side) (void)hipStreamDestroy(side);
-    if (stream2) (void)hipStreamDestroy(stream2);
+// compute stream at the highest priority (the latency-bound recurrences),
+// the weight-gradient side stream at the lowest; KCTC_OVERLAP=0 keeps
+// everything on one stream
+void kctcNnetImpl::create_streams() {
+  if (g_nparts > 1) {  // ranks sharing the device: this rank's streams on its CU share only
+    int cus = 0;
+    KCTC_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    const int per = cus / g_nparts, first = g_part * per;
+    std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+    for (int c = first; c < first + per; c++) mask[c / 32] |= 1u << (c % 32);
+    KCTC_HIP_CHECK(hipExtStreamCreateWithCUMask(&stream, (uint32_t)mask.size(), mask.data()));
+    KCTC_HIP_CHECK(hipExtStreamCreateWithCUMask(&side, (uint32_t)mask.size(), mask.data()));
+    KCTC_HIP_CHECK(hipExtStreamCreateWithCUMask(&stream2, (uint32_t)mask.size(), mask.data()));
+    kctc::rnn_set_cu_budget(per, kctc::rnn_comm_cus());
+    return;
   }
-  // compute stream at the highest priority (the latency-bound recurrences),
-  // the weight-gradient side stream at the lowest; KCTC_OVERLAP=0 keeps
-  // everything on one stream
-  void create_streams() {
-    if (g_nparts > 1) {  // ranks sharing the device: this rank's streams on its CU share only
-      int cus = 0;
-      KCTC_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-      const int per = cus / g_nparts, first = g_part * per;
-      std::vector<uint32_t> mask((cus + 31) / 32, 0u);
-      for (int c = first; c < first + per; c++) mask[c / 32] |= 1u << (c % 32);
-      KCTC_HIP_CHECK(hipExtStreamCreateWithCUMask(&stream, (uint32_t)mask.size(), mask.data()));
-      KCTC_HIP_CHECK(hipExtStreamCreateWithCUMask(&side, (uint32_t)mask.size(), mask.data()));
-      KCTC_HIP_CHECK(hipExtStreamCreateWithCUMask(&stream2, (uint32_t)mask.size(), mask.data()));
-      kctc::rnn_set_cu_budget(per, kctc::rnn_comm_cus());
-      return;
-    }
-    int lo = 0, hi = 0;
-    KCTC_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    KCTC_HIP_CHECK(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, hi));
-    const char *e = getenv("KCTC_OVERLAP");
-    if (!(e && *e == '0')) {
-      KCTC_HIP_CHECK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, lo));
-      // streamed GEMMs (default priority: a queue of its own, neither the recurrences' nor the side stream's)
-      KCTC_HIP_CHECK(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
-    }
+  int lo = 0, hi = 0;
+  KCTC_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  KCTC_HIP_CHECK(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, hi));
+  const char *e = getenv("KCTC_OVERLAP");
+  if (!(e && *e == '0')) {
+    KCTC_HIP_CHECK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, lo));
+    // streamed GEMMs (default priority: a queue of its own, neither the recurrences' nor the side stream's)
+    KCTC_HIP_CHECK(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
   }
-  void activate() {
-    KCTC_HIP_CHECK(hipSetDevice(device));
-    CuDevice::Instantiate().device = device;
-    CuDevice::Instantiate().stream = stream;
-    CuDevice::Instantiate().side = side;
-    CuDevice::Instantiate().stream2 = stream2;
-  }
-};
+}
 
 template <typename F>
 static int guarded(F f) {
@@ -729,9 +690,10 @@ int kctc_nnet_set_dp_mode(kctcNnet_t n, int mode) {
 }
 
 // nnet-am-average over the data-parallel ranks (src/nnet2bin/nnet-am-average.cc:
-// 185-241 with the default weights 1/num-models): every updatable component's
-// parameters become the mean of the ranks' copies.  Sum in place through the
-// exchange (RCCL or host transport), then scale by 1/world, on the compute stream.
+// 185-241 with the default weights 1/num-models), on the component API the tool
+// uses: every rank's updatable component is Scale(1/world)d (the tool's scale
+// of model 1 by its weight), then the collective sum adds the other ranks'
+// scaled copies (the tool's Add(weight, model i)), on the compute stream.
 int kctc_nnet_average_params(kctcNnet_t n) {
   return guarded([&] {
     KCTC_REQUIRE(n && n->dp, "kctc_nnet_average_params: data parallelism not enabled");
@@ -741,8 +703,8 @@ int kctc_nnet_average_params(kctcNnet_t n) {
     for (int c = 0; c < n->nnet.NumComponents(); c++) {
       auto *u = dynamic_cast<kctc::nnet2::UpdatableComponent *>(&n->nnet.GetComponent(c));
       if (!u) continue;
+      if (world > 1) u->Scale(1.f / (float)world);
       n->dp->AllReduceSum(u->ParamData(), u->NumParameters(), n->stream);
-      if (world > 1) kctc::scale_inplace(n->stream, u->ParamData(), u->NumParameters(), 1.f / (float)world);
     }
     KCTC_HIP_CHECK(hipStreamSynchronize(n->stream));
   });
@@ -840,8 +802,19 @@ int kctc_am_nnet_decodable(kctcNnet_t n, const float *feats_dev, int T, float pr
   return guarded([&] {
     KCTC_REQUIRE(n && feats_dev && out_host && num_rows && T > 0, "kctc_am_nnet_decodable: bad argument");
     n->activate();
-    // left/right context of this path are 0: every input row gives an output row
-    const auto &o = n->evaluator.Forward(feats_dev, T, 1);
+    // NnetComputation(nnet, feats, pad_input = true) (ctc-decodable-am-nnet.cc:28-52,
+    // nnet-compute.cc:64-90): T output frames from the T feature rows, the
+    // first / last frame repeated LeftContext / RightContext times; a spliced
+    // network reads num_splice rows per output frame (FormatNnetInput layout)
+    const float *in = feats_dev;
+    const int ns = n->nnet.NumSplice();
+    if (ns > 1) {
+      n->dec_input.ensure(sizeof(float) * (size_t)T * ns * n->nnet.InputDim());
+      kctc::pad_splice_input(n->stream, feats_dev, T, n->nnet.InputDim(), n->nnet.LeftContext(), ns,
+                             n->dec_input.f());
+      in = n->dec_input.f();
+    }
+    const auto &o = n->evaluator.Forward(in, T, 1);
     const int A = o.NumCols();
     auto &out = n->dec_out, &scratch = n->dec_scratch;
     const float *pd = nullptr;

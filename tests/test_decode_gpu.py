@@ -140,3 +140,35 @@ def test_compute_prob_matches_batches_and_oracle(kctc, gpu, oracle, tmp_path):
     np.testing.assert_allclose(res["tot_like"], rtot[0], rtol=1e-5)
     assert res["tot_weight"] == rtot[1]
     net.close()
+
+
+@pytest.mark.parametrize("ctx", [(-2, 0, 1), (0, 3)])
+def test_decode_spliced_model_pads_input(kctc, gpu, oracle, ctx):
+    """CtcDecodableAmNnet(pad_input = true) of a model with frame context: the
+    utterance's first / last frame repeated LeftContext / RightContext times
+    (NnetComputer, src/nnet2/nnet-compute.cc:64-90) -- T frames in, T rows
+    out -- vs the oracle on the same padded, spliced frames."""
+    import torch
+    D, H, A, T = 12, 64, 11, 150
+    L, R = -ctx[0], ctx[-1]
+    net = kctc.Nnet(kctc.recipe_config(num_rnn=2, input_dim=D, hidden=H, num_targets=A, param_stddev=0.1,
+                                       splice_context=ctx) + f"SoftmaxComponent dim={A}\n", seed=4)
+    assert net.context == (L, R)
+    rng = np.random.default_rng(8)
+    feats = rng.standard_normal((T, D)).astype(np.float32)
+    f = torch.from_numpy(feats).to(gpu)
+    out = net.decodable(f, T, prob_scale=1.0, blank_threshold=1.0)
+    assert out.shape == (T, A)
+    padded = np.concatenate([np.repeat(feats[:1], L, 0), feats, np.repeat(feats[-1:], R, 0)])
+    x = np.stack([np.concatenate([padded[t + L + c] for c in ctx]) for t in range(T)])
+    x = x.reshape(T, 1, -1).astype(np.float64)
+    for c in (1, 3):
+        x, _ = oracle.rnn_forward(2, x, net.get_params(c).astype(np.float64), H, 1, 2)
+    aff = net.get_params(5).astype(np.float64)
+    logits = x.reshape(T, -1) @ aff[:-A].reshape(A, -1).T + aff[-A:]
+    ref = oracle.ctc_decodable(oracle.softmax_rows(logits.astype(np.float32)), None, 1.0, 1.0, 1e-10)
+    np.testing.assert_allclose(out, ref, rtol=1e-5, atol=2e-5)
+    # the trainer's own input check: a [T, D] buffer is not a spliced network's layout
+    with pytest.raises(kctc.KctcError):
+        net.propagate(f, T, 1)
+    net.close()
