@@ -81,9 +81,12 @@ ctcStatus_t mictc_compute_ctc_loss_async(const float *activations, float *gradie
                                          int minibatch, double *costs_dev, void *workspace,
                                          ctcStream_t stream, int blank_label);
 
-/* Frames per barrier of the alpha/beta recursion (1..8; default 8, or
- * KCTC_CTC_PAIR read once at the first call).  Returns the previous value;
- * m <= 0 only queries.  Same results for every m (tests/test_ctc_gpu.py). */
+/* TEST / TUNING KNOB, not part of the warp-ctc contract: frames per barrier
+ * of the alpha/beta recursion (1..8; default 8, or KCTC_CTC_PAIR read once at
+ * the first call).  PROCESS-GLOBAL: every later launch from any thread or
+ * network reads it, so set it only while no CTC call is in flight (the tests
+ * do, one process).  Returns the previous value; m <= 0 only queries.  Same
+ * results for every m (tests/test_ctc_gpu.py). */
 int mictc_set_frame_group(int m);
 
 #ifdef __cplusplus

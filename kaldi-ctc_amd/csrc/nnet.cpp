@@ -1601,7 +1601,10 @@ void NnetCtcUpdater::Backprop(int T, int N) {  // :320-348
       if (cg->Shadow()) to_update = cg->Shadow();  // momentum: delta_nnet's copy
     }
     const CuMatrixBase od(cur->Data(), rows, comp.OutputDim());
+    const bool rec = exchange_ && dynamic_cast<CuDNNRecurrentComponent *>(&comp);
+    if (rec) exchange_->BeforeRecurrence(S());
     comp.Backprop(chunk_info_[c], chunk_info_[c + 1], in, outv, od, to_update, in_deriv);
+    if (rec) exchange_->AfterRecurrence();
     if (comp.IsUpdatable()) {
       auto *u = static_cast<UpdatableComponent *>(&comp);
       if (exchange_) exchange_->GradReady(c, u->GradData(), u->NumParameters(), u->GradStream());

@@ -457,6 +457,12 @@ class GradExchange {
  public:
   virtual ~GradExchange() = default;
   virtual void GradReady(int component, float *grad, long n, hipStream_t producer) = 0;
+  // around the Backprop of a component that launches a backward recurrence:
+  // Before (the compute stream may be made to wait for exchange work already
+  // queued), After (the recurrence is enqueued: exchange work may be queued
+  // behind its residency, rnn.h rnn_comm_gate)
+  virtual void BeforeRecurrence(hipStream_t compute) { (void)compute; }
+  virtual void AfterRecurrence() {}
   virtual void Finish() = 0;  // compute stream waits for every launched all-reduce
   virtual int WorldSize() const = 0;
   // in-place sum of buf over the ranks, ordered on stream s (s waits for it)

@@ -50,6 +50,23 @@ void rnn_set_cu_budget(int cus, int comm);
 int rnn_usable_cus();
 int rnn_comm_cus();
 
+// Residency gate of the gradient exchange.  Every workgroup
+// of a v6 backward recurrence adds 1 to a per-device registration word when
+// it starts; rnn_bwd_registrations() is the value that word reaches once all
+// backward recurrences enqueued so far on this device are resident.
+// rnn_comm_gate(s, target) enqueues on s a one-wave kernel that returns once
+// the word has reached `target` (wrap-safe; after 10 s it gives up and sets
+// bit 0 of the gate's own error word, rnn_comm_gate_errors()).  An exchange
+// that runs its kernels only behind such a gate -- i.e. only while the
+// backward recurrence launched last is fully resident -- and makes the next
+// recurrence launch wait for them declares rnn_set_comm_gated(true): the
+// backward recurrences then stay XCD-pinned with an exchange configured.
+unsigned rnn_bwd_registrations();
+void rnn_comm_gate(hipStream_t s, unsigned target);
+unsigned rnn_comm_gate_errors();
+void rnn_set_comm_gated(bool on);
+bool rnn_comm_gated();
+
 // Status codes of the RNN ABI (include/kaldi_rnn.h)
 enum { KRNN_OK = 0, KRNN_BAD_PARAM = 1, KRNN_NOT_SUPPORTED = 2, KRNN_EXEC_FAILED = 3,
        KRNN_TIMEOUT = 4 };

@@ -263,10 +263,12 @@ struct RecParams {
   float *xch;       // v4: per-step exchange images [T][dirs][KG][Npad][16] (workspace)
   int poll_sleep;   // v6: s_sleep between flag polls
   int nopf;         // diagnostic (KCTC_DIAG_NOPF): skip the operand prefetch (wrong results)
+  int gla;          // v6 forward IO waves: steps ahead the G rows are fetched (3 or 7; 8 LDS slots)
   int e_sc1;        // v6 backward: dGates rows written through (sc1) for a streaming consumer
   int wwait;        // v6: per-wave waits on the producers a wave reads (else wave 0 waits for all)
   int bfpart;       // v6 backward, bf16 mode: partial dh exchanged as bf16 (KCTC_BF16_PARTIALS)
   unsigned *cmax;   // v6 backward: column max |DX| [dirs * nW * H] (GRU: then |E|), as float bits
+  unsigned *reg;    // v6 backward: per-device registration word (+1 per workgroup at start)
 };
 
 // Phase stamps of the first kTraceSteps steps ([steps][grid][16]; thread 0 of every workgroup;
@@ -1541,6 +1543,8 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   const int g = p.xpd ? (blockIdx.x >> 3) : (blockIdx.x / dirs) % NWG;
   const int grp = p.xpd ? (blockIdx.x & 7) / dirs : blockIdx.x / (dirs * NWG);
   if (d >= dirs || g >= NWG || grp >= p.rg) return;
+  // resident: counted for the exchange's residency gate (rnn_comm_gate)
+  if (p.reg && threadIdx.x == 0) __hip_atomic_fetch_add(p.reg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // rows n0 .. nend-1 of the batch (p.gs <= 16 of the 16 MFMA rows)
   const int N = p.N, T = p.T, n0 = grp * p.gs, nend = min(N, n0 + p.gs);
   const int u0 = g * U, ct_own = u0 >> 4, fr0 = u0 & 15;
@@ -1752,6 +1756,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
     if (t_prev >= 0 && !(p.nopf & 2)) e_store(t_prev);
     if (k > 0 && !(p.nopf & 1)) prefetch(k - 1);
     __syncthreads();
+    REC_TRACE(ks, 8);
     if (bad_lds) bad = 1;
     if (gflag && ks > 0 && tid == 0) __hip_atomic_store(gflag, (unsigned)(ks + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (has_e) {
@@ -1824,6 +1829,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
         for (int q = 0; q < NW; q++) estg[en * NW * U + q * U + eu] = MODE == kGru ? dxk[q] : eg[q];
       }
     }
+    REC_TRACE(ks, 12);
     __syncthreads();
     REC_TRACE(ks, 3);
     if (k > 0) {  // partial dh of all units for the next step
@@ -2020,10 +2026,10 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   constexpr int RPR = (U % 16 == 0 && NW <= 4 && 4 * U > RP) ? 4 * U : RP;  // red floats per (wave, row)
   constexpr int kStgOff = (NWV * 16 * RPR + 3 + 3) / 4 * 4;
   AT *stg = reinterpret_cast<AT *>(smem + kStgOff);
-  // IO waves: the G rows of step k in slot k & 3, [4][NW][16 U] floats,
-  // filled by LDS-DMA three steps ahead
+  // IO waves: the G rows of step k in slot k & 7, [8][NW][16 U] floats,
+  // filled by LDS-DMA p.gla (3 or 7) steps ahead
   float *ginl = smem + kStgOff + (NP * 16 * U + 7) / 8 * 4;  // 16-B aligned
-  float *outl = ginl + 4 * NW * 16 * U;  // (IO_OUT) [2][NW + 2][16 U]
+  float *outl = ginl + 8 * NW * 16 * U;  // (IO_OUT) [2][NW + 2][16 U]
   const float *Wd = p.w + d * p.pl_stride;
   const float *R = Wd + p.r_off;
   AT *xch = reinterpret_cast<AT *>(p.xch);
@@ -2111,7 +2117,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // ginl[k & 1] before step k's K-reduction barrier
   const int iot = tid - 64 * CW, ion = iot / U, iou = iot - ion * U;
   const bool io_live = IOW && w >= CW && n0 + ion < nend;
-  // G row of forward-order step kk of this lane's element into slot kk & 3
+  // G row of forward-order step kk of this lane's element into slot kk & 7
   // by LDS-DMA (lane l of IO wave v writes element 64 v + l); NW DMAs per
   // call whatever kk, so that the waits can count them (rows past N and
   // steps past T read a valid row and are never used)
@@ -2121,7 +2127,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
 #pragma unroll
     for (int q = 0; q < NW; q++) {
       const unsigned dst = __builtin_amdgcn_readfirstlane(
-          (unsigned)reinterpret_cast<uintptr_t>(ginl + ((kk & 3) * NW + q) * 16 * U + (w - CW) * 64));
+          (unsigned)reinterpret_cast<uintptr_t>(ginl + ((kk & 7) * NW + q) * 16 * U + (w - CW) * 64));
       dma_lds_dword(p.G + gr + q * H, dst);
     }
   };
@@ -2136,13 +2142,22 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     for (int q = 0; q < NW; q++) p.G[grow + q * H] = o[(1 + q) * 16 * U];
     p.aux[yrow] = o[(NW + 1) * 16 * U];
   };
-  if constexpr (IOW) {
-    if (w >= CW) {  // steps 0..2; step 0's in place before the loop's first barrier
-      io_dma(0);
-      io_dma(1);
-      io_dma(2);
+  // the IO waves' wait for step k + 1's G: at most (gla - 1) * NW DMAs (the
+  // steps after it) still in flight
+  const bool gla7 = p.gla == 7;
+  auto io_wait = [&]() {
+    if (gla7) {
+      if constexpr (NW == 4) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+    } else {
       if constexpr (NW == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    }
+  };
+  if constexpr (IOW) {
+    if (w >= CW) {  // steps 0 .. gla - 1; step 0's in place before the loop's first barrier
+      for (int kk = 0; kk < (gla7 ? 7 : 3); kk++) io_dma(kk);
+      io_wait();
     }
     __syncthreads();
   } else {
@@ -2313,7 +2328,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
         for (int v = 1; v < CW; v++) sm += *reinterpret_cast<const floatx4 *>(red + (((long)(v * 16 + en) * U + eu) << 2));
         if constexpr (IOW) {  // this step's G row, put there by the IO waves
 #pragma unroll
-          for (int q = 0; q < NW; q++) gin[q] = ginl[((k & 3) * NW + q) * 16 * U + tid];
+          for (int q = 0; q < NW; q++) gin[q] = ginl[((k & 7) * NW + q) * 16 * U + tid];
         }
 #pragma unroll
         for (int q = 0; q < NW; q++) rh[q] = BF ? sm[q] : ldexpf(sm[q], sOut);
@@ -2377,13 +2392,12 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
       // row-major outputs of step k - 1 (written before the last barrier;
       // their slot is rewritten after the next K-reduction barrier)
       if (!(p.nopf & 1)) {
-        // step k + 3's G into slot (k + 3) & 3 (last read by the cell threads
-        // of step k - 1, before the last barrier), then wait for the DMAs
-        // issued up to step k - 2: step k + 1's G is in place before the
-        // barrier below, two steps after it was asked for
-        io_dma(k + 3);
-        if constexpr (NW == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        // step k + gla's G into slot (k + gla) & 7 (gla <= 7: last read by the
+        // cell threads of step k - 1 at the latest, before the last barrier),
+        // then wait for step k + 1's: in place before the barrier below,
+        // gla - 1 steps after it was asked for
+        io_dma(k + (gla7 ? 7 : 3));
+        io_wait();
       }
       if ((p.nopf & 4) && io_live && k + 2 < T) {
         // diagnostic (KCTC_DIAG_NOPF=5): the same G loads, never waited for
@@ -2752,7 +2766,7 @@ static size_t fwd6_lds_bytes(const RnnDesc &d, const V6Cfg &c) {
   // + the IO waves' G (and output) slots, for the shape that runs them (launch6_u)
   const bool iow = c.U == 16 && c.nth == 512;
   const size_t b = sizeof(float) * (nwv * 16 * rp + 8) + np * 16 * (size_t)c.U * 2 + 16 +
-                   (iow ? sizeof(float) * 16 * c.U * (4 * d.nw() + 2 * (d.nw() + 2)) + 16 : 0);
+                   (iow ? sizeof(float) * 16 * c.U * (8 * d.nw() + 2 * (d.nw() + 2)) + 16 : 0);
   return std::max(b, (size_t)96 * 1024);  // one recurrence workgroup per CU
 }
 static size_t bwd6_lds_bytes(const RnnDesc &d, const V6Cfg &c) {
@@ -2835,13 +2849,18 @@ namespace {
 // recurrence instead of blocking it (its blocks only wait for recurrence flags).
 int g_usable_cus = 0, g_comm_cus = 0;
 
-// XCDs an XCD-pinned v6 backward recurrence of (d, N) occupies (bit x: XCD
-// x), 0 when it is not pinned: every (row group, direction) needs one XCD of
-// kCusPerXcd workgroups (H / U == 32), and the whole chip's CUs must be usable
-// (no CU partition).  KCTC_XCD6=0 switches it off.
+// XCDs an XCD-pinned v6 recurrence of (d, N) occupies (bit x: XCD x), 0
+// when it is not pinned: every (row group, direction) runs on one XCD, its
+// H / U workgroups on kCusPerXcd (configs[1] / [4]: 32) or kCusPerXcd / 2
+// (configs[2]: U = 32 at H = 512, four row groups x two directions = all
+// eight XCDs, half of each XCD's CUs) of that XCD's CUs, and the whole chip's
+// CUs must be usable (no CU partition).  KCTC_XCD6=0 / KCTC_XCD6F=0 switch it
+// off; KCTC_XCD6_HALF=0 keeps the 16-workgroup shapes unpinned.
 unsigned xcd_mask(const RnnDesc &d, int N, bool fwd) {
   const V6Cfg c6 = pick6(d, N, fwd);
-  if (!c6 || d.H / c6.U != kCusPerXcd || d.dirs * c6.rg > 8) return 0;
+  if (!c6 || d.dirs * c6.rg > 8) return 0;
+  const int nwg = d.H / c6.U;
+  if (nwg != kCusPerXcd && !(nwg == kCusPerXcd / 2 && env_int("KCTC_XCD6_HALF", 1))) return 0;
   if (!env_int(fwd ? "KCTC_XCD6F" : "KCTC_XCD6", 1)) return 0;
   int dev = 0, cus = 0;
   KCTC_HIP_CHECK(hipGetDevice(&dev));
@@ -2853,7 +2872,9 @@ unsigned xcd_mask(const RnnDesc &d, int N, bool fwd) {
   // each mask bit selects one CU in every XCD): pinned only without an
   // exchange.  No exchange kernel runs during a forward pass (the previous
   // step's updates waited for every bucket), so the forward stays pinned.
-  if (!fwd && rnn_comm_cus() > 0) return 0;
+  // With a residency-gated exchange (rnn_set_comm_gated) no exchange kernel
+  // is in flight while a backward recurrence becomes resident, so it stays pinned.
+  if (!fwd && rnn_comm_cus() > 0 && !rnn_comm_gated()) return 0;
   return (1u << (d.dirs * c6.rg)) - 1u;
 }
 
@@ -2981,6 +3002,55 @@ int rnn_usable_cus() {
 }
 int rnn_comm_cus() { return g_comm_cus; }
 
+// ---- residency gate of the gradient exchange (rnn.h) ----
+namespace {
+struct RegWord {
+  unsigned *word = nullptr;  // [0]: registrations, [1]: gate timeouts
+  unsigned expected = 0;     // host: registrations once every enqueued launch is resident
+};
+RegWord g_reg[64];
+bool g_comm_gated = false;
+RegWord &reg_of_device() {
+  int dev = 0;
+  KCTC_HIP_CHECK(hipGetDevice(&dev));
+  RegWord &r = g_reg[dev & 63];
+  if (!r.word) {
+    KCTC_HIP_CHECK(hipMalloc(&r.word, 256));
+    KCTC_HIP_CHECK(hipMemset(r.word, 0, 256));
+  }
+  return r;
+}
+}  // namespace
+
+// one wave: wait until *word - target >= 0 (wrap-safe), at most 10 s
+__global__ __launch_bounds__(64) void comm_gate_kernel(const unsigned *word, unsigned target, unsigned *gerr) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  bool late = false;
+  while (true) {
+    const unsigned v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if ((int)(v - target) >= 0) break;
+    late = __builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull;  // 100 MHz clock
+    if (late) break;
+    __builtin_amdgcn_s_sleep(8);
+  }
+  if (late && threadIdx.x == 0) atomicOr(gerr, 1u);
+}
+
+unsigned rnn_bwd_registrations() { return reg_of_device().expected; }
+void rnn_comm_gate(hipStream_t s, unsigned target) {
+  RegWord &r = reg_of_device();
+  hipLaunchKernelGGL(comm_gate_kernel, dim3(1), dim3(64), 0, s, r.word, target, r.word + 1);
+  KCTC_HIP_CHECK(hipGetLastError());
+}
+unsigned rnn_comm_gate_errors() {
+  RegWord &r = reg_of_device();
+  unsigned h = 0;
+  KCTC_HIP_CHECK(hipMemcpy(&h, r.word + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
+  return h;
+}
+void rnn_set_comm_gated(bool on) { g_comm_gated = on; }
+bool rnn_comm_gated() { return g_comm_gated; }
+
 int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *w, float *y, void *workspace, size_t ws_bytes,
                          void *reserve, size_t res_bytes, unsigned *err, RnnFwdChain *chain,
@@ -3082,6 +3152,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
     p.poll_sleep = env_int("KCTC_POLL_SLEEP", 1);
     p.nopf = env_int("KCTC_DIAG_NOPF", 0);
+    p.gla = env_int("KCTC_FWD_GLA", 3) == 7 ? 7 : 3;  // G rows fetched 3 or 7 steps ahead (IO waves)
     p.wwait = env_int("KCTC_FWD_WWAIT", 1);  // measured: forward recurrence 29.7 -> 28.6 ms/step
     const bool chained = l == d.layers - 1 && chain_ok(d, ver, T, N, chain);
     if (ver == 6) {
@@ -3385,6 +3456,11 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
         KCTC_HIP_CHECK(hipMemsetAsync(p.cmax, 0, sizeof(unsigned) * 2 * dirs * NW * H, s));
     }
     const hipEvent_t fork = (streamed || wstream) ? fork_event(s) : nullptr;
+    if (ver == 6) {  // registration for the exchange's residency gate
+      RegWord &rw = reg_of_device();
+      p.reg = rw.word;
+      rw.expected += (unsigned)(dirs * p.nwg * p.rg);
+    }
     {
       ProfSpan ps(s, "rnn_bwd_rec");
       if (ver == 6) launch6(false, d.mode, d.prec, c6.nth, p, grid, lds, s);

@@ -50,10 +50,103 @@ int kctc_comm_ctas() {
   return std::max(1, std::min(v, 64));
 }
 
-class RcclExchange : public kctc::nnet2::GradExchange {
+// Residency-gated exchange: a bucket's reduction is queued on
+// the comm stream only behind the NEXT backward recurrence's launch, after a
+// one-wave gate kernel that waits until every workgroup of that recurrence is
+// resident (rnn_comm_gate), and the launch of the recurrence after that waits
+// for it.  So no exchange kernel holds a CU while a recurrence's workgroups
+// are being placed -- the condition under which an XCD-pinned recurrence
+// (which needs all CUs of its XCDs) could wait on an all-reduce that waits on
+// another GPU -- and the backward recurrences stay XCD-pinned with the
+// exchange configured (rnn_set_comm_gated).  The last bucket (bottom
+// component) goes out at Finish, with no recurrence after it.  KCTC_COMM_GATE=0
+// reduces every bucket at once and leaves the backward unpinned (round 3).
+class GatedExchange : public kctc::nnet2::GradExchange {
+ public:
+  GatedExchange(hipStream_t compute, int comm_cus) : compute_(compute) {
+    const char *e = getenv("KCTC_COMM_GATE");
+    gated_ = !(e && *e == '0');
+    kctc::rnn_set_cu_budget(kctc_usable_cus_override(), comm_cus);
+    kctc::rnn_set_comm_gated(gated_);
+    KCTC_HIP_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
+    KCTC_HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+  }
+  ~GatedExchange() override {
+    kctc::rnn_set_cu_budget(kctc_usable_cus_override(), 0);
+    kctc::rnn_set_comm_gated(false);
+    (void)hipStreamSynchronize(comm_stream_);
+    (void)hipStreamDestroy(comm_stream_);
+    (void)hipEventDestroy(done_);
+    for (auto ev : pool_) (void)hipEventDestroy(ev);
+  }
+  void GradReady(int, float *grad, long n, hipStream_t producer) override {
+    if (next_ev_ == pool_.size()) {
+      hipEvent_t ev;
+      KCTC_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      pool_.push_back(ev);
+    }
+    hipEvent_t ev = pool_[next_ev_++];
+    KCTC_HIP_CHECK(hipEventRecord(ev, producer));
+    pending_.push_back({grad, n, ev});
+    if (!gated_) Launch();
+  }
+  void BeforeRecurrence(hipStream_t compute) override {
+    // the reductions queued behind the previous recurrence ran while it was
+    // resident; this launch waits for them (they normally end long before)
+    if (gated_ && launched_) KCTC_HIP_CHECK(hipStreamWaitEvent(compute, done_, 0));
+    launched_ = false;
+  }
+  void AfterRecurrence() override {
+    if (!gated_ || pending_.empty()) return;
+    kctc::rnn_comm_gate(comm_stream_, kctc::rnn_bwd_registrations());
+    Launch();
+  }
+  void Finish() override {
+    Launch();
+    KCTC_HIP_CHECK(hipEventRecord(done_, comm_stream_));
+    KCTC_HIP_CHECK(hipStreamWaitEvent(compute_, done_, 0));
+    launched_ = false;
+    next_ev_ = 0;
+  }
+  void AllReduceSum(float *buf, long n, hipStream_t s) override {
+    KCTC_HIP_CHECK(hipEventRecord(done_, s));
+    KCTC_HIP_CHECK(hipStreamWaitEvent(comm_stream_, done_, 0));
+    Reduce(buf, n);
+    KCTC_HIP_CHECK(hipEventRecord(done_, comm_stream_));
+    KCTC_HIP_CHECK(hipStreamWaitEvent(s, done_, 0));
+  }
+
+ protected:
+  virtual void Reduce(float *buf, long n) = 0;  // in place on comm_stream_
+  hipStream_t compute_, comm_stream_ = nullptr;
+
+ private:
+  void Launch() {
+    if (pending_.empty()) return;
+    for (const auto &b : pending_) {
+      KCTC_HIP_CHECK(hipStreamWaitEvent(comm_stream_, b.ready, 0));
+      Reduce(b.grad, b.n);
+    }
+    pending_.clear();
+    KCTC_HIP_CHECK(hipEventRecord(done_, comm_stream_));
+    launched_ = true;
+  }
+  struct Bucket {
+    float *grad;
+    long n;
+    hipEvent_t ready;
+  };
+  bool gated_ = true, launched_ = false;
+  hipEvent_t done_ = nullptr;
+  std::vector<hipEvent_t> pool_;
+  size_t next_ev_ = 0;
+  std::vector<Bucket> pending_;
+};
+
+class RcclExchange : public GatedExchange {
  public:
   RcclExchange(const void *uid, int rank, int world, hipStream_t compute)
-      : world_(world), compute_(compute) {
+      : GatedExchange(compute, kctc_comm_ctas()), world_(world) {
     ncclUniqueId id;
     memcpy(&id, uid, sizeof(id));
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
@@ -62,44 +155,22 @@ class RcclExchange : public kctc::nnet2::GradExchange {
     cfg.minCTAs = std::min(cfg.maxCTAs, 4);
     if (ncclCommInitRankConfig(&comm_, world, id, rank, &cfg) != ncclSuccess)
       throw std::runtime_error("ncclCommInitRankConfig failed");
-    kctc::rnn_set_cu_budget(kctc_usable_cus_override(), cfg.maxCTAs);
-    KCTC_HIP_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
-    KCTC_HIP_CHECK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
-    KCTC_HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
   }
   ~RcclExchange() override {
-    kctc::rnn_set_cu_budget(kctc_usable_cus_override(), 0);
     (void)hipStreamSynchronize(comm_stream_);
     ncclCommDestroy(comm_);
-    (void)hipStreamDestroy(comm_stream_);
-    (void)hipEventDestroy(ready_);
-    (void)hipEventDestroy(done_);
-  }
-  void GradReady(int, float *grad, long n, hipStream_t producer) override {
-    KCTC_HIP_CHECK(hipEventRecord(ready_, producer));
-    KCTC_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ready_, 0));
-    if (ncclAllReduce(grad, grad, (size_t)n, ncclFloat, ncclSum, comm_, comm_stream_) != ncclSuccess)
-      throw std::runtime_error("ncclAllReduce failed");
-  }
-  void Finish() override {
-    KCTC_HIP_CHECK(hipEventRecord(done_, comm_stream_));
-    KCTC_HIP_CHECK(hipStreamWaitEvent(compute_, done_, 0));
   }
   int WorldSize() const override { return world_; }
-  void AllReduceSum(float *buf, long n, hipStream_t s) override {
-    KCTC_HIP_CHECK(hipEventRecord(ready_, s));
-    KCTC_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ready_, 0));
+
+ protected:
+  void Reduce(float *buf, long n) override {
     if (ncclAllReduce(buf, buf, (size_t)n, ncclFloat, ncclSum, comm_, comm_stream_) != ncclSuccess)
       throw std::runtime_error("ncclAllReduce failed");
-    KCTC_HIP_CHECK(hipEventRecord(done_, comm_stream_));
-    KCTC_HIP_CHECK(hipStreamWaitEvent(s, done_, 0));
   }
 
  private:
   int world_;
-  hipStream_t compute_, comm_stream_ = nullptr;
   ncclComm_t comm_ = nullptr;
-  hipEvent_t ready_ = nullptr, done_ = nullptr;
 };
 
 // The same exchange over a host transport (kctc_nnet_enable_dp_host): the
@@ -163,41 +234,25 @@ class HostExchange : public kctc::nnet2::GradExchange {
 // "all-reduce" of every gradient bucket is a kernel holding `blocks` whole CUs
 // for `usec` on the comm stream -- the worst case of an exchange kernel that
 // keeps its CUs to itself while the next component's backward recurrence and
-// streamed dx GEMM run.  The gradients are not touched (a sum over one rank).
-class CuProbeExchange : public kctc::nnet2::GradExchange {
+// streamed dx GEMM run.  Gated like RcclExchange (the backward stays pinned);
+// the gradients are not touched (a sum over one rank).
+class CuProbeExchange : public GatedExchange {
  public:
-  CuProbeExchange(int blocks, double usec, hipStream_t compute) : blocks_(blocks), usec_(usec), compute_(compute) {
-    KCTC_HIP_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
-    KCTC_HIP_CHECK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
-    KCTC_HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
-    kctc::rnn_set_cu_budget(kctc_usable_cus_override(), blocks);
-  }
-  ~CuProbeExchange() override {
-    kctc::rnn_set_cu_budget(kctc_usable_cus_override(), 0);
-    (void)hipStreamSynchronize(comm_stream_);
-    (void)hipStreamDestroy(comm_stream_);
-    (void)hipEventDestroy(ready_);
-    (void)hipEventDestroy(done_);
-  }
-  void GradReady(int, float *, long, hipStream_t producer) override {
-    KCTC_HIP_CHECK(hipEventRecord(ready_, producer));
-    KCTC_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ready_, 0));
-    kctc::cu_hold(comm_stream_, blocks_, usec_);
-    launches_++;
-  }
-  void Finish() override {
-    KCTC_HIP_CHECK(hipEventRecord(done_, comm_stream_));
-    KCTC_HIP_CHECK(hipStreamWaitEvent(compute_, done_, 0));
-  }
+  CuProbeExchange(int blocks, double usec, hipStream_t compute)
+      : GatedExchange(compute, blocks), blocks_(blocks), usec_(usec) {}
   int WorldSize() const override { return 1; }
   void AllReduceSum(float *, long, hipStream_t) override {}
   long launches_ = 0;
 
+ protected:
+  void Reduce(float *, long) override {
+    kctc::cu_hold(comm_stream_, blocks_, usec_);
+    launches_++;
+  }
+
  private:
   int blocks_;
   double usec_;
-  hipStream_t compute_, comm_stream_ = nullptr;
-  hipEvent_t ready_ = nullptr, done_ = nullptr;
 };
 
 }  // namespace

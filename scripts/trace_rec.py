@@ -37,9 +37,10 @@ def main(path):
     if ok.any():
         print(f"  shader clock (s_memtime / s_memrealtime) ~{np.median(m[ok] / r[ok]) / 1e9:.2f} GHz")
     # phases this kernel records (slot 7: hand-off stores issued, before the drain), in time order
-    stamps = [i for i in (0, 1, 2, 3, 7, 4, 5) if tr[sl, :, i].min() > 0]
+    stamps = [i for i in (0, 1, 2, 8, 12, 3, 7, 4, 5) if tr[sl, :, i].min() > 0]
     stamps.sort(key=lambda i: np.median(tr[sl, :, i] - tr[sl, :, 0]))
-    pnames = {0: "start", 1: "flags", 2: "loads", 3: "reduced", 4: "published", 5: "end", 7: "stored"}
+    pnames = {0: "start", 1: "flags", 2: "loads", 3: "reduced", 4: "published", 5: "end", 7: "stored",
+              8: "barrier1", 12: "cell"}
     for a, b in zip(stamps[:-1], stamps[1:]):
         d = (tr[sl, :, b] - tr[sl, :, a]) * us
         nm = f"{pnames[a]}->{pnames[b]}"

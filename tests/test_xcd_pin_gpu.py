@@ -7,7 +7,8 @@ ring of two step images), and the streamed dx GEMM keeps off those XCDs and
 follows sc1 copies of the recurrence's flags.  Only where the bytes travel
 changes, not the arithmetic: the trained parameters must equal the
 unpinned run's (KCTC_XCD6=0) bit for bit, for LSTM and GRU, BLSTM with one
-and two row groups, and a ragged minibatch.  The forward recurrence pins the
+and two row groups, a ragged minibatch, and the configs[2] shape (N = 64:
+four row groups x two directions of 16 workgroups, one per XCD).  The forward recurrence pins the
 same way (KCTC_XCD6F): its h hand-off through a ring of two L2-resident step
 images, the per-step images written through for the next component's
 streamed projection, which follows sc1 copies of the epochs."""
@@ -39,7 +40,10 @@ def _train(kctc, gpu, cfg, batch, pinned, steps=2, var="KCTC_XCD6"):
 
 
 @pytest.mark.parametrize("var", ["KCTC_XCD6", "KCTC_XCD6F"])
-@pytest.mark.parametrize("mode,N,T", [(2, 16, 400), (2, 8, 300), (3, 16, 300), (2, 13, 350)])
+@pytest.mark.parametrize("mode,N,T", [(2, 16, 400), (2, 8, 300), (3, 16, 300), (2, 13, 350),
+                                      # configs[2]: four 16-row groups of U = 32 (16 workgroups a
+                                      # direction): eight slots of 16 workgroups, one per XCD
+                                      (2, 64, 200), (3, 64, 160), (2, 57, 180)])
 def test_pinned_bit_identical(kctc, gpu, mode, N, T, var):
     D, H, A, R = 40, 512, 41, 2
     cfg = kctc.recipe_config(num_rnn=R, input_dim=D, hidden=H, num_targets=A, learning_rate=5e-4,
