@@ -504,7 +504,7 @@ void CuDNNRecurrentComponent::Forward(const CuMatrixBase &in, CuMatrixBase *out,
   input_projected_ = false;
   ProfScope ps("layer_rnn_forward");
   int st = rnn_forward_training(desc_, S(), T, N, in.Data(), params_.f(), out->Data(), workspace_.p,
-                                workspace_.bytes, reserve_.p, reserve_.bytes, DeviceError(), chain, projected);
+                                workspace_.bytes, reserve_.p, reserve_.bytes, DeviceError(), chain, projected, in_rows_);
   if (st) throw std::runtime_error("rnn_forward_training failed: " + std::to_string(st));
 }
 
@@ -543,7 +543,7 @@ void CuDNNRecurrentComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
       ProfScope ps("layer_rnn_backward_weights", ws);
       int st = rnn_backward_weights(desc_, ws, T, N, in_value.Data(), out_value.Data(), workspace_.p,
                                     workspace_.bytes, to_update->grad_.f(), reserve_.p, reserve_.bytes,
-                                    side_gemm_blocks(), input_bound_);
+                                    side_gemm_blocks(), input_bound_, nullptr, in_cols_);
       if (st) throw std::runtime_error("rnn_backward_weights failed: " + std::to_string(st));
     }
     return;
@@ -573,9 +573,16 @@ void CuDNNRecurrentComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
     int st = rnn_backward_weights(desc_, ws, T, N, in_value.Data(), out_value.Data(), workspace_.p,
                                   workspace_.bytes, to_update->grad_.f(), reserve_.p, reserve_.bytes,
                                   dev.side ? side_gemm_blocks() : 0, input_bound_,
-                                  (!in_deriv && dev.side) ? dev.stream2 : nullptr);
+                                  (!in_deriv && dev.side) ? dev.stream2 : nullptr, in_cols_);
     if (st) throw std::runtime_error("rnn_backward_weights failed: " + std::to_string(st));
   }
+}
+
+bool CuDNNRecurrentComponent::PackedOutput(const void **rows, const void **cols) const {
+  *rows = *cols = nullptr;
+  if (!reserve_.p || seq_length_ <= 0 || mini_batch_ <= 0) return false;
+  if (reserve_.bytes < sizeof(float) * (size_t)rnn_reserve_layout(desc_, seq_length_, mini_batch_).total) return false;
+  return rnn_packed_output(desc_, seq_length_, mini_batch_, reserve_.p, rows, cols);
 }
 
 hipStream_t UpdatableComponent::GradStream() const { return grad_stream_ ? grad_stream_ : S(); }
@@ -1542,8 +1549,17 @@ void NnetCtcUpdater::SetupChunks(int T_max, int N) {
 
 void NnetCtcUpdater::Propagate(int T, int N) {  // :136-169
   const int C = nnet_->NumComponents();
+  const CuDNNRecurrentComponent *below = nullptr;  // the last RNN, through identity components
   for (int c = 0; c < C; c++) {
     const Component &comp = nnet_->GetComponent(c);
+    if (const auto *r = dynamic_cast<const CuDNNRecurrentComponent *>(&comp)) {
+      const void *rows = nullptr, *cols = nullptr;
+      if (below && below->Desc().prec == r->Desc().prec) below->PackedOutput(&rows, &cols);
+      r->SetPackedInput(rows, cols);
+      below = r;
+    } else if (!comp.IsIdentityForward()) {
+      below = nullptr;
+    }
     const CuMatrixBase &in = forward_data_[c];
     CuMatrix &out = forward_data_[c + 1];
     if (comp.IsIdentityForward()) {

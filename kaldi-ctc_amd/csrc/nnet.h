@@ -294,6 +294,12 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   // following RNN with only identity-forward components in between; `next`
   // then skips that projection in its own Propagate.
   void PropagateChained(const CuMatrixBase &in, CuMatrixBase *out, const CuDNNRecurrentComponent &next) const;
+  // bf16 one-layer bidirectional components write their output also as the
+  // packed bf16 GEMM operands (rnn.h rnn_packed_output); the next RNN reads
+  // them instead of packing its input (set by the updater from the RNN below,
+  // through identity components; nullptrs: pack)
+  bool PackedOutput(const void **rows, const void **cols) const;
+  void SetPackedInput(const void *rows, const void *cols) const { in_rows_ = rows; in_cols_ = cols; }
 
  private:
   void Init(Rng &rng);
@@ -305,6 +311,7 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   mutable int mini_batch_ = 0, seq_length_ = 0;
   mutable bool input_projected_ = false;  // set by the previous component's PropagateChained
   mutable float input_bound_ = 0.f;       // ditto: bound on |input| (0: unknown)
+  mutable const void *in_rows_ = nullptr, *in_cols_ = nullptr;  // SetPackedInput
   unsigned *err_ = nullptr;
   mutable unsigned *err_ext_ = nullptr;
   void Forward(const CuMatrixBase &in, CuMatrixBase *out, RnnFwdChain *chain) const;

@@ -33,6 +33,13 @@ struct RnnDesc {
 // backward exactly like cuDNN's reserveSpace.
 struct RnnReserveLayout {
   long G, aux, E, DX, bias, out, dout, per_layer, total;
+  // bf16 precision: the backward recurrence's packed bf16 dGates operands
+  // (RecParams::dxr / dxt / et; float offsets, 0 bytes otherwise), frames
+  // padded to kbt64 per packed row
+  long pkxr, pkxt, pket, kbt64;
+  // bf16, one layer, bidirectional: the forward's packed bf16 copies of its
+  // output (rows [T*N][2H], columns [2H][kbt64]); see rnn_packed_output
+  long pkyr, pkyc;
 };
 RnnReserveLayout rnn_reserve_layout(const RnnDesc &d, int T, int N);
 size_t rnn_workspace_bytes(const RnnDesc &d, int T, int N);
@@ -91,10 +98,19 @@ struct RnnFwdChain {
   hipStream_t side = nullptr;
   bool done = false;
 };
+// in_rows (nullable): the input already packed as bf16 rows [T*N][D] (the
+// previous component's rnn_packed_output), used by a bf16 input projection
+// instead of packing x
 int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *w, float *y, void *workspace, size_t ws_bytes,
                          void *reserve, size_t res_bytes, unsigned *err, RnnFwdChain *chain = nullptr,
-                         bool input_projected = false);
+                         bool input_projected = false, const void *in_rows = nullptr);
+// bf16 one-layer bidirectional components: the forward recurrence also writes
+// its output as packed bf16 rows [T*N][2H] and columns [2H][kbt64] into the
+// reserve (the GEMM operands the next component's projection / dW and this
+// component's dR read).  Pointers valid after rnn_forward_training of (T, N)
+// on this reserve; false (nullptrs) for other components.
+bool rnn_packed_output(const RnnDesc &d, int T, int N, void *reserve, const void **rows, const void **cols);
 // Weight gradients of a one-layer bidirectional split-fp16 LSTM computed off
 // its RUNNING backward recurrence (the bottom component, which has no dx to
 // stream): the frames are cut into `chunks` per direction in the order the
@@ -122,6 +138,7 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
                          const float *y, void *workspace, size_t ws_bytes, float *dw,
                          void *reserve, size_t res_bytes, int max_blocks = 0,
                          float in_bound = 0.f,  // > 0: |x| <= in_bound (an LSTM/GRU below)
-                         hipStream_t s2 = nullptr);  // second stream: dW beside dR (nothing else to overlap)
+                         hipStream_t s2 = nullptr,  // second stream: dW beside dR (nothing else to overlap)
+                         const void *in_cols = nullptr);  // bf16: x packed as columns (rnn_packed_output)
 
 }  // namespace kctc

@@ -92,6 +92,15 @@ RnnReserveLayout rnn_reserve_layout(const RnnDesc &d, int T, int N) {
   r.bias = p; p += al64(dirs * 2 * nw * H * (long)((N + 7) / 8));  // v6: per row group (>= 8 rows each)
   r.out = p;  p += (d.layers > 1) ? al64(TN * dirs * H) : 0;
   r.dout = p; p += (d.layers > 1) ? al64(TN * dirs * H) : 0;
+  r.kbt64 = (TN + 63) / 64 * 64;
+  const bool pkd = d.prec == 1 /* kPrecBf16 */;  // bf16 halves: 2 per float
+  const long G4 = nw * H, kbg64 = (G4 + 63) / 64 * 64;
+  r.pkxr = p; p += pkd ? al64((dirs * TN * kbg64 + 1) / 2) : 0;
+  r.pkxt = p; p += pkd ? al64((dirs * G4 * r.kbt64 + 1) / 2) : 0;
+  const bool io = pkd && d.layers == 1 && dirs == 2;  // bf16_io: E^T shifted, apart from DX^T
+  r.pket = p; p += (pkd && (d.mode == kGru || io)) ? al64((dirs * G4 * r.kbt64 + 1) / 2) : 0;
+  r.pkyr = p; p += io ? al64((TN * dirs * H + 1) / 2) : 0;
+  r.pkyc = p; p += io ? al64((dirs * H * r.kbt64 + 1) / 2) : 0;
   r.per_layer = p;
   r.total = p * d.layers;
   return r;
@@ -190,6 +199,25 @@ static bool use_x3(int K, int min_k = 128) {
 static bool bounded_out(const RnnDesc &d) { return d.mode != kRelu; }
 
 namespace {
+int env_int(const char *name, int dflt);
+}  // namespace
+
+// bf16 recurrences write their dGates straight into the packed bf16 GEMM
+// operands (RecParams::dxr / dxt / et) -- v6 only (a v6 backward runs for
+// every bf16 shape), whole 64-element gate rows
+static bool bf16_direct(const RnnDesc &d, int ver) {
+  return d.prec == 1 /* kPrecBf16 */ && ver == 6 && (d.nw() * d.H) % 64 == 0 && env_int("KCTC_BF16_DIRECT", 0);
+}
+// ... and, one-layer bidirectional, the forward writes its output packed
+// (RecParams::yr / yc) and the backward E^T shifted (eshift); H % 32 == 0 so
+// that a workgroup's units fill whole 16-B row chunks
+static bool bf16_io(const RnnDesc &d) {
+  return bf16_direct(d, 6) && d.layers == 1 && d.dirs == 2 && d.H % 32 == 0 && (2 * d.H) % 64 == 0;
+}
+
+
+
+namespace {
 
 constexpr int NT = 256;
 constexpr unsigned kSent = 0xFFFFFFFFu;
@@ -269,17 +297,33 @@ struct RecParams {
   int bfpart;       // v6 backward, bf16 mode: partial dh exchanged as bf16 (KCTC_BF16_PARTIALS)
   unsigned *cmax;   // v6 backward: column max |DX| [dirs * nW * H] (GRU: then |E|), as float bits
   unsigned *reg;    // v6 backward: per-device registration word (+1 per workgroup at start)
+  // v6 backward, bf16 (RnnReserveLayout::pk): dGates written straight into the
+  // packed bf16 operands of the GEMMs after the recurrence, instead of fp32
+  // rows that pack kernels re-read: dxr = DX rows [dir][T*N][nW*H] (A of the
+  // dx GEMM), dxt = DX^T [dir][nW*H][kbt64] (A of dW), et = E^T (A of dR; ==
+  // dxt for an LSTM), frames along the packed rows (kbt64 >= T*N, zero tail)
+  __bf16 *dxr, *dxt, *et;
+  long kbt64;
+  // bf16 one-layer bidirectional (bf16_io): the forward writes its output h as
+  // packed bf16 too -- yr = rows [T*N][dirs*H] (A of the next component's
+  // input projection), yc = columns [dirs*H][kbt64] (B of this component's dR
+  // and of the next component's dW) -- and the backward then writes E^T
+  // shifted by one step (eshift: direction 0 frame f at f - N, direction 1 at
+  // f + N), so that dR pairs it with the unshifted yc
+  __bf16 *yr, *yc;
+  int eshift;
 };
 
 // Phase stamps of the first kTraceSteps steps ([steps][grid][16]; thread 0 of every workgroup;
 // 100 MHz constant clock), only when the host passes a trace buffer
 // (KCTC_REC_TRACE): 0 step start, 1 flags seen, 2 operand loads landed,
 // 3 MFMA + K reduction done, 4 published (+ flag), 5 step end.
-constexpr int kTraceSteps = 256;
+// v6 backward: slots 16 + w flags seen by wave w, 24 + w its hand-off loads landed.
+constexpr int kTraceSteps = 256, kTraceStride = 32;
 #define REC_TRACE(kk, ph)                                                                 \
   do {                                                                                    \
     if (p.trace && threadIdx.x == 0 && (kk) < kTraceSteps) {                              \
-      unsigned long long *tr_ = p.trace + ((long)(kk) * gridDim.x + blockIdx.x) * 16;     \
+      unsigned long long *tr_ = p.trace + ((long)(kk) * gridDim.x + blockIdx.x) * kTraceStride; \
       tr_[(ph)] = __builtin_amdgcn_s_memrealtime();                                       \
       if ((ph) == 2 || (ph) == 3) tr_[12 + (ph)] = __builtin_amdgcn_s_memtime();          \
     }                                                                                     \
@@ -289,7 +333,7 @@ constexpr int kTraceSteps = 256;
 #define REC_TRACE_W(kk, ph)                                                               \
   do {                                                                                    \
     if (p.trace && (threadIdx.x & 63) == 0 && (kk) < kTraceSteps)                         \
-      p.trace[((long)(kk) * gridDim.x + blockIdx.x) * 16 + (ph) + (threadIdx.x >> 6)] =   \
+      p.trace[((long)(kk) * gridDim.x + blockIdx.x) * kTraceStride + (ph) + (threadIdx.x >> 6)] = \
           __builtin_amdgcn_s_memrealtime();                                               \
   } while (0)
 
@@ -1637,7 +1681,56 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
 #pragma unroll
     for (int q = 0; q < NW; q++) cg[q] = ng[q];
   };
+  // bf16 packed operands (p.dxt): the step's DX tile is staged in estg and the
+  // GRU's E tile in estg2 during the cell phase; the next step writes them as
+  // 16-B bf16 chunks (DX rows; DX^T and E^T columns of 8 frames)
+  float *estg2 = estg + 16 * NW * U;
+  const bool pk = BF && p.dxt != nullptr;
+  auto pk_store = [&](int tt) {
+    if constexpr (BF) {
+      constexpr int RCH = NW * U / 8;  // 16-B row chunks per row
+      const long TNl = (long)T * N, G4 = (long)NW * H;
+      const long f0 = (long)tt * N + n0;
+      // DX rows: thread -> (row, chunk)
+      for (int i = tid; i < 16 * RCH; i += NTH) {
+        const int rn = i / RCH, ch = i - rn * RCH, q = (ch * 8) / U, u = (ch * 8) % U;
+        if (n0 + rn >= nend) continue;
+        bf16x8 v;
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = (__bf16)estg[rn * NW * U + q * U + u + j];
+        *reinterpret_cast<bf16x8 *>(p.dxr + ((long)d * TNl + f0 + rn) * G4 + q * H + u0 + u) = v;
+      }
+      // DX^T (and E^T) columns: thread -> (column, 8-frame half); aligned 16-B
+      // chunks when the 8 frames are whole, else per frame.  E^T shifted
+      // (eshift): frames of step 0 (direction 0) / T - 1 (direction 1) drop out
+      const bool vec8 = (N % 8 == 0) && (n0 % 8 == 0);
+      const int narr = (MODE == kGru || p.eshift) ? 2 : 1;
+      const long esh = p.eshift ? (d == 0 ? -(long)N : (long)N) : 0;
+      const bool edrop = p.eshift && (d == 0 ? tt == 0 : tt == T - 1);
+      for (int i = tid; i < narr * NW * U * 2; i += NTH) {
+        const int which = i / (NW * U * 2), rem = i - which * NW * U * 2, col = rem >> 1, half = rem & 1;
+        if (which && edrop) continue;
+        const float *src = (which && MODE == kGru) ? estg2 : estg;
+        __bf16 *dst = (which ? p.et : p.dxt) + ((long)d * G4 + (col / U) * H + u0 + col % U) * p.kbt64 + f0 + half * 8 +
+                      (which ? esh : 0);
+        const int r0 = half * 8;
+        if (vec8 && n0 + r0 + 8 <= nend) {
+          bf16x8 v;
+#pragma unroll
+          for (int j = 0; j < 8; j++) v[j] = (__bf16)src[(r0 + j) * NW * U + col];
+          *reinterpret_cast<bf16x8 *>(dst) = v;
+        } else {
+          for (int j = 0; j < 8; j++)
+            if (n0 + r0 + j < nend) dst[j] = (__bf16)src[(r0 + j) * NW * U + col];
+        }
+      }
+    }
+  };
   auto e_store = [&](int t) {  // row-major dGates of step t (E; GRU also DX)
+    if (pk) {
+      pk_store(t);
+      return;
+    }
     if (!live) return;
     const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + eu;
     if (p.e_sc1) {  // DX (== E for LSTM) went out through estg already
@@ -1690,7 +1783,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   if (p.xpd && tid == 0) atomicOr(p.flags + kXcdWord, 1u << xcc_id());
   if (tid == 0) loc_lds = 0;
   const int local = (p.xpd && p.allow_local) ? probe6(p, grp, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
-  if (p.trace && tid == 0) p.trace[(long)blockIdx.x * 16 + 9] = (unsigned long long)(local + 1);  // step 0, slot 9
+  if (p.trace && tid == 0) p.trace[(long)blockIdx.x * kTraceStride + 9] = (unsigned long long)(local + 1);  // step 0, slot 9
   // step t's DX rows for a streaming consumer on other XCDs, from the LDS
   // stage: written through (sc1) as whole 16-B chunks, 4 lanes per
   // contiguous 64-B run (4-B write-through stores per element cost ~8 us per
@@ -1717,6 +1810,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
         wait_flags6(flag6(p, grp, d, 0, NWG), NWG, (unsigned)(ks + 1), p.err, bad, &bad_lds, p.poll_sleep);
       }
       REC_TRACE(ks, 1);
+      REC_TRACE_W(ks, 16);
       const auto rs = rsrc(p.xch + (long)(p.ring ? (ks - 1) % p.ring : ks - 1) * xstep, (unsigned)(xstep * 4));
       floatx4 sm = floatx4{0.f, 0.f, 0.f, 0.f};
       if (bfp) {
@@ -1744,6 +1838,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
       }
       st4(red + (long)(pg * POS + pos) * 4, sm);
       REC_TRACE(ks, 2);
+      REC_TRACE_W(ks, 24);
       // behind this step's hand-off loads: the write-through copies for the
       // streamed dx GEMM -- the previous step's dGates rows (staged in LDS)
       // and the epoch the last signal drained (step ks - 2's rows).  Issued
@@ -1824,9 +1919,13 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
         }
         if (eu == 0) rowexp[en] = se + sB;
       }
-      if (p.e_sc1) {
+      if (p.e_sc1 || pk) {
 #pragma unroll
         for (int q = 0; q < NW; q++) estg[en * NW * U + q * U + eu] = MODE == kGru ? dxk[q] : eg[q];
+        if (MODE == kGru && pk) {
+#pragma unroll
+          for (int q = 0; q < NW; q++) estg2[en * NW * U + q * U + eu] = eg[q];
+        }
       }
     }
     REC_TRACE(ks, 12);
@@ -2105,6 +2204,32 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
 #pragma unroll
     for (int q = 0; q < NW; q++) dst[q] = p.G[((long)t * N + n) * ldg + (long)d * NW * H + q * H + u0 + eu];
   };
+  // bf16_io: the step's h (stg, bf16 [16][U]) as packed rows and columns
+  auto y_pk_store = [&](int tt) {
+    if constexpr (BF) {
+      constexpr int RCH = U / 8;
+      const long f0 = (long)tt * N + n0;
+      const int i = tid;
+      if (i < 16 * RCH) {
+        const int rn = i / RCH, ch = i - rn * RCH;
+        if (n0 + rn < nend)
+          *reinterpret_cast<u32x4 *>(p.yr + (f0 + rn) * ldy + (long)d * H + u0 + ch * 8) =
+              *reinterpret_cast<const u32x4 *>(stg + rn * U + ch * 8);
+      } else if (i < 16 * RCH + 2 * U) {
+        const int col = (i - 16 * RCH) >> 1, half = (i - 16 * RCH) & 1, r0 = half * 8;
+        __bf16 *dst = p.yc + ((long)d * H + u0 + col) * p.kbt64 + f0 + r0;
+        if ((N % 8 == 0) && (n0 % 8 == 0) && n0 + r0 + 8 <= nend) {
+          bf16x8 v;
+#pragma unroll
+          for (int j = 0; j < 8; j++) v[j] = stg[(r0 + j) * U + col];
+          *reinterpret_cast<bf16x8 *>(dst) = v;
+        } else {
+          for (int j = 0; j < 8; j++)
+            if (n0 + r0 + j < nend) dst[j] = stg[(r0 + j) * U + col];
+        }
+      }
+    }
+  };
   auto out_store = [&](int t) {  // row-major y, activations (in place of G), aux of step t
     if (!live) return;
     p.y[((long)t * N + n) * ldy + (long)d * H + u0 + eu] = hval;
@@ -2184,7 +2309,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   if (p.xpd && tid == 0) atomicOr(p.flags + kXcdWord, 1u << xcc_id());
   if (tid == 0) loc_lds = 0;
   const int local = (p.xpd && p.allow_local) ? probe6(p, grp, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
-  if (p.trace && tid == 0) p.trace[(long)blockIdx.x * 16 + 9] = (unsigned long long)(local + 1);  // step 0, slot 9
+  if (p.trace && tid == 0) p.trace[(long)blockIdx.x * kTraceStride + 9] = (unsigned long long)(local + 1);  // step 0, slot 9
   const long rbase = (long)T * XS;  // ring slots (p.ring > 0)
   // the published 16 B of h: live across the whole loop (used after it), so
   // that no other value of the step is allocated to the data registers of the
@@ -2282,6 +2407,8 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     asm volatile("" ::: "memory");
     // behind the hand-off loads: last step's row-major outputs, next step's input projection
     if (!IO_OUT && t_prev >= 0 && !(p.nopf & 2)) out_store(t_prev);
+    // (stg still holds step t_prev's h: the cell phase below rewrites it)
+    if (BF && p.yr && t_prev >= 0) y_pk_store(t_prev);
     if (!IOW && k + 1 < T && !(p.nopf & 1)) gin_load(d == 0 ? t + 1 : t - 1, gnx);
     // K partials through LDS.  U % 16 == 0: column ct * 16 + fr of the
     // tile is gate ct / (U / 16) of unit (ct % (U / 16)) * 16 + fr, so a lane
@@ -2444,6 +2571,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   }
   if (IOW && w >= CW) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the IO waves' DMAs (ahead of T) land
   if (t_prev >= 0 && !bad) {
+    if (BF && p.yr) y_pk_store(t_prev);
     if constexpr (IO_OUT) {
       if (w >= CW) io_out(T - 1);  // outl of the last step: written before the loop's last barrier
     } else {
@@ -2591,7 +2719,7 @@ static void launch_rec(bool fwd, int mode, const RecParams &p, dim3 grid, size_t
 
 // KCTC_REC_TRACE=<dir>: trace the first forward and the first backward
 // recurrence launch of the process into <dir>/rec_{fwd,bwd}.bin
-// (int32 header {grid, steps, nwg, T, dirs, version, xpd, 0} then [steps][grid][16] uint64 stamps).
+// (int32 header {grid, steps, nwg, T, dirs, version, xpd, stride} then [steps][grid][stride] uint64 stamps).
 struct RecTrace {
   unsigned long long *dev = nullptr;
   size_t n = 0;
@@ -2602,7 +2730,7 @@ struct RecTrace {
     bool &done = tag[0] == 'f' ? done_fwd : done_bwd;
     if (done) return false;
     done = true;
-    n = (size_t)kTraceSteps * grid * 16;
+    n = (size_t)kTraceSteps * grid * kTraceStride;
     KCTC_HIP_CHECK(hipMalloc(&dev, n * sizeof(unsigned long long)));
     KCTC_HIP_CHECK(hipMemset(dev, 0, n * sizeof(unsigned long long)));
     return true;
@@ -2617,7 +2745,7 @@ struct RecTrace {
     std::string path = std::string(getenv("KCTC_REC_TRACE")) + "/rec_" + tag + ".bin";
     FILE *f = fopen(path.c_str(), "wb");
     if (!f) return;
-    int hdr[8] = {grid, kTraceSteps, nwg, T, dirs, ver, xpd, 0};
+    int hdr[8] = {grid, kTraceSteps, nwg, T, dirs, ver, xpd, kTraceStride};
     fwrite(hdr, sizeof(int), 8, f);
     fwrite(h.data(), sizeof(unsigned long long), n, f);
     fclose(f);
@@ -2773,7 +2901,8 @@ static size_t bwd6_lds_bytes(const RnnDesc &d, const V6Cfg &c) {
   const int K = d.nw() * c.U, KB = (K + 31) / 32, AP = KB * 32 + 8;
   const size_t img = (d.prec == kPrecBf16 ? 1 : 2) * 16 * (size_t)AP * 2;
   const size_t red = sizeof(float) * std::max((size_t)c.nth * 4, (size_t)2 * 16 * c.U * d.nw());
-  const size_t estg = sizeof(float) * 16 * c.U * d.nw();  // dGates tile staged for write-through
+  // dGates tile staged for write-through, and (bf16, packed writes) the E tile beside it
+  const size_t estg = sizeof(float) * 16 * c.U * d.nw() * (d.prec == kPrecBf16 ? 2 : 1);
   // at least 96 KB so that no other workgroup (a side-stream GEMM block)
   // shares the CU with a recurrence workgroup
   return std::max(img + red + estg, (size_t)96 * 1024);
@@ -3051,10 +3180,20 @@ unsigned rnn_comm_gate_errors() {
 void rnn_set_comm_gated(bool on) { g_comm_gated = on; }
 bool rnn_comm_gated() { return g_comm_gated; }
 
+bool rnn_packed_output(const RnnDesc &d, int T, int N, void *reserve, const void **rows, const void **cols) {
+  *rows = *cols = nullptr;
+  if (!bf16_io(d) || !reserve) return false;
+  const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
+  float *res = static_cast<float *>(reserve);
+  *rows = res + lay.pkyr;
+  *cols = res + lay.pkyc;
+  return true;
+}
+
 int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *w, float *y, void *workspace, size_t ws_bytes,
                          void *reserve, size_t res_bytes, unsigned *err, RnnFwdChain *chain,
-                         bool input_projected) {
+                         bool input_projected, const void *in_rows) {
   if (chain) chain->done = false;
   if (T <= 0 || N <= 0 || N > 16 * kMaxRT || d.H % 16) return KRNN_NOT_SUPPORTED;
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
@@ -3096,11 +3235,14 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     } else if (d.prec == kPrecBf16 && use_x3(Din, 32)) {
       // bf16 gate GEMM: input rows and W rows packed as bf16, fp32 accumulation
       const PackLay pl = pack_layout(d, T, N);
-      __bf16 *Ap = pk<__bf16>(workspace, d, T, N, pl.a), *Bp = pk<__bf16>(workspace, d, T, N, pl.b);
+      // the input rows come packed from the previous component's forward (in_rows)
+      const bool rows_in = l == 0 && in_rows && Din % 64 == 0;
+      __bf16 *Ap = rows_in ? static_cast<__bf16 *>(const_cast<void *>(in_rows)) : pk<__bf16>(workspace, d, T, N, pl.a);
+      __bf16 *Bp = pk<__bf16>(workspace, d, T, N, pl.b);
       const int KB = (Din + 63) / 64;
       {
         ProfSpan ps(s, "x3_pack");
-        bf16_pack_rows(s, in, Din, (int)TN, Din, Ap);
+        if (!rows_in) bf16_pack_rows(s, in, Din, (int)TN, Din, Ap);
         bf16_pack_rows(s, wl, Din, NW * H, Din, Bp, dirs, pls, (long)NW * H * KB * 64);
       }
       X3PArgs x;
@@ -3154,6 +3296,14 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.nopf = env_int("KCTC_DIAG_NOPF", 0);
     p.gla = env_int("KCTC_FWD_GLA", 3) == 7 ? 7 : 3;  // G rows fetched 3 or 7 steps ahead (IO waves)
     p.wwait = env_int("KCTC_FWD_WWAIT", 1);  // measured: forward recurrence 29.7 -> 28.6 ms/step
+    if (ver == 6 && bf16_io(d)) {  // the output also as packed bf16 rows and columns
+      p.yr = reinterpret_cast<__bf16 *>(R0 + lay.pkyr);
+      p.yc = reinterpret_cast<__bf16 *>(R0 + lay.pkyc);
+      p.kbt64 = lay.kbt64;
+      if (lay.kbt64 > TN)
+        KCTC_HIP_CHECK(hipMemset2DAsync(p.yc + TN, sizeof(__bf16) * lay.kbt64, 0, sizeof(__bf16) * (lay.kbt64 - TN),
+                                        (size_t)dirs * H, s));
+    }
     const bool chained = l == d.layers - 1 && chain_ok(d, ver, T, N, chain);
     if (ver == 6) {
       // XCD-pinned forward (xcd_mask): each (row group, direction) on one XCD,
@@ -3450,6 +3600,30 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     const bool wstream = wgrad && wgrad->side && !dxl && ver == 6 && !p.xpd && d.layers == 1 &&
                          rnn_wgrad_stream_ok(d, T, N);
     p.e_sc1 = env_int("KCTC_DIAG_ESC1", (streamed || wstream) ? 1 : 0);  // diagnostic override (0 with streaming: wrong dx)
+    // bf16: dGates straight into the packed operands of the dx / dW / dR GEMMs
+    // (no fp32 rows, no pack passes over them; KCTC_BF16_DIRECT=0: the fp32
+    // rows and the pack kernels as in round 3)
+    const bool pkd = bf16_direct(d, ver);  // beside e_sc1's write-through rows when streamed
+    if (pkd) {
+      p.dxr = reinterpret_cast<__bf16 *>(R0 + lay.pkxr);
+      p.dxt = reinterpret_cast<__bf16 *>(R0 + lay.pkxt);
+      p.eshift = bf16_io(d) ? 1 : 0;
+      p.et = (d.mode == kGru || p.eshift) ? reinterpret_cast<__bf16 *>(R0 + lay.pket) : p.dxt;
+      p.kbt64 = lay.kbt64;
+      const size_t pitch = sizeof(__bf16) * lay.kbt64;
+      const size_t rows = (size_t)NW * H;  // per direction
+      if (lay.kbt64 > TN)  // the frame tail of every packed row stays zero
+        KCTC_HIP_CHECK(hipMemset2DAsync(p.dxt + TN, pitch, 0, sizeof(__bf16) * (lay.kbt64 - TN), dirs * rows, s));
+      if (p.eshift) {  // E^T shifted: direction 0 from TN - N on, direction 1 before N and from TN on
+        KCTC_HIP_CHECK(hipMemset2DAsync(p.et + TN - N, pitch, 0, sizeof(__bf16) * (lay.kbt64 - TN + N), rows, s));
+        KCTC_HIP_CHECK(hipMemset2DAsync(p.et + rows * lay.kbt64, pitch, 0, sizeof(__bf16) * N, rows, s));
+        if (lay.kbt64 > TN)
+          KCTC_HIP_CHECK(hipMemset2DAsync(p.et + rows * lay.kbt64 + TN, pitch, 0, sizeof(__bf16) * (lay.kbt64 - TN),
+                                          rows, s));
+      } else if (d.mode == kGru && lay.kbt64 > TN) {
+        KCTC_HIP_CHECK(hipMemset2DAsync(p.et + TN, pitch, 0, sizeof(__bf16) * (lay.kbt64 - TN), dirs * rows, s));
+      }
+    }
     if (ver == 6) {
       p.cmax = pk<unsigned>(workspace, d, T, N, pack_layout(d, T, N).cme);
       if (p.rg > 1)  // max over the row groups by atomicMax on the float bits
@@ -3495,14 +3669,15 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     if (ver == 6) xch_release(s);
     tr.dump("bwd", s, grid.x, p.nwg, T, dirs, ver, ver == 6 ? (p.xpd ? 1 : 0) : p.xpd);
     if (dxl && !streamed && d.prec == kPrecBf16 && use_x3(NW * H)) {
-      // bf16: dGates rows and W^T rows (columns of W) packed as bf16
+      // bf16: dGates rows and W^T rows (columns of W) packed as bf16 (the
+      // dGates rows written packed by the recurrence when pkd)
       const long G4 = (long)NW * H;
       const int KB = (int)((G4 + 63) / 64);
       const PackLay pl = pack_layout(d, T, N);
-      __bf16 *Ap = pk<__bf16>(workspace, d, T, N, pl.a), *Bp = pk<__bf16>(workspace, d, T, N, pl.b);
+      __bf16 *Ap = pkd ? p.dxr : pk<__bf16>(workspace, d, T, N, pl.a), *Bp = pk<__bf16>(workspace, d, T, N, pl.b);
       {
         ProfSpan ps(s, "x3_pack");
-        bf16_pack_rows(s, DX, (long)dirs * G4, (int)TN, (int)G4, Ap, dirs, G4, TN * KB * 64);
+        if (!pkd) bf16_pack_rows(s, DX, (long)dirs * G4, (int)TN, (int)G4, Ap, dirs, G4, TN * KB * 64);
         for (int dir = 0; dir < dirs; dir++)
           bf16_pack_cols(s, wl + dir * pls, Din, (int)G4, Din, 0, Bp + (long)dir * Din * KB * 64);
       }
@@ -3565,7 +3740,8 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
 // ---------------------------------------------------------------------------
 int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *y, void *workspace, size_t ws_bytes, float *dw,
-                         void *reserve, size_t res_bytes, int max_blocks, float in_bound, hipStream_t s2) {
+                         void *reserve, size_t res_bytes, int max_blocks, float in_bound, hipStream_t s2,
+                         const void *in_cols) {
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
   if (res_bytes < sizeof(float) * (size_t)lay.total) return KRNN_BAD_PARAM;
   if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
@@ -3603,15 +3779,27 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       // bf16 weight GEMMs: the transposes packed along the frames as bf16
       const int KB = (int)((TN + 63) / 64);
       const PackLay pl = pack_layout(d, T, N);
-      __bf16 *DXt = pk<__bf16>(workspace, d, T, N, pl.a), *Xt = pk<__bf16>(workspace, d, T, N, pl.b);
-      __bf16 *Yt = pk<__bf16>(workspace, d, T, N, pl.c);
-      __bf16 *Et = d.mode == kGru ? DXt + (long)dirs * G4 * KB * 64 : DXt;
+      // the dGates transposes: written packed by the backward recurrence (bf16_direct)
+      const bool pkd = bf16_direct(d, 6);
+      // bf16_io: the forward wrote y^T packed (unshifted) and the backward
+      // E^T shifted by one step; the input's columns may come packed from the
+      // previous component's forward (in_cols)
+      const bool io = bf16_io(d);
+      const bool cols_in = l == 0 && in_cols != nullptr;
+      __bf16 *DXt = pkd ? reinterpret_cast<__bf16 *>(R0 + lay.pkxt) : pk<__bf16>(workspace, d, T, N, pl.a);
+      __bf16 *Xt = cols_in ? static_cast<__bf16 *>(const_cast<void *>(in_cols)) : pk<__bf16>(workspace, d, T, N, pl.b);
+      __bf16 *Yt = io ? reinterpret_cast<__bf16 *>(R0 + lay.pkyc) : pk<__bf16>(workspace, d, T, N, pl.c);
+      __bf16 *Et = (d.mode == kGru || io)
+                       ? (pkd ? reinterpret_cast<__bf16 *>(R0 + lay.pket) : DXt + (long)dirs * G4 * KB * 64)
+                       : DXt;
       {
         ProfSpan ps(s, "x3_pack_w");
-        bf16_pack_cols(s, DX, ldg, (int)TN, (int)(dirs * G4), 0, DXt);
-        if (d.mode == kGru) bf16_pack_cols(s, E, ldg, (int)TN, (int)(dirs * G4), 0, Et);
-        bf16_pack_cols(s, in, Din, (int)TN, Din, 0, Xt);
-        if (T > 1)
+        if (!pkd) {
+          bf16_pack_cols(s, DX, ldg, (int)TN, (int)(dirs * G4), 0, DXt);
+          if (d.mode == kGru) bf16_pack_cols(s, E, ldg, (int)TN, (int)(dirs * G4), 0, Et);
+        }
+        if (!cols_in) bf16_pack_cols(s, in, Din, (int)TN, Din, 0, Xt);
+        if (T > 1 && !io)
           for (int dir = 0; dir < dirs; dir++)
             bf16_pack_cols(s, out + (long)dir * H, ldy, (int)TN, H, dir == 0 ? N : -N, Yt + (long)dir * H * KB * 64);
       }

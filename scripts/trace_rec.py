@@ -10,8 +10,8 @@ import numpy as np
 
 def main(path):
     raw = open(path, "rb").read()
-    grid, steps, nwg, T, dirs, ver, xpd, _ = np.frombuffer(raw[:32], dtype=np.int32)
-    tr = np.frombuffer(raw[32:], dtype=np.uint64).reshape(steps, grid, 16).astype(np.int64)
+    grid, steps, nwg, T, dirs, ver, xpd, stride = np.frombuffer(raw[:32], dtype=np.int32)
+    tr = np.frombuffer(raw[32:], dtype=np.uint64).reshape(steps, grid, stride or 16).astype(np.int64)
     steps = min(steps, T)
     tr = tr[:steps]
     if xpd == 0:  # v6: block b -> (dir b % dirs, g b / dirs)
@@ -45,7 +45,16 @@ def main(path):
         d = (tr[sl, :, b] - tr[sl, :, a]) * us
         nm = f"{pnames[a]}->{pnames[b]}"
         print(f"  {nm:22s} median {np.median(d):7.3f}  p90 {np.percentile(d, 90):7.3f}")
-    if ver >= 4 and tr[sl, :, 6].min() > 0:
+    if tr.shape[2] >= 32 and tr[sl, :, 16].min() > 0:  # v6 backward: per-wave flags / loads
+        nwv = max(w for w in range(8) if tr[sl, :, 16 + w].min() > 0) + 1
+        for w in range(nwv):
+            fl = (tr[sl, :, 16 + w] - tr[sl, :, 0]) * us
+            ld = (tr[sl, :, 24 + w] - tr[sl, :, 0]) * us
+            print(f"  wave {w}: start->flags {np.median(fl):7.3f}  start->loads {np.median(ld):7.3f}")
+        last = tr[sl, :, 24:24 + nwv].max(axis=2)
+        print(f"  last wave's loads->barrier1 median {np.median((tr[sl, :, 8] - last) * us):7.3f}"
+              f"  start->last loads {np.median((last - tr[sl, :, 0]) * us):7.3f}")
+    elif ver >= 4 and tr[sl, :, 6].min() > 0:
         for w in range(4):
             ld = (tr[sl, :, 6 + w] - tr[sl, :, 1]) * us
             mf = (tr[sl, :, 10 + w] - tr[sl, :, 6 + w]) * us
