@@ -86,6 +86,18 @@ struct X3PArgs {
   // blocks, no exponents): two v_mfma_f32_16x16x32_bf16 per stage, fp32
   // accumulation; streaming: A = a bf16 v6 forward's h images (eA0 = 0)
   bool bf16 = false;
+  // Consumer-gated mode (gate_flags != null; 256 x 256 tiles, no split-K,
+  // batch = the consumer's directions): C is the input projection of a v6
+  // forward recurrence that runs CONCURRENTLY and reads its rows as they are
+  // published.  Tiles are taken in the order the recurrence needs them
+  // (batch 0 row tiles ascending, batch 1 descending, all column tiles of a
+  // row tile together); C is written through (sc1) and then the tile's flag
+  // gate_flags[(b * row tiles + tm) * column tiles + tn] = gate_id.  Blocks on
+  // the XCDs in xcd_avoid (the recurrence's) exit before taking work.
+  // tile_counter is required.
+  unsigned *gate_flags = nullptr;
+  unsigned gate_id = 0;
+  unsigned xcd_avoid = 0;
 };
 void gemm_x3p(hipStream_t s, const X3PArgs &g);
 // shapes gemm_x3p runs on 256 x 256 tiles (KCTC_GEMM256=0 turns them off)

@@ -73,6 +73,10 @@ struct PParams {
   int *done;               // [2][nrt] pack jobs finished
   int *arrive;             // [nrt][gx] direction partials arrived (+1) / partial published (+2)
   float *part;             // [M][N] the first direction's partial
+  // consumer-gated projection (X3PArgs::gate_flags)
+  unsigned *gate;
+  unsigned gate_id, xcd_avoid;
+  int mt;                  // row tiles
 };
 
 
@@ -955,10 +959,18 @@ __device__ __forceinline__ void p256_tile(const PParams &p, unsigned char *lds, 
           float *c = C + (long)row * p.ldc + col;
           float o = p.alpha * v + badd[j];
           if (p.beta != 0.f) o += p.beta * *c;
-          *c = o;
+          if (p.gate) __hip_atomic_store(reinterpret_cast<unsigned *>(c), __float_as_uint(o), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);  // write-through: read by a running consumer
+          else *c = o;
         }
       }
     }
+  if (p.gate) {  // the tile's rows are out (every storing wave drained): publish it
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_store(p.gate + ((long)b * p.mt + tm) * p.gx + tn, p.gate_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 template <bool BFM>
@@ -966,6 +978,11 @@ __global__ __launch_bounds__(NTH2, 1) void gemm_p256_kernel(PParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];  // ONE shared array
   int *next = reinterpret_cast<int *>(lds + 2 * 2 * TILEB2);
   const int total = p.tiles * p.batch * p.split;
+  if (p.gate) {  // consumer-gated: off the consumer's XCDs
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    if ((p.xcd_avoid >> (x & 0xfu)) & 1u) return;
+  }
   if (p.counter) {  // dynamic scheduling (beside a persistent kernel)
     while (true) {
       if (threadIdx.x == 0) *next = atomicAdd(p.counter, 1);
@@ -974,7 +991,15 @@ __global__ __launch_bounds__(NTH2, 1) void gemm_p256_kernel(PParams p) {
       __syncthreads();
       if (id >= total) break;
       int tm, tn, b, ks;
-      decode_tile(p, id, total, false, tm, tn, b, ks);
+      if (p.gate) {  // in the consumer's order: step q's row tile of every batch, all column tiles
+        const int q = id / (p.batch * p.gx), r = id - q * p.batch * p.gx;
+        b = r / p.gx;
+        tn = r - b * p.gx;
+        tm = (b & 1) ? p.mt - 1 - q : q;
+        ks = 0;
+      } else {
+        decode_tile(p, id, total, false, tm, tn, b, ks);
+      }
       p256_tile<BFM>(p, lds, tm, tn, b, ks);
     }
     return;
@@ -1412,6 +1437,10 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
   p.xcd_word = g.stream_xcd_word; p.xcd_count = g.stream_xcd_count;
   p.sdir = 0;
   p.arrive = nullptr;
+  p.gate = g.gate_flags; p.gate_id = g.gate_id; p.xcd_avoid = g.xcd_avoid;
+  p.mt = ceil_div(g.M, TB2);
+  if (p.gate && (!t256 || p.split > 1 || !p.counter || g.beta != 0.f))
+    throw std::invalid_argument("gemm_x3p: a gated projection runs on 256 tiles, no split-K, with a tile counter");
   p.dbg = getenv("KCTC_STREAM_DBG") ? atoi(getenv("KCTC_STREAM_DBG")) : 0;
   static const int p256v = getenv("KCTC_P256") ? atoi(getenv("KCTC_P256")) : 0;
   p.p256v = p256v;

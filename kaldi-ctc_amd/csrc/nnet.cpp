@@ -83,6 +83,10 @@ void DevBuf::ensure(size_t b) {
   }
   size_t nb = align_up(std::max<size_t>(b, 256), 4096);
   KCTC_HIP_CHECK(hipMalloc(&p, nb));
+  // zeroed before any use (flag words that hold ids, e.g. the gated
+  // projection's tile flags, must not start out as one by chance)
+  KCTC_HIP_CHECK(hipMemsetAsync(p, 0, nb, nullptr));
+  KCTC_HIP_CHECK(hipStreamSynchronize(nullptr));
   bytes = nb;
 }
 
@@ -503,8 +507,13 @@ void CuDNNRecurrentComponent::Forward(const CuMatrixBase &in, CuMatrixBase *out,
   const bool projected = input_projected_;
   input_projected_ = false;
   ProfScope ps("layer_rnn_forward");
+  // the trainer's side stream (idle during the forward pass) for a projection
+  // computed beside the recurrence (rnn.h, consumer-gated projection)
+  auto &dev = CuDevice::Instantiate();
+  hipStream_t side = S() == dev.stream ? dev.side : nullptr;
   int st = rnn_forward_training(desc_, S(), T, N, in.Data(), params_.f(), out->Data(), workspace_.p,
-                                workspace_.bytes, reserve_.p, reserve_.bytes, DeviceError(), chain, projected, in_rows_);
+                                workspace_.bytes, reserve_.p, reserve_.bytes, DeviceError(), chain, projected, in_rows_,
+                                side);
   if (st) throw std::runtime_error("rnn_forward_training failed: " + std::to_string(st));
 }
 

@@ -100,11 +100,17 @@ struct RnnFwdChain {
 };
 // in_rows (nullable): the input already packed as bf16 rows [T*N][D] (the
 // previous component's rnn_packed_output), used by a bf16 input projection
-// instead of packing x
+// instead of packing x.
+// side (nullable): a stream for a consumer-gated input projection
+// (KCTC_FWD_GATE): the projection GEMM runs on `side` CONCURRENTLY with this
+// call's XCD-pinned recurrence, on the other XCDs, in the order the
+// recurrence needs its rows, and the recurrence's IO waves fetch a row tile
+// only once the GEMM has published it (gemm.h X3PArgs::gate_flags); joined
+// back into `s` before return.  Taken for the split-fp16 IO-wave forward only.
 int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *w, float *y, void *workspace, size_t ws_bytes,
                          void *reserve, size_t res_bytes, unsigned *err, RnnFwdChain *chain = nullptr,
-                         bool input_projected = false, const void *in_rows = nullptr);
+                         bool input_projected = false, const void *in_rows = nullptr, hipStream_t side = nullptr);
 // bf16 one-layer bidirectional components: the forward recurrence also writes
 // its output as packed bf16 rows [T*N][2H] and columns [2H][kbt64] into the
 // reserve (the GEMM operands the next component's projection / dW and this

@@ -150,7 +150,7 @@ static size_t xch_bytes(const RnnDesc &d, int T, int N) {
 //               shifted output^T [dirs*H][TN]
 // plus int exponents and float-bit column maxima (G = nW*H).
 struct PackLay {
-  size_t a, b, c, d, ea, eb, ec, ed, cm, part, cnt, cme, fcnt, fpart, total;
+  size_t a, b, c, d, ea, eb, ec, ed, cm, part, cnt, cme, fcnt, fpart, gtf, total;
 };
 static PackLay pack_layout(const RnnDesc &d, int T, int N) {
   const long TN = (long)T * N, G = (long)d.nw() * d.H, Dm = std::max(d.D, d.dirs * d.H), dirs = d.dirs;
@@ -176,6 +176,9 @@ static PackLay pack_layout(const RnnDesc &d, int T, int N) {
   // arrival counters of the direction-split streamed projection (this component as its consumer)
   p.fcnt = o; o = align_up(o + sizeof(int) * ((TN + 127) / 128 * dirs * ((G + 127) / 128) + 64), 256);
   p.fpart = o; o = align_up(o + sizeof(float) * ((TN + 127) / 128) * dirs * ((G + 127) / 128) * 128 * 128, 256);
+  // consumer-gated projection: its tile counter (word 0), then the tile flags
+  // [dirs][row tiles][column tiles] from word 64 (never reset: a call's id)
+  p.gtf = o; o = align_up(o + sizeof(unsigned) * (64 + dirs * ((TN + 255) / 256) * ((G + 255) / 256)), 256);
   p.total = o;
   return p;
 }
@@ -312,6 +315,13 @@ struct RecParams {
   // f + N), so that dR pairs it with the unshifted yc
   __bf16 *yr, *yc;
   int eshift;
+  // v6 forward with IO waves: the input projection G is computed CONCURRENTLY
+  // by a consumer-gated GEMM (gemm.h X3PArgs::gate_flags); before fetching a
+  // step's G rows the IO waves check that every column tile of the rows' row
+  // tile (256 rows) carries this call's id gid: gtf[(d * gmt + tile) * ggx + j]
+  const unsigned *gtf;
+  unsigned gid;
+  int gmt, ggx;
 };
 
 // Phase stamps of the first kTraceSteps steps ([steps][grid][16]; thread 0 of every workgroup;
@@ -1521,6 +1531,17 @@ __device__ __forceinline__ void dma_lds_dword(const float *g, unsigned lds) {
       : "memory");
 }
 
+// the same, system-coherent (sc1): data written by another XCD while this
+// kernel runs (a concurrent producer's write-through stores)
+__device__ __forceinline__ void dma_lds_dword_sc1(const void *g, unsigned lds) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off sc1\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g), "s"(lds)
+      : "memory");
+}
+
 // Workgroup barrier for LDS hand-offs.  RAW = true: the LDS writes drained
 // and s_barrier, without __syncthreads' fence -- with LDS-DMA in flight the
 // fence waits for every outstanding vector memory operation (vmcnt(0)),
@@ -2461,6 +2482,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // filled by LDS-DMA p.gla (3 or 7) steps ahead
   float *ginl = smem + kStgOff + (NP * 16 * U + 7) / 8 * 4;  // 16-B aligned
   float *outl = ginl + 8 * NW * 16 * U;  // (IO_OUT) [2][NW + 2][16 U]
+  unsigned *pollbuf = reinterpret_cast<unsigned *>(outl + 2 * (NW + 2) * 16 * U);  // (gated) [IO waves][64]
   const float *Wd = p.w + d * p.pl_stride;
   const float *R = Wd + p.r_off;
   AT *xch = reinterpret_cast<AT *>(p.xch);
@@ -2578,14 +2600,59 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // by LDS-DMA (lane l of IO wave v writes element 64 v + l); NW DMAs per
   // call whatever kk, so that the waits can count them (rows past N and
   // steps past T read a valid row and are never used)
+  // Consumer-gated G (p.gtf): an IO wave checks the row tile(s) of a step's
+  // rows before fetching them.  gvt = last verified row tile in this
+  // direction's order; the flags of the next tile are fetched by LDS-DMA into
+  // pollbuf right after a tile is verified (gpt, gpd steps ago) and read when
+  // that tile is first needed, >= 3 steps later (landed by then: see io_wait);
+  // otherwise, or if they do not all hold this call's id yet, the wave polls
+  // the flags itself (gate_spin, compiler-counted loads: a full drain).
+  const bool gate = IOW && p.gtf != nullptr;
+  int gvt = d == 0 ? -1 : p.gmt, gpt = -1, gpd = 3;
+  auto gate_spin = [&](int tile) {
+    const unsigned *f = p.gtf + ((long)d * p.gmt + tile) * p.ggx;
+    int spins = 0;
+    while (true) {
+      const unsigned v = lane < p.ggx ? __hip_atomic_load(f + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : p.gid;
+      if (__all(v == p.gid)) return;
+      if (++spins > kSpinLimit ||
+          ((spins & 255) == 0 && __hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        if (lane == 0) bad_lds = 1;
+        return;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  };
+  auto gate_rows = [&](int kk) {  // before the G fetch of forward-order step kk
+    const int tt = d == 0 ? min(kk, T - 1) : max(T - 1 - kk, 0);
+    const int lo = (int)(((long)tt * N + n0) >> 8), hi = (int)(((long)tt * N + nend - 1) >> 8);
+    bool moved = false;
+    while (d == 0 ? gvt < hi : gvt > lo) {
+      const int nt = d == 0 ? gvt + 1 : gvt - 1;
+      const unsigned *pb = pollbuf + (w - CW) * 64;
+      const bool have = gpt == nt && gpd >= 3 && __all(lane >= p.ggx || pb[lane] == p.gid);
+      if (!have) gate_spin(nt);
+      gvt = nt;
+      moved = true;
+    }
+    const int nx = d == 0 ? gvt + 1 : gvt - 1;
+    if (moved && nx >= 0 && nx < p.gmt) {  // the next tile's flags, checked when it is first needed
+      const unsigned *f = p.gtf + ((long)d * p.gmt + nx) * p.ggx + (lane < p.ggx ? lane : 0);
+      dma_lds_dword_sc1(f, __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(pollbuf + (w - CW) * 64)));
+      gpt = nx;
+      gpd = 0;
+    }
+  };
   auto io_dma = [&](int kk) {
+    if (gate) gate_rows(kk);
     const int tt = d == 0 ? min(kk, T - 1) : max(T - 1 - kk, 0);
     const long gr = ((long)tt * N + n0 + (io_live ? ion : 0)) * ldg + (long)d * NW * H + u0 + iou;
 #pragma unroll
     for (int q = 0; q < NW; q++) {
       const unsigned dst = __builtin_amdgcn_readfirstlane(
           (unsigned)reinterpret_cast<uintptr_t>(ginl + ((kk & 7) * NW + q) * 16 * U + (w - CW) * 64));
-      dma_lds_dword(p.G + gr + q * H, dst);
+      if (gate) dma_lds_dword_sc1(p.G + gr + q * H, dst);  // written by the GEMM's XCDs during this kernel
+      else dma_lds_dword(p.G + gr + q * H, dst);
     }
   };
   auto io_out = [&](int kk) {  // row-major outputs of step kk from outl[kk & 1]
@@ -2603,7 +2670,15 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // steps after it) still in flight
   const bool gla7 = p.gla == 7;
   auto io_wait = [&]() {
-    if (gla7) {
+    if (gate) {  // gla 3; a flag fetch issued this step or the last one sits among the G fetches
+      if constexpr (NW == 4) {
+        if (gpd <= 1) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        if (gpd <= 1) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      }
+    } else if (gla7) {
       if constexpr (NW == 4) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
     } else {
@@ -2614,7 +2689,13 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   if constexpr (IOW) {
     if (w >= CW) {  // steps 0 .. gla - 1; step 0's in place before the loop's first barrier
       for (int kk = 0; kk < (gla7 ? 7 : 3); kk++) io_dma(kk);
-      io_wait();
+      if (gate) {  // a flag fetch here is older than every G fetch: the plain count holds
+        if constexpr (NW == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        gpd = 3;
+      } else {
+        io_wait();
+      }
     }
     __syncthreads();
   } else {
@@ -2680,6 +2761,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
         wait_flags6(flag6(p, grp, d, 0, NWG), NWG, (unsigned)(k + 1), p.err, bad, &bad_lds, p.poll_sleep);
       }
       REC_TRACE(k, 1);
+      REC_TRACE_W(k, 16);
       const auto rs = rsrc(xch + (p.ring ? rbase + (long)((k - 1) % p.ring) * XS : (long)tp * XS),
                            (unsigned)(XS * sizeof(AT)));
       u32x4 ah[KBW], al[KBW];
@@ -2735,6 +2817,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
           }
         }
       }
+      REC_TRACE_W(k, 24);  // (issued: the MFMAs retire at the K-partial stores)
     }
     asm volatile("" ::: "memory");
     // behind the hand-off loads: last step's row-major outputs, next step's input projection
@@ -2857,6 +2940,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
         // gla - 1 steps after it was asked for
         io_dma(k + (gla7 ? 7 : 3));
         io_wait();
+        gpd++;
       }
       if ((p.nopf & 4) && io_live && k + 2 < T) {
         // diagnostic (KCTC_DIAG_NOPF=5): the same G loads, never waited for
@@ -3234,7 +3318,7 @@ static size_t fwd6_lds_bytes(const RnnDesc &d, const V6Cfg &c) {
   // + the IO waves' G (and output) slots, for the shape that runs them (launch6_u)
   const bool iow = c.U == 16 && c.nth == 512;
   const size_t b = sizeof(float) * (nwv * 16 * rp + 8) + np * 16 * (size_t)c.U * 2 + 16 +
-                   (iow ? sizeof(float) * 16 * c.U * (8 * d.nw() + 2 * (d.nw() + 2)) + 16 : 0);
+                   (iow ? sizeof(float) * 16 * c.U * (8 * d.nw() + 2 * (d.nw() + 2)) + 16 + 4 * 64 * 4 : 0);
   return std::max(b, (size_t)96 * 1024);  // one recurrence workgroup per CU
 }
 static size_t bwd6_lds_bytes(const RnnDesc &d, const V6Cfg &c) {
@@ -3533,7 +3617,7 @@ bool rnn_packed_output(const RnnDesc &d, int T, int N, void *reserve, const void
 int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *w, float *y, void *workspace, size_t ws_bytes,
                          void *reserve, size_t res_bytes, unsigned *err, RnnFwdChain *chain,
-                         bool input_projected, const void *in_rows) {
+                         bool input_projected, const void *in_rows, hipStream_t side) {
   if (chain) chain->done = false;
   if (T <= 0 || N <= 0 || N > 16 * kMaxRT || d.H % 16) return KRNN_NOT_SUPPORTED;
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
@@ -3550,6 +3634,13 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
   const long TN = (long)T * N;
   float *res = static_cast<float *>(reserve);
   const float *in = x;
+  // consumer-gated projection: the split-fp16 forward with IO waves
+  // (launch6_u), XCD-pinned so that the GEMM keeps to the other XCDs
+  const bool gate_ok = side && ver == 6 && c6.U == 16 && c6.nth == 512 && d.prec == kPrecX3 &&
+                       env_int("KCTC_FWD_IOW", 1) && !(c6.gs <= 8 && env_int("KCTC_STK", 0)) &&
+                       env_int("KCTC_FWD_GATE", 0) && xcd_mask(d, N, true) != 0 &&
+                       x3p_use_256((int)TN, d.nw() * d.H);
+  static unsigned gate_calls = 0x5eed0000u;  // a projection's id (never 0, never repeated in practice)
   for (int l = 0; l < d.layers; l++) {
     float *R0 = res + lay.per_layer * l;
     float *out = (l == d.layers - 1) ? y : R0 + lay.out;
@@ -3565,6 +3656,9 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     g.transA = false; g.transB = true;
     g.M = (int)TN; g.N = NW * H; g.K = Din;
     const bool skip_proj = l == 0 && input_projected;  // streamed by the previous component
+    const bool gated = gate_ok && !skip_proj && use_x3(Din, 32);
+    const unsigned gid = gated ? ++gate_calls : 0u;
+    unsigned *gtf = gated ? pk<unsigned>(workspace, d, T, N, pack_layout(d, T, N).gtf) : nullptr;
     g.A = in; g.lda = Din;
     g.B = wl; g.ldb = Din;
     g.C = R0 + lay.G; g.ldc = (long)dirs * NW * H;
@@ -3601,10 +3695,13 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       _Float16 *Ap = pk<_Float16>(workspace, d, T, N, pl.a), *Bp = pk<_Float16>(workspace, d, T, N, pl.b);
       int *eA = pk<int>(workspace, d, T, N, pl.ea), *eB = pk<int>(workspace, d, T, N, pl.eb);
       const int KB = (Din + 31) / 32;
+      // gated: packs and GEMM on `side` from here on, beside the recurrence
+      const hipStream_t ps_ = gated ? side : s;
+      if (gated) KCTC_HIP_CHECK(hipStreamWaitEvent(side, fork_event(s), 0));
       {
-        ProfSpan ps(s, "x3_pack");
-        x3p_pack_rows(s, in, Din, (int)TN, Din, Ap, eA, (l > 0 && bounded_out(d)) ? 1.f : 0.f);
-        x3p_pack_rows(s, wl, Din, NW * H, Din, Bp, eB, 0.f, dirs, pls, (long)NW * H * KB * 64, (long)NW * H);
+        ProfSpan ps(ps_, "x3_pack");
+        x3p_pack_rows(ps_, in, Din, (int)TN, Din, Ap, eA, (l > 0 && bounded_out(d)) ? 1.f : 0.f);
+        x3p_pack_rows(ps_, wl, Din, NW * H, Din, Bp, eB, 0.f, dirs, pls, (long)NW * H * KB * 64, (long)NW * H);
       }
       X3PArgs x;
       x.M = (int)TN; x.N = NW * H; x.KB = KB;
@@ -3612,8 +3709,15 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       x.C = g.C; x.ldc = g.ldc; x.bias = g.bias; x.bias2 = g.bias2;
       x.batch = dirs; x.sA = 0; x.seA = 0; x.sB = (long)NW * H * KB * 64; x.seB = (long)NW * H;
       x.sC = g.strideC; x.sBias = g.strideBias;
-      ProfSpan ps(s, "gemm_fwd_proj");
-      gemm_x3p(s, x);
+      if (gated) {  // enqueued BEFORE the recurrence: on a shared hardware queue it runs first
+        x.gate_flags = gtf + 64;
+        x.gate_id = gid;
+        x.xcd_avoid = xcd_mask(d, N, true);  // slot s on XCD s (probe6 checks the recurrence's side)
+        x.tile_counter = reinterpret_cast<int *>(gtf);
+        x.max_blocks = 8 * kCusPerXcd;  // one per CU of the chip; those on the recurrence's XCDs exit
+      }
+      ProfSpan ps(ps_, "gemm_fwd_proj");
+      gemm_x3p(ps_, x);
     } else {
       ProfSpan ps(s, "gemm_fwd_proj");
       gemm_f32(s, g);
@@ -3634,7 +3738,13 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
     p.poll_sleep = env_int("KCTC_POLL_SLEEP", 1);
     p.nopf = env_int("KCTC_DIAG_NOPF", 0);
-    p.gla = env_int("KCTC_FWD_GLA", 3) == 7 ? 7 : 3;  // G rows fetched 3 or 7 steps ahead (IO waves)
+    p.gla = env_int("KCTC_FWD_GLA", 3) == 7 && !gated ? 7 : 3;  // G rows fetched 3 or 7 steps ahead (IO waves)
+    if (gated) {
+      p.gtf = gtf + 64;
+      p.gid = gid;
+      p.gmt = (int)((TN + 255) / 256);
+      p.ggx = (NW * H + 255) / 256;
+    }
     p.wwait = env_int("KCTC_FWD_WWAIT", 1);  // measured: forward recurrence 29.7 -> 28.6 ms/step
     if (ver == 6 && bf16_io(d)) {  // the output also as packed bf16 rows and columns
       p.yr = reinterpret_cast<__bf16 *>(R0 + lay.pkyr);
@@ -3664,6 +3774,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       else launch_rec(true, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
+    if (gated) join_stream(s, side);  // (complete by the recurrence's end: it read every row)
     if (chained) {
       launch_chain_proj(d, p, fork, T, N, *chain, err);
       join_stream(s, chain->side);

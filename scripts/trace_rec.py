@@ -50,10 +50,12 @@ def main(path):
         for w in range(nwv):
             fl = (tr[sl, :, 16 + w] - tr[sl, :, 0]) * us
             ld = (tr[sl, :, 24 + w] - tr[sl, :, 0]) * us
-            print(f"  wave {w}: start->flags {np.median(fl):7.3f}  start->loads {np.median(ld):7.3f}")
+            print(f"  wave {w}: start->flags {np.median(fl):7.3f}  start->{'mfma issued' if 'fwd' in path else 'loads'} "
+                  f"{np.median(ld):7.3f}")
         last = tr[sl, :, 24:24 + nwv].max(axis=2)
-        print(f"  last wave's loads->barrier1 median {np.median((tr[sl, :, 8] - last) * us):7.3f}"
-              f"  start->last loads {np.median((last - tr[sl, :, 0]) * us):7.3f}")
+        nxt = 8 if tr[sl, :, 8].min() > 0 else 3
+        print(f"  last wave's stamp->{pnames[nxt]} median {np.median((tr[sl, :, nxt] - last) * us):7.3f}"
+              f"  start->last wave's stamp {np.median((last - tr[sl, :, 0]) * us):7.3f}")
     elif ver >= 4 and tr[sl, :, 6].min() > 0:
         for w in range(4):
             ld = (tr[sl, :, 6 + w] - tr[sl, :, 1]) * us
