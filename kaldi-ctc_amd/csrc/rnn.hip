@@ -3639,6 +3639,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
   const bool gate_ok = side && ver == 6 && c6.U == 16 && c6.nth == 512 && d.prec == kPrecX3 &&
                        env_int("KCTC_FWD_IOW", 1) && !(c6.gs <= 8 && env_int("KCTC_STK", 0)) &&
                        env_int("KCTC_FWD_GATE", 0) && xcd_mask(d, N, true) != 0 &&
+                       __builtin_popcount(xcd_mask(d, N, true)) <= 4 &&  // XCDs left to the GEMM
                        x3p_use_256((int)TN, d.nw() * d.H);
   static unsigned gate_calls = 0x5eed0000u;  // a projection's id (never 0, never repeated in practice)
   for (int l = 0; l < d.layers; l++) {
