@@ -180,6 +180,11 @@ int kctc_nnet_enable_cu_probe(kctcNnet_t nnet, int blocks, double usec);
  * holding CU share `part` of `nparts`, and the persistent kernels size
  * themselves for that share.  Call before kctc_nnet_create. */
 int kctc_set_cu_partition(int part, int nparts);
+/* Check of the shares: runs 8 blocks per CU on a stream masked to share
+ * `part` of `nparts` (the mask kctc_set_cu_partition builds) and returns the
+ * distinct CUs they ran on as (XCC_ID << 16) | HW_ID[15:8] (CU, SH, SE) in
+ * ids[0 .. *n_ids) (at most max_ids).  Test support; synchronous. */
+int kctc_cu_partition_probe(int part, int nparts, unsigned *ids, int max_ids, int *n_ids);
 
 /* Arithmetic of every CuDNNRecurrentComponent's recurrences and gate GEMMs:
  * 0 fp32-class (default), 1 bf16 operands with fp32 accumulation and fp32

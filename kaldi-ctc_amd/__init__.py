@@ -790,6 +790,16 @@ def set_cu_partition(part, nparts):
     _tcheck(lib().kctc_set_cu_partition(int(part), int(nparts)), "kctc_set_cu_partition")
 
 
+def cu_partition_probe(part, nparts):
+    """The distinct CUs (XCC_ID << 16 | HW_ID[15:8]) a launch on CU share
+    `part` of `nparts` runs on (kctc_cu_partition_probe)."""
+    ids = np.zeros(4096, dtype=np.uint32)
+    n = ctypes.c_int(0)
+    _tcheck(lib().kctc_cu_partition_probe(int(part), int(nparts), ids.ctypes.data, ids.size, ctypes.byref(n)),
+            "kctc_cu_partition_probe")
+    return ids[:n.value].copy()
+
+
 def softmax_rows(x, stream=None):
     """SoftmaxComponent forward of a 2-D torch CUDA tensor (kctc_softmax_rows)."""
     import torch

@@ -64,5 +64,8 @@ void flag_to_err_word(hipStream_t s, const float *flag, unsigned *err);
 // Holds `blocks` whole CUs (1024 threads and 160 KB LDS each) for `usec`
 // microseconds: the stand-in for a communication kernel in the CU-budget test.
 void cu_hold(hipStream_t s, int blocks, double usec);
+// Where the blocks of a launch on `s` run: `blocks` blocks, each ~usec long,
+// write (XCC_ID << 16) | (HW_ID bits 8..15: CU, SH, SE) into ids[block].
+void cu_where(hipStream_t s, unsigned *ids, int blocks, double usec);
 
 }  // namespace kctc

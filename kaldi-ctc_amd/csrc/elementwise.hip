@@ -387,6 +387,21 @@ __global__ __launch_bounds__(1024) void k_cu_hold(unsigned long long ticks) {
   while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
 }
 
+__global__ __launch_bounds__(64) void k_cu_where(unsigned *ids, unsigned long long ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned x, h;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(h));
+  if (threadIdx.x == 0) ids[blockIdx.x] = ((x & 0xfu) << 16) | ((h >> 8) & 0xffu);
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+void cu_where(hipStream_t s, unsigned *ids, int blocks, double usec) {
+  if (blocks <= 0) return;
+  hipLaunchKernelGGL(k_cu_where, dim3(blocks), dim3(64), 0, s, ids, (unsigned long long)(usec * 100.0));
+  KCTC_HIP_CHECK(hipGetLastError());
+}
+
 void cu_hold(hipStream_t s, int blocks, double usec) {
   if (blocks <= 0 || usec <= 0) return;
   const int lds = 160 * 1024;

@@ -270,6 +270,15 @@ int kctc_usable_cus_override() {
 
 void kctc_set_error(const char *msg) { g_err = msg ? msg : ""; }
 
+// the CU mask of share `part` of `nparts`: a contiguous range of mask bits
+// (bit b: one CU of XCD b mod 8, scripts/cumask_probe.hip)
+static std::vector<uint32_t> partition_mask(int part, int nparts, int cus) {
+  const int per = cus / nparts, first = part * per;
+  std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+  for (int c = first; c < first + per; c++) mask[c / 32] |= 1u << (c % 32);
+  return mask;
+}
+
 // compute stream at the highest priority (the latency-bound recurrences),
 // the weight-gradient side stream at the lowest; KCTC_OVERLAP=0 keeps
 // everything on one stream
@@ -277,9 +286,8 @@ void kctcNnetImpl::create_streams() {
   if (g_nparts > 1) {  // ranks sharing the device: this rank's streams on its CU share only
     int cus = 0;
     KCTC_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-    const int per = cus / g_nparts, first = g_part * per;
-    std::vector<uint32_t> mask((cus + 31) / 32, 0u);
-    for (int c = first; c < first + per; c++) mask[c / 32] |= 1u << (c % 32);
+    const int per = cus / g_nparts;
+    const std::vector<uint32_t> mask = partition_mask(g_part, g_nparts, cus);
     KCTC_HIP_CHECK(hipExtStreamCreateWithCUMask(&stream, (uint32_t)mask.size(), mask.data()));
     KCTC_HIP_CHECK(hipExtStreamCreateWithCUMask(&side, (uint32_t)mask.size(), mask.data()));
     KCTC_HIP_CHECK(hipExtStreamCreateWithCUMask(&stream2, (uint32_t)mask.size(), mask.data()));
@@ -725,6 +733,32 @@ int kctc_set_cu_partition(int part, int nparts) {
     g_part = part;
     g_nparts = nparts;
     kctc::rnn_set_cu_budget(kctc_usable_cus_override(), kctc::rnn_comm_cus());
+  });
+}
+
+int kctc_cu_partition_probe(int part, int nparts, unsigned *ids, int max_ids, int *n_ids) {
+  return guarded([&] {
+    KCTC_REQUIRE(nparts >= 1 && nparts <= 8 && part >= 0 && part < nparts && ids && n_ids && max_ids > 0,
+                 "kctc_cu_partition_probe: bad arguments");
+    int dev = 0, cus = 0;
+    KCTC_HIP_CHECK(hipGetDevice(&dev));
+    KCTC_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const std::vector<uint32_t> mask = partition_mask(part, nparts, cus);
+    hipStream_t s = nullptr;
+    KCTC_HIP_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+    const int blocks = 8 * cus;
+    unsigned *d = nullptr;
+    KCTC_HIP_CHECK(hipMalloc(&d, sizeof(unsigned) * blocks));
+    kctc::cu_where(s, d, blocks, 50.0);  // long enough that the blocks spread over every CU of the share
+    std::vector<unsigned> h(blocks);
+    KCTC_HIP_CHECK(hipMemcpyAsync(h.data(), d, sizeof(unsigned) * blocks, hipMemcpyDeviceToHost, s));
+    KCTC_HIP_CHECK(hipStreamSynchronize(s));
+    (void)hipFree(d);
+    (void)hipStreamDestroy(s);
+    std::sort(h.begin(), h.end());
+    h.erase(std::unique(h.begin(), h.end()), h.end());
+    *n_ids = (int)std::min<size_t>(h.size(), (size_t)max_ids);
+    std::copy(h.begin(), h.begin() + *n_ids, ids);
   });
 }
 
