@@ -3659,6 +3659,9 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     g.M = (int)TN; g.N = NW * H; g.K = Din;
     const bool skip_proj = l == 0 && input_projected;  // streamed by the previous component
     const bool gated = gate_ok && !skip_proj && use_x3(Din, 32);
+    // diagnostic (KCTC_GATE_DIAG): 1 the gated GEMM stream-ordered before an
+    // ungated recurrence, 2 stream-ordered before the gated recurrence
+    const int gdiag = gated ? env_int("KCTC_GATE_DIAG", 0) : 0;
     const unsigned gid = gated ? ++gate_calls : 0u;
     unsigned *gtf = gated ? pk<unsigned>(workspace, d, T, N, pack_layout(d, T, N).gtf) : nullptr;
     g.A = in; g.lda = Din;
@@ -3698,8 +3701,8 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       int *eA = pk<int>(workspace, d, T, N, pl.ea), *eB = pk<int>(workspace, d, T, N, pl.eb);
       const int KB = (Din + 31) / 32;
       // gated: packs and GEMM on `side` from here on, beside the recurrence
-      const hipStream_t ps_ = gated ? side : s;
-      if (gated) KCTC_HIP_CHECK(hipStreamWaitEvent(side, fork_event(s), 0));
+      const hipStream_t ps_ = gated && !gdiag ? side : s;
+      if (gated && !gdiag) KCTC_HIP_CHECK(hipStreamWaitEvent(side, fork_event(s), 0));
       {
         ProfSpan ps(ps_, "x3_pack");
         x3p_pack_rows(ps_, in, Din, (int)TN, Din, Ap, eA, (l > 0 && bounded_out(d)) ? 1.f : 0.f);
@@ -3742,7 +3745,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.nopf = env_int("KCTC_DIAG_NOPF", 0);
     p.gla = env_int("KCTC_FWD_GLA", 3) == 7 && !gated ? 7 : 3;  // G rows fetched 3 or 7 steps ahead (IO waves)
     if (gated) {
-      p.gtf = gtf + 64;
+      p.gtf = gdiag == 1 ? nullptr : gtf + 64;
       p.gid = gid;
       p.gmt = (int)((TN + 255) / 256);
       p.ggx = (NW * H + 255) / 256;
@@ -3776,7 +3779,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       else launch_rec(true, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
-    if (gated) join_stream(s, side);  // (complete by the recurrence's end: it read every row)
+    if (gated && !gdiag) join_stream(s, side);  // (complete by the recurrence's end: it read every row)
     if (chained) {
       launch_chain_proj(d, p, fork, T, N, *chain, err);
       join_stream(s, chain->side);
