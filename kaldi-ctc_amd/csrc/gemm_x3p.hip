@@ -959,17 +959,21 @@ __device__ __forceinline__ void p256_tile(const PParams &p, unsigned char *lds, 
           float *c = C + (long)row * p.ldc + col;
           float o = p.alpha * v + badd[j];
           if (p.beta != 0.f) o += p.beta * *c;
-          if (p.gate) __hip_atomic_store(reinterpret_cast<unsigned *>(c), __float_as_uint(o), __ATOMIC_RELAXED,
+          if (p.gate && !(p.dbg & 0x200)) __hip_atomic_store(reinterpret_cast<unsigned *>(c), __float_as_uint(o), __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);  // write-through: read by a running consumer
           else *c = o;
         }
       }
     }
-  if (p.gate) {  // the tile's rows are out (every storing wave drained): publish it
+  if (p.gate && !(p.dbg & 0x400)) {  // the tile's rows are out (every storing wave drained): publish it
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0)
       __hip_atomic_store(p.gate + ((long)b * p.mt + tm) * p.gx + tn, p.gate_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // reconverge: without it hipcc structured the job loop with this
+    // lane-0 store as a divergent exit and left lane 0 -- the one that takes
+    // the next job -- behind (the loop then spun on a stale job id)
+    __syncthreads();
   }
 }
 
@@ -981,7 +985,7 @@ __global__ __launch_bounds__(NTH2, 1) void gemm_p256_kernel(PParams p) {
   if (p.gate) {  // consumer-gated: off the consumer's XCDs
     unsigned x;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-    if ((p.xcd_avoid >> (x & 0xfu)) & 1u) return;
+    if (((p.xcd_avoid >> (x & 0xfu)) & 1u) && !(p.dbg & 0x100)) return;
   }
   if (p.counter) {  // dynamic scheduling (beside a persistent kernel)
     while (true) {

@@ -1682,6 +1682,33 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   const bool live = has_e && n < nend;
   float carry = 0.f, bsx[NW], bsh[NW], dxk[NW], eg[NW], cg[NW], ng[NW], cmx[NW], cme[NW];
   float cdy = 0.f, ca = 0.f, cap = 0.f, ndy = 0.f, na = 0.f, nap = 0.f;
+  // The cell's coefficients -- everything of the pointwise backward that does
+  // not depend on the hand-off -- computed from the step's forward values
+  // after the previous step's publish (while the other producers' epochs are
+  // on their way), so that the cell after the hand-off is a few FMAs:
+  //   LSTM: dc = dh kc[0] + carry, dG_q = dc kc[1+q] (q < 3), dG_3 = dh kc[4], carry = dc kc[5]
+  //   GRU : dh += carry, dX_q = dh kc[q], dE_2 = dh kc[3], carry = dh kc[4]
+  float kc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  auto coef = [&]() {
+    if (MODE == kLstm) {
+      const float ig = cg[0], fg = cg[1], gg = cg[2], og = cg[3];
+      const float tc = ftanh(ca);
+      kc[0] = og * (1.f - tc * tc);
+      kc[1] = gg * ig * (1.f - ig);
+      kc[2] = cap * fg * (1.f - fg);
+      kc[3] = ig * (1.f - gg * gg);
+      kc[4] = tc * og * (1.f - og);
+      kc[5] = fg;
+    } else {
+      const float r = cg[0], z = cg[1], nn = cg[2];
+      const float kn = (1.f - z) * (1.f - nn * nn);
+      kc[0] = kn * ca * r * (1.f - r);
+      kc[1] = (cap - nn) * z * (1.f - z);
+      kc[2] = kn;
+      kc[3] = kn * r;
+      kc[4] = z;
+    }
+  };
 #pragma unroll
   for (int q = 0; q < NW; q++) bsx[q] = bsh[q] = dxk[q] = eg[q] = cg[q] = ng[q] = cmx[q] = cme[q] = 0.f;
   auto prefetch = [&](int k) {  // operands of forward-order step k into n*
@@ -1790,6 +1817,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   const int epos = (eu >> 4) * 64 + (en >> 2) * (U < 16 ? U : 16) + (eu & 15);
   prefetch(T - 1);
   rotate();
+  coef();
   int bad = 0;
   unsigned *myflag = flag6(p, grp, d, g, NWG);
   // XCD-slot launches keep the hand-off in the XCD's L2 (plain flag stores
@@ -1883,37 +1911,21 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
       }
       float dh = cdy + dhr;
       if (MODE == kLstm) {
-        const float ig = cg[0], fg = cg[1], gg = cg[2], og = cg[3];
-        const float tc = ftanh(ca);
-        const float dO = dh * tc;
-        const float dc = dh * og * (1.f - tc * tc) + carry;
-        eg[0] = dc * gg * ig * (1.f - ig);
-        eg[1] = dc * cap * fg * (1.f - fg);
-        eg[2] = dc * ig * (1.f - gg * gg);
-        eg[3] = dO * og * (1.f - og);
-        carry = dc * fg;
+        const float dc = dh * kc[0] + carry;
+        eg[0] = dc * kc[1];
+        eg[1] = dc * kc[2];
+        eg[2] = dc * kc[3];
+        eg[3] = dh * kc[4];
+        carry = dc * kc[5];
       } else {
         dh += carry;
-        const float r = cg[0], z = cg[1], nn = cg[2];
-        const float dn = dh * (1.f - z), dz = dh * (cap - nn);
-        const float dpn = dn * (1.f - nn * nn);
-        const float dpr = dpn * ca * r * (1.f - r);
-        const float dpz = dz * z * (1.f - z);
-        carry = dh * z;
-        dxk[0] = dpr; dxk[1] = dpz; dxk[2] = dpn;
-        eg[0] = dpr; eg[1] = dpz; eg[2] = dpn * r;
-        bsh[0] += dpr; bsh[1] += dpz; bsh[2] += dpn * r;
+        dxk[0] = dh * kc[0]; dxk[1] = dh * kc[1]; dxk[2] = dh * kc[2];
+        eg[0] = dxk[0]; eg[1] = dxk[1]; eg[2] = dh * kc[3];
+        carry = dh * kc[4];
       }
       float m = 0.f;
 #pragma unroll
-      for (int q = 0; q < NW; q++) {
-        bsx[q] += (MODE == kGru) ? dxk[q] : eg[q];
-        m = fmaxf(m, fabsf(eg[q]));
-        if (live) {  // column maxima for the weight GEMMs' packed transposes
-          cmx[q] = fmaxf(cmx[q], fabsf(MODE == kGru ? dxk[q] : eg[q]));
-          if (MODE == kGru) cme[q] = fmaxf(cme[q], fabsf(eg[q]));
-        }
-      }
+      for (int q = 0; q < NW; q++) m = fmaxf(m, fabsf(eg[q]));
       if constexpr (BF) {
 #pragma unroll
         for (int q = 0; q < NW; q++) Ahi[en * AP + q * U + eu] = (__bf16)eg[q];
@@ -1939,14 +1951,6 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
           }
         }
         if (eu == 0) rowexp[en] = se + sB;
-      }
-      if (p.e_sc1 || pk) {
-#pragma unroll
-        for (int q = 0; q < NW; q++) estg[en * NW * U + q * U + eu] = MODE == kGru ? dxk[q] : eg[q];
-        if (MODE == kGru && pk) {
-#pragma unroll
-          for (int q = 0; q < NW; q++) estg2[en * NW * U + q * U + eu] = eg[q];
-        }
       }
     }
     REC_TRACE(ks, 12);
@@ -2017,10 +2021,33 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
         }
       }
     }
+    // off the hand-off path (beside the MFMAs and the store drain): bias and
+    // column-maximum bookkeeping, the dGates stage for the next step's row
+    // writes (read after the publish barrier)
+    if (has_e) {
+#pragma unroll
+      for (int q = 0; q < NW; q++) {
+        bsx[q] += (MODE == kGru) ? dxk[q] : eg[q];
+        if (MODE == kGru) bsh[q] += eg[q];
+        if (live) {  // column maxima for the weight GEMMs' packed transposes
+          cmx[q] = fmaxf(cmx[q], fabsf(MODE == kGru ? dxk[q] : eg[q]));
+          if (MODE == kGru) cme[q] = fmaxf(cme[q], fabsf(eg[q]));
+        }
+      }
+      if (p.e_sc1 || pk) {
+#pragma unroll
+        for (int q = 0; q < NW; q++) estg[en * NW * U + q * U + eu] = MODE == kGru ? dxk[q] : eg[q];
+        if (MODE == kGru && pk) {
+#pragma unroll
+          for (int q = 0; q < NW; q++) estg2[en * NW * U + q * U + eu] = eg[q];
+        }
+      }
+    }
     REC_TRACE(ks, 7);
     signal_epoch(myflag, (unsigned)(ks + 2), local);
     REC_TRACE(ks, 4);
     rotate();
+    if (k > 0) coef();  // the next step's, while its producers' epochs travel
     t_prev = t;
     REC_TRACE(ks, 5);
   }
@@ -2069,338 +2096,6 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
       for (int r = 0; r < 16; r++) m2 = fmaxf(m2, bs[(long)part * 16 * U * NW + ((long)r * U + u) * NW + gt]);
       unsigned *dst = p.cmax + (long)part * dirs * NW * H + (long)d * NW * H + gt * H + u0 + u;
       if (p.rg > 1) atomicMax(dst, __float_as_uint(m2));  // non-negative floats order as their bits
-      else *dst = __float_as_uint(m2);
-    }
-  }
-  if (bad && tid == 0) atomicOr(p.err, 1u);
-}
-
-// ---------------------------------------------------------------------------
-// v6 backward with IO waves (KCTC_BWD_IOW): XCD-pinned split-fp16 LSTM at
-// U = 16, H = 512, 512 threads (configs[1]).
-//  * Waves 0-3 ("compute waves") own the (row, unit) elements -- wave w rows
-//    4w .. 4w+3, which are exactly the rows of C-fragment lane quad w -- and
-//    do the whole hand-off: each waits for every producer's flag itself (no
-//    poll barrier), loads its 256 B of each producer's partial tile (one
-//    dword per lane and producer) and sums them in registers in the order of
-//    rnn_bwd_rec6's producer groups (no LDS reduce, no barrier before the
-//    cell; partials and dGates bit-identical), runs the cell, writes the A
-//    image and, after one barrier, multiplies it by 8 column tiles of R each
-//    (the same 48 MFMAs per SIMD as 8 waves x 4 tiles).
-//  * Waves 4-7 ("IO waves") never hand off: they fetch the step operands (dy,
-//    four gates, c, c_prev) three steps ahead by LDS-DMA into a ring of four
-//    slots and write the step's dGates rows from the LDS stage (sc1 for the
-//    streamed dx GEMM, else plain), so the compute waves' vmcnt holds only
-//    their own hand-off loads and partial stores.
-// Two barriers per step (A image ready; publish) instead of four.  An IO
-// wave's stores are drained by its own wait two steps later, so the rows of
-// step k are complete one publish later than in rnn_bwd_rec6: workgroup 0's
-// IO wave publishes agg_flag6 = ks after the A barrier of step ks (wave 0
-// has seen every producer's epoch ks + 1, published after their rows of step
-// ks - 3 were out), and "rows of step k complete at agg epoch k + 3" holds for
-// the consumer as before.  XCD-pinned launches only (the consumer of an
-// unpinned recurrence reads the per-workgroup flags).
-template <int MODE, int U, int H, int NTH, int P>
-__global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6io(RecParams p) {
-  static_assert(MODE == kLstm && U == 16 && NTH == 512 && P == kPrecX3, "the configs[1] shape");
-  constexpr int NW = 4, CW = 4;  // gates; compute waves
-  constexpr int K = NW * U, KB = K / 32, AP = KB * 32 + 8;
-  constexpr int NWG = H / U, CTW = H / (16 * CW), CTT = H / 16;
-  constexpr int NGRP = NTH / (4 * U), PER = NWG / NGRP;  // rnn_bwd_rec6's producer groups (summation order)
-  constexpr int NOP = 7;           // operands per element and step: dy, 4 gates, c, c_prev
-  constexpr int RING = 4;          // operand slots (fetched three steps ahead)
-  constexpr int CPR = NW * U / 4;  // 16-B chunks per dGates row
-  static_assert(16 * U == 64 * CW && 16 * CPR == 64 * (NTH / 64 - CW), "one element per compute lane, one chunk per IO lane");
-  static_assert(NWG <= 64 && NWG % NGRP == 0 && K == KB * 32, "shape");
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ int bad_lds, loc_lds;
-  __shared__ int rowexp[16];
-  __shared__ float wmax[NTH / 64];
-  const int dirs = p.dirs;
-  const int d = (blockIdx.x & 7) % dirs, g = blockIdx.x >> 3, grp = (blockIdx.x & 7) / dirs;
-  if (g >= NWG || grp >= p.rg) return;
-  if (p.reg && threadIdx.x == 0) __hip_atomic_fetch_add(p.reg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int N = p.N, T = p.T, n0 = grp * p.gs, nend = min(N, n0 + p.gs);
-  const int u0 = g * U, ct_own = u0 >> 4;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
-  const bool cw = w < CW;
-  const long ldy = (long)dirs * H, ldg = (long)dirs * NW * H;
-  const long PSTR = (long)CTT * 64 * 4 + 64;  // floats per producer image (fp32 partials, as rnn_bwd_rec6)
-  const long xgrp = (long)dirs * NWG * PSTR, xstep = xgrp * p.rg;
-  _Float16 *Ahi = reinterpret_cast<_Float16 *>(smem);       // [16][AP]
-  _Float16 *Alo = Ahi + 16 * AP;                            // [16][AP]
-  float *estg = reinterpret_cast<float *>(Alo + 16 * AP);   // [16][NW U] the step's dGates
-  float *ring = estg + 16 * NW * U;                         // [RING][NOP][256] step operands
-  const float *Wd = p.w + d * p.pl_stride;
-  const float *R = Wd + p.r_off;
-  if (tid == 0) bad_lds = 0;
-  for (int i = tid; i < 32 * AP; i += NTH) Ahi[i] = (_Float16)0.f;
-  auto rval = [&](int kk, int col) -> float {
-    const int q = kk / U, u = kk - q * U;
-    return R[(long)(q * H + u0 + u) * H + col];
-  };
-  // (every wave loads a valid slice -- the IO waves their compute twin's --
-  // so that the loads are unconditional and pipelined; the IO waves' values
-  // are dropped)
-  const int wc = w & (CW - 1);
-  float mx = 0.f;
-#pragma unroll
-  for (int c = 0; c < CTW; c++)
-#pragma unroll
-    for (int kb = 0; kb < KB; kb++)
-#pragma unroll
-      for (int j = 0; j < 8; j++) mx = fmaxf(mx, fabsf(rval(kb * 32 + fq * 8 + j, (wc * CTW + c) * 16 + fr)));
-  if (!cw) mx = 0.f;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-  if (lane == 0) wmax[w] = mx;
-  __syncthreads();
-  float m8 = wmax[0];
-#pragma unroll
-  for (int i = 1; i < NTH / 64; i++) m8 = fmaxf(m8, wmax[i]);
-  const int sB = split_exp(m8);
-  halfx8 bhi[CTW][KB], blo[CTW][KB];
-#pragma unroll
-  for (int c = 0; c < CTW; c++)
-#pragma unroll
-    for (int kb = 0; kb < KB; kb++)
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const float v = rval(kb * 32 + fq * 8 + j, (wc * CTW + c) * 16 + fr);
-        _Float16 h, l;
-        split16(ldexpf(v, sB), h, l);
-        bhi[c][kb][j] = h;
-        blo[c][kb][j] = l;
-      }
-  // compute waves: element (en, eu) = thread tid; its partial sits in lane
-  // w * 16 + eu, register en % 4 of the own column tile of every producer
-  const int en = tid / U, eu = tid - en * U;
-  const bool live = cw && n0 + en < nend;
-  const bool quad_live = cw && n0 + 4 * w < nend;  // this wave's rows (any of them) exist
-  const bool prow_live = n0 + 4 * fq < nend;       // C-fragment row quad of an MFMA lane
-  const long hbase = (long)grp * xgrp + (long)d * NWG * PSTR + (long)ct_own * 64 * 4 + w * 64 + (lane & 15) * 4 + (lane >> 4);
-  float carry = 0.f, bsx[NW], cmx[NW];
-#pragma unroll
-  for (int q = 0; q < NW; q++) bsx[q] = cmx[q] = 0.f;
-  // IO waves: lane i = tid - 64 CW <-> element (ion, iou) for the operand
-  // fetch, dGates row chunk (rn, ch) for the row stores
-  const int io = tid - 64 * CW, ion = io / U, iou = io - ion * U;
-  const int rn = io / CPR, ch = io - rn * CPR;
-  auto io_dma = [&](int kss) {  // operands of loop step kss (clamped: past T read a valid row, never used)
-    const int kk = T - 1 - min(kss, T - 1);  // forward-order step
-    const int t = d == 0 ? kk : T - 1 - kk, tp = kk > 0 ? (d == 0 ? t - 1 : t + 1) : t;
-    const int nn = n0 + ion < nend ? n0 + ion : n0;
-    const long yrow = ((long)t * N + nn) * ldy + (long)d * H + u0 + iou;
-    const long grow = ((long)t * N + nn) * ldg + (long)d * NW * H + u0 + iou;
-    const long prow = ((long)tp * N + nn) * ldy + (long)d * H + u0 + iou;
-    float *slot = ring + (kss % RING) * NOP * 256 + (w - CW) * 64;
-    auto dst = [&](int j) { return __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(slot + j * 256)); };
-    dma_lds_dword(p.dy + yrow, dst(0));
-#pragma unroll
-    for (int q = 0; q < NW; q++) dma_lds_dword(p.G + grow + q * H, dst(1 + q));
-    dma_lds_dword(p.aux + yrow, dst(5));
-    dma_lds_dword(p.aux + prow, dst(6));
-  };
-  // two stores per IO wave and step, dropped (offset past the buffer) when not
-  // needed, so that the explicit wait counts below hold: the step's dGates
-  // row chunk, and (workgroup 0's wave CW, lane 0) the aggregated epoch
-  unsigned *gflag = (p.e_sc1 && g == 0) ? agg_flag6(p, grp, d) : nullptr;
-  const auto grs = rsrc(gflag ? (const void *)gflag : (const void *)p.flags, 4u);
-  auto io_store = [&](int tt, bool real, unsigned gval, bool greal) {
-    u32x4 v = u32x4{0u, 0u, 0u, 0u};
-    if (real) v = *reinterpret_cast<const u32x4 *>(estg + rn * NW * U + ch * 4);
-    const int q = (ch * 4) / U, u = (ch * 4) % U;
-    const bool ok = real && n0 + rn < nend;
-    const int off = ok ? (int)(((long)(n0 + rn) * ldg + (long)d * NW * H + q * H + u0 + u) * 4) : 0x7ffffff0;
-    const auto rs = rsrc(p.DX + (long)(real ? tt : 0) * N * ldg, (unsigned)(N * ldg * 4));
-    const int goff = (greal && gflag && io == 0) ? 0 : 0x7ffffff0;
-    if (p.e_sc1) {
-      __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);
-    } else {
-      __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
-    }
-    __builtin_amdgcn_raw_buffer_store_b32(gval, grs, goff, 0, 16);
-  };
-  int bad = 0;
-  unsigned *myflag = flag6(p, grp, d, g, NWG);
-  if (tid == 0) atomicOr(p.flags + kXcdWord, 1u << xcc_id());
-  if (tid == 0) loc_lds = 0;
-  const int local = p.allow_local ? probe6(p, grp, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
-  if (p.trace && tid == 0) p.trace[(long)blockIdx.x * kTraceStride + 9] = (unsigned long long)(local + 1);
-  // operands of steps 0, 1, 2 (step 0's in place before the first barrier);
-  // per step an IO wave issues 2 stores then 7 DMAs, so "step ks + 1's DMAs
-  // landed" after step ks + 3's are issued is vmcnt(2 + 7 + 2 + 7)
-  if (!cw) {
-    io_dma(0);
-    io_store(0, false, 0u, false);
-    io_dma(1);
-    io_store(0, false, 0u, false);
-    io_dma(2);
-    asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-  }
-  lds_barrier<true>();
-  for (int ks = 0; ks < T && !bad; ks++) {
-    const int k = T - 1 - ks;
-    const int t = d == 0 ? k : T - 1 - k;
-    REC_TRACE(ks, 0);
-    if (cw) {
-      float dhr = 0.f;
-      if (ks > 0 && quad_live) {
-        wave_wait_prod(flag6(p, grp, d, 0, NWG), lane < NWG ? lane : -1, (unsigned)(ks + 1), p.err, &bad_lds,
-                       p.poll_sleep);
-        REC_TRACE(ks, 1);
-        REC_TRACE_W(ks, 16);
-        const auto rs = rsrc(p.xch + (long)(p.ring ? (ks - 1) % p.ring : ks - 1) * xstep, (unsigned)(xstep * 4));
-        float v[NWG];
-#pragma unroll
-        for (int pp = 0; pp < NWG; pp++)
-          v[pp] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)((hbase + pp * PSTR) * 4), 0, 16));
-#pragma unroll
-        for (int gg = 0; gg < NGRP; gg++) {
-          float s = v[gg];
-#pragma unroll
-          for (int i = 1; i < PER; i++) s += v[gg + i * NGRP];
-          dhr += s;
-        }
-        REC_TRACE(ks, 2);
-        REC_TRACE_W(ks, 24);
-      }
-      const float *sl = ring + (ks % RING) * NOP * 256 + tid;
-      float cdy = 0.f, cg[NW] = {0.f, 0.f, 0.f, 0.f}, ca = 0.f, cap = 0.f;
-      if (live) {
-        cdy = sl[0];
-#pragma unroll
-        for (int q = 0; q < NW; q++) cg[q] = sl[(1 + q) * 256];
-        ca = sl[5 * 256];
-        cap = k > 0 ? sl[6 * 256] : 0.f;
-      }
-      float eg[NW];
-      float dh = cdy + dhr;
-      {
-        const float ig = cg[0], fg = cg[1], gg = cg[2], og = cg[3];
-        const float tc = ftanh(ca);
-        const float dO = dh * tc;
-        const float dc = dh * og * (1.f - tc * tc) + carry;
-        eg[0] = dc * gg * ig * (1.f - ig);
-        eg[1] = dc * cap * fg * (1.f - fg);
-        eg[2] = dc * ig * (1.f - gg * gg);
-        eg[3] = dO * og * (1.f - og);
-        carry = dc * fg;
-      }
-      float m = 0.f;
-#pragma unroll
-      for (int q = 0; q < NW; q++) {
-        bsx[q] += eg[q];
-        m = fmaxf(m, fabsf(eg[q]));
-        if (live) cmx[q] = fmaxf(cmx[q], fabsf(eg[q]));
-      }
-      const int se = split_exp(group_maxU(m, U));
-#pragma unroll
-      for (int q = 0; q < NW; q++) {
-        _Float16 h, l;
-        split16(ldexpf(eg[q], se), h, l);
-        Ahi[en * AP + q * U + eu] = h;
-        Alo[en * AP + q * U + eu] = l;
-        estg[en * NW * U + q * U + eu] = eg[q];
-      }
-      if (eu == 0) rowexp[en] = se + sB;
-      REC_TRACE(ks, 12);
-    }
-    lds_barrier<true>();  // A image, row exponents, dGates stage
-    REC_TRACE(ks, 3);
-    if (bad_lds) bad = 1;
-    if (cw) {
-      if (k > 0) {  // partial dh of all units for the next step
-        floatx4 acc[CTW];
-#pragma unroll
-        for (int c = 0; c < CTW; c++) acc[c] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kb = 0; kb < KB; kb++) {
-          const halfx8 ah = *reinterpret_cast<const halfx8 *>(Ahi + fr * AP + kb * 32 + fq * 8);
-          const halfx8 al = *reinterpret_cast<const halfx8 *>(Alo + fr * AP + kb * 32 + fq * 8);
-#pragma unroll
-          for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bhi[c][kb], acc[c], 0, 0, 0);
-#pragma unroll
-          for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, blo[c][kb], acc[c], 0, 0, 0);
-#pragma unroll
-          for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bhi[c][kb], acc[c], 0, 0, 0);
-        }
-        int ex[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) ex[i] = -rowexp[fq * 4 + i];
-        const auto ro = rsrc(p.xch + (long)(p.ring ? ks % p.ring : ks) * xstep, (unsigned)(xstep * 4));
-        const long obase = (long)grp * xgrp + (long)(d * NWG + g) * PSTR;
-#pragma unroll
-        for (int c = 0; c < CTW; c++) {
-          floatx4 o;
-#pragma unroll
-          for (int i = 0; i < 4; i++) o[i] = ldexpf(acc[c][i], ex[i]);
-          const int off = (int)((obase + ((long)(w * CTW + c) * 64 + lane) * 4) * 4);
-          if (!prow_live) {
-          } else if (local) {
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ro, off, 0, 0);
-          } else {
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ro, off, 0, 16);
-          }
-        }
-      }
-      REC_TRACE(ks, 7);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partials are out
-    } else {
-      // this step's dGates rows out (and workgroup 0's aggregated epoch: wave
-      // 0 saw every producer's epoch ks + 1 before the barrier above), step
-      // ks + 3's operands in, step ks + 1's landed before the barrier below
-      io_store(t, true, (unsigned)ks, ks > 0);
-      io_dma(ks + 3);
-      asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-    }
-    lds_barrier<true>();
-    if (tid == 0) {
-      if (local) __hip_atomic_store(myflag, (unsigned)(ks + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      else __hip_atomic_store(myflag, (unsigned)(ks + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    REC_TRACE(ks, 4);
-    REC_TRACE(ks, 5);
-  }
-  if (!cw) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last rows, and the fetches past T
-  if (!bad) {
-    signal_epoch(myflag, (unsigned)(T + 2), 0);  // every row is out
-    if (gflag) {
-      wait_flags6(flag6(p, grp, d, 0, NWG), NWG, (unsigned)(T + 2), p.err, bad, &bad_lds, p.poll_sleep);
-      if (!bad && tid == 0) __hip_atomic_store(gflag, (unsigned)(T + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  // bias partial sums and column maxima of this row group (as rnn_bwd_rec6)
-  float *bs = ring;  // [2][16][U][NW] floats
-  __syncthreads();
-  if (cw) {
-#pragma unroll
-    for (int q = 0; q < NW; q++) {
-      const long b0 = ((long)en * U + eu) * NW + q;
-      bs[b0] = live ? bsx[q] : 0.f;
-      bs[(long)16 * U * NW + b0] = live ? bsx[q] : 0.f;
-    }
-  }
-  __syncthreads();
-  for (int q = tid; q < 2 * NW * U; q += NTH) {
-    const int part = q / (NW * U), rem = q - part * NW * U, gt = rem / U, u = rem - gt * U;
-    float s2 = 0.f;
-    for (int r = 0; r < 16; r++) s2 += bs[(long)part * 16 * U * NW + ((long)r * U + u) * NW + gt];
-    p.bias[(((long)grp * dirs + d) * 2 + part) * NW * H + gt * H + u0 + u] = s2;
-  }
-  if (p.cmax) {
-    __syncthreads();
-    if (cw) {
-#pragma unroll
-      for (int q = 0; q < NW; q++) bs[((long)en * U + eu) * NW + q] = cmx[q];
-    }
-    __syncthreads();
-    for (int q = tid; q < NW * U; q += NTH) {
-      const int gt = q / U, u = q - gt * U;
-      float m2 = 0.f;
-      for (int r = 0; r < 16; r++) m2 = fmaxf(m2, bs[((long)r * U + u) * NW + gt]);
-      unsigned *dst = p.cmax + (long)d * NW * H + gt * H + u0 + u;
-      if (p.rg > 1) atomicMax(dst, __float_as_uint(m2));
       else *dst = __float_as_uint(m2);
     }
   }
@@ -2761,7 +2456,6 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
         wait_flags6(flag6(p, grp, d, 0, NWG), NWG, (unsigned)(k + 1), p.err, bad, &bad_lds, p.poll_sleep);
       }
       REC_TRACE(k, 1);
-      REC_TRACE_W(k, 16);
       const auto rs = rsrc(xch + (p.ring ? rbase + (long)((k - 1) % p.ring) * XS : (long)tp * XS),
                            (unsigned)(XS * sizeof(AT)));
       u32x4 ah[KBW], al[KBW];
@@ -2817,7 +2511,6 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
           }
         }
       }
-      REC_TRACE_W(k, 24);  // (issued: the MFMAs retire at the K-partial stores)
     }
     asm volatile("" ::: "memory");
     // behind the hand-off loads: last step's row-major outputs, next step's input projection
@@ -3095,14 +2788,6 @@ static void launch6_u(bool fwd, int nth, const RecParams &p, dim3 grid, size_t l
         if constexpr (P == kPrecX3) {
           if (p.gs <= 8 && stk) {
             launch6_h<MODE, 16, 512, kPrecX3S>(fwd, p, grid, lds, s);
-            break;
-          }
-        }
-        // backward with IO waves (rnn_bwd_rec6io: XCD-pinned LSTM; KCTC_BWD_IOW=0: rnn_bwd_rec6)
-        if constexpr (MODE == kLstm && P == kPrecX3) {
-          if (!fwd && p.xpd && p.H == 512 && env_int("KCTC_BWD_IOW", 0)) {
-            set_lds(rnn_bwd_rec6io<MODE, 16, 512, 512, P>, lds);
-            hipLaunchKernelGGL((rnn_bwd_rec6io<MODE, 16, 512, 512, P>), grid, dim3(512), lds, s, p);
             break;
           }
         }

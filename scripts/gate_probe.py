@@ -1,6 +1,7 @@
 """One gated-projection train step per setting, under the caller's timeout:
 prints the step's wall time and whether the parameters equal the ungated run."""
-import os, sys, time
+import faulthandler, os, sys, time
+faulthandler.enable()
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import importlib
@@ -16,10 +17,15 @@ res = {}
 for tag in sys.argv[1:]:
     os.environ["KCTC_FWD_GATE"] = "0" if tag == "off" else "1"
     os.environ["KCTC_GATE_DIAG"] = {"d1": "1", "d2": "2"}.get(tag, "0")
+    print("start", tag, flush=True)
     net = kctc.Nnet(cfg, seed=5)
     t0 = time.time()
-    st = net.train_step(f, T, N, nf, fl, ll)
-    torch.cuda.synchronize()
+    try:
+        st = net.train_step(f, T, N, nf, fl, ll)
+        torch.cuda.synchronize()
+    except Exception as e:
+        print(tag, "FAILED", repr(e), flush=True)
+        raise
     res[tag] = [net.get_params(c) for c in range(net.num_components) if net.num_params(c)]
     same = all(np.array_equal(a, b) for a, b in zip(res[tag], res["off"])) if "off" in res else None
     print(tag, f"{time.time() - t0:.2f}s", "same_as_off", same, flush=True)
