@@ -982,13 +982,26 @@ __global__ __launch_bounds__(NTH2, 1) void gemm_p256_kernel(PParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];  // ONE shared array
   int *next = reinterpret_cast<int *>(lds + 2 * 2 * TILEB2);
   const int total = p.tiles * p.batch * p.split;
-  if (p.gate) {  // consumer-gated: off the consumer's XCDs
-    unsigned x;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-    if (((p.xcd_avoid >> (x & 0xfu)) & 1u) && !(p.dbg & 0x100)) return;
+  // consumer-gated: off the consumer's XCDs -- the static mask, and the XCDs
+  // the running consumer has tagged with this call's id (gate - 56 + XCC_ID),
+  // checked before every job, so a block that started before the consumer's
+  // workgroups arrived on its XCD leaves after its current tile
+  unsigned xcc = 0;
+  if (p.gate) {
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 0xfu;
+    if (((p.xcd_avoid >> xcc) & 1u) && !(p.dbg & 0x100)) return;
   }
   if (p.counter) {  // dynamic scheduling (beside a persistent kernel)
     while (true) {
+      if (p.gate && !(p.dbg & 0x100)) {
+        if (threadIdx.x == 0)
+          next[1] = __hip_atomic_load(p.gate - 56 + xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.gate_id;
+        __syncthreads();
+        const int here = __builtin_amdgcn_readfirstlane(next[1]);
+        __syncthreads();
+        if (here) return;
+      }
       if (threadIdx.x == 0) *next = atomicAdd(p.counter, 1);
       __syncthreads();
       const int id = __builtin_amdgcn_readfirstlane(*next);

@@ -2415,6 +2415,9 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   const bool fcopy = IOW && p.xpd && p.fcopy;
   unsigned *gflag = (fcopy && g == 0) ? agg_flag6(p, grp, d) : nullptr;
   if (p.xpd && tid == 0) atomicOr(p.flags + kXcdWord, 1u << xcc_id());
+  // gated projection: tell the GEMM's blocks which XCDs this launch holds
+  // (this call's id in the tag word of the XCD; they leave those XCDs)
+  if (p.gtf && tid == 0) __hip_atomic_store(const_cast<unsigned *>(p.gtf) - 56 + xcc_id(), p.gid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (tid == 0) loc_lds = 0;
   const int local = (p.xpd && p.allow_local) ? probe6(p, grp, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
   if (p.trace && tid == 0) p.trace[(long)blockIdx.x * kTraceStride + 9] = (unsigned long long)(local + 1);  // step 0, slot 9
@@ -3347,6 +3350,13 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     // diagnostic (KCTC_GATE_DIAG): 1 the gated GEMM stream-ordered before an
     // ungated recurrence, 2 stream-ordered before the gated recurrence
     const int gdiag = gated ? env_int("KCTC_GATE_DIAG", 0) : 0;
+    // diagnostic: the GEMM on a stream of its own at normal priority (KCTC_GATE_STREAM=1)
+    hipStream_t gside = side;
+    if (gated && env_int("KCTC_GATE_STREAM", 0)) {
+      static hipStream_t own = nullptr;
+      if (!own) KCTC_HIP_CHECK(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
+      gside = own;
+    }
     const unsigned gid = gated ? ++gate_calls : 0u;
     unsigned *gtf = gated ? pk<unsigned>(workspace, d, T, N, pack_layout(d, T, N).gtf) : nullptr;
     g.A = in; g.lda = Din;
@@ -3386,8 +3396,8 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       int *eA = pk<int>(workspace, d, T, N, pl.ea), *eB = pk<int>(workspace, d, T, N, pl.eb);
       const int KB = (Din + 31) / 32;
       // gated: packs and GEMM on `side` from here on, beside the recurrence
-      const hipStream_t ps_ = gated && !gdiag ? side : s;
-      if (gated && !gdiag) KCTC_HIP_CHECK(hipStreamWaitEvent(side, fork_event(s), 0));
+      const hipStream_t ps_ = gated && !gdiag ? gside : s;
+      if (gated && !gdiag) KCTC_HIP_CHECK(hipStreamWaitEvent(gside, fork_event(s), 0));
       {
         ProfSpan ps(ps_, "x3_pack");
         x3p_pack_rows(ps_, in, Din, (int)TN, Din, Ap, eA, (l > 0 && bounded_out(d)) ? 1.f : 0.f);
@@ -3402,9 +3412,11 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       if (gated) {  // enqueued BEFORE the recurrence: on a shared hardware queue it runs first
         x.gate_flags = gtf + 64;
         x.gate_id = gid;
-        x.xcd_avoid = xcd_mask(d, N, true);  // slot s on XCD s (probe6 checks the recurrence's side)
+        x.xcd_avoid = 0;  // (the recurrence's XCDs come from its tags at run time)
         x.tile_counter = reinterpret_cast<int *>(gtf);
-        x.max_blocks = 8 * kCusPerXcd;  // one per CU of the chip; those on the recurrence's XCDs exit
+        // 24 blocks an XCD: on the recurrence's XCDs the first of its
+        // workgroups find free CUs, tag the XCD, and the GEMM blocks there leave
+        x.max_blocks = 8 * kCusPerXcd * 3 / 4;
       }
       ProfSpan ps(ps_, "gemm_fwd_proj");
       gemm_x3p(ps_, x);
@@ -3464,7 +3476,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       else launch_rec(true, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
-    if (gated && !gdiag) join_stream(s, side);  // (complete by the recurrence's end: it read every row)
+    if (gated && !gdiag) join_stream(s, gside);  // (complete by the recurrence's end: it read every row)
     if (chained) {
       launch_chain_proj(d, p, fork, T, N, *chain, err);
       join_stream(s, chain->side);
