@@ -2133,6 +2133,9 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // held up that wave's next flag poll / hand-off loads / publish drain
   // (measured: forward 2.38 -> 1.89 us/step with the G loads left out)
   constexpr bool IOW = (P & 4) != 0;
+  // P & 8: the consumer-gated input projection (p.gtf), a variant of its own
+  // so that the plain IO-wave kernel compiles exactly as before
+  constexpr bool GATE = IOW && (P & 8) != 0;
   // the row-major outputs through the IO waves too: measured slower (forward
   // 2.46 -> 2.52 us/step; the IO waves' waits then delay the post-cell barrier)
   constexpr bool IO_OUT = false;
@@ -2302,7 +2305,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // that tile is first needed, >= 3 steps later (landed by then: see io_wait);
   // otherwise, or if they do not all hold this call's id yet, the wave polls
   // the flags itself (gate_spin, compiler-counted loads: a full drain).
-  const bool gate = IOW && p.gtf != nullptr;
+  const bool gate = GATE && p.gtf != nullptr;
   int gvt = d == 0 ? -1 : p.gmt, gpt = -1, gpd = 3;
   auto gate_spin = [&](int tile) {
     const unsigned *f = p.gtf + ((long)d * p.gmt + tile) * p.ggx;
@@ -2417,7 +2420,8 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   if (p.xpd && tid == 0) atomicOr(p.flags + kXcdWord, 1u << xcc_id());
   // gated projection: tell the GEMM's blocks which XCDs this launch holds
   // (this call's id in the tag word of the XCD; they leave those XCDs)
-  if (p.gtf && tid == 0) __hip_atomic_store(const_cast<unsigned *>(p.gtf) - 56 + xcc_id(), p.gid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (GATE && p.gtf && tid == 0)
+    __hip_atomic_store(const_cast<unsigned *>(p.gtf) - 56 + xcc_id(), p.gid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (tid == 0) loc_lds = 0;
   const int local = (p.xpd && p.allow_local) ? probe6(p, grp, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
   if (p.trace && tid == 0) p.trace[(long)blockIdx.x * kTraceStride + 9] = (unsigned long long)(local + 1);  // step 0, slot 9
@@ -2797,7 +2801,8 @@ static void launch6_u(bool fwd, int nth, const RecParams &p, dim3 grid, size_t l
         // forward with IO waves (the G loads off the hand-off waves; KCTC_FWD_IOW=0: all waves hand off)
         if constexpr (MODE == kLstm || MODE == kGru) {
           if (fwd && env_int("KCTC_FWD_IOW", 1)) {
-            launch6_h<MODE, 16, 512, P | 4>(fwd, p, grid, lds, s);
+            if (p.gtf) launch6_h<MODE, 16, 512, P | 4 | 8>(fwd, p, grid, lds, s);
+            else launch6_h<MODE, 16, 512, P | 4>(fwd, p, grid, lds, s);
             break;
           }
         }
