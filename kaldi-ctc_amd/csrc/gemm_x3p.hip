@@ -988,6 +988,7 @@ __global__ __launch_bounds__(NTH2, 1) void gemm_p256_kernel(PParams p) {
   // workgroups arrived on its XCD leaves after its current tile
   unsigned xcc = 0;
   if (p.gate) {
+    if (threadIdx.x == 0) __hip_atomic_store(p.gate - 63, p.gate_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     xcc &= 0xfu;
     if (((p.xcd_avoid >> xcc) & 1u) && !(p.dbg & 0x100)) return;

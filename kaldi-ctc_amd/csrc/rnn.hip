@@ -59,6 +59,8 @@
 #include "prof.h"
 #include "rnn.h"
 
+#include <functional>
+
 namespace kctc {
 
 long RnnDesc::params_size() const {
@@ -1870,6 +1872,9 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
           v[i] = crow_live ? __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
                                  rs, (int)((coff + (long)i * NGRP * PSTR) * 4), 0, 16 /* sc1 */))
                            : u32x2{0u, 0u};
+        __builtin_amdgcn_sched_barrier(0);
+        coef();  // while the hand-off loads are in flight
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < PER; i++) {
           const bf16x4 b = __builtin_bit_cast(bf16x4, v[i]);
@@ -1881,6 +1886,9 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
 #pragma unroll
         for (int i = 0; i < PER; i++)
           v[i] = crow_live ? ld_sc1(rs, (unsigned)((coff + (long)i * NGRP * PSTR) * 4)) : u32x4{0u, 0u, 0u, 0u};
+        __builtin_amdgcn_sched_barrier(0);
+        coef();  // while the hand-off loads are in flight
+        __builtin_amdgcn_sched_barrier(0);
         sm = __builtin_bit_cast(floatx4, v[0]);
 #pragma unroll
         for (int i = 1; i < PER; i++) sm += __builtin_bit_cast(floatx4, v[i]);
@@ -2021,9 +2029,10 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
         }
       }
     }
-    // off the hand-off path (beside the MFMAs and the store drain): bias and
-    // column-maximum bookkeeping, the dGates stage for the next step's row
-    // writes (read after the publish barrier)
+    // off the hand-off path (behind the partial-dh stores, during their
+    // drain): bias and column-maximum bookkeeping, the dGates stage for the
+    // next step's row writes (read after the publish barrier)
+    __builtin_amdgcn_sched_barrier(0);
     if (has_e) {
 #pragma unroll
       for (int q = 0; q < NW; q++) {
@@ -2047,7 +2056,6 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
     signal_epoch(myflag, (unsigned)(ks + 2), local);
     REC_TRACE(ks, 4);
     rotate();
-    if (k > 0) coef();  // the next step's, while its producers' epochs travel
     t_prev = t;
     REC_TRACE(ks, 5);
   }
@@ -2315,7 +2323,13 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
       if (__all(v == p.gid)) return;
       if (++spins > kSpinLimit ||
           ((spins & 255) == 0 && __hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-        if (lane == 0) bad_lds = 1;
+        if (lane == 0) {
+          bad_lds = 1;
+          // diagnosis in the error word: 0x10 the GEMM had started (its tag), 0x20 it had not
+          const bool started =
+              __hip_atomic_load(p.gtf - 63, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.gid;
+          atomicOr(p.err, started ? 0x10u : 0x20u);
+        }
         return;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -3352,6 +3366,8 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     g.M = (int)TN; g.N = NW * H; g.K = Din;
     const bool skip_proj = l == 0 && input_projected;  // streamed by the previous component
     const bool gated = gate_ok && !skip_proj && use_x3(Din, 32);
+    hipEvent_t gfork = nullptr;
+    std::function<void()> gated_launch;  // the deferred packs + gated GEMM
     // diagnostic (KCTC_GATE_DIAG): 1 the gated GEMM stream-ordered before an
     // ungated recurrence, 2 stream-ordered before the gated recurrence
     const int gdiag = gated ? env_int("KCTC_GATE_DIAG", 0) : 0;
@@ -3400,21 +3416,31 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       _Float16 *Ap = pk<_Float16>(workspace, d, T, N, pl.a), *Bp = pk<_Float16>(workspace, d, T, N, pl.b);
       int *eA = pk<int>(workspace, d, T, N, pl.ea), *eB = pk<int>(workspace, d, T, N, pl.eb);
       const int KB = (Din + 31) / 32;
-      // gated: packs and GEMM on `side` from here on, beside the recurrence
+      // gated: packs and GEMM on `gside`, enqueued right AFTER the recurrence
+      // (like the streamed GEMMs: the side stream forks at an event recorded
+      // before the recurrence launch); enqueued before it, on another stream,
+      // the GEMM was measured not to start while the recurrence waited
       const hipStream_t ps_ = gated && !gdiag ? gside : s;
-      if (gated && !gdiag) KCTC_HIP_CHECK(hipStreamWaitEvent(gside, fork_event(s), 0));
-      {
+      const bool defer = gated && !gdiag;
+      if (defer) {
+        static thread_local hipEvent_t ev = nullptr;
+        if (!ev) KCTC_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        KCTC_HIP_CHECK(hipEventRecord(ev, s));
+        gfork = ev;
+      }
+      auto packs = [=]() {
         ProfSpan ps(ps_, "x3_pack");
         x3p_pack_rows(ps_, in, Din, (int)TN, Din, Ap, eA, (l > 0 && bounded_out(d)) ? 1.f : 0.f);
         x3p_pack_rows(ps_, wl, Din, NW * H, Din, Bp, eB, 0.f, dirs, pls, (long)NW * H * KB * 64, (long)NW * H);
-      }
+      };
+      if (!defer) packs();
       X3PArgs x;
       x.M = (int)TN; x.N = NW * H; x.KB = KB;
       x.A = Ap; x.B = Bp; x.eA = eA; x.eB = eB;
       x.C = g.C; x.ldc = g.ldc; x.bias = g.bias; x.bias2 = g.bias2;
       x.batch = dirs; x.sA = 0; x.seA = 0; x.sB = (long)NW * H * KB * 64; x.seB = (long)NW * H;
       x.sC = g.strideC; x.sBias = g.strideBias;
-      if (gated) {  // enqueued BEFORE the recurrence: on a shared hardware queue it runs first
+      if (gated) {
         x.gate_flags = gtf + 64;
         x.gate_id = gid;
         x.xcd_avoid = 0;  // (the recurrence's XCDs come from its tags at run time)
@@ -3423,8 +3449,17 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
         // workgroups find free CUs, tag the XCD, and the GEMM blocks there leave
         x.max_blocks = 8 * kCusPerXcd * 3 / 4;
       }
-      ProfSpan ps(ps_, "gemm_fwd_proj");
-      gemm_x3p(ps_, x);
+      if (defer) {
+        gated_launch = [=]() {
+          KCTC_HIP_CHECK(hipStreamWaitEvent(ps_, gfork, 0));
+          packs();
+          ProfSpan ps(ps_, "gemm_fwd_proj");
+          gemm_x3p(ps_, x);
+        };
+      } else {
+        ProfSpan ps(ps_, "gemm_fwd_proj");
+        gemm_x3p(ps_, x);
+      }
     } else {
       ProfSpan ps(s, "gemm_fwd_proj");
       gemm_f32(s, g);
@@ -3481,7 +3516,10 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       else launch_rec(true, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
-    if (gated && !gdiag) join_stream(s, gside);  // (complete by the recurrence's end: it read every row)
+    if (gated_launch) {
+      gated_launch();
+      join_stream(s, gside);  // (complete by the recurrence's end: it read every row)
+    }
     if (chained) {
       launch_chain_proj(d, p, fork, T, N, *chain, err);
       join_stream(s, chain->side);
