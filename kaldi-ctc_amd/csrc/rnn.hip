@@ -3416,24 +3416,27 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       _Float16 *Ap = pk<_Float16>(workspace, d, T, N, pl.a), *Bp = pk<_Float16>(workspace, d, T, N, pl.b);
       int *eA = pk<int>(workspace, d, T, N, pl.ea), *eB = pk<int>(workspace, d, T, N, pl.eb);
       const int KB = (Din + 31) / 32;
-      // gated: packs and GEMM on `gside`, enqueued right AFTER the recurrence
-      // (like the streamed GEMMs: the side stream forks at an event recorded
-      // before the recurrence launch); enqueued before it, on another stream,
-      // the GEMM was measured not to start while the recurrence waited
+      // gated: the packs stay on s before the recurrence, the GEMM goes on
+      // `gside` right AFTER the recurrence launch (forked at an event recorded
+      // before it, like the streamed GEMMs).  A kernel's workgroups are dealt
+      // to the XCDs round-robin whatever is free, so a kernel launched beside
+      // the pinned recurrence has blocks that cannot start on its XCDs until
+      // it ends: fine for the GEMM (its jobs come from a counter, the blocks
+      // elsewhere take them all), a deadlock for a static-grid pack kernel
+      // the GEMM would wait for -- measured before the packs moved here
       const hipStream_t ps_ = gated && !gdiag ? gside : s;
       const bool defer = gated && !gdiag;
+      {
+        ProfSpan ps(s, "x3_pack");
+        x3p_pack_rows(s, in, Din, (int)TN, Din, Ap, eA, (l > 0 && bounded_out(d)) ? 1.f : 0.f);
+        x3p_pack_rows(s, wl, Din, NW * H, Din, Bp, eB, 0.f, dirs, pls, (long)NW * H * KB * 64, (long)NW * H);
+      }
       if (defer) {
         static thread_local hipEvent_t ev = nullptr;
         if (!ev) KCTC_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         KCTC_HIP_CHECK(hipEventRecord(ev, s));
         gfork = ev;
       }
-      auto packs = [=]() {
-        ProfSpan ps(ps_, "x3_pack");
-        x3p_pack_rows(ps_, in, Din, (int)TN, Din, Ap, eA, (l > 0 && bounded_out(d)) ? 1.f : 0.f);
-        x3p_pack_rows(ps_, wl, Din, NW * H, Din, Bp, eB, 0.f, dirs, pls, (long)NW * H * KB * 64, (long)NW * H);
-      };
-      if (!defer) packs();
       X3PArgs x;
       x.M = (int)TN; x.N = NW * H; x.KB = KB;
       x.A = Ap; x.B = Bp; x.eA = eA; x.eB = eB;
@@ -3445,14 +3448,13 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
         x.gate_id = gid;
         x.xcd_avoid = 0;  // (the recurrence's XCDs come from its tags at run time)
         x.tile_counter = reinterpret_cast<int *>(gtf);
-        // 24 blocks an XCD: on the recurrence's XCDs the first of its
-        // workgroups find free CUs, tag the XCD, and the GEMM blocks there leave
-        x.max_blocks = 8 * kCusPerXcd * 3 / 4;
+        // one block per CU: those dealt to the recurrence's XCDs start only
+        // after it (or leave at once if they get there first: its XCD tags)
+        x.max_blocks = 8 * kCusPerXcd;
       }
       if (defer) {
         gated_launch = [=]() {
           KCTC_HIP_CHECK(hipStreamWaitEvent(ps_, gfork, 0));
-          packs();
           ProfSpan ps(ps_, "gemm_fwd_proj");
           gemm_x3p(ps_, x);
         };

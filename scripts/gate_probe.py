@@ -16,7 +16,7 @@ f = torch.from_numpy(feats).to("cuda:0")
 res = {}
 for tag in sys.argv[1:]:
     os.environ["KCTC_FWD_GATE"] = "0" if tag == "off" else "1"
-    os.environ["KCTC_GATE_DIAG"] = {"d1": "1", "d2": "2"}.get(tag, "0")
+    os.environ["KCTC_GATE_DIAG"] = {"d1": "1", "d2": "2", "d4": "4", "d5": "5"}.get(tag, "0")
     print("start", tag, flush=True)
     net = kctc.Nnet(cfg, seed=5)
     t0 = time.time()
@@ -25,7 +25,8 @@ for tag in sys.argv[1:]:
         torch.cuda.synchronize()
     except Exception as e:
         print(tag, "FAILED", repr(e), flush=True)
-        raise
+        net.close()
+        continue
     res[tag] = [net.get_params(c) for c in range(net.num_components) if net.num_params(c)]
     same = all(np.array_equal(a, b) for a, b in zip(res[tag], res["off"])) if "off" in res else None
     print(tag, f"{time.time() - t0:.2f}s", "same_as_off", same, flush=True)
