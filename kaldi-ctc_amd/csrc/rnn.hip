@@ -324,6 +324,7 @@ struct RecParams {
   const unsigned *gtf;
   unsigned gid;
   int gmt, ggx;
+  int gplain;  // diagnostic (KCTC_GATE_PLAIN): the gated G rows fetched without sc1
 };
 
 // Phase stamps of the first kTraceSteps steps ([steps][grid][16]; thread 0 of every workgroup;
@@ -2363,7 +2364,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     for (int q = 0; q < NW; q++) {
       const unsigned dst = __builtin_amdgcn_readfirstlane(
           (unsigned)reinterpret_cast<uintptr_t>(ginl + ((kk & 7) * NW + q) * 16 * U + (w - CW) * 64));
-      if (gate) dma_lds_dword_sc1(p.G + gr + q * H, dst);  // written by the GEMM's XCDs during this kernel
+      if (gate && !p.gplain) dma_lds_dword_sc1(p.G + gr + q * H, dst);  // written by the GEMM's XCDs during this kernel
       else dma_lds_dword(p.G + gr + q * H, dst);
     }
   };
@@ -3488,6 +3489,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       p.gid = gid;
       p.gmt = (int)((TN + 255) / 256);
       p.ggx = (NW * H + 255) / 256;
+      p.gplain = env_int("KCTC_GATE_PLAIN", 0);
     }
     p.wwait = env_int("KCTC_FWD_WWAIT", 1);  // measured: forward recurrence 29.7 -> 28.6 ms/step
     if (ver == 6 && bf16_io(d)) {  // the output also as packed bf16 rows and columns
