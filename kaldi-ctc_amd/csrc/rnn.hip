@@ -2316,6 +2316,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // the flags itself (gate_spin, compiler-counted loads: a full drain).
   const bool gate = GATE && p.gtf != nullptr;
   int gvt = d == 0 ? -1 : p.gmt, gpt = -1, gpd = 3;
+  int gnext = 0;  // first forward-order step whose rows need a tile past gvt
   auto gate_spin = [&](int tile) {
     const unsigned *f = p.gtf + ((long)d * p.gmt + tile) * p.ggx;
     int spins = 0;
@@ -2337,6 +2338,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     }
   };
   auto gate_rows = [&](int kk) {  // before the G fetch of forward-order step kk
+    if (kk < gnext) return;  // (one compare on most steps)
     const int tt = d == 0 ? min(kk, T - 1) : max(T - 1 - kk, 0);
     const int lo = (int)(((long)tt * N + n0) >> 8), hi = (int)(((long)tt * N + nend - 1) >> 8);
     bool moved = false;
@@ -2348,6 +2350,17 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
       gvt = nt;
       moved = true;
     }
+    // the first step past the verified tiles: direction 0 rows reach tile
+    // gvt + 1 at frame ceil(((gvt + 1) 256 - (nend - 1)) / N), direction 1
+    // rows reach below tile gvt at frame floor((gvt 256 - n0 - 1) / N)
+    if (d == 0) {
+      const long num = (long)(gvt + 1) * 256 - (nend - 1);
+      gnext = num <= 0 ? kk + 1 : (int)min((num + N - 1) / N, (long)T + 64);
+    } else {
+      const long num = (long)gvt * 256 - n0 - 1;
+      gnext = num < 0 ? T + 64 : T - 1 - (int)(num / N);
+    }
+    gnext = max(gnext, kk + 1);
     const int nx = d == 0 ? gvt + 1 : gvt - 1;
     if (moved && nx >= 0 && nx < p.gmt) {  // the next tile's flags, checked when it is first needed
       const unsigned *f = p.gtf + ((long)d * p.gmt + nx) * p.ggx + (lane < p.ggx ? lane : 0);
