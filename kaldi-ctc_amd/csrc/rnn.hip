@@ -217,7 +217,8 @@ static bool bf16_direct(const RnnDesc &d, int ver) {
 // (RecParams::yr / yc) and the backward E^T shifted (eshift); H % 32 == 0 so
 // that a workgroup's units fill whole 16-B row chunks
 static bool bf16_io(const RnnDesc &d) {
-  return bf16_direct(d, 6) && d.layers == 1 && d.dirs == 2 && d.H % 32 == 0 && (2 * d.H) % 64 == 0;
+  return bf16_direct(d, 6) && d.layers == 1 && d.dirs == 2 && d.H % 32 == 0 && (2 * d.H) % 64 == 0 &&
+         env_int("KCTC_BF16_IO", 1);
 }
 
 

@@ -4,7 +4,12 @@ instead of fp32 rows that pack kernels convert afterwards.  The conversion is
 the same round-to-nearest cast of the same fp32 values, so training is bit
 identical to the packing path (KCTC_BF16_DIRECT=0), for GRU (separate DX and E
 transposes) and LSTM (one), ragged frame counts whose packed rows end in a
-zero tail (T*N not a multiple of 64), and groups of fewer than 16 rows."""
+zero tail (T*N not a multiple of 64), and groups of fewer than 16 rows
+(KCTC_BF16_IO=0).  With the forward's output packed too (bf16_io: y rows and
+columns from the recurrence, E^T written shifted by one step so that dR pairs
+it with the unshifted y^T) the dR products are the same but sit N frames
+further along the GEMM's K: its k-blocks group them differently, so the sums
+round differently -- same to 1e-6 of the parameters instead of bit for bit."""
 import os
 
 import numpy as np
@@ -13,11 +18,13 @@ import pytest
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
 
 
-def _train(kctc, gpu, cfg, batch, direct, steps=2):
+def _train(kctc, gpu, cfg, batch, direct, steps=2, io=False):
     import torch
     feats, nf, fl, ll, T, N = batch
     old = os.environ.get("KCTC_BF16_DIRECT")
+    old_io = os.environ.get("KCTC_BF16_IO")
     os.environ["KCTC_BF16_DIRECT"] = "1" if direct else "0"
+    os.environ["KCTC_BF16_IO"] = "1" if io else "0"
     try:
         net = kctc.Nnet(cfg, seed=3)
         net.set_precision("bf16")
@@ -26,10 +33,11 @@ def _train(kctc, gpu, cfg, batch, direct, steps=2):
         params = [net.get_params(c) for c in range(net.num_components) if net.num_params(c)]
         net.close()
     finally:
-        if old is None:
-            os.environ.pop("KCTC_BF16_DIRECT", None)
-        else:
-            os.environ["KCTC_BF16_DIRECT"] = old
+        for k, v in (("KCTC_BF16_DIRECT", old), ("KCTC_BF16_IO", old_io)):
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     return stats, params
 
 
@@ -45,3 +53,8 @@ def test_direct_packing_bit_identical(kctc, gpu, mode, H, N, T):
     assert a[0] == b[0]
     for x, y in zip(a[1], b[1]):
         np.testing.assert_array_equal(x, y)
+    c = _train(kctc, gpu, cfg, batch, direct=True, io=True)
+    for sa, sc in zip(a[0], c[0]):
+        np.testing.assert_allclose(np.asarray(sc, dtype=np.float64), np.asarray(sa, dtype=np.float64), rtol=1e-5)
+    for x, y in zip(a[1], c[1]):
+        np.testing.assert_allclose(y, x, rtol=0, atol=1e-6)
