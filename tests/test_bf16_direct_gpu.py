@@ -9,7 +9,8 @@ zero tail (T*N not a multiple of 64), and groups of fewer than 16 rows
 columns from the recurrence, E^T written shifted by one step so that dR pairs
 it with the unshifted y^T) the dR products are the same but sit N frames
 further along the GEMM's K: its k-blocks group them differently, so the sums
-round differently -- same to 1e-6 of the parameters instead of bit for bit."""
+round differently -- same to 1e-6 of the parameters after one step instead
+of bit for bit."""
 import os
 
 import numpy as np
@@ -53,7 +54,11 @@ def test_direct_packing_bit_identical(kctc, gpu, mode, H, N, T):
     assert a[0] == b[0]
     for x, y in zip(a[1], b[1]):
         np.testing.assert_array_equal(x, y)
-    c = _train(kctc, gpu, cfg, batch, direct=True, io=True)
+    # one step: the next one's bf16 casts of the updated weights turn a 1e-8
+    # difference into whole bf16 ulps, so the runs drift apart (both equally
+    # far from the fp64 oracle: test_train_step_bf16_matches_oracle)
+    a = _train(kctc, gpu, cfg, batch, direct=False, steps=1)
+    c = _train(kctc, gpu, cfg, batch, direct=True, io=True, steps=1)
     for sa, sc in zip(a[0], c[0]):
         np.testing.assert_allclose(np.asarray(sc, dtype=np.float64), np.asarray(sa, dtype=np.float64), rtol=1e-5)
     for x, y in zip(a[1], c[1]):
