@@ -65,6 +65,9 @@ int krnnDestroy(krnnDescriptor_t desc);
  * accumulation and master weights (LSTM / GRU only, BASELINE configs[4]). */
 enum { KRNN_PREC_FP32 = 0, KRNN_PREC_BF16 = 1 };
 int krnnSetPrecision(krnnDescriptor_t desc, int precision);
+/* (as cuDNN's data type, precision is part of the descriptor: query the
+ * workspace / reserve sizes after setting it -- with KCTC_BF16_DIRECT=1 a
+ * bf16 reserve also holds the recurrences' packed GEMM operands) */
 const char *krnnGetStatusString(int status);
 
 /* bytes of the opaque weight buffer (cudnnGetRNNParamsSize) */

@@ -82,6 +82,12 @@ long RnnDesc::lin_offset(int p, int lin, bool bias) const {
 }
 
 static long al64(long x) { return (x + 63) / 64 * 64; }
+// bf16_direct's switch (KCTC_BF16_DIRECT, off by default), for the reserve
+// layout defined before the helpers below
+static bool bf16_direct_env() {
+  const char *e = getenv("KCTC_BF16_DIRECT");
+  return e && atoi(e) != 0;
+}
 
 RnnReserveLayout rnn_reserve_layout(const RnnDesc &d, int T, int N) {
   RnnReserveLayout r;
@@ -95,7 +101,7 @@ RnnReserveLayout rnn_reserve_layout(const RnnDesc &d, int T, int N) {
   r.out = p;  p += (d.layers > 1) ? al64(TN * dirs * H) : 0;
   r.dout = p; p += (d.layers > 1) ? al64(TN * dirs * H) : 0;
   r.kbt64 = (TN + 63) / 64 * 64;
-  const bool pkd = d.prec == 1 /* kPrecBf16 */;  // bf16 halves: 2 per float
+  const bool pkd = d.prec == 1 /* kPrecBf16 */ && bf16_direct_env();  // bf16 halves: 2 per float
   const long G4 = nw * H, kbg64 = (G4 + 63) / 64 * 64;
   r.pkxr = p; p += pkd ? al64((dirs * TN * kbg64 + 1) / 2) : 0;
   r.pkxt = p; p += pkd ? al64((dirs * G4 * r.kbt64 + 1) / 2) : 0;
