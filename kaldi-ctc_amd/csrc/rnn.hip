@@ -1618,6 +1618,10 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   static_assert(NWG % NGRP == 0, "producer groups");
   constexpr bool BF = P == kPrecBf16;
   constexpr bool STK = P == kPrecX3S;  // dGates hi / lo stacked in one 16-row A image (groups of <= 8 rows)
+  // split-fp16: the cell's coefficients before the hand-off (see kc below);
+  // bf16 (configs[4], every wave an element wave) measured faster with the
+  // whole pointwise backward in the cell (3.65 vs 3.46 us/step)
+  constexpr bool PRE = !BF;
   using AT = typename std::conditional<BF, __bf16, _Float16>::type;
   using AV = typename std::conditional<BF, bf16x8, halfx8>::type;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1733,6 +1737,27 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
       kc[4] = z;
     }
   };
+  // bias and column-maximum bookkeeping of the step's dGates, and their LDS
+  // stage for the next step's row writes
+  auto book = [&]() {
+#pragma unroll
+    for (int q = 0; q < NW; q++) {
+      bsx[q] += (MODE == kGru) ? dxk[q] : eg[q];
+      if (MODE == kGru) bsh[q] += eg[q];
+      if (live) {  // column maxima for the weight GEMMs' packed transposes
+        cmx[q] = fmaxf(cmx[q], fabsf(MODE == kGru ? dxk[q] : eg[q]));
+        if (MODE == kGru) cme[q] = fmaxf(cme[q], fabsf(eg[q]));
+      }
+    }
+    if (p.e_sc1 || (BF && p.dxt != nullptr)) {
+#pragma unroll
+      for (int q = 0; q < NW; q++) estg[en * NW * U + q * U + eu] = MODE == kGru ? dxk[q] : eg[q];
+      if (MODE == kGru && BF && p.dxt != nullptr) {
+#pragma unroll
+        for (int q = 0; q < NW; q++) estg[16 * NW * U + en * NW * U + q * U + eu] = eg[q];
+      }
+    }
+  };
 #pragma unroll
   for (int q = 0; q < NW; q++) bsx[q] = bsh[q] = dxk[q] = eg[q] = cg[q] = ng[q] = cmx[q] = cme[q] = 0.f;
   auto prefetch = [&](int k) {  // operands of forward-order step k into n*
@@ -1841,7 +1866,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   const int epos = (eu >> 4) * 64 + (en >> 2) * (U < 16 ? U : 16) + (eu & 15);
   prefetch(T - 1);
   rotate();
-  coef();
+  if constexpr (PRE) coef();
   int bad = 0;
   unsigned *myflag = flag6(p, grp, d, g, NWG);
   // XCD-slot launches keep the hand-off in the XCD's L2 (plain flag stores
@@ -1894,9 +1919,11 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
           v[i] = crow_live ? __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
                                  rs, (int)((coff + (long)i * NGRP * PSTR) * 4), 0, 16 /* sc1 */))
                            : u32x2{0u, 0u};
-        __builtin_amdgcn_sched_barrier(0);
-        coef();  // while the hand-off loads are in flight
-        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (PRE) {
+          __builtin_amdgcn_sched_barrier(0);
+          coef();  // while the hand-off loads are in flight
+          __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int i = 0; i < PER; i++) {
           const bf16x4 b = __builtin_bit_cast(bf16x4, v[i]);
@@ -1908,9 +1935,11 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
 #pragma unroll
         for (int i = 0; i < PER; i++)
           v[i] = crow_live ? ld_sc1(rs, (unsigned)((coff + (long)i * NGRP * PSTR) * 4)) : u32x4{0u, 0u, 0u, 0u};
-        __builtin_amdgcn_sched_barrier(0);
-        coef();  // while the hand-off loads are in flight
-        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (PRE) {
+          __builtin_amdgcn_sched_barrier(0);
+          coef();  // while the hand-off loads are in flight
+          __builtin_amdgcn_sched_barrier(0);
+        }
         sm = __builtin_bit_cast(floatx4, v[0]);
 #pragma unroll
         for (int i = 1; i < PER; i++) sm += __builtin_bit_cast(floatx4, v[i]);
@@ -1940,22 +1969,45 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
         for (int gg = 0; gg < NGRP; gg++) dhr += red[(long)(gg * POS + epos) * 4 + (en & 3)];
       }
       float dh = cdy + dhr;
-      if (MODE == kLstm) {
-        const float dc = dh * kc[0] + carry;
-        eg[0] = dc * kc[1];
-        eg[1] = dc * kc[2];
-        eg[2] = dc * kc[3];
-        eg[3] = dh * kc[4];
-        carry = dc * kc[5];
+      if constexpr (PRE) {
+        if (MODE == kLstm) {
+          const float dc = dh * kc[0] + carry;
+          eg[0] = dc * kc[1];
+          eg[1] = dc * kc[2];
+          eg[2] = dc * kc[3];
+          eg[3] = dh * kc[4];
+          carry = dc * kc[5];
+        } else {
+          dh += carry;
+          dxk[0] = dh * kc[0]; dxk[1] = dh * kc[1]; dxk[2] = dh * kc[2];
+          eg[0] = dxk[0]; eg[1] = dxk[1]; eg[2] = dh * kc[3];
+          carry = dh * kc[4];
+        }
+      } else if (MODE == kLstm) {
+        const float ig = cg[0], fg = cg[1], gg = cg[2], og = cg[3];
+        const float tc = ftanh(ca);
+        const float dO = dh * tc;
+        const float dc = dh * og * (1.f - tc * tc) + carry;
+        eg[0] = dc * gg * ig * (1.f - ig);
+        eg[1] = dc * cap * fg * (1.f - fg);
+        eg[2] = dc * ig * (1.f - gg * gg);
+        eg[3] = dO * og * (1.f - og);
+        carry = dc * fg;
       } else {
         dh += carry;
-        dxk[0] = dh * kc[0]; dxk[1] = dh * kc[1]; dxk[2] = dh * kc[2];
-        eg[0] = dxk[0]; eg[1] = dxk[1]; eg[2] = dh * kc[3];
-        carry = dh * kc[4];
+        const float r = cg[0], z = cg[1], nn = cg[2];
+        const float dn = dh * (1.f - z), dz = dh * (cap - nn);
+        const float dpn = dn * (1.f - nn * nn);
+        const float dpr = dpn * ca * r * (1.f - r);
+        const float dpz = dz * z * (1.f - z);
+        carry = dh * z;
+        dxk[0] = dpr; dxk[1] = dpz; dxk[2] = dpn;
+        eg[0] = dpr; eg[1] = dpz; eg[2] = dpn * r;
       }
       float m = 0.f;
 #pragma unroll
       for (int q = 0; q < NW; q++) m = fmaxf(m, fabsf(eg[q]));
+      if constexpr (!PRE) book();
       if constexpr (BF) {
 #pragma unroll
         for (int q = 0; q < NW; q++) Ahi[en * AP + q * U + eu] = (__bf16)eg[q];
@@ -2054,25 +2106,9 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
     // off the hand-off path (behind the partial-dh stores, during their
     // drain): bias and column-maximum bookkeeping, the dGates stage for the
     // next step's row writes (read after the publish barrier)
-    __builtin_amdgcn_sched_barrier(0);
-    if (has_e) {
-#pragma unroll
-      for (int q = 0; q < NW; q++) {
-        bsx[q] += (MODE == kGru) ? dxk[q] : eg[q];
-        if (MODE == kGru) bsh[q] += eg[q];
-        if (live) {  // column maxima for the weight GEMMs' packed transposes
-          cmx[q] = fmaxf(cmx[q], fabsf(MODE == kGru ? dxk[q] : eg[q]));
-          if (MODE == kGru) cme[q] = fmaxf(cme[q], fabsf(eg[q]));
-        }
-      }
-      if (p.e_sc1 || pk) {
-#pragma unroll
-        for (int q = 0; q < NW; q++) estg[en * NW * U + q * U + eu] = MODE == kGru ? dxk[q] : eg[q];
-        if (MODE == kGru && pk) {
-#pragma unroll
-          for (int q = 0; q < NW; q++) estg2[en * NW * U + q * U + eu] = eg[q];
-        }
-      }
+    if constexpr (PRE) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (has_e) book();
     }
     REC_TRACE(ks, 7);
     signal_epoch(myflag, (unsigned)(ks + 2), local);
