@@ -12,10 +12,12 @@ from conftest import rel_err
 pytestmark = pytest.mark.gpu
 
 
-def _mk(kctc, gpu, mode, T, N, D, H, layers, bidir, seed, wscale=0.15):
+def _mk(kctc, gpu, mode, T, N, D, H, layers, bidir, seed, wscale=0.15, prec=None):
     import torch
     rng = np.random.default_rng(seed)
     r = kctc.Rnn(mode, D, H, layers, bidir)
+    if prec is not None:  # part of the descriptor: before the size queries (kaldi_rnn.h)
+        r.set_precision(prec)
     P = r.num_params
     w = (rng.standard_normal(P) * wscale).astype(np.float32)
     x = rng.standard_normal((T, N, D)).astype(np.float32)
@@ -123,8 +125,8 @@ BF16_CASES = [
 def test_rnn_bf16_matches_oracle(kctc, gpu, oracle, case):
     """krnnSetPrecision(KRNN_PREC_BF16): bf16 recurrences and gate GEMMs."""
     mode, T, N, D, H, layers, bidir = case
-    r, (w, x, dy), b = _mk(kctc, gpu, mode, T, N, D, H, layers, bidir, seed=sum(case) + 1, wscale=0.05)
-    r.set_precision("bf16")
+    r, (w, x, dy), b = _mk(kctc, gpu, mode, T, N, D, H, layers, bidir, seed=sum(case) + 1, wscale=0.05,
+                           prec="bf16")
     y, dx, dw = _run_gpu(r, b)
     ry, res = oracle.rnn_forward(mode, x.astype(np.float64), w.astype(np.float64), H, layers, r.dirs)
     rdx, rdw = oracle.rnn_backward(mode, x.astype(np.float64), w.astype(np.float64), ry,
