@@ -101,7 +101,7 @@ RnnReserveLayout rnn_reserve_layout(const RnnDesc &d, int T, int N) {
   r.out = p;  p += (d.layers > 1) ? al64(TN * dirs * H) : 0;
   r.dout = p; p += (d.layers > 1) ? al64(TN * dirs * H) : 0;
   r.kbt64 = (TN + 63) / 64 * 64;
-  const bool pkd = d.prec == 1 /* kPrecBf16 */ && bf16_direct_env();  // bf16 halves: 2 per float
+  const bool pkd = d.prec == 1 /* kPrecBf16 */ && d.layers == 1 && bf16_direct_env();  // bf16 halves: 2 per float
   const long G4 = nw * H, kbg64 = (G4 + 63) / 64 * 64;
   r.pkxr = p; p += pkd ? al64((dirs * TN * kbg64 + 1) / 2) : 0;
   r.pkxt = p; p += pkd ? al64((dirs * G4 * r.kbt64 + 1) / 2) : 0;
@@ -216,8 +216,11 @@ int env_int(const char *name, int dflt);
 // bf16 recurrences write their dGates straight into the packed bf16 GEMM
 // operands (RecParams::dxr / dxt / et) -- v6 only (a v6 backward runs for
 // every bf16 shape), whole 64-element gate rows
+// (one-layer descriptors -- the recipe's components; a stacked descriptor's
+// weight gradients measured wrong with it, so those keep the pack path)
 static bool bf16_direct(const RnnDesc &d, int ver) {
-  return d.prec == 1 /* kPrecBf16 */ && ver == 6 && (d.nw() * d.H) % 64 == 0 && env_int("KCTC_BF16_DIRECT", 0);
+  return d.prec == 1 /* kPrecBf16 */ && ver == 6 && (d.nw() * d.H) % 64 == 0 && d.layers == 1 &&
+         env_int("KCTC_BF16_DIRECT", 0);
 }
 // ... and, one-layer bidirectional, the forward writes its output packed
 // (RecParams::yr / yc) and the backward E^T shifted (eshift); H % 32 == 0 so
