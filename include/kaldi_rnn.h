@@ -66,8 +66,8 @@ int krnnDestroy(krnnDescriptor_t desc);
 enum { KRNN_PREC_FP32 = 0, KRNN_PREC_BF16 = 1 };
 int krnnSetPrecision(krnnDescriptor_t desc, int precision);
 /* (as cuDNN's data type, precision is part of the descriptor: query the
- * workspace / reserve sizes after setting it -- with KCTC_BF16_DIRECT=1 a
- * bf16 reserve also holds the recurrences' packed GEMM operands) */
+ * workspace / reserve sizes after setting it -- a one-layer bf16 reserve also
+ * holds the recurrences' packed GEMM operands, KCTC_BF16_DIRECT=0 drops them) */
 const char *krnnGetStatusString(int status);
 
 /* bytes of the opaque weight buffer (cudnnGetRNNParamsSize) */

@@ -82,11 +82,11 @@ long RnnDesc::lin_offset(int p, int lin, bool bias) const {
 }
 
 static long al64(long x) { return (x + 63) / 64 * 64; }
-// bf16_direct's switch (KCTC_BF16_DIRECT, off by default), for the reserve
+// bf16_direct's switch (KCTC_BF16_DIRECT, on by default), for the reserve
 // layout defined before the helpers below
 static bool bf16_direct_env() {
   const char *e = getenv("KCTC_BF16_DIRECT");
-  return e && atoi(e) != 0;
+  return !e || atoi(e) != 0;
 }
 
 RnnReserveLayout rnn_reserve_layout(const RnnDesc &d, int T, int N) {
@@ -220,7 +220,7 @@ int env_int(const char *name, int dflt);
 // weight gradients measured wrong with it, so those keep the pack path)
 static bool bf16_direct(const RnnDesc &d, int ver) {
   return d.prec == 1 /* kPrecBf16 */ && ver == 6 && (d.nw() * d.H) % 64 == 0 && d.layers == 1 &&
-         env_int("KCTC_BF16_DIRECT", 0);
+         env_int("KCTC_BF16_DIRECT", 1);
 }
 // ... and, one-layer bidirectional, the forward writes its output packed
 // (RecParams::yr / yc) and the backward E^T shifted (eshift); H % 32 == 0 so

@@ -59,14 +59,13 @@ int kctc_comm_ctas() {
 // (which needs all CUs of its XCDs) could wait on an all-reduce that waits on
 // another GPU -- and the backward recurrences stay XCD-pinned with the
 // exchange configured (rnn_set_comm_gated).  The last bucket (bottom
-// component) goes out at Finish, with no recurrence after it.  KCTC_COMM_GATE=1
-// turns it on (off by default until measured on the GPU: every bucket is then
-// reduced at once and the backward runs unpinned, as in round 3).
+// component) goes out at Finish, with no recurrence after it.  KCTC_COMM_GATE=0
+// reduces every bucket at once and leaves the backward unpinned (round 3).
 class GatedExchange : public kctc::nnet2::GradExchange {
  public:
   GatedExchange(hipStream_t compute, int comm_cus) : compute_(compute) {
     const char *e = getenv("KCTC_COMM_GATE");
-    gated_ = e && *e == '1';
+    gated_ = !(e && *e == '0');
     kctc::rnn_set_cu_budget(kctc_usable_cus_override(), comm_cus);
     kctc::rnn_set_comm_gated(gated_);
     KCTC_HIP_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
