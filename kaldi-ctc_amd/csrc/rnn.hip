@@ -2375,26 +2375,17 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // otherwise, or if they do not all hold this call's id yet, the wave polls
   // the flags itself (gate_spin, compiler-counted loads: a full drain).
   const bool gate = GATE && p.gtf != nullptr;
-  // the gate's state and arguments live in VGPRs (asm laundering: divergent
-  // to the compiler): kept in SGPRs they pushed the kernel past the SGPR
-  // budget, and the spills (v_readlane / v_writelane all over the loop) made
-  // the gated recurrence 2.06 -> 2.45 us/step
-  const unsigned *gtf_v = p.gtf;
-  unsigned gid_v = p.gid;
-  int gmt_v = p.gmt, ggx_v = p.ggx;
-  if constexpr (GATE) asm volatile("" : "+v"(gtf_v), "+v"(gid_v), "+v"(gmt_v), "+v"(ggx_v));
-  int gvt = d == 0 ? -1 : gmt_v, gpt = -1, gpd = 3;
+  int gvt = d == 0 ? -1 : p.gmt, gpt = -1, gpd = 3;
   int gnext = 0;  // first forward-order step whose rows need a tile past gvt
-  if constexpr (GATE) asm volatile("" : "+v"(gvt), "+v"(gpt), "+v"(gpd), "+v"(gnext));
   auto gate_spin = [&](int tile) {  // (asm loads only: see ld_u32_sc1_now)
-    const unsigned *f = gtf_v + ((long)d * gmt_v + tile) * ggx_v + (lane < ggx_v ? lane : 0);
+    const unsigned *f = p.gtf + ((long)d * p.gmt + tile) * p.ggx + (lane < p.ggx ? lane : 0);
     int spins = 0;
     while (true) {
       const unsigned v = ld_u32_sc1_now(f);
-      if (__all(v == gid_v)) return;
+      if (__all(v == p.gid)) return;
       if (++spins > kSpinLimit || ((spins & 255) == 0 && ld_u32_sc1_now(p.err))) {
         // timeout: the error word gets 0x10 if the GEMM had started (its tag), 0x20 if not
-        if (lane == 0) bad_lds = ld_u32_sc1_now(gtf_v - 63) == gid_v ? 0x11 : 0x21;
+        if (lane == 0) bad_lds = ld_u32_sc1_now(p.gtf - 63) == p.gid ? 0x11 : 0x21;
         return;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -2408,7 +2399,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     while (d == 0 ? gvt < hi : gvt > lo) {
       const int nt = d == 0 ? gvt + 1 : gvt - 1;
       const unsigned *pb = pollbuf + (w - CW) * 64;
-      const bool have = gpt == nt && gpd >= 3 && __all(lane >= ggx_v || pb[lane] == gid_v);
+      const bool have = gpt == nt && gpd >= 3 && __all(lane >= p.ggx || pb[lane] == p.gid);
       if (!have) gate_spin(nt);
       gvt = nt;
       moved = true;
@@ -2425,8 +2416,8 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     }
     gnext = max(gnext, kk + 1);
     const int nx = d == 0 ? gvt + 1 : gvt - 1;
-    if (moved && nx >= 0 && nx < gmt_v) {  // the next tile's flags, checked when it is first needed
-      const unsigned *f = gtf_v + ((long)d * gmt_v + nx) * ggx_v + (lane < ggx_v ? lane : 0);
+    if (moved && nx >= 0 && nx < p.gmt) {  // the next tile's flags, checked when it is first needed
+      const unsigned *f = p.gtf + ((long)d * p.gmt + nx) * p.ggx + (lane < p.ggx ? lane : 0);
       dma_lds_dword_sc1(f, __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(pollbuf + (w - CW) * 64)));
       gpt = nx;
       gpd = 0;
