@@ -2868,11 +2868,12 @@ static void launch6_u(bool fwd, int nth, const RecParams &p, dim3 grid, size_t l
       if (nth == 1024) launch6_h<MODE, 16, 1024, P>(fwd, p, grid, lds, s);
       else if (nth == 512) {
         // row groups of <= 8 sequences: hi / lo stacked in one MFMA operand
-        // (KCTC_STK=1, off by default: equally accurate or better -- all four
-        // products -- but not faster at configs[1]: forward 2.31 vs 2.32,
-        // backward 2.54 vs 2.49 us/step; the steps are bound by the hand-off
-        // latencies, and the fold adds a cross-lane exchange)
-        const int stk = env_int("KCTC_STK", 0);  // read per launch (tests toggle it)
+        // (all four products: equally accurate or better).  Forward on by
+        // default since round 4: the stacked forward (one A load per k block,
+        // 2/3 of the MFMAs) runs 1.76 us/step against 2.05 for the IO-wave
+        // forward, same box; backward off (2.53 vs 2.43: the fold's cross-lane
+        // exchange).  KCTC_STK_FWD / KCTC_STK_BWD (or KCTC_STK for both)
+        const int stk = env_int(fwd ? "KCTC_STK_FWD" : "KCTC_STK_BWD", env_int("KCTC_STK", fwd ? 1 : 0));
         if constexpr (P == kPrecX3) {
           if (p.gs <= 8 && stk) {
             launch6_h<MODE, 16, 512, kPrecX3S>(fwd, p, grid, lds, s);
@@ -3248,7 +3249,8 @@ bool chain_ok(const RnnDesc &d, int ver, int T, int N, const RnnFwdChain *c) {
   // and only the IO-wave variant (U = 16, 512 threads) carries the copies
   // (launch6_u: U = 16 / 512 threads, KCTC_FWD_IOW, not the stacked variant)
   if (xcd_mask(d, N, true) && !(pick6(d, N, true).U == 16 && pick6(d, N, true).nth == 512 &&
-                                env_int("KCTC_FWD_IOW", 1) && !env_int("KCTC_STK", 0)))
+                                env_int("KCTC_FWD_IOW", 1) &&
+                                !(pick6(d, N, true).gs <= 8 && env_int("KCTC_STK_FWD", env_int("KCTC_STK", 1)))))
     return false;
   const V6Cfg c6 = pick6(d, N, true);
   if (!c6 || !stream_block_budget(d.dirs * (d.H / c6.U) * c6.rg, false)) return false;
@@ -3413,7 +3415,8 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
   // consumer-gated projection: the split-fp16 forward with IO waves
   // (launch6_u), XCD-pinned so that the GEMM keeps to the other XCDs
   const bool gate_ok = side && ver == 6 && c6.U == 16 && c6.nth == 512 && d.prec == kPrecX3 &&
-                       env_int("KCTC_FWD_IOW", 1) && !(c6.gs <= 8 && env_int("KCTC_STK", 0)) &&
+                       env_int("KCTC_FWD_IOW", 1) &&
+                       !(c6.gs <= 8 && env_int("KCTC_STK_FWD", env_int("KCTC_STK", 1))) &&
                        env_int("KCTC_FWD_GATE", 0) && xcd_mask(d, N, true) != 0 &&
                        __builtin_popcount(xcd_mask(d, N, true)) <= 4 &&  // XCDs left to the GEMM
                        x3p_use_256((int)TN, d.nw() * d.H);
