@@ -2876,7 +2876,11 @@ static void launch6_u(bool fwd, int nth, const RecParams &p, dim3 grid, size_t l
         const int stk = env_int(fwd ? "KCTC_STK_FWD" : "KCTC_STK_BWD", env_int("KCTC_STK", fwd ? 1 : 0));
         if constexpr (P == kPrecX3) {
           if (p.gs <= 8 && stk) {
-            launch6_h<MODE, 16, 512, kPrecX3S>(fwd, p, grid, lds, s);
+            // the stacked forward with IO waves (KCTC_STK_IOW=1, measuring)
+            if (fwd && env_int("KCTC_FWD_IOW", 1) && env_int("KCTC_STK_IOW", 0))
+              launch6_h<MODE, 16, 512, kPrecX3S | 4>(fwd, p, grid, lds, s);
+            else
+              launch6_h<MODE, 16, 512, kPrecX3S>(fwd, p, grid, lds, s);
             break;
           }
         }
