@@ -39,7 +39,7 @@ def _train(kctc, gpu, cfg, batch, pinned, steps=2, var="KCTC_XCD6"):
     return stats, params
 
 
-@pytest.mark.parametrize("var", ["KCTC_XCD6", "KCTC_XCD6F"])
+@pytest.mark.parametrize("var", ["KCTC_XCD6", "KCTC_XCD6F", "KCTC_XCD6F-stk"])
 @pytest.mark.parametrize("mode,N,T", [(2, 16, 400), (2, 8, 300), (3, 16, 300), (2, 13, 350),
                                       # configs[2]: four 16-row groups of U = 32 (16 workgroups a
                                       # direction): eight slots of 16 workgroups, one per XCD
@@ -50,18 +50,27 @@ def test_pinned_bit_identical(kctc, gpu, mode, N, T, var):
                              max_seq_length=T, rnn_mode=mode)
     feats, nf, fl, ll = kctc.synth_minibatch(7 + N, T, N, D, A, 0.125)
     batch = (feats, nf, fl, ll, T, N)
-    # the pinned forward's streamed projection (off by default, rnn.hip
-    # chain_ok) is part of what the forward case checks
-    old = os.environ.get("KCTC_FWD_STREAM_PINNED")
-    os.environ["KCTC_FWD_STREAM_PINNED"] = "1"
+    # KCTC_XCD6F: the IO-wave forward, whose pinned form feeds a streamed
+    # projection here (KCTC_FWD_STREAM_PINNED, off by default: rnn.hip
+    # chain_ok) as its unpinned form does; KCTC_XCD6F-stk: the default
+    # stacked forward of <= 8-row groups, projections after the recurrence
+    env = {"KCTC_FWD_STREAM_PINNED": "1"}
+    if var == "KCTC_XCD6F":
+        env["KCTC_STK_FWD"] = "0"
+    elif var == "KCTC_XCD6F-stk":
+        env = {"KCTC_FWD_STREAM": "0"}
+        var = "KCTC_XCD6F"
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         a = _train(kctc, gpu, cfg, batch, pinned=False, var=var)
         b = _train(kctc, gpu, cfg, batch, pinned=True, var=var)
     finally:
-        if old is None:
-            os.environ.pop("KCTC_FWD_STREAM_PINNED", None)
-        else:
-            os.environ["KCTC_FWD_STREAM_PINNED"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     assert a[0] == b[0]
     for x, y in zip(a[1], b[1]):
         np.testing.assert_array_equal(x, y)
