@@ -25,11 +25,16 @@ sketch_step*.npz, fp64 oracle, same parameters and minibatch) must match at
 1e-4 -- configs[4] (bf16 operands) at its error model's per-output bar
 (tests/sketch_common.py) -- (`loss_match`).
 
-`value` is the HBM-resident pass (the measurement contract: inputs resident
-when the timed region starts; the trainer's boundary takes device features).
-`h2d_inclusive` repeats the K steps with the features copied from pinned host
-memory inside every step -- SURVEY §8d's timed region, which starts at the
-H2D copy -- and is reported beside it.
+Three timed passes of K steps each, all after the warm-up:
+  1. `value`: HBM-resident features, no profiling events (the measurement
+     contract: inputs resident when the timed region starts; the trainer's
+     boundary takes device features);
+  2. the same with per-family HIP events on the trainer's streams, from which
+     the `roofline` of the dominant kernel is priced (events cost a little
+     time, so this pass is never `value`);
+  3. `h2d_inclusive`: the features copied from pinned host memory inside every
+     step -- SURVEY §8d's timed region, which starts at the H2D copy --
+     reported beside `value` (the PCIe-inclusive rate is never `value`).
 
 Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (HIP
 events on the trainer's stream over the timed region) and a CPU baseline
@@ -76,7 +81,7 @@ CONFIGS = {
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=1, choices=sorted(CONFIGS),
                     help="BASELINE.json configs[i] to measure (1: the metric's config)")
@@ -200,21 +205,40 @@ def ctc_bytes(T_max, A, num_frames, label_lengths):
             "ctc_grad": float(np.sum(8 * T * S + 16 * T + 4 * T * A + 4 * T)) + rows * A * 4}
 
 
-def pmc_traffic(kernel):
-    """HBM-side bytes per launch of `kernel` from the newest committed rocprofv3
-    PMC pass (profiles/*_pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE; produced by
-    scripts/gpu_bench_prof.sh on this workload).  bench.py cannot read counters
-    itself; None when no measurement of this kernel is committed."""
+def _committed_pmc(kind, config):
+    """Newest committed rocprofv3 PMC summary of `kind` ("traffic" or "mfma")
+    for `config`: profiles/rNN*_pmc_<kind>.json for configs[1],
+    profiles/rNN*_cfg<N>_pmc_<kind>.json otherwise (scripts/gpu_bench_prof.sh
+    and scripts/gpu_cfg_prof.sh on this workload).  bench.py cannot read
+    counters itself."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{kind}.json")))
+    tag = f"_cfg{config}_"
+    files = [f for f in files if (tag in os.path.basename(f)) == (config != 1)]
+    out = []
     for f in reversed(files):
         try:
-            d = json.load(open(f))
+            out.append((json.load(open(f)), os.path.basename(f)))
         except (OSError, ValueError):
             continue
+    return out
+
+
+def pmc_traffic(kernel, config=1):
+    """HBM-side bytes per launch of `kernel` (FETCH_SIZE x2 + WRITE_SIZE, the
+    guide's gfx950 correction); (None, None) when none is committed."""
+    for d, name in _committed_pmc("traffic", config):
         if kernel in d and "traffic_bytes_per_launch" in d[kernel]:
-            return d[kernel]["traffic_bytes_per_launch"], os.path.basename(f)
+            return d[kernel]["traffic_bytes_per_launch"], name
     return None, None
+
+
+def pmc_mfma(config=1):
+    """Counter-based MFMA utilisation per kernel family (SQ_VALU_MFMA_BUSY_CYCLES
+    against GRBM_GUI_ACTIVE x the 4 SIMDs of every CU; scripts/pmc_mfma.py)."""
+    for d, name in _committed_pmc("mfma", config):
+        return {"source": name, **d}
+    return None
 
 
 # ---- checks and baselines ---------------------------------------------------------
@@ -379,7 +403,6 @@ def main():
         warm_stats.append(net.train_step(f, T, N, nf, fl, ll))
 
     profile = not args.no_profile
-    net.set_profiling(profile)
     ext = torch.cuda.ExternalStream(net.stream, device=dev)
 
     def barrier():
@@ -421,6 +444,7 @@ def main():
         step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
         return dt, frames, stats, step_ms
 
+    net.set_profiling(False)
     dt, frames, stats, step_ms = timed_pass(False)
     traj = np.array([[o, w] for o, _, w in warm_stats + stats], np.float64)
     objf = sum(o for o, _, _ in stats)
@@ -435,7 +459,10 @@ def main():
         traj = tt.numpy()
     fam_flops = model_flops(T, N, D, H, A, L, nw=nw)
     prof = {}
+    prof_dt = None
     if profile:
+        net.set_profiling(True)
+        prof_dt, prof_frames, _, _ = timed_pass(False)
         # *_stream / x3_pack_chain / x3_pack_bwd_stream: GEMMs and packs on the
         # overlap streams, running concurrently with the recurrence that feeds
         # them (their spans include the waiting); off the critical path
@@ -497,13 +524,14 @@ def main():
         avg_s = ms / n / 1e3
         flops_per_launch = flops_total / n
         achieved = flops_per_launch / avg_s / 1e12
-        traffic, tsrc = pmc_traffic(dom) if args.config == 1 else (None, None)
+        traffic, tsrc = pmc_traffic(dom, args.config)
         # a split-fp16 GEMM can outrun the fp32 MFMA peak (it issues on the f16
         # engine): then the engine it issues on is the peak (frac <= 1)
         peak = peak_mfma if achieved <= peak_mfma else peak_engine
         roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": tsrc,
-                "peak_basis": ("fp32 MFMA peak (the precision class)" if peak == peak_mfma else
+                "peak_basis": ("bf16 dense MFMA peak (the dtype's)" if bf16 else
+                               "fp32 MFMA peak (the precision class)" if peak == peak_mfma else
                                f"the engine the products issue on ({engine}); "
                                f"{achieved / peak_mfma:.2f}x the fp32 MFMA peak"),
                 "kernel": dom, "avg_launch_ms": round(ms / n, 4), "flops_per_launch": flops_per_launch,
@@ -557,6 +585,14 @@ def main():
             aux["ctc_alpha_beta"]["us_per_frame"] = round(aux["ctc_alpha_beta"]["ms_per_launch"] / T * 1e3, 4)
             aux["ctc_alpha_beta"]["note"] = ("serial over T (one barrier per group of 8 frames): latency-bound; "
                                              "bytes = emission rows read + alpha/beta spill + fp64 offsets written")
+        # counter evidence beside the algorithmic fractions (north_star's
+        # "MFMA utilisation against gfx950 peak"): SQ_VALU_MFMA_BUSY_CYCLES
+        # of each kernel family from the committed rocprofv3 pass
+        aux["mfma_util_pmc"] = pmc_mfma(args.config)
+        if prof_dt:
+            aux["profiled_pass"] = {"value": round(prof_frames / prof_dt, 1),
+                                    "note": "the same K steps with per-family HIP events (the roofline's "
+                                            "source); not `value`"}
         roof["secondary"] = aux
 
     cpu = None

@@ -776,10 +776,13 @@ def set_perturb_seed(seed):
 
 
 def average_models(nnets, weights=None, skip_last_layer=False):
-    """nnet-am-average in process: nnets[0] = sum_i weights[i] * nnets[i]
-    (default weights 1/len(nnets)) through the components' Scale / Add."""
+    """nnet-am-average in process: nnets[0] = sum_i w[i] * nnets[i], with the
+    weights normalised to sum to one as GetWeights does (nnet-am-average.cc:
+    45-53; default 1/len(nnets)) through the components' Scale / Add."""
     arr = (ctypes.c_void_p * len(nnets))(*[n.h.value if hasattr(n.h, "value") else n.h for n in nnets])
-    w = None if weights is None else np.ascontiguousarray(weights, dtype=np.float32)
+    w = None if weights is None else np.ascontiguousarray(weights, dtype=np.float32).ravel()
+    if w is not None and w.size != len(nnets):
+        raise ValueError(f"average_models: {w.size} weights for {len(nnets)} models")
     _tcheck(lib().kctc_nnet_average_models(arr, None if w is None else w.ctypes.data, len(nnets),
                                            int(bool(skip_last_layer))), "kctc_nnet_average_models")
 

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <fstream>
 #include <memory>
@@ -319,6 +320,9 @@ int kctc_component_backprop(kctcComponent_t h, int T, int N, const float *in_val
     // AffineComponent::UpdateSimple); the mirror defers it to ApplyUpdate
     if (tu && tu->IsUpdatable()) static_cast<UpdatableComponent *>(tu)->ApplyUpdate();
     h->sync();
+    // the gradient is complete: to_update must not keep h's stream (h may be
+    // destroyed before to_update's next DotProduct / Add waits on it)
+    if (tu && tu->IsUpdatable()) static_cast<UpdatableComponent *>(tu)->ResetGradStream();
   });
 }
 
@@ -487,6 +491,11 @@ int kctc_nnet_average_models(kctcNnet_t *nnets, const float *weights, int num, i
       KCTC_REQUIRE(nnets[i]->device == nnets[0]->device, "kctc_nnet_average_models: networks on different devices");
     std::vector<float> w(num, 1.0f / (float)num);  // GetWeights' default: 1/num-models
     if (weights) w.assign(weights, weights + num);
+    // GetWeights (nnet-am-average.cc:45-53) normalises the weights to sum to one
+    float wsum = 0.f;
+    for (int i = 0; i < num; i++) wsum += w[i];
+    KCTC_REQUIRE(wsum != 0.f && std::isfinite(wsum), "kctc_nnet_average_models: weights sum to zero");
+    for (int i = 0; i < num; i++) w[i] /= wsum;
     kctcNnetImpl *avg = nnets[0];
     KCTC_REQUIRE(avg->trainer.Pending() == 0, "kctc_nnet_average_models with minibatches in flight");
     avg->activate();

@@ -506,6 +506,8 @@ void CuDNNRecurrentComponent::Forward(const CuMatrixBase &in, CuMatrixBase *out,
   workspace_.ensure(rnn_workspace_bytes(desc_, T, N));
   const bool projected = input_projected_;
   input_projected_ = false;
+  in_tn_[0] = T;
+  in_tn_[1] = N;
   ProfScope ps("layer_rnn_forward");
   // the trainer's side stream (idle during the forward pass) for a projection
   // computed beside the recurrence (rnn.h, consumer-gated projection)
@@ -552,7 +554,7 @@ void CuDNNRecurrentComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
       ProfScope ps("layer_rnn_backward_weights", ws);
       int st = rnn_backward_weights(desc_, ws, T, N, in_value.Data(), out_value.Data(), workspace_.p,
                                     workspace_.bytes, to_update->grad_.f(), reserve_.p, reserve_.bytes,
-                                    side_gemm_blocks(), input_bound_, nullptr, in_cols_);
+                                    side_gemm_blocks(), input_bound_, nullptr, packed_input_cols(T, N));
       if (st) throw std::runtime_error("rnn_backward_weights failed: " + std::to_string(st));
     }
     return;
@@ -582,7 +584,7 @@ void CuDNNRecurrentComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
     int st = rnn_backward_weights(desc_, ws, T, N, in_value.Data(), out_value.Data(), workspace_.p,
                                   workspace_.bytes, to_update->grad_.f(), reserve_.p, reserve_.bytes,
                                   dev.side ? side_gemm_blocks() : 0, input_bound_,
-                                  (!in_deriv && dev.side) ? dev.stream2 : nullptr, in_cols_);
+                                  (!in_deriv && dev.side) ? dev.stream2 : nullptr, packed_input_cols(T, N));
     if (st) throw std::runtime_error("rnn_backward_weights failed: " + std::to_string(st));
   }
 }
@@ -1282,6 +1284,9 @@ void Nnet::SetComponent(int c, Component *component) {
   }
   delete components_[c];
   components_[c] = component;
+  // packed operands point into the replaced component's reserve
+  for (Component *x : components_)
+    if (auto *r = dynamic_cast<CuDNNRecurrentComponent *>(x)) r->ClearPackedInput();
 }
 
 void Nnet::ZeroStats() {

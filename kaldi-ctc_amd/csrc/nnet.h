@@ -194,6 +194,9 @@ class UpdatableComponent : public Component {
   virtual float *ParamData() = 0;
   // stream on which GradData() was produced (the exchange waits on it)
   hipStream_t GradStream() const;
+  // forget the stream of the last Backprop (standalone components: the
+  // Backprop's stream belongs to the calling handle, which may go first)
+  void ResetGradStream() { grad_stream_ = nullptr; }
   // params += lr * (clipped) grad; skipped on device when *skip != 0 (the
   // step's recurrence hand-off failed: its gradients are not trusted)
   virtual void ApplyUpdate(const unsigned *skip = nullptr) = 0;
@@ -284,7 +287,7 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   void SetPrecision(int prec) {
     if (prec == 1 && desc_.mode != kLstm && desc_.mode != kGru)
       throw std::invalid_argument("bf16 products exist for LSTM / GRU only");
-    desc_.prec = prec;
+    rnn_set_precision(desc_, prec);
   }
   void SetMiniBatch(int n) const { mini_batch_ = n; }  // Init(mini_batch) on change
   // whether the last Propagate ran on a T x N input (Backprop's reserve-space precondition)
@@ -299,7 +302,13 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   // them instead of packing its input (set by the updater from the RNN below,
   // through identity components; nullptrs: pack)
   bool PackedOutput(const void **rows, const void **cols) const;
-  void SetPackedInput(const void *rows, const void *cols) const { in_rows_ = rows; in_cols_ = cols; }
+  void SetPackedInput(const void *rows, const void *cols) const {
+    in_rows_ = rows;
+    in_cols_ = cols;
+    in_tn_[0] = in_tn_[1] = -1;  // bound to a shape by the next Propagate
+  }
+  // the component below changed (Nnet::SetComponent): its packed output is gone
+  void ClearPackedInput() const { SetPackedInput(nullptr, nullptr); }
 
  private:
   void Init(Rng &rng);
@@ -312,6 +321,10 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   mutable bool input_projected_ = false;  // set by the previous component's PropagateChained
   mutable float input_bound_ = 0.f;       // ditto: bound on |input| (0: unknown)
   mutable const void *in_rows_ = nullptr, *in_cols_ = nullptr;  // SetPackedInput
+  mutable int in_tn_[2] = {-1, -1};  // (T, N) of the Propagate that read in_rows_ / in_cols_
+  const void *packed_input_cols(int T, int N) const {  // Backprop: only for the pass they were set for
+    return in_tn_[0] == T && in_tn_[1] == N ? in_cols_ : nullptr;
+  }
   unsigned *err_ = nullptr;
   mutable unsigned *err_ext_ = nullptr;
   void Forward(const CuMatrixBase &in, CuMatrixBase *out, RnnFwdChain *chain) const;

@@ -17,6 +17,11 @@ struct RnnDesc {
   // products of the recurrences and gate GEMMs: 0 fp32-class (split-fp16
   // pairs, fp32 accumulation), 1 bf16 (fp32 accumulation, fp32 master weights)
   int prec = 0;
+  // bf16 only, latched by rnn_set_precision (not re-read per call: the reserve
+  // layout must not change between the size query, the forward and the
+  // backward): the recurrences write their GEMM operands packed (pk) and, one
+  // layer bidirectional, the forward its output too (pkio)
+  int pk = 1, pkio = 1;
   int nw() const { return rnn_nw(mode); }
   int din(int layer) const { return layer == 0 ? D : dirs * H; }
   // floats of one pseudo-layer block [W | R | bW | bR] of stacked layer `layer`
@@ -42,6 +47,9 @@ struct RnnReserveLayout {
   long pkyr, pkyc;
 };
 RnnReserveLayout rnn_reserve_layout(const RnnDesc &d, int T, int N);
+// set d.prec and latch the packed-operand switches (KCTC_BF16_DIRECT /
+// KCTC_BF16_IO, both on by default) into d.pk / d.pkio
+void rnn_set_precision(RnnDesc &d, int prec);
 size_t rnn_workspace_bytes(const RnnDesc &d, int T, int N);
 
 // CU budget of the persistent kernels.  A v6 recurrence needs

@@ -82,11 +82,12 @@ long RnnDesc::lin_offset(int p, int lin, bool bias) const {
 }
 
 static long al64(long x) { return (x + 63) / 64 * 64; }
-// bf16_direct's switch (KCTC_BF16_DIRECT, on by default), for the reserve
-// layout defined before the helpers below
-static bool bf16_direct_env() {
+void rnn_set_precision(RnnDesc &d, int prec) {
+  d.prec = prec;
   const char *e = getenv("KCTC_BF16_DIRECT");
-  return !e || atoi(e) != 0;
+  d.pk = !e || atoi(e) != 0;
+  e = getenv("KCTC_BF16_IO");
+  d.pkio = !e || atoi(e) != 0;
 }
 
 RnnReserveLayout rnn_reserve_layout(const RnnDesc &d, int T, int N) {
@@ -101,7 +102,7 @@ RnnReserveLayout rnn_reserve_layout(const RnnDesc &d, int T, int N) {
   r.out = p;  p += (d.layers > 1) ? al64(TN * dirs * H) : 0;
   r.dout = p; p += (d.layers > 1) ? al64(TN * dirs * H) : 0;
   r.kbt64 = (TN + 63) / 64 * 64;
-  const bool pkd = d.prec == 1 /* kPrecBf16 */ && d.layers == 1 && bf16_direct_env();  // bf16 halves: 2 per float
+  const bool pkd = d.prec == 1 /* kPrecBf16 */ && d.layers == 1 && d.pk;  // bf16 halves: 2 per float
   const long G4 = nw * H, kbg64 = (G4 + 63) / 64 * 64;
   r.pkxr = p; p += pkd ? al64((dirs * TN * kbg64 + 1) / 2) : 0;
   r.pkxt = p; p += pkd ? al64((dirs * G4 * r.kbt64 + 1) / 2) : 0;
@@ -219,15 +220,13 @@ int env_int(const char *name, int dflt);
 // (one-layer descriptors -- the recipe's components; a stacked descriptor's
 // weight gradients measured wrong with it, so those keep the pack path)
 static bool bf16_direct(const RnnDesc &d, int ver) {
-  return d.prec == 1 /* kPrecBf16 */ && ver == 6 && (d.nw() * d.H) % 64 == 0 && d.layers == 1 &&
-         env_int("KCTC_BF16_DIRECT", 1);
+  return d.prec == 1 /* kPrecBf16 */ && ver == 6 && (d.nw() * d.H) % 64 == 0 && d.layers == 1 && d.pk;
 }
 // ... and, one-layer bidirectional, the forward writes its output packed
 // (RecParams::yr / yc) and the backward E^T shifted (eshift); H % 32 == 0 so
 // that a workgroup's units fill whole 16-B row chunks
 static bool bf16_io(const RnnDesc &d) {
-  return bf16_direct(d, 6) && d.layers == 1 && d.dirs == 2 && d.H % 32 == 0 && (2 * d.H) % 64 == 0 &&
-         env_int("KCTC_BF16_IO", 1);
+  return bf16_direct(d, 6) && d.layers == 1 && d.dirs == 2 && d.H % 32 == 0 && (2 * d.H) % 64 == 0 && d.pkio;
 }
 
 
@@ -3344,7 +3343,12 @@ struct RegWord {
   unsigned expected = 0;     // host: registrations once every enqueued launch is resident
 };
 RegWord g_reg[64];
-bool g_comm_gated = false;
+int g_comm_gated[64] = {0};  // per device: live gated exchanges (at most one, GatedExchange)
+int current_device() {
+  int dev = 0;
+  KCTC_HIP_CHECK(hipGetDevice(&dev));
+  return dev & 63;
+}
 RegWord &reg_of_device() {
   int dev = 0;
   KCTC_HIP_CHECK(hipGetDevice(&dev));
@@ -3383,8 +3387,11 @@ unsigned rnn_comm_gate_errors() {
   KCTC_HIP_CHECK(hipMemcpy(&h, r.word + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
   return h;
 }
-void rnn_set_comm_gated(bool on) { g_comm_gated = on; }
-bool rnn_comm_gated() { return g_comm_gated; }
+void rnn_set_comm_gated(bool on) {
+  int &c = g_comm_gated[current_device()];
+  c = on ? c + 1 : std::max(0, c - 1);
+}
+bool rnn_comm_gated() { return g_comm_gated[current_device()] > 0; }
 
 bool rnn_packed_output(const RnnDesc &d, int T, int N, void *reserve, const void **rows, const void **cols) {
   *rows = *cols = nullptr;

@@ -43,7 +43,7 @@ int krnnSetPrecision(krnnDescriptor_t desc, int precision) {
   if (!desc || (precision != KRNN_PREC_FP32 && precision != KRNN_PREC_BF16)) return KRNN_STATUS_BAD_PARAM;
   if (precision == KRNN_PREC_BF16 && desc->desc.mode != kctc::kLstm && desc->desc.mode != kctc::kGru)
     return KRNN_STATUS_NOT_SUPPORTED;
-  desc->desc.prec = precision;
+  kctc::rnn_set_precision(desc->desc, precision);
   return KRNN_STATUS_SUCCESS;
 }
 

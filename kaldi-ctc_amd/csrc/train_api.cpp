@@ -66,14 +66,20 @@ class GatedExchange : public kctc::nnet2::GradExchange {
   GatedExchange(hipStream_t compute, int comm_cus) : compute_(compute) {
     const char *e = getenv("KCTC_COMM_GATE");
     gated_ = !(e && *e == '0');
+    // the gate waits on the device's registration word, which every network's
+    // backward recurrences add to: two gated exchanges on one device would
+    // wait on each other's recurrences
+    if (gated_ && kctc::rnn_comm_gated())
+      throw std::runtime_error("a gated gradient exchange is already active on this device (one data-parallel "
+                               "network per device and process; KCTC_COMM_GATE=0 lifts the limit)");
     kctc::rnn_set_cu_budget(kctc_usable_cus_override(), comm_cus);
-    kctc::rnn_set_comm_gated(gated_);
+    if (gated_) kctc::rnn_set_comm_gated(true);
     KCTC_HIP_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
     KCTC_HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
   }
   ~GatedExchange() override {
     kctc::rnn_set_cu_budget(kctc_usable_cus_override(), 0);
-    kctc::rnn_set_comm_gated(false);
+    if (gated_) kctc::rnn_set_comm_gated(false);
     (void)hipStreamSynchronize(comm_stream_);
     (void)hipStreamDestroy(comm_stream_);
     (void)hipEventDestroy(done_);
@@ -707,6 +713,8 @@ int kctc_nnet_enable_dp_host(kctcNnet_t n, kctc_host_allreduce_fn fn, void *user
     KCTC_REQUIRE(n->trainer.Pending() == 0, "kctc_nnet_enable_dp_host with minibatches in flight");
     n->activate();
     delete n->dp;
+    n->dp = nullptr;
+    n->trainer.SetExchange(nullptr);
     n->dp = new HostExchange(fn, user, world_size, n->stream);
     n->trainer.SetExchange(n->dp_average ? nullptr : n->dp);
   });

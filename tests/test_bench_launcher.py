@@ -38,7 +38,7 @@ def test_device_map():
 
 def test_args_defaults():
     a = bench.parse_args([])
-    assert (a.gpus, a.steps, a.warmup, a.config, a.dp_transport) == (1, 20, 3, 1, "rccl")
+    assert (a.gpus, a.steps, a.warmup, a.config, a.dp_transport) == (1, 100, 3, 1, "rccl")
     a = bench.parse_args(["--gpus", "2", "--dp-transport", "host"])
     assert (a.gpus, a.dp_transport) == (2, "host")
 

@@ -355,3 +355,49 @@ def test_nnet_component_get_set_and_average(kctc, gpu):
     for n in nets + [a, b]:
         n.close()
     comp.close()
+
+
+def test_average_models_normalises_weights(kctc, gpu):
+    """GetWeights (nnet-am-average.cc:45-53) divides the weights by their sum:
+    2:1 averages as 2/3 : 1/3; a weight list of the wrong length is refused."""
+    cfg = kctc.recipe_config(num_rnn=1, input_dim=16, hidden=32, num_targets=9)
+    nets = [kctc.Nnet(cfg, seed=s) for s in (4, 5)]
+    upd = [c for c in range(nets[0].num_components) if nets[0].num_params(c) > 0]
+    params = [[n.get_params(c).astype(np.float64) for c in upd] for n in nets]
+    kctc.average_models(nets, [2.0, 1.0])
+    for k, c in enumerate(upd):
+        ref = 2.0 / 3.0 * params[0][k] + 1.0 / 3.0 * params[1][k]
+        np.testing.assert_allclose(nets[0].get_params(c), ref, rtol=1e-5, atol=1e-7)
+    with pytest.raises(ValueError):
+        kctc.average_models(nets, [1.0])
+    with pytest.raises(kctc.KctcError):
+        kctc.average_models(nets, [1.0, -1.0])
+    for n in nets:
+        n.close()
+
+
+def test_gradient_outlives_backprop_handle(kctc, gpu):
+    """Kaldi's gradient-check order: Backprop into a SetZero(true) copy, destroy
+    the component that ran Backprop, then DotProduct / Add on the gradient --
+    the gradient must not wait on the destroyed handle's stream."""
+    import torch
+    line = ("CuDNNRecurrentComponent input-dim=24 output-dim=32 bidirectional=true max-seq-length=50 "
+            "learning-rate=0.0005 rnn-mode=2 num-layers=1 param-stddev=0.02 bias-stddev=0.2")
+    comp = kctc.Component(line, seed=3)
+    T, N = 10, 3
+    g = torch.Generator(device=gpu)
+    g.manual_seed(9)
+    inp = torch.randn((T * N, 24), generator=g, device=gpu)
+    out = comp.Propagate(T, N, inp)
+    dy = torch.randn(out.shape, generator=g, device=gpu)
+    grad = comp.Copy()
+    grad.SetZero(True)
+    comp.Backprop(T, N, inp, out, dy, grad, None)
+    ref = comp.Copy()
+    comp.close()  # its stream is gone
+    d1 = grad.DotProduct(grad)
+    assert np.isfinite(d1) and d1 > 0
+    ref.Add(1.0, grad)
+    assert np.isfinite(ref.DotProduct(grad))
+    grad.close()
+    ref.close()
