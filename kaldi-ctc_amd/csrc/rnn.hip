@@ -304,10 +304,8 @@ struct RecParams {
   int fcopy;        // v6 forward, XCD-pinned: h images also written through (sc1) per step for a streamed projection
   float *xch;       // v4: per-step exchange images [T][dirs][KG][Npad][16] (workspace)
   int poll_sleep;   // v6: s_sleep between flag polls
-  int nopf;         // diagnostic (KCTC_DIAG_NOPF): skip the operand prefetch (wrong results)
   int gla;          // v6 forward IO waves: steps ahead the G rows are fetched (3 or 7; 8 LDS slots)
   int e_sc1;        // v6 backward: dGates rows written through (sc1) for a streaming consumer
-  int wwait;        // v6: per-wave waits on the producers a wave reads (else wave 0 waits for all)
   int bfpart;       // v6 backward, bf16 mode: partial dh exchanged as bf16 (KCTC_BF16_PARTIALS)
   unsigned *cmax;   // v6 backward: column max |DX| [dirs * nW * H] (GRU: then |E|), as float bits
   unsigned *reg;    // v6 backward: per-device registration word (+1 per workgroup at start)
@@ -334,6 +332,12 @@ struct RecParams {
   unsigned gid;
   int gmt, ggx;
   int gplain;  // diagnostic (KCTC_GATE_PLAIN): the gated G rows fetched without sc1
+  // v6 backward, fp32 partials, ring of 2: self-tagged hand-off (see
+  // rnn_bwd_rec6): the consumers poll the partial-dh words themselves instead
+  // of the producers' epoch flags; taken by the slots probe6 finds XCD-local
+  // (v6 forward, split-fp16 without IO waves: the same for the h hi / lo
+  // halves, each carrying the tag in its LSB)
+  int dtag;
 };
 
 // Phase stamps of the first kTraceSteps steps ([steps][grid][16]; thread 0 of every workgroup;
@@ -342,10 +346,16 @@ struct RecParams {
 // 3 MFMA + K reduction done, 4 published (+ flag), 5 step end.
 // v6 backward: slots 16 + w flags seen by wave w, 24 + w its hand-off loads landed.
 constexpr int kTraceSteps = 256, kTraceStride = 32;
+// (the cursor trc_ / trg_ of REC_TRACE_INIT lives in VGPRs: the stamps cost
+// the step loop no scalar registers)
+#define REC_TRACE_INIT                                                                    \
+  unsigned long long *trc_ = p.trace ? p.trace + (long)blockIdx.x * kTraceStride : nullptr; \
+  long trg_ = (long)gridDim.x * kTraceStride;                                             \
+  asm volatile("" : "+v"(trc_), "+v"(trg_))
 #define REC_TRACE(kk, ph)                                                                 \
   do {                                                                                    \
-    if (p.trace && threadIdx.x == 0 && (kk) < kTraceSteps) {                              \
-      unsigned long long *tr_ = p.trace + ((long)(kk) * gridDim.x + blockIdx.x) * kTraceStride; \
+    if (trc_ && threadIdx.x == 0 && (kk) < kTraceSteps) {                                 \
+      unsigned long long *tr_ = trc_ + (long)(kk) * trg_;                                 \
       tr_[(ph)] = __builtin_amdgcn_s_memrealtime();                                       \
       if ((ph) == 2 || (ph) == 3) tr_[12 + (ph)] = __builtin_amdgcn_s_memtime();          \
     }                                                                                     \
@@ -354,9 +364,8 @@ constexpr int kTraceSteps = 256, kTraceStride = 32;
 // slots 14/15: shader-clock counter (s_memtime) at phases 2/3 (clock estimate)
 #define REC_TRACE_W(kk, ph)                                                               \
   do {                                                                                    \
-    if (p.trace && (threadIdx.x & 63) == 0 && (kk) < kTraceSteps)                         \
-      p.trace[((long)(kk) * gridDim.x + blockIdx.x) * kTraceStride + (ph) + (threadIdx.x >> 6)] = \
-          __builtin_amdgcn_s_memrealtime();                                               \
+    if (trc_ && (threadIdx.x & 63) == 0 && (kk) < kTraceSteps)                            \
+      trc_[(long)(kk) * trg_ + (ph) + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 // Hand-off protocols (selected per launch; both placement-independent):
@@ -493,6 +502,7 @@ __device__ __forceinline__ void settle_all(u32x4 (&af)[RT][CH], __amdgpu_buffer_
 // ---------------------------------------------------------------------------
 template <int MODE, int RT>
 __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec(RecParams p) {
+  REC_TRACE_INIT;
   constexpr int NW = MODE == kLstm ? 4 : MODE == kGru ? 3 : 1;
   constexpr int CH = 32 / RT;  // k-groups per wave per pass (<= 32 A-fragment registers x4)
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -653,6 +663,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec(RecParams p) {
 // ---------------------------------------------------------------------------
 template <int MODE, int RT>
 __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec(RecParams p) {
+  REC_TRACE_INIT;
   constexpr int NW = MODE == kLstm ? 4 : MODE == kGru ? 3 : 1;
   constexpr int CH = 32 / RT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1025,6 +1036,7 @@ __device__ __forceinline__ void bwd_step_generic(floatx4 (&acc)[RT], __amdgpu_bu
 // them: a wave's vector memory operations complete in issue order.
 template <int MODE, int RT>
 __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
+  REC_TRACE_INIT;
   constexpr int NW = MODE == kLstm ? 4 : MODE == kGru ? 3 : 1;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int bad_lds, loc_lds;
@@ -1196,6 +1208,7 @@ __global__ __launch_bounds__(NT, 1) void rnn_fwd_rec4(RecParams p) {
 
 template <int MODE, int RT>
 __global__ __launch_bounds__(NT, 1) void rnn_bwd_rec4(RecParams p) {
+  REC_TRACE_INIT;
   constexpr int NW = MODE == kLstm ? 4 : MODE == kGru ? 3 : 1;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int bad_lds, loc_lds;
@@ -1486,7 +1499,7 @@ __device__ __forceinline__ void wait_flags6(const unsigned *f0, int nwg, unsigne
   __syncthreads();
   if (*bad_lds) bad = 1;
 }
-// Per-wave wait (KCTC_FWD_WWAIT / KCTC_BWD_WWAIT): a wave waits only for the
+// Per-wave wait (the forward's flagged hand-off): a wave waits only for the
 // producers whose rows IT loads -- lane j polls producer prod (-1: none) --
 // and goes on to its own loads and MFMAs while the other waves still wait, so
 // the hand-off of the last producer to publish costs only the loads of the
@@ -1608,6 +1621,7 @@ __device__ __forceinline__ void split16(float x, _Float16 &hi, _Float16 &lo) {
 // block, no scaling; partial dh stay fp32).
 template <int MODE, int U, int H, int NTH, int P>
 __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
+  REC_TRACE_INIT;
   constexpr int NW = MODE == kLstm ? 4 : 3;
   constexpr int NWV = NTH / 64;
   constexpr int K = NW * U, KB = (K + 31) / 32, AP = KB * 32 + 8;  // A image row pitch (halves)
@@ -1665,9 +1679,13 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   if (tid == 0) bad_lds = 0;
   for (int i = tid; i < (BF ? 16 : 32) * AP; i += NTH) Ahi[i] = (AT)0.f;  // the image(s), padding included
   // ---- R slice -> B fragments in registers (x3: scaled hi/lo; bf16: as is) ----
+  // K order of the dGates operand: split-fp16 paths unit-major (k = u NW + q:
+  // an element's NW gates are adjacent halves, one 8-B LDS write per part),
+  // bf16 gate-major (k = q U + u)
+  constexpr bool KUM = !BF;
   auto rval = [&](int kk, int col) -> float {
     if (kk >= K) return 0.f;
-    const int q = kk / U, u = kk - q * U;
+    const int q = KUM ? kk % NW : kk / U, u = KUM ? kk / NW : kk - (kk / U) * U;
     return R[(long)(q * H + u0 + u) * H + col];
   };
   int sB = 0;
@@ -1762,18 +1780,23 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   };
 #pragma unroll
   for (int q = 0; q < NW; q++) bsx[q] = bsh[q] = dxk[q] = eg[q] = cg[q] = ng[q] = cmx[q] = cme[q] = 0.f;
+  // this element's operand columns as per-lane pointers, opaque to the
+  // compiler: they stay in VGPRs and the kernel-argument bases die here
+  // (the loop's scalar registers spill otherwise)
+  const float *dy_e = p.dy + (long)n * ldy + (long)d * H + u0 + eu;
+  const float *g_e = p.G + (long)n * ldg + (long)d * NW * H + u0 + eu;
+  const float *aux_e = p.aux + (long)n * ldy + (long)d * H + u0 + eu;
+  const float *prv_e = (MODE == kLstm ? p.aux : p.y) + (long)n * ldy + (long)d * H + u0 + eu;
+  asm volatile("" : "+v"(dy_e), "+v"(g_e), "+v"(aux_e), "+v"(prv_e));
   auto prefetch = [&](int k) {  // operands of forward-order step k into n*
     if (!live) return;
     const int t = d == 0 ? k : T - 1 - k, tp = d == 0 ? t - 1 : t + 1;
-    const long yrow = ((long)t * N + n) * ldy + (long)d * H + u0 + eu;
-    const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + eu;
-    const long prow = ((long)tp * N + n) * ldy + (long)d * H + u0 + eu;
-    ndy = p.dy[yrow];
+    const long yo = (long)t * N * ldy, go = (long)t * N * ldg, po = (long)tp * N * ldy;
+    ndy = dy_e[yo];
 #pragma unroll
-    for (int q = 0; q < NW; q++) ng[q] = p.G[grow + q * H];
-    na = p.aux[yrow];
-    if (MODE == kLstm) nap = k > 0 ? p.aux[prow] : 0.f;
-    else nap = k > 0 ? p.y[prow] : 0.f;
+    for (int q = 0; q < NW; q++) ng[q] = g_e[go + q * H];
+    na = aux_e[yo];
+    nap = k > 0 ? prv_e[po] : 0.f;
   };
   auto rotate = [&]() {
     cdy = ndy; ca = na; cap = nap;
@@ -1853,19 +1876,14 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   const long coff = (long)grp * xgrp + (long)d * NWG * PSTR + ((long)ct_own * 64 + pln) * LW + (long)pg * PSTR;
   // a C-fragment lane holds rows 4 (lane / 16) .. +3 of the group: quads past N
   // are neither stored nor loaded (a group of fewer than 16 sequences moves
-  // only its own rows)
-  const bool crow_live = n0 + 4 * ((pln & 63) >> 4) < nend;
-  const bool prow_live = n0 + 4 * fq < nend;
-  // per-wave wait: the producers of the groups this wave's threads sum
-  int wprod = -1;
-  {
-    const int pgA = (tid & ~63) / POS, pgB = min(NGRP - 1, ((tid & ~63) + 63) / POS);
-    const int gi = lane / PER, i = lane - gi * PER;
-    if (pgA + gi <= pgB) wprod = pgA + gi + i * NGRP;
-  }
+  // only its own rows).  STK (transposed, U = 16): chunk j = 8 (unit / 4) +
+  // row of a tile holds units 4 (j / 8) .. +3 of row j % 8, chunks 32..63 unused
+  const bool crow_live = STK ? (pln < 32 && n0 + (pln & 7) < nend) : n0 + 4 * ((pln & 63) >> 4) < nend;
+  const bool prow_live = STK ? (fr < 8 && n0 + fr < nend) : n0 + 4 * fq < nend;
   // where element (en, eu) finds its sum: own tile eu / 16, lane (en / 4) * 16
   // + (eu % 16) (U = 8: compacted to 8 per row quad), register en % 4
-  const int epos = (eu >> 4) * 64 + (en >> 2) * (U < 16 ? U : 16) + (eu & 15);
+  const int epos = STK ? (eu >> 2) * 8 + en : (eu >> 4) * 64 + (en >> 2) * (U < 16 ? U : 16) + (eu & 15);
+  const int ereg = STK ? (eu & 3) : (en & 3);
   prefetch(T - 1);
   rotate();
   if constexpr (PRE) coef();
@@ -1883,14 +1901,27 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   if (p.xpd && tid == 0) atomicOr(p.flags + kXcdWord, 1u << xcc_id());
   if (tid == 0) loc_lds = 0;
   const int local = (p.xpd && p.allow_local) ? probe6(p, grp, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
-  if (p.trace && tid == 0) p.trace[(long)blockIdx.x * kTraceStride + 9] = (unsigned long long)(local + 1);  // step 0, slot 9
+  if (trc_ && tid == 0) trc_[9] = (unsigned long long)(local + 1);  // step 0, slot 9
+  // Self-tagged hand-off (fp32 partials, XCD-local slot, ring of two step
+  // images set to tag 1 before the launch): the producer's partial-dh words
+  // carry ((step >> 1) & 1) in their LSB, the consumers re-load a chunk until
+  // all its words carry the step's tag.  No per-step drain, signal barrier,
+  // flag store or flag poll -- the poll IS the payload load.  Ring safety as
+  // before: a producer writes slot ks % 2 only after it has read every
+  // consumer's step ks - 1 words, stored after that consumer's loads of step
+  // ks - 2 had returned.
+  const bool dtag = !BF && p.dtag && local && p.ring == 2;
   // step t's DX rows for a streaming consumer on other XCDs, from the LDS
   // stage: written through (sc1) as whole 16-B chunks, 4 lanes per
   // contiguous 64-B run (4-B write-through stores per element cost ~8 us per
   // step); the next signal drains them, so they are complete at epoch t + 3
   auto e_sc1_store = [&](int tt) {
     constexpr int CPR = NW * U / 4;  // chunks per row
-    const int rn = tid / CPR, c = tid - rn * CPR;
+    // self-tagged (issued after the first barrier): the LAST 16 CPR threads,
+    // i.e. the waves past the element waves when there are any, store while
+    // the element waves do the cell
+    const int et = dtag ? tid - (NTH - 16 * CPR) : tid;
+    const int rn = et >= 0 ? et / CPR : 16, c = et - rn * CPR;
     if (rn < 16 && n0 + rn < nend) {
       const int q = (c * 4) / U, u = (c * 4) % U;
       const u32x4 v = *reinterpret_cast<const u32x4 *>(estg + rn * NW * U + c * 4);
@@ -1904,14 +1935,14 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
     const int ks = T - 1 - k;  // steps done before this one
     REC_TRACE(ks, 0);
     if (ks > 0) {
-      if (p.wwait) {
-        if (!wave_wait_prod(flag6(p, grp, d, 0, NWG), wprod, (unsigned)(ks + 1), p.err, &bad_lds, p.poll_sleep)) bad = 1;
+      if (dtag) {
+        // self-tagged: no flags; the poll below is the wait
       } else {
         wait_flags6(flag6(p, grp, d, 0, NWG), NWG, (unsigned)(ks + 1), p.err, bad, &bad_lds, p.poll_sleep);
       }
       REC_TRACE(ks, 1);
       REC_TRACE_W(ks, 16);
-      const auto rs = rsrc(p.xch + (long)(p.ring ? (ks - 1) % p.ring : ks - 1) * xstep, (unsigned)(xstep * 4));
+      const auto rs = rsrc(p.xch + (long)(p.ring ? (ks - 1) & 1 : ks - 1) * xstep, (unsigned)(xstep * 4));  // (ring: 2 images)
       floatx4 sm = floatx4{0.f, 0.f, 0.f, 0.f};
       if (bfp) {
         typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
@@ -1934,13 +1965,46 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
         }
       } else {
         u32x4 v[PER];
+        // unconditional loads (a dead row quad at an offset past the buffer:
+        // the hardware returns zeros), so that the compiler counts them
+        // exactly and the coefficients below overlap them
+        auto hoff = [&](int i) { return crow_live ? (unsigned)((coff + (long)i * NGRP * PSTR) * 4) : 0x7fff0000u; };
 #pragma unroll
-        for (int i = 0; i < PER; i++)
-          v[i] = crow_live ? ld_sc1(rs, (unsigned)((coff + (long)i * NGRP * PSTR) * 4)) : u32x4{0u, 0u, 0u, 0u};
+        for (int i = 0; i < PER; i++) v[i] = ld_sc1(rs, hoff(i));
         if constexpr (PRE) {
           __builtin_amdgcn_sched_barrier(0);
           coef();  // while the hand-off loads are in flight
+          // (pinned here: IR passes had sunk the coefficients past the loads' wait)
+#pragma unroll
+          for (int q = 0; q < 6; q++) asm volatile("" : "+v"(kc[q]));
           __builtin_amdgcn_sched_barrier(0);
+        }
+        if (dtag) {
+          // every word of step ks - 1 carries tag ((ks - 1) >> 1) & 1 in its
+          // LSB; a chunk still holding step ks - 3's words (the other tag) is
+          // loaded again.  4-B words are single-copy atomic, so a 16-B load
+          // that tears between the two steps is caught word by word.
+          const unsigned want = (unsigned)((ks - 1) >> 1) & 1u;
+          auto ready = [&]() {
+            unsigned bad4 = 0u;
+#pragma unroll
+            for (int i = 0; i < PER; i++) bad4 |= (v[i][0] ^ want) | (v[i][1] ^ want) | (v[i][2] ^ want) | (v[i][3] ^ want);
+            return !crow_live || (bad4 & 1u) == 0u;
+          };
+          int spins = 0;
+          while (!__all(ready())) {  // (not all there yet: the wave loads all its chunks again)
+            if (++spins > kSpinLimit ||
+                ((spins & 255) == 0 &&
+                 __builtin_amdgcn_readfirstlane(__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))) {
+              bad = 1;
+              if (lane == 0) bad_lds = 1;
+              break;
+            }
+            if (p.poll_sleep) __builtin_amdgcn_s_sleep(1);
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int i = 0; i < PER; i++) v[i] = ld_sc1(rs, hoff(i));
+          }
         }
         sm = __builtin_bit_cast(floatx4, v[0]);
 #pragma unroll
@@ -1954,21 +2018,35 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
       // and the epoch the last signal drained (step ks - 2's rows).  Issued
       // after the signal instead, they were still in flight at the next flag
       // poll, which waits for every older store (one vmcnt for loads and stores)
-      if (p.e_sc1) e_sc1_store(t_prev);
+      // (self-tagged: after the barrier below, which orders it behind the
+      // previous step's book() writes of estg -- no signal barrier in between)
+      if (p.e_sc1 && !dtag) e_sc1_store(t_prev);
     }
     asm volatile("" ::: "memory");
     // behind the hand-off loads: next step's operands, last step's row-major dGates
-    if (t_prev >= 0 && !(p.nopf & 2)) e_store(t_prev);
-    if (k > 0 && !(p.nopf & 1)) prefetch(k - 1);
+    if (t_prev >= 0) e_store(t_prev);
+    if (k > 0) prefetch(k - 1);
     __syncthreads();
     REC_TRACE(ks, 8);
     if (bad_lds) bad = 1;
-    if (gflag && ks > 0 && tid == 0) __hip_atomic_store(gflag, (unsigned)(ks + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // self-tagged: every producer's words of step ks - 1 were stored after its
+    // poll of step ks - 2 had retired (in-order vmcnt) its write-through rows
+    // of step ks - 3 -> epoch ks (rows of step k out at epoch k + 3);
+    // flagged: its signal of step ks - 1 drained the rows of step ks - 2
+    if (gflag && ks > 0 && tid == 0)
+      __hip_atomic_store(gflag, (unsigned)(dtag ? ks : ks + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (dtag && p.e_sc1 && ks > 0) e_sc1_store(t_prev);
     if (has_e) {
       float dhr = 0.f;
       if (ks > 0) {
+        // all NGRP reads in flight before the first add (one LDS latency,
+        // not NGRP), then the fixed-order sum
+        float rr[NGRP];
 #pragma unroll
-        for (int gg = 0; gg < NGRP; gg++) dhr += red[(long)(gg * POS + epos) * 4 + (en & 3)];
+        for (int gg = 0; gg < NGRP; gg++) rr[gg] = red[(long)(gg * POS + epos) * 4 + ereg];
+        __builtin_amdgcn_sched_group_barrier(0x100, NGRP, 0);
+#pragma unroll
+        for (int gg = 0; gg < NGRP; gg++) dhr += rr[gg];
       }
       float dh = cdy + dhr;
       if constexpr (PRE) {
@@ -2015,23 +2093,26 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
         for (int q = 0; q < NW; q++) Ahi[en * AP + q * U + eu] = (__bf16)eg[q];
       } else {
         const int se = split_exp(group_maxU(m, U));
-        if constexpr (STK) {  // rows en < 8 only: lo parts go to rows en + 8
-          if (en < 8) {
+        // unit-major K: the element's NW gates are halves eu NW .. eu NW + NW - 1
+        // of its row (STK: hi in row en < 8, lo in row en + 8)
+        _Float16 hh[4], hl[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) hh[q] = hl[q] = (_Float16)0.f;
+#pragma unroll
+        for (int q = 0; q < NW; q++) split16(ldexpf(eg[q], se), hh[q], hl[q]);
+        _Float16 *dhi = Ahi + en * AP + eu * NW;
+        _Float16 *dlo = STK ? Ahi + (en + 8) * AP + eu * NW : Alo + en * AP + eu * NW;
+        if (!STK || en < 8) {
+          if constexpr (NW == 4) {
+            typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<half4 *>(dhi) = half4{hh[0], hh[1], hh[2], hh[3]};
+            *reinterpret_cast<half4 *>(dlo) = half4{hl[0], hl[1], hl[2], hl[3]};
+          } else {
 #pragma unroll
             for (int q = 0; q < NW; q++) {
-              _Float16 h, l;
-              split16(ldexpf(eg[q], se), h, l);
-              Ahi[en * AP + q * U + eu] = h;
-              Ahi[(en + 8) * AP + q * U + eu] = l;
+              dhi[q] = hh[q];
+              dlo[q] = hl[q];
             }
-          }
-        } else {
-#pragma unroll
-          for (int q = 0; q < NW; q++) {
-            _Float16 h, l;
-            split16(ldexpf(eg[q], se), h, l);
-            Ahi[en * AP + q * U + eu] = h;
-            Alo[en * AP + q * U + eu] = l;
           }
         }
         if (eu == 0) rowexp[en] = se + sB;
@@ -2051,10 +2132,12 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
 #pragma unroll
           for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bhi[c][kb], acc[c], 0, 0, 0);
         } else if constexpr (STK) {
+          // transposed: C^T[unit][row'] = R_slice^T dG^T, row' < 8 hi, >= 8 lo
+          // (the R fragments as the A operand: same registers, A[unit][k])
 #pragma unroll
-          for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bhi[c][kb], acc[c], 0, 0, 0);
+          for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bhi[c][kb], ah, acc[c], 0, 0, 0);
 #pragma unroll
-          for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, blo[c][kb], acc[c], 0, 0, 0);
+          for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(blo[c][kb], ah, acc[c], 0, 0, 0);
         } else {
           const AV al = *reinterpret_cast<const AV *>(Alo + fr * AP + kb * 32 + fq * 8);
 #pragma unroll
@@ -2065,29 +2148,42 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
           for (int c = 0; c < CTW; c++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bhi[c][kb], acc[c], 0, 0, 0);
         }
       }
-      if constexpr (STK) {  // rows 8..15 hold the lo parts' products: fold them into rows 0..7
+      if constexpr (STK) {  // columns 8..15 (lo rows) onto 0..7: one DPP add (row_ror:8) per register
 #pragma unroll
         for (int c = 0; c < CTW; c++)
 #pragma unroll
-          for (int i = 0; i < 4; i++) acc[c][i] = fold_rows8(acc[c][i]);
+          for (int i = 0; i < 4; i++)  // (mov_dpp with bound_ctrl: combined into one v_add_f32_dpp)
+            acc[c][i] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(acc[c][i]), 0x128, 0xF, 0xF, true));
       }
       int ex[4] = {0, 0, 0, 0};
-      if constexpr (!BF) {
+      if constexpr (STK) {
+        const int e1 = -rowexp[fr & 7];  // one row per lane
 #pragma unroll
-        for (int i = 0; i < 4; i++) ex[i] = -rowexp[(fq & (STK ? 1 : 3)) * 4 + i];
+        for (int i = 0; i < 4; i++) ex[i] = e1;
+      } else if constexpr (!BF) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) ex[i] = -rowexp[fq * 4 + i];
       }
       // a ring of >= 2 images is safe: every workgroup is a consumer of every
       // producer, so before a producer writes slot ks % ring at step ks it saw
       // all flags of step ks - 1, i.e. every consumer had finished reading
       // that slot's previous contents (step ks - ring, read during ks - ring + 1)
-      const auto ro = rsrc(p.xch + (long)(p.ring ? ks % p.ring : ks) * xstep, (unsigned)(xstep * 4));
+      const auto ro = rsrc(p.xch + (long)(p.ring ? ks & 1 : ks) * xstep, (unsigned)(xstep * 4));
       const long obase = (long)grp * xgrp + (long)(d * NWG + g) * PSTR;
+      // fp32 partials carry the step tag ((ks >> 1) & 1) in their LSB in every
+      // mode (the self-tagged hand-off reads it; the others keep the same
+      // arithmetic, so that pinned and unpinned runs stay bit-identical)
+      const unsigned tg = (unsigned)(ks >> 1) & 1u;
 #pragma unroll
       for (int c = 0; c < CTW; c++) {
         floatx4 o;
 #pragma unroll
-        for (int i = 0; i < 4; i++) o[i] = BF ? acc[c][i] : ldexpf(acc[c][i], ex[i]);
-        const int off = (int)((obase + ((long)(w * CTW + c) * 64 + lane) * LW) * 4);
+        for (int i = 0; i < 4; i++) {
+          o[i] = BF ? acc[c][i] : ldexpf(acc[c][i], ex[i]);
+          if (!bfp) o[i] = __uint_as_float((__float_as_uint(o[i]) & ~1u) | tg);
+        }
+        const int slot = STK ? (fq * 8 + (fr & 7)) : lane;  // STK: compact chunks of the 8 live columns
+        const int off = (int)((obase + ((long)(w * CTW + c) * 64 + slot) * LW) * 4);
         // local: plain stores keep the lines in the XCD's shared L2, where the
         // consumers' sc1 loads find them; else write-through (sc1)
         if (!prow_live) {
@@ -2113,12 +2209,13 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
       if (has_e) book();
     }
     REC_TRACE(ks, 7);
-    signal_epoch(myflag, (unsigned)(ks + 2), local);
+    if (!dtag) signal_epoch(myflag, (unsigned)(ks + 2), local);
     REC_TRACE(ks, 4);
     rotate();
     t_prev = t;
     REC_TRACE(ks, 5);
   }
+  if (dtag) __syncthreads();  // the last step's book() writes of estg, before e_sc1_store reads them
   if (t_prev >= 0 && !bad) e_store(t_prev);
   if (!bad) {
     if (p.e_sc1 && t_prev >= 0) e_sc1_store(t_prev);
@@ -2192,6 +2289,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
 // and multiplies by a bf16 R slice (one MFMA per block, no scaling).
 template <int MODE, int U, int H, int NTH, int P>
 __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
+  REC_TRACE_INIT;
   constexpr int NW = MODE == kLstm ? 4 : 3;
   constexpr int NWV = NTH / 64;
   // P & 4: IO waves.  The upper half of the waves neither waits for the
@@ -2504,8 +2602,15 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   if (GATE && p.gtf && tid == 0) st_u32_sc1(const_cast<unsigned *>(p.gtf) - 56 + xcc_id(), p.gid);
   if (tid == 0) loc_lds = 0;
   const int local = (p.xpd && p.allow_local) ? probe6(p, grp, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
-  if (p.trace && tid == 0) p.trace[(long)blockIdx.x * kTraceStride + 9] = (unsigned long long)(local + 1);  // step 0, slot 9
+  if (trc_ && tid == 0) trc_[9] = (unsigned long long)(local + 1);  // step 0, slot 9
   const long rbase = (long)T * XS;  // ring slots (p.ring > 0)
+  // Self-tagged hand-off (as rnn_bwd_rec6): every fp16 half of step k's h
+  // image carries ((k >> 1) & 1) in its LSB (hi's change is taken up by lo,
+  // lo's own LSB costs 2^-21 of |h| at most); the consumers poll the image
+  // words themselves: no drain, no flag.  Split-fp16 without IO waves, no
+  // write-through copy for a streamed projection, ring of two L2 images set
+  // to tag 1 before the launch.
+  const bool dtag = !BF && !IOW && !fcopy && p.dtag && local && p.ring == 2;
   // the published 16 B of h: live across the whole loop (used after it), so
   // that no other value of the step is allocated to the data registers of the
   // write-through copy still in flight (gfx9 waits for a store's completion
@@ -2537,15 +2642,16 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     for (int ct = 0; ct < CT; ct++) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
     REC_TRACE(k, 0);
     if (k > 0 && (!IOW || w < CW)) {
-      if (p.wwait || IOW) {
-        if (!wave_wait_prod(flag6(p, grp, d, 0, NWG), wprod, (unsigned)(k + 1), p.err, &bad_lds, p.poll_sleep)) bad = 1;
+      if (dtag) {
+        // self-tagged: the poll below is the wait
       } else {
-        wait_flags6(flag6(p, grp, d, 0, NWG), NWG, (unsigned)(k + 1), p.err, bad, &bad_lds, p.poll_sleep);
+        if (!wave_wait_prod(flag6(p, grp, d, 0, NWG), wprod, (unsigned)(k + 1), p.err, &bad_lds, p.poll_sleep)) bad = 1;
       }
       REC_TRACE(k, 1);
-      const auto rs = rsrc(xch + (p.ring ? rbase + (long)((k - 1) % p.ring) * XS : (long)tp * XS),
+      const auto rs = rsrc(xch + (p.ring ? rbase + (long)((k - 1) & 1) * XS : (long)tp * XS),
                            (unsigned)(XS * sizeof(AT)));
       u32x4 ah[KBW], al[KBW];
+      unsigned aoff[KBW];
       // unconditional loads (rows past N and k blocks past KB at an offset
       // past the buffer: the hardware returns zeros), so that the compiler
       // counts them exactly and the first MFMAs wait for their own loads only
@@ -2555,8 +2661,47 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
         const long o = STK ? gimg + ((((long)d * KB + kb) * NP + (fr >> 3)) * 16 + (fr & 7)) * 32 + fq * 8
                            : gimg + ((((long)d * KB + kb) * NP) * 16 + fr) * 32 + fq * 8;
         const unsigned off = (kb < KB && arow_live) ? (unsigned)(o * sizeof(AT)) : 0x7fff0000u;
+        aoff[i] = off;
         ah[i] = ld_sc1(rs, off);
         if constexpr (!BF && !STK) al[i] = ld_sc1(rs, off + 16 * 32 * sizeof(AT));
+      }
+      if constexpr (!BF) {
+        if (dtag) {
+          // every half of step k - 1 carries ((k - 1) >> 1) & 1 in its LSB
+          // (bits 0 and 16 of a word; 4-B words are single-copy atomic); a
+          // chunk still holding step k - 3's halves is loaded again
+          const unsigned want = ((unsigned)((k - 1) >> 1) & 1u) * 0x00010001u;
+          // (rows past N and k blocks past KB: zeros from past the buffer, no tag)
+          const bool any_live = arow_live && w < KB;
+          auto ready = [&]() {
+            unsigned bad4 = 0u;
+#pragma unroll
+            for (int i = 0; i < KBW; i++) {
+              if (w + CW * i < KB) {
+                bad4 |= (ah[i][0] ^ want) | (ah[i][1] ^ want) | (ah[i][2] ^ want) | (ah[i][3] ^ want);
+                if constexpr (!STK) bad4 |= (al[i][0] ^ want) | (al[i][1] ^ want) | (al[i][2] ^ want) | (al[i][3] ^ want);
+              }
+            }
+            return !any_live || (bad4 & 0x00010001u) == 0u;
+          };
+          int spins = 0;
+          while (!__all(ready())) {  // (not all there yet: the wave loads all its chunks again)
+            if (++spins > kSpinLimit ||
+                ((spins & 255) == 0 &&
+                 __builtin_amdgcn_readfirstlane(__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))) {
+              bad = 1;
+              if (lane == 0) bad_lds = 1;
+              break;
+            }
+            if (p.poll_sleep) __builtin_amdgcn_s_sleep(1);
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int i = 0; i < KBW; i++) {
+              ah[i] = ld_sc1(rs, aoff[i]);
+              if constexpr (!BF && !STK) al[i] = ld_sc1(rs, aoff[i] + 16 * 32 * sizeof(AT));
+            }
+          }
+        }
       }
       // all hand-off loads in flight before the first MFMA waits: without
       // this the scheduler (U = 32) issued the second k block's loads only
@@ -2601,10 +2746,10 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     }
     asm volatile("" ::: "memory");
     // behind the hand-off loads: last step's row-major outputs, next step's input projection
-    if (!IO_OUT && t_prev >= 0 && !(p.nopf & 2)) out_store(t_prev);
+    if (!IO_OUT && t_prev >= 0) out_store(t_prev);
     // (stg still holds step t_prev's h: the cell phase below rewrites it)
     if (BF && p.yr && t_prev >= 0) y_pk_store(t_prev);
-    if (!IOW && k + 1 < T && !(p.nopf & 1)) gin_load(d == 0 ? t + 1 : t - 1, gnx);
+    if (!IOW && k + 1 < T) gin_load(d == 0 ? t + 1 : t - 1, gnx);
     // K partials through LDS.  U % 16 == 0: column ct * 16 + fr of the
     // tile is gate ct / (U / 16) of unit (ct % (U / 16)) * 16 + fr, so a lane
     // holds every gate of its (row, unit) elements: one float4 per (wave,
@@ -2701,7 +2846,16 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
         stg[en * U + eu] = (__bf16)h;
       } else {
         _Float16 hh, hl;
-        split16(h * 16384.f, hh, hl);
+        if (!IOW) {  // hi's LSB := tag, lo takes up the change, then lo's LSB := tag
+          // (in every mode a self-tagged launch may take: pinned and unpinned
+          // runs stay bit-identical)
+          const unsigned short tgh = (unsigned short)((k >> 1) & 1);
+          const float x = h * 16384.f;
+          hh = __builtin_bit_cast(_Float16, (unsigned short)((__builtin_bit_cast(unsigned short, (_Float16)x) & 0xFFFEu) | tgh));
+          hl = __builtin_bit_cast(_Float16, (unsigned short)((__builtin_bit_cast(unsigned short, (_Float16)(x - (float)hh)) & 0xFFFEu) | tgh));
+        } else {
+          split16(h * 16384.f, hh, hl);
+        }
         stg[en * U + eu] = hh;
         stg[(16 + en) * U + eu] = hl;
       }
@@ -2713,7 +2867,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
       // barrier below last step -- then step k + 2's loads, then the
       // row-major outputs of step k - 1 (written before the last barrier;
       // their slot is rewritten after the next K-reduction barrier)
-      if (!(p.nopf & 1)) {
+      {
         // step k + gla's G into slot (k + gla) & 7 (gla <= 7: last read by the
         // cell threads of step k - 1 at the latest, before the last barrier),
         // then wait for step k + 1's: in place before the barrier below,
@@ -2722,23 +2876,12 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
         io_wait();
         gpd++;
       }
-      if ((p.nopf & 4) && io_live && k + 2 < T) {
-        // diagnostic (KCTC_DIAG_NOPF=5): the same G loads, never waited for
-        // (inline asm: the compiler does not count them) -- timing only
-        const int tt = d == 0 ? k + 2 : T - 3 - k;
-        const float *gp = p.G + ((long)tt * N + n0 + ion) * ldg + (long)d * NW * H + u0 + iou;
-#pragma unroll
-        for (int q = 0; q < NW; q++) {
-          float dummy;
-          asm volatile("global_load_dword %0, %1, off" : "=v"(dummy) : "v"(gp + q * H) : "memory");
-        }
-      }
-      if (IO_OUT && k > 0 && !(p.nopf & 2)) io_out(k - 1);
+      if (IO_OUT && k > 0) io_out(k - 1);
     }
     lds_barrier<IOW>();
     if (pub) {
       pv = *reinterpret_cast<const u32x4 *>(stg + (sp * 16 + sn) * U + sch * 8);
-      const auto ro = rsrc(xch + (p.ring ? rbase + (long)(k % p.ring) * XS : (long)t * XS), (unsigned)(XS * sizeof(AT)));
+      const auto ro = rsrc(xch + (p.ring ? rbase + (long)(k & 1) * XS : (long)t * XS), (unsigned)(XS * sizeof(AT)));
       // local: plain stores stay in the XCD's L2 for the consumers' sc1 loads
       if (local) __builtin_amdgcn_raw_buffer_store_b128(pv, ro, (int)(po * sizeof(AT)), 0, 0);
       else __builtin_amdgcn_raw_buffer_store_b128(pv, ro, (int)(po * sizeof(AT)), 0, 16);
@@ -2751,14 +2894,14 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
       // step all came before the barrier above, and the next writes of either
       // follow the next K-reduction barrier, which wave 0 reaches only after
       // its stg read
-      if (w == 0) {
+      if (w == 0 && !dtag) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) {
           if (local) __hip_atomic_store(myflag, (unsigned)(k + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           else __hip_atomic_store(myflag, (unsigned)(k + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
-    } else {
+    } else if (!dtag) {
       signal_epoch(myflag, (unsigned)(k + 2), local);
     }
     REC_TRACE(k, 4);
@@ -2872,7 +3015,7 @@ static void launch6_u(bool fwd, int nth, const RecParams &p, dim3 grid, size_t l
         // 2/3 of the MFMAs) runs 1.76 us/step against 2.05 for the IO-wave
         // forward, same box; backward off (2.53 vs 2.43: the fold's cross-lane
         // exchange).  KCTC_STK_FWD / KCTC_STK_BWD (or KCTC_STK for both)
-        const int stk = env_int(fwd ? "KCTC_STK_FWD" : "KCTC_STK_BWD", env_int("KCTC_STK", fwd ? 1 : 0));
+        const int stk = env_int(fwd ? "KCTC_STK_FWD" : "KCTC_STK_BWD", env_int("KCTC_STK", 1));
         if constexpr (P == kPrecX3) {
           if (p.gs <= 8 && stk) {
             // the stacked forward with IO waves (KCTC_STK_IOW=1, measuring)
@@ -3563,7 +3706,6 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.gs = ver == 6 ? c6.gs : 16;
     p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
     p.poll_sleep = env_int("KCTC_POLL_SLEEP", 1);
-    p.nopf = env_int("KCTC_DIAG_NOPF", 0);
     p.gla = env_int("KCTC_FWD_GLA", 3) == 7 && !gated ? 7 : 3;  // G rows fetched 3 or 7 steps ahead (IO waves)
     if (gated) {
       p.gtf = gdiag == 1 ? nullptr : gtf + 64;
@@ -3572,7 +3714,6 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       p.ggx = (NW * H + 255) / 256;
       p.gplain = env_int("KCTC_GATE_PLAIN", 0);
     }
-    p.wwait = env_int("KCTC_FWD_WWAIT", 1);  // measured: forward recurrence 29.7 -> 28.6 ms/step
     if (ver == 6 && bf16_io(d)) {  // the output also as packed bf16 rows and columns
       p.yr = reinterpret_cast<__bf16 *>(R0 + lay.pkyr);
       p.yc = reinterpret_cast<__bf16 *>(R0 + lay.pkyc);
@@ -3590,6 +3731,13 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       p.ring = p.xpd ? 2 : 0;
       p.fcopy = p.xpd && chained;
       p.allow_local = p.xpd ? env_int("KCTC_LOCAL", 1) : 0;
+      // self-tagged hand-off (the kernel takes it for split-fp16 without IO
+      // waves or a write-through copy): the ring's two images start at tag 1
+      p.dtag = d.prec != kPrecBf16 && p.ring == 2 && !p.fcopy && T >= 2 && env_int("KCTC_FWD_DTAG", 1);
+      if (p.dtag) {  // rnn_fwd_rec6's ring: after T step images of XS = 64 H rg halves (2 dirs, hi / lo, 16 rows)
+        const size_t xs = sizeof(_Float16) * 64 * (size_t)d.H * p.rg;
+        KCTC_HIP_CHECK(hipMemsetAsync(reinterpret_cast<char *>(p.xch) + xs * T, 0x01, 2 * xs, s));
+      }
     }
     const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : ver == 6 && p.xpd ? 8 * p.nwg : dirs * p.nwg * p.rg);
     RecTrace tr;
@@ -3851,17 +3999,16 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
       // step images (L2-resident).  configs[1]: 3.36 -> 2.70 us per step with
       // the streamed dx GEMM beside it (2.41 without), 468k -> 511k frames/s
       p.xpd = xcd_mask(d, N, false) ? 1 : 0;
-      p.ring = std::max(0, env_int("KCTC_BWD_RING", p.xpd ? 2 : 0));
-      if (p.ring == 1) p.ring = 2;
+      p.ring = p.xpd ? 2 : 0;
       p.allow_local = env_int("KCTC_LOCAL", 1);
       p.poll_sleep = env_int("KCTC_POLL_SLEEP", 1);
-      p.nopf = env_int("KCTC_DIAG_NOPF", 0);
-      // off: the backward's waves 0-3 still have the step's write-through
-      // dGates rows outstanding when they would poll (their first poll waits
-      // for them): measured 34.2 -> 35.4 ms/step with per-wave waits
-      p.wwait = env_int("KCTC_BWD_WWAIT", 0);
       p.bfpart = env_int("KCTC_BF16_PARTIALS", 1);
       p.xch = xch_acquire(sizeof(float) * (size_t)T * dirs * p.nwg * (16 * H + 64) * p.rg, s);
+      // self-tagged hand-off (fp32 partials through the L2 ring): the two ring
+      // images start with tag 1 in every word (steps 0 and 1 publish tag 0)
+      p.dtag = d.prec != kPrecBf16 && p.ring == 2 && p.xpd && T >= 2 && env_int("KCTC_BWD_DTAG", 1);
+      if (p.dtag)
+        KCTC_HIP_CHECK(hipMemsetAsync(p.xch, 0x01, sizeof(float) * 2 * (size_t)dirs * p.nwg * (16 * H + 64) * p.rg, s));
     } else {
       p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
     }
