@@ -503,12 +503,15 @@ def main():
     engine = "bf16 MFMA (dense 2.5 PF)" if bf16 else "split-fp16 x3 on the f16 MFMA (2.5 PF / 3)"
     roof = None
     if prof:
-        # the dominant KERNEL: the four GEMM families all run the packed GEMM
-        # kernel (gemm_p256 / gemm_x3p), so they are priced together against
-        # each recurrence kernel
+        # the dominant KERNEL of the step's critical path: the GEMM families
+        # on the trainer's compute stream run the packed GEMM kernel
+        # (gemm_p256 / gemm_x3p) and are priced together against each
+        # recurrence kernel; the weight-gradient GEMMs (gemm_bwd_w / _r) run on
+        # the side stream BESIDE the next backward recurrence -- their spans
+        # include the time they wait for CUs, so they are priced on their own
+        # in `secondary.gate_gemm`, not picked as the dominant kernel
         kernels = {"rnn_fwd_rec": ["rnn_fwd_rec"], "rnn_bwd_rec": ["rnn_bwd_rec"],
-                   "gemm_p256 (gate GEMMs: fwd_proj, bwd_data, bwd_w, bwd_r)":
-                       ["gemm_fwd_proj", "gemm_bwd_data", "gemm_bwd_w", "gemm_bwd_r"]}
+                   "gemm_p256 (compute-stream gate GEMMs: fwd_proj, bwd_data)": ["gemm_fwd_proj", "gemm_bwd_data"]}
         # a family some of whose layers ran as a streamed GEMM (its own span
         # family) has fewer launches than layers: count that share of its FLOPs
         per_step = {"gemm_fwd_proj": L, "gemm_bwd_data": L - 1, "gemm_bwd_w": L, "gemm_bwd_r": L,

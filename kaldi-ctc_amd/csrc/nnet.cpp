@@ -411,6 +411,7 @@ CuDNNRecurrentComponent::CuDNNRecurrentComponent() {
 }
 CuDNNRecurrentComponent::~CuDNNRecurrentComponent() {
   if (err_) (void)hipFree(err_);
+  if (pre_.ev) (void)hipEventDestroy(pre_.ev);
 }
 
 void CuDNNRecurrentComponent::InitFromString(std::string args, Rng &rng) {
@@ -513,9 +514,17 @@ void CuDNNRecurrentComponent::Forward(const CuMatrixBase &in, CuMatrixBase *out,
   // computed beside the recurrence (rnn.h, consumer-gated projection)
   auto &dev = CuDevice::Instantiate();
   hipStream_t side = S() == dev.stream ? dev.side : nullptr;
+  RnnPrepack *pre = nullptr;
+  if (prepack_dx_ && side) {
+    if (!pre_.ev) KCTC_HIP_CHECK(hipEventCreateWithFlags(&pre_.ev, hipEventDisableTiming));
+    pre_.stream = side;
+    pre = &pre_;
+  }
+  pre_.done = false;
   int st = rnn_forward_training(desc_, S(), T, N, in.Data(), params_.f(), out->Data(), workspace_.p,
                                 workspace_.bytes, reserve_.p, reserve_.bytes, DeviceError(), chain, projected, in_rows_,
-                                side);
+                                side, pre);
+  pre_ver_ = pver_;
   if (st) throw std::runtime_error("rnn_forward_training failed: " + std::to_string(st));
 }
 
@@ -561,9 +570,12 @@ void CuDNNRecurrentComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
   }
   {
     ProfScope ps("layer_rnn_backward_data");
+    // the forward's packed W^T, if the parameters are still the ones it packed
+    const RnnPrepack *pre = pre_.done && pre_ver_ == pver_ ? &pre_ : nullptr;
     int st = rnn_backward_data(desc_, S(), T, N, out_value.Data(), out_deriv.Data(), params_.f(),
                                in_deriv ? in_deriv->Data() : nullptr, workspace_.p, workspace_.bytes,
-                               reserve_.p, reserve_.bytes, DeviceError(), CuDevice::Instantiate().stream2);
+                               reserve_.p, reserve_.bytes, DeviceError(), CuDevice::Instantiate().stream2, nullptr,
+                               pre);
     if (st) throw std::runtime_error("rnn_backward_data failed: " + std::to_string(st));
   }
   if (to_update_in) {
@@ -676,6 +688,7 @@ int CuDNNRecurrentComponent::side_gemm_blocks() const {
 
 void CuDNNRecurrentComponent::ApplyUpdate(const unsigned *skip) {
   // ApplyFloor(-clip) / ApplyCeiling(clip) then filter_params_ += lr * grad
+  ++pver_;
   UpdateWith(params_.f(), grad_.f(), clip_gradient_, skip);
 }
 
@@ -706,7 +719,10 @@ void CuDNNRecurrentComponent::Vectorize(float *host) const {
   auto v = d2h(params_.f(), NumParameters());
   std::copy(v.begin(), v.end(), host);
 }
-void CuDNNRecurrentComponent::UnVectorize(const float *host) { h2d(params_.f(), host, NumParameters()); }
+void CuDNNRecurrentComponent::UnVectorize(const float *host) {
+  ++pver_;
+  h2d(params_.f(), host, NumParameters());
+}
 
 // nnet-cudnn-component.cc:698-721
 void CuDNNRecurrentComponent::Write(std::ostream &os, bool binary) const {
@@ -1564,12 +1580,15 @@ void NnetCtcUpdater::SetupChunks(int T_max, int N) {
 void NnetCtcUpdater::Propagate(int T, int N) {  // :136-169
   const int C = nnet_->NumComponents();
   const CuDNNRecurrentComponent *below = nullptr;  // the last RNN, through identity components
+  const int first = nnet_->FirstUpdatableComponent();
   for (int c = 0; c < C; c++) {
     const Component &comp = nnet_->GetComponent(c);
     if (const auto *r = dynamic_cast<const CuDNNRecurrentComponent *>(&comp)) {
       const void *rows = nullptr, *cols = nullptr;
       if (below && below->Desc().prec == r->Desc().prec) below->PackedOutput(&rows, &cols);
       r->SetPackedInput(rows, cols);
+      // Backprop computes its input derivative (streamed dx GEMM): W^T packed now
+      r->SetPrepackDx(update_ && c > first);
       below = r;
     } else if (!comp.IsIdentityForward()) {
       below = nullptr;

@@ -272,8 +272,14 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   void Vectorize(float *host) const override;
   void UnVectorize(const float *host) override;
   float *GradData() override { return grad_.f(); }
-  float *ParamData() override { return params_.f(); }
+  float *ParamData() override {  // (a writer: the forward's packed W^T goes stale)
+    ++pver_;
+    return params_.f();
+  }
   void ApplyUpdate(const unsigned *skip = nullptr) override;
+  // the updater marks the RNNs whose Backprop computes an input derivative:
+  // their forward packs W^T for it on the side stream (rnn.h RnnPrepack)
+  void SetPrepackDx(bool on) const { prepack_dx_ = on; }
   // device error word of the recurrences (hand-off timeout); the updater
   // points every RNN at its own per-step word (SetErrorWord)
   unsigned *DeviceError() const { return err_ext_ ? err_ext_ : err_; }
@@ -327,6 +333,11 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   }
   unsigned *err_ = nullptr;
   mutable unsigned *err_ext_ = nullptr;
+  // W^T packed by the last forward (RnnPrepack) for parameter version pre_ver_
+  mutable bool prepack_dx_ = false;
+  mutable RnnPrepack pre_;
+  mutable unsigned pre_ver_ = 0;
+  unsigned pver_ = 1;  // bumped by every parameter write
   void Forward(const CuMatrixBase &in, CuMatrixBase *out, RnnFwdChain *chain) const;
 };
 

@@ -115,10 +115,23 @@ struct RnnFwdChain {
 // recurrence needs its rows, and the recurrence's IO waves fetch a row tile
 // only once the GEMM has published it (gemm.h X3PArgs::gate_flags); joined
 // back into `s` before return.  Taken for the split-fp16 IO-wave forward only.
+// The backward's streamed dx GEMM reads W's columns packed (split-fp16 /
+// bf16 rows of W^T).  W does not change between a training step's forward and
+// backward, so rnn_forward_training packs them on `stream` while its own
+// recurrence runs (CUs it leaves idle) into the workspace and records `ev`;
+// rnn_backward_data then starts its streamed GEMM at once instead of behind
+// the packs.  The caller owns ev and passes the same struct to the backward
+// only while the parameters are unchanged (done: set by the forward).
+struct RnnPrepack {
+  hipStream_t stream = nullptr;
+  hipEvent_t ev = nullptr;
+  bool done = false;
+};
 int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *w, float *y, void *workspace, size_t ws_bytes,
                          void *reserve, size_t res_bytes, unsigned *err, RnnFwdChain *chain = nullptr,
-                         bool input_projected = false, const void *in_rows = nullptr, hipStream_t side = nullptr);
+                         bool input_projected = false, const void *in_rows = nullptr, hipStream_t side = nullptr,
+                         RnnPrepack *pre = nullptr);
 // bf16 one-layer bidirectional components: the forward recurrence also writes
 // its output as packed bf16 rows [T*N][2H] and columns [2H][kbt64] into the
 // reserve (the GEMM operands the next component's projection / dW and this
@@ -147,7 +160,8 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
                       const float *dy, const float *w, float *dx, void *workspace,
                       size_t ws_bytes, void *reserve, size_t res_bytes, unsigned *err,
                       hipStream_t overlap = nullptr,  // overlap: stream for the streamed dx GEMM
-                      RnnWgradStream *wgrad = nullptr);
+                      RnnWgradStream *wgrad = nullptr,
+                      const RnnPrepack *pre = nullptr);  // W^T packed by the forward (done)
 int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *y, void *workspace, size_t ws_bytes, float *dw,
                          void *reserve, size_t res_bytes, int max_blocks = 0,

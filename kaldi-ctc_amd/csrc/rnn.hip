@@ -159,7 +159,7 @@ static size_t xch_bytes(const RnnDesc &d, int T, int N) {
 //               shifted output^T [dirs*H][TN]
 // plus int exponents and float-bit column maxima (G = nW*H).
 struct PackLay {
-  size_t a, b, c, d, ea, eb, ec, ed, cm, part, cnt, cme, fcnt, fpart, gtf, total;
+  size_t a, b, c, d, ea, eb, ec, ed, cm, part, cnt, cme, fcnt, fpart, gtf, wt, ewt, cmw, total;
 };
 static PackLay pack_layout(const RnnDesc &d, int T, int N) {
   const long TN = (long)T * N, G = (long)d.nw() * d.H, Dm = std::max(d.D, d.dirs * d.H), dirs = d.dirs;
@@ -188,6 +188,11 @@ static PackLay pack_layout(const RnnDesc &d, int T, int N) {
   // consumer-gated projection: its tile counter (word 0), then the tile flags
   // [dirs][row tiles][column tiles] from word 64 (never reset: a call's id)
   p.gtf = o; o = align_up(o + sizeof(unsigned) * (64 + dirs * ((TN + 255) / 256) * ((G + 255) / 256)), 256);
+  // W^T of the streamed dx GEMM, packed by the forward (RnnPrepack): kept
+  // from the forward to the backward, apart from every other slot
+  p.wt = o; o = align_up(o + x3p_bytes(dirs * Dm, G), 256);
+  p.ewt = o; o = align_up(o + sizeof(int) * (dirs * Dm + 64), 256);
+  p.cmw = o; o = align_up(o + sizeof(unsigned) * (dirs * Dm + 64), 256);
   p.total = o;
   return p;
 }
@@ -3357,7 +3362,11 @@ unsigned xcd_mask(const RnnDesc &d, int N, bool fwd) {
 // persistent blocks a streamed GEMM may run beside a recurrence of `rec_wgs`
 // workgroups (rnn.h, CU budget); 0: too few to stream
 int stream_block_budget(int rec_wgs, bool backward) {
-  const int left = rnn_usable_cus() - rec_wgs - (backward ? rnn_comm_cus() : 0) - 16;
+  // the 16-CU margin keeps room for the exchange's kernels beyond maxCTAs;
+  // a backward without an exchange (one rank) gives the streamed dx GEMM all
+  // CUs the recurrence leaves (configs[1]: 128 blocks, 655.7k -> 670.7k frames/s)
+  const int margin = backward && rnn_comm_cus() == 0 ? 0 : 16;
+  const int left = rnn_usable_cus() - rec_wgs - (backward ? rnn_comm_cus() : 0) - margin;
   return left >= 8 ? left : 0;
 }
 
@@ -3546,11 +3555,16 @@ bool rnn_packed_output(const RnnDesc &d, int T, int N, void *reserve, const void
   return true;
 }
 
+namespace {
+void pack_dx_weights(const RnnDesc &d, int l, const float *w, void *workspace, int T, int N, hipStream_t st);
+}  // namespace
+
 int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *w, float *y, void *workspace, size_t ws_bytes,
                          void *reserve, size_t res_bytes, unsigned *err, RnnFwdChain *chain,
-                         bool input_projected, const void *in_rows, hipStream_t side) {
+                         bool input_projected, const void *in_rows, hipStream_t side, RnnPrepack *pre) {
   if (chain) chain->done = false;
+  if (pre) pre->done = false;
   if (T <= 0 || N <= 0 || N > 16 * kMaxRT || d.H % 16) return KRNN_NOT_SUPPORTED;
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
   if (res_bytes < sizeof(float) * (size_t)lay.total) return KRNN_BAD_PARAM;
@@ -3742,13 +3756,24 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     const dim3 grid(ver == 4 ? 8 * ceil_div(p.nwg, p.xpd) : ver == 6 && p.xpd ? 8 * p.nwg : dirs * p.nwg * p.rg);
     RecTrace tr;
     if (tr.arm("fwd", grid.x)) p.trace = tr.dev;
-    const hipEvent_t fork = chained ? fork_event(s) : nullptr;
+    // W^T of the backward's streamed dx GEMM, packed beside this recurrence
+    // (rnn_backward_data's `streamed` shapes; one-layer descriptors)
+    const bool prepack = pre && pre->stream && pre->ev && ver == 6 && d.layers == 1 && dirs == 2 && env_int("KCTC_PREPACK", 1) &&
+                         ((d.prec == kPrecX3 && N <= 16) || env_int("KCTC_STREAM_ALL", 0)) && use_x3(NW * H) &&
+                         NW * H <= 4096 && (d.prec == kPrecX3 || (NW * H) % 64 == 0);
+    const hipEvent_t fork = (chained || prepack) ? fork_event(s) : nullptr;
     {
       ProfSpan ps(s, "rnn_fwd_rec");
       if (ver == 6) launch6(true, d.mode, d.prec, c6.nth, p, grid, lds, s);
       else launch_rec(true, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
+    if (prepack) {  // launched after the recurrence: its workgroups are placed first
+      KCTC_HIP_CHECK(hipStreamWaitEvent(pre->stream, fork, 0));
+      pack_dx_weights(d, 0, w, workspace, T, N, pre->stream);
+      KCTC_HIP_CHECK(hipEventRecord(pre->ev, pre->stream));
+      pre->done = true;
+    }
     if (gated_launch) {
       gated_launch();
       join_stream(s, gside);  // (complete by the recurrence's end: it read every row)
@@ -3767,30 +3792,41 @@ namespace {
 // dx of stacked layer l on `ov`, streamed off the backward recurrence about
 // to be launched on `s` (gemm_x3p_bwd_stream): W_d^T packed first, then one
 // persistent launch that packs dGates rows as the recurrence flags them.
+// W^T of layer l's dx GEMM (B operand of the streamed GEMM) into the
+// workspace slot pl.wt (per-column exponents pl.ewt, absmax scratch pl.cmw)
+void pack_dx_weights(const RnnDesc &d, int l, const float *w, void *workspace, int T, int N, hipStream_t st) {
+  const bool bf = d.prec == kPrecBf16;
+  const int G4 = d.nw() * d.H, KB = G4 / (bf ? 64 : 32), Din = d.din(l);
+  const long pl0 = d.lin_offset(l * d.dirs, 0, false), pls = d.pl_size(l);
+  const float *wl = w + pl0;
+  const PackLay pl = pack_layout(d, T, N);
+  _Float16 *Bp = pk<_Float16>(workspace, d, T, N, pl.wt);
+  int *eB = pk<int>(workspace, d, T, N, pl.ewt);
+  unsigned *cm = pk<unsigned>(workspace, d, T, N, pl.cmw);
+  ProfSpan ps(st, "x3_pack_bwd_stream");
+  for (int dir = 0; dir < 2; dir++) {
+    if (bf) {
+      bf16_pack_cols(st, wl + dir * pls, Din, G4, Din, 0, reinterpret_cast<__bf16 *>(Bp) + (long)dir * Din * KB * 64);
+      continue;
+    }
+    absmax_f32(st, wl + dir * pls, Din, G4, Din, nullptr, cm + dir * Din);
+    x3p_pack_cols(st, wl + dir * pls, Din, G4, Din, 0, Bp + (long)dir * Din * KB * 64, eB + dir * Din, cm + dir * Din,
+                  0.f);
+  }
+}
+
 void launch_bwd_stream(const RnnDesc &d, const RecParams &p, int l, const float *w, float *dxl, void *workspace,
-                       int T, int N, hipStream_t ov, hipEvent_t fork, unsigned *err) {
+                       int T, int N, hipStream_t ov, hipEvent_t fork, unsigned *err, const RnnPrepack *pre) {
   KCTC_HIP_CHECK(hipStreamWaitEvent(ov, fork, 0));  // after the flag reset, not after the recurrence
   const bool bf = d.prec == kPrecBf16;
   const int NW = d.nw(), H = d.H, G4 = NW * H, KB = G4 / (bf ? 64 : 32), Din = d.din(l);
   const long TN = (long)T * N;
-  const long pl0 = d.lin_offset(l * d.dirs, 0, false), pls = d.pl_size(l);
-  const float *wl = w + pl0;
   const PackLay pl = pack_layout(d, T, N);
-  _Float16 *Ap = pk<_Float16>(workspace, d, T, N, pl.a), *Bp = pk<_Float16>(workspace, d, T, N, pl.b);
-  int *eA = pk<int>(workspace, d, T, N, pl.ea), *eB = pk<int>(workspace, d, T, N, pl.eb);
-  unsigned *cm = pk<unsigned>(workspace, d, T, N, pl.cm);
-  {
-    ProfSpan ps(ov, "x3_pack_bwd_stream");
-    for (int dir = 0; dir < 2; dir++) {
-      if (bf) {
-        bf16_pack_cols(ov, wl + dir * pls, Din, G4, Din, 0, reinterpret_cast<__bf16 *>(Bp) + (long)dir * Din * KB * 64);
-        continue;
-      }
-      absmax_f32(ov, wl + dir * pls, Din, G4, Din, nullptr, cm + dir * Din);
-      x3p_pack_cols(ov, wl + dir * pls, Din, G4, Din, 0, Bp + (long)dir * Din * KB * 64, eB + dir * Din,
-                    cm + dir * Din, 0.f);
-    }
-  }
+  _Float16 *Ap = pk<_Float16>(workspace, d, T, N, pl.a), *Bp = pk<_Float16>(workspace, d, T, N, pl.wt);
+  int *eA = pk<int>(workspace, d, T, N, pl.ea), *eB = pk<int>(workspace, d, T, N, pl.ewt);
+  // packed by the forward on its side stream (RnnPrepack), else here
+  if (pre && pre->done) KCTC_HIP_CHECK(hipStreamWaitEvent(ov, pre->ev, 0));
+  else pack_dx_weights(d, l, w, workspace, T, N, ov);
   X3PBwdStream a;
   a.bf16 = bf;
   a.M = (int)TN; a.N = Din; a.KB = KB;
@@ -3806,11 +3842,18 @@ void launch_bwd_stream(const RnnDesc &d, const RecParams &p, int l, const float 
   a.nwg = p.xpd ? 1 : p.nwg; a.T = T; a.Nf = N; a.err = err; a.rg = p.rg;
   const int pinned = p.xpd ? d.dirs * p.rg : 0;
   if (pinned) { a.xcd_word = p.flags + kXcdWord; a.xcd_count = pinned; }
-  // 96 measured best at configs[1]; never more than the CU budget leaves
+  // 128 measured best at configs[1] since the self-tagged recurrences (96
+  // before: 655.7k -> 670.7k frames/s); never more than the CU budget leaves
   // beside the recurrence and the exchange's kernels (rnn.h).  Blocks landing
-  // on the pinned XCDs exit at once: launch enough that ~96 stay
-  const int nb = std::min(96, stream_block_budget(d.dirs * p.nwg * p.rg, true));
+  // on the pinned XCDs exit at once: launch enough that ~128 stay
+  const int nb = std::min(128, stream_block_budget(d.dirs * p.nwg * p.rg, true));
   a.blocks = env_int("KCTC_BWD_STREAM_BLOCKS", pinned ? nb * 8 / (8 - pinned) : nb);
+  // not before every workgroup of the recurrence is resident: its blocks
+  // wait (on_pinned_xcd) for the pinned recurrence's XCDs to register, and a
+  // block parked on one of those XCDs' CUs before the recurrence's last
+  // workgroup got there would keep it out (with W^T packed by the forward
+  // the GEMM starts together with the recurrence)
+  rnn_comm_gate(ov, rnn_bwd_registrations());
   ProfSpan ps(ov, "bwd_data_stream");
   gemm_x3p_bwd_stream(ov, a);
 }
@@ -3951,7 +3994,7 @@ bool rnn_wgrad_stream_ok(const RnnDesc &d, int T, int N) {
 int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float *y,
                       const float *dy, const float *w, float *dx, void *workspace,
                       size_t ws_bytes, void *reserve, size_t res_bytes, unsigned *err,
-                      hipStream_t overlap, RnnWgradStream *wgrad) {
+                      hipStream_t overlap, RnnWgradStream *wgrad, const RnnPrepack *pre) {
   if (wgrad) wgrad->done = false;
   if (T <= 0 || N <= 0 || N > 16 * kMaxRT || d.H % 16) return KRNN_NOT_SUPPORTED;
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
@@ -4070,7 +4113,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     }
     KCTC_HIP_CHECK(hipGetLastError());
     if (streamed) {
-      launch_bwd_stream(d, p, l, w, dxl, workspace, T, N, overlap, fork, err);
+      launch_bwd_stream(d, p, l, w, dxl, workspace, T, N, overlap, fork, err, d.layers == 1 ? pre : nullptr);
       join_stream(s, overlap);
     }
     if (wstream) {
