@@ -98,8 +98,23 @@ struct X3PArgs {
   unsigned *gate_flags = nullptr;
   unsigned gate_id = 0;
   unsigned xcd_avoid = 0;
+  // Beside an XCD-pinned recurrence (non-gated, non-streaming 256-tile GEMMs
+  // with a tile counter): blocks whose XCD has its bit set in *avoid_word
+  // (rnn.hip rnn_pinned_xcds: the XCDs pinned backward recurrences ran on)
+  // exit before taking work, so no block ever holds a CU the recurrence
+  // needs and the launch ends when the other XCDs' blocks run out of tiles
+  // (no block exits while the word names all avoid_xcds XCDs of the device:
+  // then no XCD is left to the GEMM's tiles)
+  const unsigned *avoid_word = nullptr;
+  int avoid_xcds = 8;
 };
 void gemm_x3p(hipStream_t s, const X3PArgs &g);
+// two independent 256-tile problems (e.g. a layer's dW and dR) as ONE launch
+// sharing g1's tile counter, then each one's split-K reduction: beside a
+// pinned recurrence a launch completes only once its blocks on the
+// recurrence's XCDs could start, so one launch per recurrence keeps the
+// side stream from falling a GEMM behind per layer
+void gemm_x3p_pair(hipStream_t s, const X3PArgs &g1, const X3PArgs &g2);
 // shapes gemm_x3p runs on 256 x 256 tiles (KCTC_GEMM256=0 turns them off)
 bool x3p_use_256(int M, int N);
 // split-K for gemm_x3p on a (M x N, KB k-blocks, batch) problem so that the
@@ -132,7 +147,7 @@ struct X3PBwdStream {
   long sB = 0, seB = 0;
   float *C = nullptr;
   long ldc = 0;
-  float *part = nullptr;               // [M][N] floats
+  float *part = nullptr;               // x3p_bwd_stream_part_floats(M, N) floats
   int *cnt = nullptr;                  // x3p_bwd_stream_ints(M, N) ints (zeroed here)
   const unsigned *flags = nullptr;     // producer flag lines
   int nwg = 0, T = 0, Nf = 0;
@@ -147,6 +162,10 @@ struct X3PBwdStream {
   int xcd_count = 0;
 };
 size_t x3p_bwd_stream_ints(int M, int N);
+// the launch runs on 256 x 256 tiles (512 threads, 128 KB LDS per block);
+// part then needs x3p_bwd_stream_part_floats(M, N) floats
+bool x3p_bwd_stream_256(int M, int N, int KB, bool bf16);
+size_t x3p_bwd_stream_part_floats(int M, int N);
 void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a);
 // pack rows r < R of X (K values each, row stride ldx) -> out[b][r][KB][64],
 // exponent per row into eout (bound > 0: from the bound, else the row max)
@@ -157,7 +176,9 @@ void x3p_pack_rows(hipStream_t s, const float *X, long ldx, int R, int K, _Float
 // bits of max |x| of the column) or the bound
 void x3p_pack_cols(hipStream_t s, const float *X, long ldx, int R, int Cn, int shift, _Float16 *out, int *eout,
                    const unsigned *cmax, float bound, int batch = 1, long sX = 0, long sOut = 0, long sE = 0,
-                   long sCm = 0);
+                   long sCm = 0,
+                   // avoid: X3PArgs::avoid_word; then counter: a zeroed int (dynamic item runs)
+                   const unsigned *avoid = nullptr, int nxcd = 8, int *counter = nullptr);
 inline size_t x3p_bytes(long rows, long K) { return (size_t)rows * ((K + 31) / 32) * 64 * 2; }
 
 // column sums: out[b][j] (+)= alpha * sum_i X[b][i*ldx + j], i < rows  (accumulate if beta=1)

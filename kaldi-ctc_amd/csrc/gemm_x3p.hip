@@ -77,6 +77,8 @@ struct PParams {
   unsigned *gate;
   unsigned gate_id, xcd_avoid;
   int mt;                  // row tiles
+  const unsigned *avoid;   // X3PArgs::avoid_word, avoid_xcds
+  int nxcd;
 };
 
 
@@ -805,7 +807,9 @@ __device__ __forceinline__ void p256_row(floatx4 (&acc)[4], halfx8 ah, halfx8 al
 // barrier, with no matrix work to hide behind).  Source pointers are computed
 // once per tile; the loads of the last iteration re-read the last k block
 // (clamped) so the body is straight-line.  KCTC_P256=1: the previous loop.
-template <bool BFM>
+// AUXA: cache policy of the A pieces (16: sc1, rows packed by other CUs
+// while this kernel runs)
+template <bool BFM, int AUXA = 0>
 __device__ __forceinline__ void p256_kloop_spread(const _Float16 *A, const _Float16 *B, int M, int N, int KB, int m0,
                                                   int n0, int kb0, int nk, unsigned char *lds, int wm, int wn, int fr,
                                                   int fq, floatx4 (&acc)[8][4]) {
@@ -820,8 +824,10 @@ __device__ __forceinline__ void p256_kloop_spread(const _Float16 *A, const _Floa
     src[i] = (i < 4 ? A : B) + ((long)gr * KB + kb0) * 64 + c * 8;
   }
 #pragma unroll
-  for (int i = 0; i < 8; i++)
-    __builtin_amdgcn_global_load_lds(src[i], lds + (i < 4 ? 0 : TILEB2) + (w * 4 + (i & 3)) * 1024, 16, 0, 0);
+  for (int i = 0; i < 8; i++) {
+    if (i < 4) __builtin_amdgcn_global_load_lds(src[i], lds + (w * 4 + i) * 1024, 16, 0, AUXA);
+    else __builtin_amdgcn_global_load_lds(src[i], lds + TILEB2 + (w * 4 + (i & 3)) * 1024, 16, 0, 0);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int it = 0; it < nk; it++) {
@@ -838,9 +844,10 @@ __device__ __forceinline__ void p256_kloop_spread(const _Float16 *A, const _Floa
     for (int i = 0; i < 8; i++) {
       if (i < 4) {  // two pieces per row block of the first half: the last lands behind half the MFMAs
 #pragma unroll
-        for (int h = 2 * i; h < 2 * i + 2; h++)
-          __builtin_amdgcn_global_load_lds(src[h] + adv, nxt + (h < 4 ? 0 : TILEB2) + (w * 4 + (h & 3)) * 1024, 16, 0,
-                                           0);
+        for (int h = 2 * i; h < 2 * i + 2; h++) {
+          if (h < 4) __builtin_amdgcn_global_load_lds(src[h] + adv, nxt + (w * 4 + h) * 1024, 16, 0, AUXA);
+          else __builtin_amdgcn_global_load_lds(src[h] + adv, nxt + TILEB2 + (w * 4 + (h & 3)) * 1024, 16, 0, 0);
+        }
       }
       const halfx8 ah = frag(cur, wm + i * 16 + fr, fq);
       const halfx8 al = frag(cur, wm + i * 16 + fr, 4 + fq);
@@ -977,11 +984,26 @@ __device__ __forceinline__ void p256_tile(const PParams &p, unsigned char *lds, 
   }
 }
 
+// beside a pinned recurrence (X3PArgs::avoid_word): true on one of its XCDs
+// (block-uniform; the word only ever gains bits)
+__device__ __forceinline__ bool avoid_here(const PParams &p, int *bc) {
+  if (!p.avoid) return false;
+  if (threadIdx.x == 0) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    const unsigned m = __hip_atomic_load(p.avoid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *bc = (int)((m >> (x & 0xfu)) & 1u) && __builtin_popcount(m) < p.nxcd;
+  }
+  __syncthreads();
+  return __builtin_amdgcn_readfirstlane(*bc) != 0;
+}
+
 template <bool BFM>
 __global__ __launch_bounds__(NTH2, 1) void gemm_p256_kernel(PParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];  // ONE shared array
   int *next = reinterpret_cast<int *>(lds + 2 * 2 * TILEB2);
   const int total = p.tiles * p.batch * p.split;
+  if (avoid_here(p, next + 1)) return;
   // consumer-gated: off the consumer's XCDs -- the static mask, and the XCDs
   // the running consumer has tagged with this call's id (gate - 56 + XCC_ID),
   // checked before every job, so a block that started before the consumer's
@@ -1026,6 +1048,30 @@ __global__ __launch_bounds__(NTH2, 1) void gemm_p256_kernel(PParams p) {
     int tm, tn, b, ks;
     decode_tile(p, id, total, true, tm, tn, b, ks);
     p256_tile<BFM>(p, lds, tm, tn, b, ks);
+  }
+}
+
+// two problems, one job space (p's jobs, then q's), p's tile counter
+template <bool BFM>
+__global__ __launch_bounds__(NTH2, 1) void gemm_p256_pair_kernel(PParams p, PParams q) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];  // ONE shared array
+  int *next = reinterpret_cast<int *>(lds + 2 * 2 * TILEB2);
+  const int t1 = p.tiles * p.batch * p.split, t2 = q.tiles * q.batch * q.split;
+  if (avoid_here(p, next + 1)) return;
+  while (true) {
+    if (threadIdx.x == 0) *next = atomicAdd(p.counter, 1);
+    __syncthreads();
+    const int id = __builtin_amdgcn_readfirstlane(*next);
+    __syncthreads();
+    if (id >= t1 + t2) break;
+    int tm, tn, b, ks;
+    if (id < t1) {
+      decode_tile(p, id, t1, false, tm, tn, b, ks);
+      p256_tile<BFM>(p, lds, tm, tn, b, ks);
+    } else {
+      decode_tile(q, id - t1, t2, false, tm, tn, b, ks);
+      p256_tile<BFM>(q, lds, tm, tn, b, ks);
+    }
   }
 }
 
@@ -1117,11 +1163,11 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(const float *__restrict_
 // (wait done == P, then the tile with sc1 LDS-DMA, combine epilogue).  Slots
 // alternate directions in production order; jobs are taken from one counter,
 // so a GEMM job only ever waits for pack jobs that running blocks own.
-template <int KW, bool BFM>
+template <int KW, bool BFM, int NWV = 4>
 __device__ __forceinline__ void bwd_pack_rows(const PParams &p, int d, int r0, int r1) {
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int K = p.KB * (BFM ? 64 : 32);
-  for (int r = r0 + w; r < r1; r += 4) {
+  for (int r = r0 + w; r < r1; r += NWV) {
     const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p.E + (long)r * p.lde + d * p.edoff), 0,
                                                       K * 4, 0x00020000);
     floatx4 v[KW];
@@ -1209,15 +1255,130 @@ __global__ __launch_bounds__(NTH, 2) void x3p_bwd_stream_kernel(PParams p) {
   }
 }
 
+// ---- the backward stream on 256 x 256 tiles ------------------------------
+// x3p_bwd_stream_kernel's job list at the p256 tile (512 threads, 128 KB
+// LDS, one block per CU): per (row tile, direction) slot P pack jobs of
+// 256 / P rows (8 waves) and gx GEMM jobs of 256 x 256 over the direction's
+// whole K, A by sc1 LDS-DMA (rows packed by other CUs during this launch).
+// A 256 x 256 tile issues 2x the MFMAs per LDS byte of the 128 tile, so the
+// dx GEMM keeps up with the recurrence on about a third of the CUs the 128
+// version needed, and the rest run the weight GEMMs (gemm_x3p avoid_word).
+// The two directions' partials meet in the accumulator layout
+// (part + tile * 256 * 256: thread t's (i, j) fragment is 16 B at
+// [i * 4 + j][t]): the first to arrive stores its partial (sc1), the second
+// adds it and writes C -- part0 + part1 either way round.
+template <bool BFM>
+__device__ __forceinline__ void p256_bwd_tile(const PParams &p, unsigned char *lds, int tm, int tn, int d, int *bc) {
+  const _Float16 *A = p.A + (long)d * p.sA, *B = p.B + (long)d * p.sB;
+  const int m0 = tm * TB2, n0 = tn * TB2;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = (wid >> 2) * 128, wn = (wid & 3) * 64;
+  const int fr = lane & 15, fq = lane >> 4;
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  p256_kloop_spread<BFM, 16>(A, B, p.M, p.N, p.KB, m0, n0, 0, p.KB, lds, wm, wn, fr, fq, acc);
+  if constexpr (!BFM) {  // to values: 2^-(eA[row] + eB[col]) (eA written by other CUs: sc1 loads)
+    const int *eA = p.eA + (long)d * p.seA, *eB = p.eB + (long)d * p.seB;
+    int eb[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int col = n0 + wn + j * 16 + fr;
+      eb[j] = col < p.N ? eB[col] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = m0 + wm + i * 16 + fq * 4 + r;
+        const int ea = row < p.M ? __hip_atomic_load(eA + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j][r] = ldexpf(acc[i][j][r], -(ea + eb[j]));
+      }
+  }
+  const long tile = (long)tm * p.gx + tn;
+  int *arr = p.arrive + tile;
+  if (threadIdx.x == 0) *bc = __hip_atomic_fetch_add(arr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const bool first = __builtin_amdgcn_readfirstlane(*bc) == 0;
+  const auto rp = __builtin_amdgcn_make_buffer_rsrc(p.part + tile * (TB2 * TB2), 0, TB2 * TB2 * 4, 0x00020000);
+  if (first) {
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rp,
+                                               ((i * 4 + j) * NTH2 + (int)threadIdx.x) * 16, 0, 16);
+  } else {
+    wait_count(arr, 4, p.serr);
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const floatx4 o = __builtin_bit_cast(
+            floatx4, __builtin_amdgcn_raw_buffer_load_b128(rp, ((i * 4 + j) * NTH2 + (int)threadIdx.x) * 16, 0, 16));
+        const int col = n0 + wn + j * 16 + fr;
+        if (col >= p.N) continue;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int row = m0 + wm + i * 16 + fq * 4 + r;
+          if (row < p.M) p.C[(long)row * p.ldc + col] = acc[i][j][r] + o[r];
+        }
+      }
+  }
+  // unconditional barrier (see fwd_combine)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (first && threadIdx.x == 0) __hip_atomic_fetch_add(arr, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int KW, bool BFM>
+__global__ __launch_bounds__(NTH2, 1) void x3p_bwd_stream256_kernel(PParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  int *next = reinterpret_cast<int *>(lds + 2 * 2 * TILEB2);
+  int *seen = next + 1;  // [2] producer epochs seen
+  int *bc = next + 3;    // combine broadcast
+  if (threadIdx.x == 0) { seen[0] = 0; seen[1] = 0; }
+  const int J = p.P + p.gx, total = 2 * p.nrt * J, rows_per = TB2 / p.P;
+  if (on_pinned_xcd(p, bc)) return;  // before taking any job
+  while (true) {
+    if (threadIdx.x == 0) *next = atomicAdd(p.counter, 1);
+    __syncthreads();
+    const int id = __builtin_amdgcn_readfirstlane(*next);
+    __syncthreads();
+    if (id >= total) break;
+    const int slot = id / J, r = id - slot * J, d = slot & 1, rank = slot >> 1;
+    const int rt = d == 0 ? p.nrt - 1 - rank : rank;
+    if (r < p.P) {
+      const int ra = rt * TB2 + r * rows_per, rb = min(p.M, ra + rows_per);
+      if (ra < rb) {
+        // E rows of step s are complete at epoch s + 3 (the last step's at T + 2)
+        const int ta = ra / p.sN, tb = (rb - 1) / p.sN;
+        wait_epoch(p, d, d == 0 ? p.sT + 2 - ta : tb + 3, seen);
+        bwd_pack_rows<KW, BFM, NTH2 / 64>(p, d, ra, rb);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_fetch_add(p.done + d * p.nrt + rt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();  // (see x3p_bwd_stream_kernel: reconverge after the lane-0 atomic)
+    } else {
+      wait_count(p.done + d * p.nrt + rt, p.P, p.serr);
+      p256_bwd_tile<BFM>(p, lds, rt, r - p.P, d, bc);
+      __syncthreads();
+    }
+  }
+}
+
 // Column packing (transpose): packed row c = column c of X, K = X's rows
 // (k -> X row k - shift, zero outside [0, R)).  Exponent from cmax[c] (max |x|
 // of the column, float bits) or the bound.  Block: 64 columns x one 32-k block.
-__global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict__ X, long ldx, int R, int Cn, int KB,
-                                                        int shift, long sX, _Float16 *__restrict__ out, long sOut,
-                                                        int *__restrict__ eout, long sE,
-                                                        const unsigned *__restrict__ cmax, long sCm, float bound) {
-  __shared__ float tile[32][65];
-  const int b = blockIdx.z, c0 = blockIdx.x * 64, kb = blockIdx.y;
+__device__ __forceinline__ void pack_cols_item(const float *__restrict__ X, long ldx, int R, int Cn, int KB, int shift,
+                                               long sX, _Float16 *__restrict__ out, long sOut, int *__restrict__ eout,
+                                               long sE, const unsigned *__restrict__ cmax, long sCm, float bound,
+                                               int bx, int kb, int b, float (*tile)[65]) {
+  const int c0 = bx * 64;
   const float *x = X + (long)b * sX;
   const int t = threadIdx.x;
   // load 32 rows x 64 columns (each row: 64 consecutive floats)
@@ -1231,20 +1392,62 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
   }
   __syncthreads();
   const int c = t >> 2, part = t & 3;
-  if (c0 + c >= Cn) return;
-  const int e = bound > 0.f ? split_exp_d(bound)
-                            : split_exp_d(__uint_as_float(cmax[(long)b * sCm + c0 + c]));
-  halfx8 h, l;
+  if (c0 + c < Cn) {
+    const int e = bound > 0.f ? split_exp_d(bound)
+                              : split_exp_d(__uint_as_float(cmax[(long)b * sCm + c0 + c]));
+    halfx8 h, l;
 #pragma unroll
-  for (int j = 0; j < 8; j++) {
-    const float xv = ldexpf(tile[part * 8 + j][c], e);
-    h[j] = (_Float16)xv;
-    l[j] = (_Float16)(xv - (float)h[j]);
+    for (int j = 0; j < 8; j++) {
+      const float xv = ldexpf(tile[part * 8 + j][c], e);
+      h[j] = (_Float16)xv;
+      l[j] = (_Float16)(xv - (float)h[j]);
+    }
+    _Float16 *o = out + (long)b * sOut + ((long)(c0 + c) * KB + kb) * 64;
+    *reinterpret_cast<halfx8 *>(o + part * 8) = h;
+    *reinterpret_cast<halfx8 *>(o + 32 + part * 8) = l;
+    if (kb == 0 && part == 0 && eout) eout[(long)b * sE + c0 + c] = e;
   }
-  _Float16 *o = out + (long)b * sOut + ((long)(c0 + c) * KB + kb) * 64;
-  *reinterpret_cast<halfx8 *>(o + part * 8) = h;
-  *reinterpret_cast<halfx8 *>(o + 32 + part * 8) = l;
-  if (kb == 0 && part == 0 && eout) eout[(long)b * sE + c0 + c] = e;
+}
+
+// Column packing (transpose): packed row c = column c of X, K = X's rows
+// (k -> X row k - shift, zero outside [0, R)).  Exponent from cmax[c] (max |x|
+// of the column, float bits) or the bound.  Item: 64 columns x one 32-k block
+// (grid (columns / 64, KB, batch)).  With `avoid` (beside a pinned
+// recurrence, X3PArgs::avoid_word) a 1-D grid takes runs of 8 items from
+// a zeroed counter and the blocks on the recurrence's XCDs leave at once: a
+// stream of short blocks cycling through its CUs kept the recurrence's
+// workgroups from becoming resident for the length of the pack (configs[1]:
+// ~230 us a layer).
+__global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict__ X, long ldx, int R, int Cn, int KB,
+                                                        int shift, long sX, _Float16 *__restrict__ out, long sOut,
+                                                        int *__restrict__ eout, long sE,
+                                                        const unsigned *__restrict__ cmax, long sCm, float bound,
+                                                        const unsigned *avoid, int nxcd, int batch, int *counter) {
+  __shared__ float tile[32][65];
+  __shared__ int bc;
+  if (!avoid) {
+    pack_cols_item(X, ldx, R, Cn, KB, shift, sX, out, sOut, eout, sE, cmax, sCm, bound, blockIdx.x, blockIdx.y,
+                   blockIdx.z, tile);
+    return;
+  }
+  PParams q;
+  q.avoid = avoid;
+  q.nxcd = nxcd;
+  if (avoid_here(q, &bc)) return;
+  const int gx = (Cn + 63) / 64;
+  const int items = gx * KB * batch;
+  while (true) {
+    __syncthreads();  // bc and the tile are reused
+    if (threadIdx.x == 0) bc = atomicAdd(counter, 8);
+    __syncthreads();
+    const int i0 = __builtin_amdgcn_readfirstlane(bc);
+    if (i0 >= items) break;
+    for (int it = i0; it < min(items, i0 + 8); it++) {
+      const int bx = it % gx, r = it / gx;
+      pack_cols_item(X, ldx, R, Cn, KB, shift, sX, out, sOut, eout, sE, cmax, sCm, bound, bx, r % KB, r / KB, tile);
+      __syncthreads();
+    }
+  }
 }
 
 // bf16 packing: out[b][r][kb][64] = bf16(x[r][64 kb + j]), zero past K.
@@ -1348,11 +1551,19 @@ void x3p_pack_rows(hipStream_t s, const float *X, long ldx, int R, int K, _Float
 }
 
 void x3p_pack_cols(hipStream_t s, const float *X, long ldx, int R, int Cn, int shift, _Float16 *out, int *eout,
-                   const unsigned *cmax, float bound, int batch, long sX, long sOut, long sE, long sCm) {
+                   const unsigned *cmax, float bound, int batch, long sX, long sOut, long sE, long sCm,
+                   const unsigned *avoid, int nxcd, int *counter) {
   if (R <= 0 || Cn <= 0 || batch <= 0) return;
   const int KB = (R + 31) / 32;
+  if (avoid) {
+    const long items = (long)ceil_div(Cn, 64) * KB * batch;
+    if (!counter || items + 8 >= (1L << 31)) throw std::invalid_argument("x3p_pack_cols: avoid needs a counter");
+    hipLaunchKernelGGL(pack_cols_kernel, dim3((int)std::min<long>((items + 7) / 8, 1024)), dim3(256), 0, s, X, ldx, R,
+                       Cn, KB, shift, sX, out, sOut, eout, sE, cmax, sCm, bound, avoid, nxcd, batch, counter);
+    return;
+  }
   hipLaunchKernelGGL(pack_cols_kernel, dim3(ceil_div(Cn, 64), KB, batch), dim3(256), 0, s, X, ldx, R, Cn, KB, shift,
-                     sX, out, sOut, eout, sE, cmax, sCm, bound);
+                     sX, out, sOut, eout, sE, cmax, sCm, bound, nullptr, 0, batch, nullptr);
 }
 
 namespace {
@@ -1422,9 +1633,9 @@ int x3p_pick_split(int M, int N, int KB, int batch) {
   return want < 1 ? 1 : (int)want;
 }
 
-void gemm_x3p(hipStream_t s, const X3PArgs &g) {
-  if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return;
-  PParams p;
+// kernel parameters of a gemm_x3p call (t256: it runs on 256 x 256 tiles)
+static PParams x3p_params(const X3PArgs &g, bool &t256) {
+  PParams p{};
   p.A = g.A; p.B = g.B; p.eA = g.eA; p.eB = g.eB; p.C = g.C; p.bias = g.bias; p.bias2 = g.bias2;
   p.ldc = g.ldc; p.sA = g.sA; p.sB = g.sB; p.sC = g.sC; p.sBias = g.sBias; p.seA = g.seA; p.seB = g.seB;
   p.M = g.M; p.N = g.N; p.KB = g.KB; p.alpha = g.alpha; p.beta = g.beta;
@@ -1436,14 +1647,11 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
   if (p.split > 1) p.split = ceil_div(g.KB, p.kbchunk);
   p.ws = g.ws;
   // large shapes on 256 x 256 tiles (KCTC_GEMM256=0: 128 x 128 everywhere)
-  const bool t256 = !g.stream_flags && x3p_use_256(g.M, g.N);
+  t256 = !g.stream_flags && x3p_use_256(g.M, g.N);
   if (t256) {
     p.gx = ceil_div(g.N, TB2);
     p.tiles = p.gx * ceil_div(g.M, TB2);
   }
-  const int total = p.tiles * p.batch * p.split;
-  int blocks = total;
-  if (g.max_blocks > 0 && total > g.max_blocks) blocks = std::max(8, g.max_blocks / 8 * 8);
   p.counter = g.tile_counter;
   p.eA0 = g.eA0; p.eB0 = g.eB0;
   p.sflags = g.stream_flags; p.snwg = g.stream_nwg; p.sT = g.stream_T; p.sN = g.stream_N;
@@ -1462,6 +1670,48 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
   p.dbg = getenv("KCTC_STREAM_DBG") ? atoi(getenv("KCTC_STREAM_DBG")) : 0;
   static const int p256v = getenv("KCTC_P256") ? atoi(getenv("KCTC_P256")) : 0;
   p.p256v = p256v;
+  p.avoid = g.avoid_word;
+  p.nxcd = g.avoid_xcds;
+  if (p.avoid && (!t256 || !p.counter || p.gate))
+    throw std::invalid_argument("gemm_x3p: avoid_word needs a 256-tile launch with a tile counter");
+  return p;
+}
+
+static void x3p_set_attrs() {
+  static bool attr = false;  // dynamic LDS above 64 KB
+  if (attr) return;
+  KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_x3p_kernel<false>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBase));
+  KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_x3p_kernel<false, true>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBase));
+  KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_x3p_kernel<true>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsStream));
+  KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_x3p_kernel<true, true>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsStream));
+  KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_p256_kernel<false>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds256));
+  KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_p256_kernel<true>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds256));
+  KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_p256_pair_kernel<false>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds256));
+  KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_p256_pair_kernel<true>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds256));
+  attr = true;
+}
+
+static void x3p_reduce(hipStream_t s, const PParams &p) {
+  if (p.split <= 1) return;
+  const long tot = (long)p.batch * p.M * p.N;
+  hipLaunchKernelGGL(x3p_splitk_reduce, dim3((int)std::min<long>(2048, (tot + 255) / 256)), dim3(256), 0, s, p);
+}
+
+void gemm_x3p(hipStream_t s, const X3PArgs &g) {
+  if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return;
+  bool t256 = false;
+  PParams p = x3p_params(g, t256);
+  const int total = p.tiles * p.batch * p.split;
+  int blocks = total;
+  if (g.max_blocks > 0 && total > g.max_blocks) blocks = std::max(8, g.max_blocks / 8 * 8);
   if (g.stream_flags && g.stream_arrive && g.stream_part && g.KB % 2 == 0 && (long)g.M * g.ldc * 4 + (long)(g.batch - 1) * g.sC * 4 < (1L << 31)) {
     p.sdir = 1;
     p.kbchunk = g.KB / 2;  // the producer's two directions
@@ -1470,22 +1720,7 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
     KCTC_HIP_CHECK(hipMemsetAsync(p.arrive, 0, sizeof(int) * (size_t)stream_total(p) / 2, s));
   }
   if (p.counter) KCTC_HIP_CHECK(hipMemsetAsync(p.counter, 0, sizeof(int), s));
-  static bool attr = false;  // dynamic LDS above 64 KB
-  if (!attr) {
-    KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_x3p_kernel<false>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBase));
-    KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_x3p_kernel<false, true>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBase));
-    KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_x3p_kernel<true>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsStream));
-    KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_x3p_kernel<true, true>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsStream));
-    KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_p256_kernel<false>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds256));
-    KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_p256_kernel<true>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds256));
-    attr = true;
-  }
+  x3p_set_attrs();
   if (t256) {
     if (g.bf16 && (p.eA || p.eB)) throw std::invalid_argument("gemm_x3p: bf16 operands take no exponents");
     if (g.bf16) hipLaunchKernelGGL(gemm_p256_kernel<true>, dim3(blocks), dim3(NTH2), kLds256, s, p);
@@ -1510,15 +1745,44 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g) {
   } else {
     hipLaunchKernelGGL(gemm_x3p_kernel<false>, dim3(blocks), dim3(NTH), kLdsBase, s, p);
   }
-  if (p.split > 1) {
-    const long tot = (long)p.batch * p.M * p.N;
-    hipLaunchKernelGGL(x3p_splitk_reduce, dim3((int)std::min<long>(2048, (tot + 255) / 256)), dim3(256), 0, s, p);
-  }
+  x3p_reduce(s, p);
+}
+
+void gemm_x3p_pair(hipStream_t s, const X3PArgs &g1, const X3PArgs &g2) {
+  if (g2.M <= 0 || g2.N <= 0 || g2.batch <= 0) return gemm_x3p(s, g1);
+  if (g1.M <= 0 || g1.N <= 0 || g1.batch <= 0) return gemm_x3p(s, g2);
+  bool a = false, b = false;
+  PParams p = x3p_params(g1, a), q = x3p_params(g2, b);
+  if (!a || !b || !p.counter || g1.bf16 != g2.bf16 || g1.stream_flags || g2.stream_flags || g1.gate_flags ||
+      g2.gate_flags)
+    throw std::invalid_argument("gemm_x3p_pair: two 256-tile problems with a tile counter");
+  if (g1.bf16 && (p.eA || p.eB || q.eA || q.eB)) throw std::invalid_argument("gemm_x3p: bf16 operands take no exponents");
+  const int total = p.tiles * p.batch * p.split + q.tiles * q.batch * q.split;
+  int blocks = total;
+  if (g1.max_blocks > 0 && total > g1.max_blocks) blocks = std::max(8, g1.max_blocks / 8 * 8);
+  KCTC_HIP_CHECK(hipMemsetAsync(p.counter, 0, sizeof(int), s));
+  x3p_set_attrs();
+  if (g1.bf16) hipLaunchKernelGGL(gemm_p256_pair_kernel<true>, dim3(blocks), dim3(NTH2), kLds256, s, p, q);
+  else hipLaunchKernelGGL(gemm_p256_pair_kernel<false>, dim3(blocks), dim3(NTH2), kLds256, s, p, q);
+  x3p_reduce(s, p);
+  x3p_reduce(s, q);
 }
 
 size_t x3p_bwd_stream_ints(int M, int N) {
   const long nrt = ceil_div(M, TB), gx = ceil_div(N, TB);
   return (size_t)(1 + 2 * nrt + nrt * gx);
+}
+
+bool x3p_bwd_stream_256(int M, int N, int KB, bool bf16) {
+  static const int on = [] {
+    const char *e = getenv("KCTC_BWD_S256");
+    return e ? atoi(e) : 1;
+  }();
+  // per-tile buffer offsets stay below 2^31 (C rows are addressed as [M][ldc])
+  return on && x3p_use_256(M, N) && KB * (bf16 ? 64 : 32) <= 4096;
+}
+size_t x3p_bwd_stream_part_floats(int M, int N) {
+  return std::max((size_t)M * N, (size_t)ceil_div(M, TB2) * ceil_div(N, TB2) * TB2 * TB2);
 }
 
 void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a) {
@@ -1543,6 +1807,32 @@ void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a) {
   p.backoff = env_backoff();
   p.dbg = getenv("KCTC_STREAM_DBG") ? atoi(getenv("KCTC_STREAM_DBG")) : 0;
   KCTC_HIP_CHECK(hipMemsetAsync(a.cnt, 0, sizeof(int) * x3p_bwd_stream_ints(a.M, a.N), s));
+  if (x3p_bwd_stream_256(a.M, a.N, a.KB, a.bf16)) {
+    p.gx = ceil_div(a.N, TB2); p.nrt = ceil_div(a.M, TB2);
+    p.tiles = p.gx * p.nrt;
+    p.done = a.cnt + 1; p.arrive = a.cnt + 1 + 2 * p.nrt;  // within x3p_bwd_stream_ints (128-tile counts)
+    const int total = 2 * p.nrt * (p.P + p.gx);
+    const dim3 grid(std::min(total, a.blocks > 0 ? a.blocks : 96));
+    auto go = [&](auto kern) {
+      static bool attr = false;
+      if (!attr) {
+        KCTC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds256));
+        attr = true;
+      }
+      hipLaunchKernelGGL(kern, grid, dim3(NTH2), kLds256, s, p);
+    };
+    if (a.bf16) {
+      if (K <= 1024) go(x3p_bwd_stream256_kernel<4, true>);
+      else if (K <= 2048) go(x3p_bwd_stream256_kernel<8, true>);
+      else go(x3p_bwd_stream256_kernel<16, true>);
+    } else {
+      if (K <= 1024) go(x3p_bwd_stream256_kernel<4, false>);
+      else if (K <= 2048) go(x3p_bwd_stream256_kernel<8, false>);
+      else go(x3p_bwd_stream256_kernel<16, false>);
+    }
+    return;
+  }
   const int total = 2 * p.nrt * (p.P + p.gx);
   const dim3 grid(std::min(total, a.blocks > 0 ? a.blocks : 96));
   auto go = [&](auto kern) {

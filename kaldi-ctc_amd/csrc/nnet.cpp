@@ -596,7 +596,8 @@ void CuDNNRecurrentComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
     int st = rnn_backward_weights(desc_, ws, T, N, in_value.Data(), out_value.Data(), workspace_.p,
                                   workspace_.bytes, to_update->grad_.f(), reserve_.p, reserve_.bytes,
                                   dev.side ? side_gemm_blocks() : 0, input_bound_,
-                                  (!in_deriv && dev.side) ? dev.stream2 : nullptr, packed_input_cols(T, N));
+                                  (!in_deriv && dev.side) ? dev.stream2 : nullptr, packed_input_cols(T, N),
+                                  in_deriv && dev.side);  // the next component's backward runs beside
     if (st) throw std::runtime_error("rnn_backward_weights failed: " + std::to_string(st));
   }
 }

@@ -79,6 +79,9 @@ int rnn_comm_cus();
 unsigned rnn_bwd_registrations();
 void rnn_comm_gate(hipStream_t s, unsigned target);
 unsigned rnn_comm_gate_errors();
+// device word: bit x set once an XCD-pinned backward recurrence ran on XCD x
+// (never cleared; GEMMs launched beside one avoid those XCDs, X3PArgs::avoid_word)
+const unsigned *rnn_pinned_xcds();
 void rnn_set_comm_gated(bool on);
 bool rnn_comm_gated();
 
@@ -167,6 +170,10 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
                          void *reserve, size_t res_bytes, int max_blocks = 0,
                          float in_bound = 0.f,  // > 0: |x| <= in_bound (an LSTM/GRU below)
                          hipStream_t s2 = nullptr,  // second stream: dW beside dR (nothing else to overlap)
-                         const void *in_cols = nullptr);  // bf16: x packed as columns (rnn_packed_output)
+                         const void *in_cols = nullptr,  // bf16: x packed as columns (rnn_packed_output)
+                         // runs beside another component's backward recurrence
+                         // (the side stream): dW and dR as one launch, kept
+                         // off the XCDs pinned recurrences run on
+                         bool beside = false);
 
 }  // namespace kctc

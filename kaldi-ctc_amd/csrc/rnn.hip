@@ -179,7 +179,7 @@ static PackLay pack_layout(const RnnDesc &d, int T, int N) {
   p.ec = o; o = align_up(o + sizeof(int) * ne, 256);
   p.ed = o; o = align_up(o + sizeof(int) * ne, 256);
   p.cm = o; o = align_up(o + sizeof(unsigned) * ne, 256);
-  p.part = o; o = align_up(o + sizeof(float) * TN * Dm, 256);            // backward stream partials
+  p.part = o; o = align_up(o + sizeof(float) * x3p_bwd_stream_part_floats((int)TN, (int)Dm), 256);  // backward stream partials
   p.cnt = o; o = align_up(o + sizeof(int) * x3p_bwd_stream_ints((int)TN, (int)Dm), 256);
   p.cme = o; o = align_up(o + sizeof(unsigned) * 2 * dirs * G, 256);  // dGates column maxima (v6 backward)
   // arrival counters of the direction-split streamed projection (this component as its consumer)
@@ -1658,7 +1658,10 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   const int grp = p.xpd ? (blockIdx.x & 7) / dirs : blockIdx.x / (dirs * NWG);
   if (d >= dirs || g >= NWG || grp >= p.rg) return;
   // resident: counted for the exchange's residency gate (rnn_comm_gate)
-  if (p.reg && threadIdx.x == 0) __hip_atomic_fetch_add(p.reg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (p.reg && threadIdx.x == 0) {
+    __hip_atomic_fetch_add(p.reg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (p.xpd) __hip_atomic_fetch_or(p.reg + 2, 1u << xcc_id(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // rnn_pinned_xcds
+  }
   // rows n0 .. nend-1 of the batch (p.gs <= 16 of the 16 MFMA rows)
   const int N = p.N, T = p.T, n0 = grp * p.gs, nend = min(N, n0 + p.gs);
   const int u0 = g * U, ct_own = u0 >> 4, fr0 = u0 & 15;
@@ -3528,6 +3531,7 @@ __global__ __launch_bounds__(64) void comm_gate_kernel(const unsigned *word, uns
 }
 
 unsigned rnn_bwd_registrations() { return reg_of_device().expected; }
+const unsigned *rnn_pinned_xcds() { return reg_of_device().word + 2; }
 void rnn_comm_gate(hipStream_t s, unsigned target) {
   RegWord &r = reg_of_device();
   hipLaunchKernelGGL(comm_gate_kernel, dim3(1), dim3(64), 0, s, r.word, target, r.word + 1);
@@ -3846,7 +3850,11 @@ void launch_bwd_stream(const RnnDesc &d, const RecParams &p, int l, const float 
   // before: 655.7k -> 670.7k frames/s); never more than the CU budget leaves
   // beside the recurrence and the exchange's kernels (rnn.h).  Blocks landing
   // on the pinned XCDs exit at once: launch enough that ~128 stay
-  const int nb = std::min(128, stream_block_budget(d.dirs * p.nwg * p.rg, true));
+  // 256-tile launch: 48 blocks keep up with the recurrence and leave the
+  // other CUs beside it to the weight GEMMs (rnn_backward_weights beside)
+  const bool t256 = x3p_bwd_stream_256(a.M, a.N, a.KB, bf);
+  const int nb = std::min(t256 ? env_int("KCTC_BWD_S256_BLOCKS", 64) : 128,
+                          stream_block_budget(d.dirs * p.nwg * p.rg, true));
   a.blocks = env_int("KCTC_BWD_STREAM_BLOCKS", pinned ? nb * 8 / (8 - pinned) : nb);
   // not before every workgroup of the recurrence is resident: its blocks
   // wait (on_pinned_xcd) for the pinned recurrence's XCDs to register, and a
@@ -4212,7 +4220,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
 int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *y, void *workspace, size_t ws_bytes, float *dw,
                          void *reserve, size_t res_bytes, int max_blocks, float in_bound, hipStream_t s2,
-                         const void *in_cols) {
+                         const void *in_cols, bool beside) {
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
   if (res_bytes < sizeof(float) * (size_t)lay.total) return KRNN_BAD_PARAM;
   if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
@@ -4345,26 +4353,44 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       // the transposes, packed over the frames: dGates^T (per-gate exponents),
       // input^T (per-dim), and for dR the output shifted by one step per direction
       ProfSpan ps(s, "x3_pack_w");
+      // beside a pinned recurrence: off its XCDs (x3p_pack_cols avoid)
+      const unsigned *av = beside && env_int("KCTC_PACK_AVOID", 1) ? rnn_pinned_xcds() : nullptr;
+      const int nx = std::max(1, rnn_usable_cus() / kCusPerXcd);
+      // their item counters: flag words 1010..1014 (this component's
+      // recurrences, which use the flag words, are done)
+      int *pc = reinterpret_cast<int *>(fl + 1010);
+      if (av) KCTC_HIP_CHECK(hipMemsetAsync(pc, 0, sizeof(int) * 5, s));
       // the v6 backward recurrence leaves the dGates column maxima behind
       const unsigned *cme = cme0;
       if (!cme) absmax_f32(s, DX, ldg, (int)TN, (int)(dirs * G4), nullptr, cm);
-      x3p_pack_cols(s, DX, ldg, (int)TN, (int)(dirs * G4), 0, DXt, eDX, cme ? cme : cm, 0.f);
+      x3p_pack_cols(s, DX, ldg, (int)TN, (int)(dirs * G4), 0, DXt, eDX, cme ? cme : cm, 0.f, 1, 0, 0, 0, 0, av, nx,
+                    pc);
       if (d.mode == kGru) {
         if (!cme) absmax_f32(s, E, ldg, (int)TN, (int)(dirs * G4), nullptr, cm);
-        x3p_pack_cols(s, E, ldg, (int)TN, (int)(dirs * G4), 0, Et, eE, cme ? cme + dirs * G4 : cm, 0.f);
+        x3p_pack_cols(s, E, ldg, (int)TN, (int)(dirs * G4), 0, Et, eE, cme ? cme + dirs * G4 : cm, 0.f, 1, 0, 0, 0,
+                      0, av, nx, pc + 1);
       }
       const bool xb = (l > 0 && bounded_out(d)) || (l == 0 && in_bound > 0.f);
       if (!xb) absmax_f32(s, in, Din, (int)TN, Din, nullptr, cm);
-      x3p_pack_cols(s, in, Din, (int)TN, Din, 0, Xt, eX, cm, xb ? (l > 0 ? 1.f : in_bound) : 0.f);
+      x3p_pack_cols(s, in, Din, (int)TN, Din, 0, Xt, eX, cm, xb ? (l > 0 ? 1.f : in_bound) : 0.f, 1, 0, 0, 0, 0, av,
+                    nx, pc + 2);
       if (T > 1) {
         if (!bounded_out(d)) absmax_f32(s, out, ldy, (int)TN, (int)ldy, nullptr, cm);
         for (int dir = 0; dir < dirs; dir++)
           x3p_pack_cols(s, out + (long)dir * H, ldy, (int)TN, H, dir == 0 ? N : -N, Yt + (long)dir * H * KBt * 64,
-                        eY + dir * H, bounded_out(d) ? nullptr : cm + dir * H, bounded_out(d) ? 1.f : 0.f);
+                        eY + dir * H, bounded_out(d) ? nullptr : cm + dir * H, bounded_out(d) ? 1.f : 0.f, 1, 0, 0,
+                        0, 0, av, nx, pc + 3 + dir);
       }
     }
+    // beside another component's pinned backward recurrence: dW and dR as
+    // one launch on the CUs it leaves (gemm_x3p_pair; configs[1]: the side
+    // stream fell one GEMM per layer behind, 4 ms of weight GEMMs after the
+    // last recurrence)
+    const bool pair = beside && x3 && !two && T > 1 && x3p_use_256((int)G4, Din) && x3p_use_256((int)G4, H) &&
+                      max_blocks > 0 && env_int("KCTC_WGRAD_PAIR", 1);
+    X3PArgs xw;
     if (x3) {
-      X3PArgs x;
+      X3PArgs &x = xw;
       x.M = (int)G4; x.N = Din; x.KB = KBt;
       x.A = DXt; x.eA = eDX; x.sA = G4 * KBt * 64; x.seA = G4;
       x.B = Xt; x.eB = eX;
@@ -4374,10 +4400,16 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       // concurrent with dR: its own split slab past dR's (none when dR is not
       // split: drec_split_floats reserves a dR slab only for a split > 1)
       const long sR = x3p_pick_split((int)G4, H, KBt, dirs);
-      x.ws = two && sR > 1 ? ws + al64(sR * dirs * G4 * H) : ws;
+      x.ws = (two || pair) && sR > 1 ? ws + al64(sR * dirs * G4 * H) : ws;
       x.max_blocks = g.max_blocks; x.tile_counter = g.tile_counter;
-      ProfSpan ps(sx, "gemm_bwd_w");
-      gemm_x3p(sx, x);
+      if (pair) {
+        x.max_blocks = env_int("KCTC_SIDE_BESIDE_BLOCKS", 192);
+        x.avoid_word = rnn_pinned_xcds();
+        x.avoid_xcds = std::max(1, rnn_usable_cus() / kCusPerXcd);
+      } else {
+        ProfSpan ps(sx, "gemm_bwd_w");
+        gemm_x3p(sx, x);
+      }
     } else {
       ProfSpan ps(s, "gemm_bwd_w");
       gemm_f32(s, g);
@@ -4410,7 +4442,8 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
         x.batch = dirs; x.sC = pls;
         x.split_k = x3p_pick_split((int)G4, H, KBt, dirs); x.ws = ws;
         x.max_blocks = max_blocks; x.tile_counter = r.tile_counter;
-        gemm_x3p(s, x);
+        if (pair) gemm_x3p_pair(s, xw, x);  // xw's tile counter, block count and avoid word
+        else gemm_x3p(s, x);
       } else {
         gemm_f32(s, r);
       }

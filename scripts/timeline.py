@@ -19,7 +19,8 @@ idle = 0.0
 for r in seg:
     s = (int(r["Start_Timestamp"]) - t0) / 1e3
     e = (int(r["End_Timestamp"]) - t0) / 1e3
-    name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("kctc::", "")[:58]
+    name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").replace("kctc::", "")
+    name = name.split("(")[0][:58]
     gap = ""
     if r["Queue_Id"] == rec_q:
         if busy_end is not None and s > busy_end:
