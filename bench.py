@@ -386,8 +386,6 @@ def main():
                    else "gradient sum every step"}
 
     lm = None
-    if rank == 0 and not args.no_loss_match and (T, N, H, L) == (cf["T"], cf["N"], cf["H"], 5):
-        lm = loss_match(k, dev, {1: "cfg1", 2: "cfg2", 4: "cfg4"}[args.config])
 
     total = args.warmup + args.steps
     batches, host_batches = [], []
@@ -597,6 +595,12 @@ def main():
                                     "note": "the same K steps with per-family HIP events (the roofline's "
                                             "source); not `value`"}
         roof["secondary"] = aux
+
+    # after the timed passes: with this second Nnet created and freed before
+    # them, the trainer's recurrences ran 2-4 % slower (configs[1]: 727.8k vs
+    # 752.2k frames/s, same box, profiles/r05e_lossmatch_ab.txt)
+    if rank == 0 and not args.no_loss_match and (T, N, H, L) == (cf["T"], cf["N"], cf["H"], 5):
+        lm = loss_match(k, dev, {1: "cfg1", 2: "cfg2", 4: "cfg4"}[args.config])
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -160,6 +160,14 @@ struct X3PBwdStream {
   // xcd_count XCDs are registered and exits if it is on one of them
   const unsigned *xcd_word = nullptr;
   int xcd_count = 0;
+  // FORWARD producer (the next component's input projection streamed off a
+  // v6 forward's y rows, written through with the same epochs): direction 0
+  // walks the frames upwards, 1 downwards; C += bias + bias2 of column c at
+  // (c / bias_cols) * sbias + c % bias_cols.  256-tile launches only.
+  bool forward = false;
+  const float *bias = nullptr, *bias2 = nullptr;
+  int bias_cols = 1;
+  long sbias = 0;
 };
 size_t x3p_bwd_stream_ints(int M, int N);
 // the launch runs on 256 x 256 tiles (512 threads, 128 KB LDS per block);

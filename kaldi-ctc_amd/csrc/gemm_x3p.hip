@@ -79,6 +79,10 @@ struct PParams {
   int mt;                  // row tiles
   const unsigned *avoid;   // X3PArgs::avoid_word, avoid_xcds
   int nxcd;
+  // row stream (x3p_bwd_stream256_kernel) off a FORWARD producer: direction 0
+  // frames ascending, direction 1 descending; bias + bias2 of column c at
+  // (c / bcols) * sBias + c % bcols, added by the second partial
+  int fwdp, bcols;
 };
 
 
@@ -1321,10 +1325,16 @@ __device__ __forceinline__ void p256_bwd_tile(const PParams &p, unsigned char *l
             floatx4, __builtin_amdgcn_raw_buffer_load_b128(rp, ((i * 4 + j) * NTH2 + (int)threadIdx.x) * 16, 0, 16));
         const int col = n0 + wn + j * 16 + fr;
         if (col >= p.N) continue;
+        float badd = 0.f;  // (as gemm_x3p's epilogue: bias, then bias2)
+        if (p.bias) {
+          const long bo = (long)(col / p.bcols) * p.sBias + col % p.bcols;
+          badd += p.bias[bo];
+          if (p.bias2) badd += p.bias2[bo];
+        }
 #pragma unroll
         for (int r = 0; r < 4; r++) {
           const int row = m0 + wm + i * 16 + fq * 4 + r;
-          if (row < p.M) p.C[(long)row * p.ldc + col] = acc[i][j][r] + o[r];
+          if (row < p.M) p.C[(long)row * p.ldc + col] = p.bias ? (acc[i][j][r] + o[r]) + badd : acc[i][j][r] + o[r];
         }
       }
   }
@@ -1350,13 +1360,17 @@ __global__ __launch_bounds__(NTH2, 1) void x3p_bwd_stream256_kernel(PParams p) {
     __syncthreads();
     if (id >= total) break;
     const int slot = id / J, r = id - slot * J, d = slot & 1, rank = slot >> 1;
-    const int rt = d == 0 ? p.nrt - 1 - rank : rank;
+    // the producer's direction that walks the frames downwards takes the
+    // row tiles from the last (a backward producer's direction 0, a forward
+    // producer's direction 1)
+    const bool down = (d == 0) != (p.fwdp != 0);
+    const int rt = down ? p.nrt - 1 - rank : rank;
     if (r < p.P) {
       const int ra = rt * TB2 + r * rows_per, rb = min(p.M, ra + rows_per);
       if (ra < rb) {
         // E rows of step s are complete at epoch s + 3 (the last step's at T + 2)
         const int ta = ra / p.sN, tb = (rb - 1) / p.sN;
-        wait_epoch(p, d, d == 0 ? p.sT + 2 - ta : tb + 3, seen);
+        wait_epoch(p, d, down ? p.sT + 2 - ta : tb + 3, seen);
         bwd_pack_rows<KW, BFM, NTH2 / 64>(p, d, ra, rb);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1371,23 +1385,24 @@ __global__ __launch_bounds__(NTH2, 1) void x3p_bwd_stream256_kernel(PParams p) {
   }
 }
 
-// Column packing (transpose): packed row c = column c of X, K = X's rows
-// (k -> X row k - shift, zero outside [0, R)).  Exponent from cmax[c] (max |x|
-// of the column, float bits) or the bound.  Block: 64 columns x one 32-k block.
+// one item: 64 columns x KPI consecutive 32-k blocks (KPI = 4, 512
+// contiguous bytes per packed row, measured slower: configs[1] dGates^T
+// 351 -> 511 us, fewer blocks in flight)
+constexpr int KPI = 1;
 __device__ __forceinline__ void pack_cols_item(const float *__restrict__ X, long ldx, int R, int Cn, int KB, int shift,
                                                long sX, _Float16 *__restrict__ out, long sOut, int *__restrict__ eout,
                                                long sE, const unsigned *__restrict__ cmax, long sCm, float bound,
-                                               int bx, int kb, int b, float (*tile)[65]) {
-  const int c0 = bx * 64;
+                                               int bx, int kq, int b, float (*tile)[65]) {
+  const int c0 = bx * 64, kb0 = kq * KPI;
   const float *x = X + (long)b * sX;
   const int t = threadIdx.x;
-  // load 32 rows x 64 columns (each row: 64 consecutive floats)
+  // load KPI * 32 rows x 64 columns (each row: 64 consecutive floats)
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
+  for (int i = 0; i < 8 * KPI; i++) {
     const int kr = (t >> 6) + 4 * i, cc = t & 63;
-    const int src = kb * 32 + kr - shift;
+    const int k = kb0 * 32 + kr, src = k - shift;
     float v = 0.f;
-    if (kb * 32 + kr < R && src >= 0 && src < R && c0 + cc < Cn) v = x[(long)src * ldx + c0 + cc];
+    if (k < R && src >= 0 && src < R && c0 + cc < Cn) v = x[(long)src * ldx + c0 + cc];
     tile[kr][cc] = v;
   }
   __syncthreads();
@@ -1395,24 +1410,28 @@ __device__ __forceinline__ void pack_cols_item(const float *__restrict__ X, long
   if (c0 + c < Cn) {
     const int e = bound > 0.f ? split_exp_d(bound)
                               : split_exp_d(__uint_as_float(cmax[(long)b * sCm + c0 + c]));
-    halfx8 h, l;
+    _Float16 *o = out + (long)b * sOut + ((long)(c0 + c) * KB + kb0) * 64;
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const float xv = ldexpf(tile[part * 8 + j][c], e);
-      h[j] = (_Float16)xv;
-      l[j] = (_Float16)(xv - (float)h[j]);
+    for (int q = 0; q < KPI; q++) {
+      if (kb0 + q >= KB) break;
+      halfx8 h, l;
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const float xv = ldexpf(tile[q * 32 + part * 8 + j][c], e);
+        h[j] = (_Float16)xv;
+        l[j] = (_Float16)(xv - (float)h[j]);
+      }
+      *reinterpret_cast<halfx8 *>(o + q * 64 + part * 8) = h;
+      *reinterpret_cast<halfx8 *>(o + q * 64 + 32 + part * 8) = l;
     }
-    _Float16 *o = out + (long)b * sOut + ((long)(c0 + c) * KB + kb) * 64;
-    *reinterpret_cast<halfx8 *>(o + part * 8) = h;
-    *reinterpret_cast<halfx8 *>(o + 32 + part * 8) = l;
-    if (kb == 0 && part == 0 && eout) eout[(long)b * sE + c0 + c] = e;
+    if (kb0 == 0 && part == 0 && eout) eout[(long)b * sE + c0 + c] = e;
   }
 }
 
 // Column packing (transpose): packed row c = column c of X, K = X's rows
 // (k -> X row k - shift, zero outside [0, R)).  Exponent from cmax[c] (max |x|
-// of the column, float bits) or the bound.  Item: 64 columns x one 32-k block
-// (grid (columns / 64, KB, batch)).  With `avoid` (beside a pinned
+// of the column, float bits) or the bound.  Item: 64 columns x KPI 32-k blocks
+// (grid (columns / 64, KB / KPI, batch)).  With `avoid` (beside a pinned
 // recurrence, X3PArgs::avoid_word) a 1-D grid takes runs of 8 items from
 // a zeroed counter and the blocks on the recurrence's XCDs leave at once: a
 // stream of short blocks cycling through its CUs kept the recurrence's
@@ -1423,7 +1442,7 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
                                                         int *__restrict__ eout, long sE,
                                                         const unsigned *__restrict__ cmax, long sCm, float bound,
                                                         const unsigned *avoid, int nxcd, int batch, int *counter) {
-  __shared__ float tile[32][65];
+  __shared__ float tile[32 * KPI][65];
   __shared__ int bc;
   if (!avoid) {
     pack_cols_item(X, ldx, R, Cn, KB, shift, sX, out, sOut, eout, sE, cmax, sCm, bound, blockIdx.x, blockIdx.y,
@@ -1434,8 +1453,8 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
   q.avoid = avoid;
   q.nxcd = nxcd;
   if (avoid_here(q, &bc)) return;
-  const int gx = (Cn + 63) / 64;
-  const int items = gx * KB * batch;
+  const int gx = (Cn + 63) / 64, KQ = (KB + KPI - 1) / KPI;
+  const int items = gx * KQ * batch;
   while (true) {
     __syncthreads();  // bc and the tile are reused
     if (threadIdx.x == 0) bc = atomicAdd(counter, 8);
@@ -1444,7 +1463,7 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
     if (i0 >= items) break;
     for (int it = i0; it < min(items, i0 + 8); it++) {
       const int bx = it % gx, r = it / gx;
-      pack_cols_item(X, ldx, R, Cn, KB, shift, sX, out, sOut, eout, sE, cmax, sCm, bound, bx, r % KB, r / KB, tile);
+      pack_cols_item(X, ldx, R, Cn, KB, shift, sX, out, sOut, eout, sE, cmax, sCm, bound, bx, r % KQ, r / KQ, tile);
       __syncthreads();
     }
   }
@@ -1556,14 +1575,14 @@ void x3p_pack_cols(hipStream_t s, const float *X, long ldx, int R, int Cn, int s
   if (R <= 0 || Cn <= 0 || batch <= 0) return;
   const int KB = (R + 31) / 32;
   if (avoid) {
-    const long items = (long)ceil_div(Cn, 64) * KB * batch;
+    const long items = (long)ceil_div(Cn, 64) * ceil_div(KB, KPI) * batch;
     if (!counter || items + 8 >= (1L << 31)) throw std::invalid_argument("x3p_pack_cols: avoid needs a counter");
     hipLaunchKernelGGL(pack_cols_kernel, dim3((int)std::min<long>((items + 7) / 8, 1024)), dim3(256), 0, s, X, ldx, R,
                        Cn, KB, shift, sX, out, sOut, eout, sE, cmax, sCm, bound, avoid, nxcd, batch, counter);
     return;
   }
-  hipLaunchKernelGGL(pack_cols_kernel, dim3(ceil_div(Cn, 64), KB, batch), dim3(256), 0, s, X, ldx, R, Cn, KB, shift,
-                     sX, out, sOut, eout, sE, cmax, sCm, bound, nullptr, 0, batch, nullptr);
+  hipLaunchKernelGGL(pack_cols_kernel, dim3(ceil_div(Cn, 64), ceil_div(KB, KPI), batch), dim3(256), 0, s, X, ldx, R,
+                     Cn, KB, shift, sX, out, sOut, eout, sE, cmax, sCm, bound, nullptr, 0, batch, nullptr);
 }
 
 namespace {
@@ -1806,8 +1825,12 @@ void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a) {
   p.xcd_word = a.xcd_word; p.xcd_count = a.xcd_count;
   p.backoff = env_backoff();
   p.dbg = getenv("KCTC_STREAM_DBG") ? atoi(getenv("KCTC_STREAM_DBG")) : 0;
+  p.fwdp = a.forward ? 1 : 0;
+  p.bias = a.bias; p.bias2 = a.bias2; p.bcols = a.bias_cols > 0 ? a.bias_cols : 1; p.sBias = a.sbias;
+  const bool t256 = x3p_bwd_stream_256(a.M, a.N, a.KB, a.bf16);
+  if ((a.forward || a.bias) && !t256) throw std::invalid_argument("gemm_x3p_bwd_stream: forward producer needs 256 tiles");
   KCTC_HIP_CHECK(hipMemsetAsync(a.cnt, 0, sizeof(int) * x3p_bwd_stream_ints(a.M, a.N), s));
-  if (x3p_bwd_stream_256(a.M, a.N, a.KB, a.bf16)) {
+  if (t256) {
     p.gx = ceil_div(a.N, TB2); p.nrt = ceil_div(a.M, TB2);
     p.tiles = p.gx * p.nrt;
     p.done = a.cnt + 1; p.arrive = a.cnt + 1 + 2 * p.nrt;  // within x3p_bwd_stream_ints (128-tile counts)

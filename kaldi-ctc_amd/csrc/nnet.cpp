@@ -412,6 +412,7 @@ CuDNNRecurrentComponent::CuDNNRecurrentComponent() {
 CuDNNRecurrentComponent::~CuDNNRecurrentComponent() {
   if (err_) (void)hipFree(err_);
   if (pre_.ev) (void)hipEventDestroy(pre_.ev);
+  if (pre_.wev) (void)hipEventDestroy(pre_.wev);
 }
 
 void CuDNNRecurrentComponent::InitFromString(std::string args, Rng &rng) {
@@ -515,12 +516,20 @@ void CuDNNRecurrentComponent::Forward(const CuMatrixBase &in, CuMatrixBase *out,
   auto &dev = CuDevice::Instantiate();
   hipStream_t side = S() == dev.stream ? dev.side : nullptr;
   RnnPrepack *pre = nullptr;
-  if (prepack_dx_ && side) {
+  if ((prepack_dx_ || prepack_w_) && side) {
     if (!pre_.ev) KCTC_HIP_CHECK(hipEventCreateWithFlags(&pre_.ev, hipEventDisableTiming));
-    pre_.stream = side;
+    if (!pre_.wev) KCTC_HIP_CHECK(hipEventCreateWithFlags(&pre_.wev, hipEventDisableTiming));
+    // the dx-stream queue (idle in the forward pass): the side stream carries
+    // the next component's projection streamed off this recurrence
+    pre_.stream = dev.stream2 ? dev.stream2 : side;
+    pre_.dx = prepack_dx_;
+    pre_.wgrad = prepack_w_;
+    pre_.in_bound = input_bound_;
     pre = &pre_;
   }
-  pre_.done = false;
+  pre_.done = pre_.wdone = false;
+  pre_x_ = in.Data();
+  pre_y_ = out->Data();
   int st = rnn_forward_training(desc_, S(), T, N, in.Data(), params_.f(), out->Data(), workspace_.p,
                                 workspace_.bytes, reserve_.p, reserve_.bytes, DeviceError(), chain, projected, in_rows_,
                                 side, pre);
@@ -563,7 +572,8 @@ void CuDNNRecurrentComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
       ProfScope ps("layer_rnn_backward_weights", ws);
       int st = rnn_backward_weights(desc_, ws, T, N, in_value.Data(), out_value.Data(), workspace_.p,
                                     workspace_.bytes, to_update->grad_.f(), reserve_.p, reserve_.bytes,
-                                    side_gemm_blocks(), input_bound_, nullptr, packed_input_cols(T, N));
+                                    side_gemm_blocks(), input_bound_, nullptr, packed_input_cols(T, N), false,
+                                    wgrad_prepack(in_value, out_value));
       if (st) throw std::runtime_error("rnn_backward_weights failed: " + std::to_string(st));
     }
     return;
@@ -597,9 +607,16 @@ void CuDNNRecurrentComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
                                   workspace_.bytes, to_update->grad_.f(), reserve_.p, reserve_.bytes,
                                   dev.side ? side_gemm_blocks() : 0, input_bound_,
                                   (!in_deriv && dev.side) ? dev.stream2 : nullptr, packed_input_cols(T, N),
-                                  in_deriv && dev.side);  // the next component's backward runs beside
+                                  in_deriv && dev.side,  // the next component's backward runs beside
+                                  wgrad_prepack(in_value, out_value));
     if (st) throw std::runtime_error("rnn_backward_weights failed: " + std::to_string(st));
   }
+}
+
+// x^T / y^T packed by the last forward, if this backward is for that forward's data
+const RnnPrepack *CuDNNRecurrentComponent::wgrad_prepack(const CuMatrixBase &in_value,
+                                                         const CuMatrixBase &out_value) const {
+  return pre_.wdone && in_value.Data() == pre_x_ && out_value.Data() == pre_y_ ? &pre_ : nullptr;
 }
 
 bool CuDNNRecurrentComponent::PackedOutput(const void **rows, const void **cols) const {
@@ -1590,6 +1607,7 @@ void NnetCtcUpdater::Propagate(int T, int N) {  // :136-169
       r->SetPackedInput(rows, cols);
       // Backprop computes its input derivative (streamed dx GEMM): W^T packed now
       r->SetPrepackDx(update_ && c > first);
+      r->SetPrepackW(update_ && c >= first);
       below = r;
     } else if (!comp.IsIdentityForward()) {
       below = nullptr;

@@ -280,6 +280,9 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   // the updater marks the RNNs whose Backprop computes an input derivative:
   // their forward packs W^T for it on the side stream (rnn.h RnnPrepack)
   void SetPrepackDx(bool on) const { prepack_dx_ = on; }
+  // ... and the RNNs it updates: their forward packs x^T / y^T for the weight
+  // GEMMs on the side stream (RnnPrepack::wgrad)
+  void SetPrepackW(bool on) const { prepack_w_ = on; }
   // device error word of the recurrences (hand-off timeout); the updater
   // points every RNN at its own per-step word (SetErrorWord)
   unsigned *DeviceError() const { return err_ext_ ? err_ext_ : err_; }
@@ -287,6 +290,7 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   // workgroup cap of the side-stream weight GEMMs: the CUs left over by the
   // backward recurrence (KCTC_SIDE_BLOCKS overrides)
   int side_gemm_blocks() const;
+  const RnnPrepack *wgrad_prepack(const CuMatrixBase &in_value, const CuMatrixBase &out_value) const;
   const RnnDesc &Desc() const { return desc_; }
   // arithmetic of the recurrences and gate GEMMs (rnn.h RnnDesc::prec); the
   // parameters and the model file stay fp32
@@ -334,8 +338,9 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   unsigned *err_ = nullptr;
   mutable unsigned *err_ext_ = nullptr;
   // W^T packed by the last forward (RnnPrepack) for parameter version pre_ver_
-  mutable bool prepack_dx_ = false;
+  mutable bool prepack_dx_ = false, prepack_w_ = false;
   mutable RnnPrepack pre_;
+  mutable const float *pre_x_ = nullptr, *pre_y_ = nullptr;  // the forward's input / output (pre_.wdone)
   mutable unsigned pre_ver_ = 0;
   unsigned pver_ = 1;  // bumped by every parameter write
   void Forward(const CuMatrixBase &in, CuMatrixBase *out, RnnFwdChain *chain) const;

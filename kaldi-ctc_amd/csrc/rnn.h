@@ -129,6 +129,16 @@ struct RnnPrepack {
   hipStream_t stream = nullptr;
   hipEvent_t ev = nullptr;
   bool done = false;
+  // the weight GEMMs' input^T and output^T (x and y packed along the frames,
+  // one-layer split-fp16 components with bounded x and y): packed on `stream`
+  // by the forward -- x beside its recurrence, y after it -- instead of on the
+  // backward's side stream, where the CUs beside the next component's
+  // recurrence are short (wev: recorded after both; wdone: packed)
+  hipEvent_t wev = nullptr;
+  bool dx = true;        // W^T (ev / done) requested
+  bool wgrad = false;    // requested
+  float in_bound = 0.f;  // |x| <= in_bound (> 0 required)
+  bool wdone = false;
 };
 int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *w, float *y, void *workspace, size_t ws_bytes,
@@ -174,6 +184,7 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
                          // runs beside another component's backward recurrence
                          // (the side stream): dW and dR as one launch, kept
                          // off the XCDs pinned recurrences run on
-                         bool beside = false);
+                         bool beside = false,
+                         const RnnPrepack *pre = nullptr);  // wdone: x^T / y^T packed by the forward
 
 }  // namespace kctc

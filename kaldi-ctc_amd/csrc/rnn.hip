@@ -159,7 +159,7 @@ static size_t xch_bytes(const RnnDesc &d, int T, int N) {
 //               shifted output^T [dirs*H][TN]
 // plus int exponents and float-bit column maxima (G = nW*H).
 struct PackLay {
-  size_t a, b, c, d, ea, eb, ec, ed, cm, part, cnt, cme, fcnt, fpart, gtf, wt, ewt, cmw, total;
+  size_t a, b, c, d, ea, eb, ec, ed, cm, part, cnt, cme, fcnt, fpart, gtf, wt, ewt, cmw, xt, yt, ext, eyt, total;
 };
 static PackLay pack_layout(const RnnDesc &d, int T, int N) {
   const long TN = (long)T * N, G = (long)d.nw() * d.H, Dm = std::max(d.D, d.dirs * d.H), dirs = d.dirs;
@@ -180,11 +180,14 @@ static PackLay pack_layout(const RnnDesc &d, int T, int N) {
   p.ed = o; o = align_up(o + sizeof(int) * ne, 256);
   p.cm = o; o = align_up(o + sizeof(unsigned) * ne, 256);
   p.part = o; o = align_up(o + sizeof(float) * x3p_bwd_stream_part_floats((int)TN, (int)Dm), 256);  // backward stream partials
-  p.cnt = o; o = align_up(o + sizeof(int) * x3p_bwd_stream_ints((int)TN, (int)Dm), 256);
+  // (also the row stream of this component's projection off the previous
+  // component's forward, launch_chain_rows: N = dirs * G columns)
+  p.cnt = o; o = align_up(o + sizeof(int) * x3p_bwd_stream_ints((int)TN, (int)std::max(Dm, dirs * G)), 256);
   p.cme = o; o = align_up(o + sizeof(unsigned) * 2 * dirs * G, 256);  // dGates column maxima (v6 backward)
   // arrival counters of the direction-split streamed projection (this component as its consumer)
   p.fcnt = o; o = align_up(o + sizeof(int) * ((TN + 127) / 128 * dirs * ((G + 127) / 128) + 64), 256);
-  p.fpart = o; o = align_up(o + sizeof(float) * ((TN + 127) / 128) * dirs * ((G + 127) / 128) * 128 * 128, 256);
+  p.fpart = o; o = align_up(o + sizeof(float) * std::max((size_t)((TN + 127) / 128) * dirs * ((G + 127) / 128) * 128 * 128,
+                                                          x3p_bwd_stream_part_floats((int)TN, (int)(dirs * G))), 256);
   // consumer-gated projection: its tile counter (word 0), then the tile flags
   // [dirs][row tiles][column tiles] from word 64 (never reset: a call's id)
   p.gtf = o; o = align_up(o + sizeof(unsigned) * (64 + dirs * ((TN + 255) / 256) * ((G + 255) / 256)), 256);
@@ -193,6 +196,11 @@ static PackLay pack_layout(const RnnDesc &d, int T, int N) {
   p.wt = o; o = align_up(o + x3p_bytes(dirs * Dm, G), 256);
   p.ewt = o; o = align_up(o + sizeof(int) * (dirs * Dm + 64), 256);
   p.cmw = o; o = align_up(o + sizeof(unsigned) * (dirs * Dm + 64), 256);
+  // x^T / y^T of the weight GEMMs, packed by the forward (RnnPrepack::wgrad)
+  p.xt = o; o = align_up(o + bw_b, 256);
+  p.yt = o; o = align_up(o + bw_c, 256);
+  p.ext = o; o = align_up(o + sizeof(int) * (Dm + 64), 256);
+  p.eyt = o; o = align_up(o + sizeof(int) * (dirs * d.H + 64), 256);
   p.total = o;
   return p;
 }
@@ -311,6 +319,8 @@ struct RecParams {
   int poll_sleep;   // v6: s_sleep between flag polls
   int gla;          // v6 forward IO waves: steps ahead the G rows are fetched (3 or 7; 8 LDS slots)
   int e_sc1;        // v6 backward: dGates rows written through (sc1) for a streaming consumer
+  int ysc1;         // v6 forward: y rows written through (sc1) and the aggregated epochs published
+                    // for the next component's projection streamed off them (launch_chain_rows)
   int bfpart;       // v6 backward, bf16 mode: partial dh exchanged as bf16 (KCTC_BF16_PARTIALS)
   unsigned *cmax;   // v6 backward: column max |DX| [dirs * nW * H] (GRU: then |E|), as float bits
   unsigned *reg;    // v6 backward: per-device registration word (+1 per workgroup at start)
@@ -2458,7 +2468,9 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   };
   auto out_store = [&](int t) {  // row-major y, activations (in place of G), aux of step t
     if (!live) return;
-    p.y[((long)t * N + n) * ldy + (long)d * H + u0 + eu] = hval;
+    if (p.ysc1) __hip_atomic_store(p.y + ((long)t * N + n) * ldy + (long)d * H + u0 + eu, hval, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);  // read by other XCDs during this kernel
+    else p.y[((long)t * N + n) * ldy + (long)d * H + u0 + eu] = hval;
     const long grow = ((long)t * N + n) * ldg + (long)d * NW * H + u0 + eu;
 #pragma unroll
     for (int q = 0; q < NW; q++) p.G[grow + q * H] = act[q];
@@ -2603,7 +2615,12 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // off a pinned producer: the dead code of it in the other variants changed
   // their schedules -- U = 32 forward 3.19 -> 4.0 us/step at configs[2])
   const bool fcopy = IOW && p.xpd && p.fcopy;
-  unsigned *gflag = (fcopy && g == 0) ? agg_flag6(p, grp, d) : nullptr;
+  // y rows streamed (p.ysc1): step m's y goes out in step m + 1, behind that
+  // step's hand-off loads, so it has landed once the workgroup publishes step
+  // m + 2; workgroup 0 has every producer's step k - 1 image in step k, so
+  // gflag = k there means rows of steps <= k - 3 are out ("epoch s + 3" as
+  // the backward's rows), T + 2 at exit
+  unsigned *gflag = ((fcopy || p.ysc1) && g == 0) ? agg_flag6(p, grp, d) : nullptr;
   if (p.xpd && tid == 0) atomicOr(p.flags + kXcdWord, 1u << xcc_id());
   // gated projection: tell the GEMM's blocks which XCDs this launch holds
   // (this call's id in the tag word of the XCD; they leave those XCDs)
@@ -2925,13 +2942,15 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
       out_store(t_prev);
     }
   }
-  if (fcopy && !bad) {  // the last step's copy, then (workgroup 0) every producer's, then the epoch
-    if (pub) __builtin_amdgcn_raw_buffer_store_b128(pv, rsrc(xch + (long)t_prev * XS, (unsigned)(XS * sizeof(AT))),
-                                                    (int)(po * sizeof(AT)), 0, 16);
+  if ((fcopy || p.ysc1) && !bad) {  // the last step's copy / rows, then (workgroup 0) every producer's, then the epoch
+    if (fcopy && pub)
+      __builtin_amdgcn_raw_buffer_store_b128(pv, rsrc(xch + (long)t_prev * XS, (unsigned)(XS * sizeof(AT))),
+                                             (int)(po * sizeof(AT)), 0, 16);
     signal_epoch(myflag, (unsigned)(T + 2), local);
     if (gflag) {
       wait_flags6(flag6(p, grp, d, 0, NWG), NWG, (unsigned)(T + 2), p.err, bad, &bad_lds, p.poll_sleep);
-      if (!bad && tid == 0) __hip_atomic_store(gflag, (unsigned)(T + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!bad && tid == 0)
+        __hip_atomic_store(gflag, (unsigned)(fcopy ? T + 1 : T + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   asm volatile("" ::"v"(pv));
@@ -3475,6 +3494,77 @@ void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
   c.done = true;
 }
 
+// Can `c`'s layer-0 projection stream off this component's y rows
+// (launch_chain_rows)?  Split-fp16 into split-fp16, the 256-tile row stream.
+bool chain_rows_ok(const RnnDesc &d, int ver, int T, int N, const RnnFwdChain *c) {
+  if (!c || !c->d || !c->side || ver != 6 || d.dirs != 2 || d.prec == kPrecBf16 || !env_int("KCTC_FWD_ROWS", 1))
+    return false;
+  const RnnDesc &n = *c->d;
+  const long TN = (long)T * N;
+  if (n.D != d.dirs * d.H || n.prec != d.prec || !use_x3(n.D) || d.H % 32 || d.H > 4096 || T < 2) return false;
+  if (!x3p_bwd_stream_256((int)TN, n.dirs * n.nw() * n.H, d.H / 32, false)) return false;
+  if (TN * n.dirs * n.nw() * n.H * 4 >= (1L << 31) || TN * (d.H / 32) * 128 >= (1L << 31)) return false;
+  // at N <= 16 (configs[1]); larger batches run the 256-tile GEMM after the
+  // recurrence (shorter recurrences, less time to hide the GEMM behind)
+  if (N > 16 && !env_int("KCTC_STREAM_ALL", 0)) return false;
+  const V6Cfg c6 = pick6(d, N, true);
+  if (!c6 || !stream_block_budget(d.dirs * (d.H / c6.U) * c6.rg, false)) return false;
+  return c->ws_bytes >= rnn_workspace_bytes(n, T, N) &&
+         c->res_bytes >= sizeof(float) * (size_t)rnn_reserve_layout(n, T, N).total;
+}
+
+// The consumer's layer-0 projection G' = [y_fwd | y_bwd] W'^T + b' streamed
+// off this forward recurrence's y rows (written through, p.ysc1): the
+// direction-split row stream of gemm_x3p_bwd_stream with a forward producer --
+// the K half of direction 0 of frame t is out at producer step t, direction
+// 1's at step T - 1 - t, so each 256 x 256 tile of G' is two half-K jobs whose
+// partials meet (plus the biases) in the second.  The K halves of W' are
+// packed as rows of their own (per-half exponents).
+void launch_chain_rows(const RnnDesc &d, const RecParams &p, hipEvent_t fork, int T, int N, RnnFwdChain &c,
+                       unsigned *err) {
+  KCTC_HIP_CHECK(hipStreamWaitEvent(c.side, fork, 0));  // after the producer's flag reset
+  const RnnDesc &n = *c.d;
+  const int NW = n.nw(), G = NW * n.H, H = d.H, KBh = H / 32, Din = n.D;
+  const long TN = (long)T * N;
+  const long pl0 = n.lin_offset(0, 0, false), pls = n.pl_size(0);
+  const float *wl = c.w + pl0;
+  const PackLay pl = pack_layout(n, T, N);
+  _Float16 *Bp = pk<_Float16>(c.workspace, n, T, N, pl.b);
+  int *eB = pk<int>(c.workspace, n, T, N, pl.eb);
+  const long sB = (long)n.dirs * G * KBh * 64;
+  {
+    ProfSpan ps(c.side, "x3_pack_chain");
+    for (int h = 0; h < 2; h++)  // K half h of the rows of both consumer directions
+      x3p_pack_rows(c.side, wl + h * H, Din, G, H, Bp + h * sB, eB + h * n.dirs * G, 0.f, n.dirs, pls,
+                    (long)G * KBh * 64, G);
+  }
+  const RnnReserveLayout lay = rnn_reserve_layout(n, T, N);
+  X3PBwdStream a;
+  a.forward = true;
+  a.M = (int)TN; a.N = n.dirs * G; a.KB = KBh;
+  a.E = p.y; a.lde = 2L * H; a.edoff = H;
+  a.Ap = pk<_Float16>(c.workspace, n, T, N, pl.a); a.eA = pk<int>(c.workspace, n, T, N, pl.ea);
+  a.B = Bp; a.eB = eB; a.sB = sB; a.seB = n.dirs * G;
+  a.C = static_cast<float *>(c.reserve) + lay.G; a.ldc = (long)n.dirs * G;
+  a.bias = wl + (n.lin_offset(0, 0, true) - pl0);
+  a.bias2 = n.mode == kGru ? nullptr : wl + (n.lin_offset(0, NW, true) - pl0);
+  a.bias_cols = G; a.sbias = pls;
+  a.part = pk<float>(c.workspace, n, T, N, pl.fpart);
+  a.cnt = pk<int>(c.workspace, n, T, N, pl.cnt);
+  a.flags = p.flags + 1024 + (p.xpd ? 256 * kFlagStride : 0);  // pinned: agg_flag6 lines
+  a.nwg = p.xpd ? 1 : p.nwg; a.T = T; a.Nf = N; a.err = err; a.rg = p.rg;
+  const int pinned = p.xpd ? d.dirs * p.rg : 0;
+  if (pinned) { a.xcd_word = p.flags + kXcdWord; a.xcd_count = pinned; }
+  // 128: every CU the recurrence leaves (configs[1]: 96 -> 128 blocks 720k -> 751k frames/s)
+  const int nb = std::min(env_int("KCTC_FWD_ROWS_BLOCKS", 128), stream_block_budget(d.dirs * p.nwg * p.rg, false));
+  a.blocks = pinned ? nb * 8 / (8 - pinned) : nb;
+  {
+    ProfSpan ps(c.side, "fwd_proj_rows");
+    gemm_x3p_bwd_stream(c.side, a);
+  }
+  c.done = true;
+}
+
 }  // namespace
 
 void rnn_set_cu_budget(int cus, int comm) {
@@ -3568,7 +3658,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
                          void *reserve, size_t res_bytes, unsigned *err, RnnFwdChain *chain,
                          bool input_projected, const void *in_rows, hipStream_t side, RnnPrepack *pre) {
   if (chain) chain->done = false;
-  if (pre) pre->done = false;
+  if (pre) pre->done = pre->wdone = false;
   if (T <= 0 || N <= 0 || N > 16 * kMaxRT || d.H % 16) return KRNN_NOT_SUPPORTED;
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
   if (res_bytes < sizeof(float) * (size_t)lay.total) return KRNN_BAD_PARAM;
@@ -3741,6 +3831,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
                                         (size_t)dirs * H, s));
     }
     const bool chained = l == d.layers - 1 && chain_ok(d, ver, T, N, chain);
+    const bool rowchain = !chained && l == d.layers - 1 && chain_rows_ok(d, ver, T, N, chain);
     if (ver == 6) {
       // XCD-pinned forward (xcd_mask): each (row group, direction) on one XCD,
       // the h hand-off in its L2 through a ring of two step images; a
@@ -3748,6 +3839,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       p.xpd = xcd_mask(d, N, true) ? 1 : 0;
       p.ring = p.xpd ? 2 : 0;
       p.fcopy = p.xpd && chained;
+      p.ysc1 = rowchain ? 1 : 0;
       p.allow_local = p.xpd ? env_int("KCTC_LOCAL", 1) : 0;
       // self-tagged hand-off (the kernel takes it for split-fp16 without IO
       // waves or a write-through copy): the ring's two images start at tag 1
@@ -3762,10 +3854,12 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     if (tr.arm("fwd", grid.x)) p.trace = tr.dev;
     // W^T of the backward's streamed dx GEMM, packed beside this recurrence
     // (rnn_backward_data's `streamed` shapes; one-layer descriptors)
-    const bool prepack = pre && pre->stream && pre->ev && ver == 6 && d.layers == 1 && dirs == 2 && env_int("KCTC_PREPACK", 1) &&
+    const bool prepack = pre && pre->dx && pre->stream && pre->ev && ver == 6 && d.layers == 1 && dirs == 2 && env_int("KCTC_PREPACK", 1) &&
                          ((d.prec == kPrecX3 && N <= 16) || env_int("KCTC_STREAM_ALL", 0)) && use_x3(NW * H) &&
                          NW * H <= 4096 && (d.prec == kPrecX3 || (NW * H) % 64 == 0);
-    const hipEvent_t fork = (chained || prepack) ? fork_event(s) : nullptr;
+    const bool prepack_w = pre && pre->stream && pre->wev && pre->wgrad && pre->in_bound > 0.f && ver == 6 &&
+                           d.layers == 1 && d.prec != kPrecBf16 && T > 1 && bounded_out(d) && use_x3((int)TN);
+    const hipEvent_t fork = (chained || prepack || prepack_w || rowchain) ? fork_event(s) : nullptr;
     {
       ProfSpan ps(s, "rnn_fwd_rec");
       if (ver == 6) launch6(true, d.mode, d.prec, c6.nth, p, grid, lds, s);
@@ -3778,6 +3872,19 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       KCTC_HIP_CHECK(hipEventRecord(pre->ev, pre->stream));
       pre->done = true;
     }
+    if (prepack_w) {  // x^T beside the recurrence, y^T after it, off its XCDs (rnn_backward_weights' packs)
+      hipStream_t ss = pre->stream;
+      if (!prepack) KCTC_HIP_CHECK(hipStreamWaitEvent(ss, fork, 0));
+      const PackLay pl = pack_layout(d, T, N);
+      const int Din = d.din(0);
+      int *pc = reinterpret_cast<int *>(p.flags + 1010);  // item counters (the recurrence's flags are after them)
+      KCTC_HIP_CHECK(hipMemsetAsync(pc, 0, sizeof(int) * 3, ss));
+      const unsigned *av = rnn_pinned_xcds();
+      const int nx = std::max(1, rnn_usable_cus() / kCusPerXcd);
+      ProfSpan ps(ss, "x3_pack_w_fwd");
+      x3p_pack_cols(ss, in, Din, (int)TN, Din, 0, pk<_Float16>(workspace, d, T, N, pl.xt),
+                    pk<int>(workspace, d, T, N, pl.ext), nullptr, pre->in_bound, 1, 0, 0, 0, 0, av, nx, pc);
+    }
     if (gated_launch) {
       gated_launch();
       join_stream(s, gside);  // (complete by the recurrence's end: it read every row)
@@ -3785,6 +3892,30 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     if (chained) {
       launch_chain_proj(d, p, fork, T, N, *chain, err);
       join_stream(s, chain->side);
+    }
+    if (rowchain) {
+      launch_chain_rows(d, p, fork, T, N, *chain, err);
+      join_stream(s, chain->side);
+    }
+    if (prepack_w) {  // y^T after the recurrence (and after the joins: s does not wait for it)
+      hipStream_t ss = pre->stream;
+      KCTC_HIP_CHECK(hipStreamWaitEvent(ss, fork_event(s), 0));
+      const PackLay pl = pack_layout(d, T, N);
+      const long KBt = (TN + 31) / 32;
+      int *pc = reinterpret_cast<int *>(p.flags + 1010);
+      const unsigned *av = rnn_pinned_xcds();
+      const int nx = std::max(1, rnn_usable_cus() / kCusPerXcd);
+      const long ldy = (long)dirs * H;
+      {
+        ProfSpan ps(ss, "x3_pack_w_fwd");
+        for (int dir = 0; dir < dirs; dir++)
+          x3p_pack_cols(ss, out + (long)dir * H, ldy, (int)TN, H, dir == 0 ? N : -N,
+                        pk<_Float16>(workspace, d, T, N, pl.yt) + (long)dir * H * KBt * 64,
+                        pk<int>(workspace, d, T, N, pl.eyt) + dir * H, nullptr, 1.f, 1, 0, 0, 0, 0, av, nx,
+                        pc + 1 + dir);
+      }
+      KCTC_HIP_CHECK(hipEventRecord(pre->wev, ss));
+      pre->wdone = true;
     }
     tr.dump("fwd", s, grid.x, p.nwg, T, dirs, ver, ver == 6 ? (p.xpd ? 1 : 0) : p.xpd);
     in = out;
@@ -4220,7 +4351,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
 int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *y, void *workspace, size_t ws_bytes, float *dw,
                          void *reserve, size_t res_bytes, int max_blocks, float in_bound, hipStream_t s2,
-                         const void *in_cols, bool beside) {
+                         const void *in_cols, bool beside, const RnnPrepack *pre) {
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
   if (res_bytes < sizeof(float) * (size_t)lay.total) return KRNN_BAD_PARAM;
   if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
@@ -4314,11 +4445,15 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     } else {
     const int KBt = (int)((TN + 31) / 32);
     const PackLay pl = pack_layout(d, T, N);
-    _Float16 *DXt = pk<_Float16>(workspace, d, T, N, pl.a), *Xt = pk<_Float16>(workspace, d, T, N, pl.b);
-    _Float16 *Yt = pk<_Float16>(workspace, d, T, N, pl.c);
+    // x^T and y^T packed by the forward (RnnPrepack::wgrad), else here
+    const bool wpre = pre && pre->wdone && pre->wev && use_x3((int)TN) && d.layers == 1 && T > 1;
+    _Float16 *DXt = pk<_Float16>(workspace, d, T, N, pl.a);
+    _Float16 *Xt = pk<_Float16>(workspace, d, T, N, wpre ? pl.xt : pl.b);
+    _Float16 *Yt = pk<_Float16>(workspace, d, T, N, wpre ? pl.yt : pl.c);
     _Float16 *Et = d.mode == kGru ? DXt + (long)dirs * G4 * KBt * 64 : DXt;
-    int *eDX = pk<int>(workspace, d, T, N, pl.ea), *eX = pk<int>(workspace, d, T, N, pl.eb);
-    int *eY = pk<int>(workspace, d, T, N, pl.ec), *eE = d.mode == kGru ? pk<int>(workspace, d, T, N, pl.ed) : eDX;
+    int *eDX = pk<int>(workspace, d, T, N, pl.ea), *eX = pk<int>(workspace, d, T, N, wpre ? pl.ext : pl.eb);
+    int *eY = pk<int>(workspace, d, T, N, wpre ? pl.eyt : pl.ec), *eE = d.mode == kGru ? pk<int>(workspace, d, T, N, pl.ed) : eDX;
+    if (wpre) KCTC_HIP_CHECK(hipStreamWaitEvent(s, pre->wev, 0));
     unsigned *cm = pk<unsigned>(workspace, d, T, N, pl.cm);
     // two streams (s2, the bottom component's tail, where nothing else
     // overlaps): input^T and output^T are packed and dW runs on s2 while
@@ -4341,11 +4476,13 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       const bool xb = l == 0 && in_bound > 0.f;
       // absmax scratch of its own: the GRU-only E^T exponent array (free for an LSTM)
       unsigned *cmx = reinterpret_cast<unsigned *>(pk<int>(workspace, d, T, N, pl.ed));
-      if (!xb) absmax_f32(s2, in, Din, (int)TN, Din, nullptr, cmx);
-      x3p_pack_cols(s2, in, Din, (int)TN, Din, 0, Xt, eX, cmx, xb ? in_bound : 0.f);
-      for (int dir = 0; dir < dirs; dir++)
-        x3p_pack_cols(s2, out + (long)dir * H, ldy, (int)TN, H, dir == 0 ? N : -N, Yt + (long)dir * H * KBt * 64,
-                      eY + dir * H, nullptr, 1.f);
+      if (!wpre) {
+        if (!xb) absmax_f32(s2, in, Din, (int)TN, Din, nullptr, cmx);
+        x3p_pack_cols(s2, in, Din, (int)TN, Din, 0, Xt, eX, cmx, xb ? in_bound : 0.f);
+        for (int dir = 0; dir < dirs; dir++)
+          x3p_pack_cols(s2, out + (long)dir * H, ldy, (int)TN, H, dir == 0 ? N : -N, Yt + (long)dir * H * KBt * 64,
+                        eY + dir * H, nullptr, 1.f);
+      }
       KCTC_HIP_CHECK(hipEventRecord(ev_y, s2));
       KCTC_HIP_CHECK(hipStreamWaitEvent(s2, ev_dx, 0));
       KCTC_HIP_CHECK(hipStreamWaitEvent(s, ev_y, 0));
@@ -4371,10 +4508,11 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
                       0, av, nx, pc + 1);
       }
       const bool xb = (l > 0 && bounded_out(d)) || (l == 0 && in_bound > 0.f);
-      if (!xb) absmax_f32(s, in, Din, (int)TN, Din, nullptr, cm);
-      x3p_pack_cols(s, in, Din, (int)TN, Din, 0, Xt, eX, cm, xb ? (l > 0 ? 1.f : in_bound) : 0.f, 1, 0, 0, 0, 0, av,
-                    nx, pc + 2);
-      if (T > 1) {
+      if (!xb && !wpre) absmax_f32(s, in, Din, (int)TN, Din, nullptr, cm);
+      if (!wpre)
+        x3p_pack_cols(s, in, Din, (int)TN, Din, 0, Xt, eX, cm, xb ? (l > 0 ? 1.f : in_bound) : 0.f, 1, 0, 0, 0, 0,
+                      av, nx, pc + 2);
+      if (T > 1 && !wpre) {
         if (!bounded_out(d)) absmax_f32(s, out, ldy, (int)TN, (int)ldy, nullptr, cm);
         for (int dir = 0; dir < dirs; dir++)
           x3p_pack_cols(s, out + (long)dir * H, ldy, (int)TN, H, dir == 0 ? N : -N, Yt + (long)dir * H * KBt * 64,
