@@ -164,6 +164,8 @@ struct X3PBwdStream {
   // v6 forward's y rows, written through with the same epochs): direction 0
   // walks the frames upwards, 1 downwards; C += bias + bias2 of column c at
   // (c / bias_cols) * sbias + c % bias_cols.  256-tile launches only.
+  float *part2 = nullptr;              // x3p_bwd_stream_part2_floats(N) floats (null: no split-K tail)
+  int tail_rows = -1;                  // split-K tail slots per direction (-1: x3p_stream_tail_rows())
   bool forward = false;
   const float *bias = nullptr, *bias2 = nullptr;
   int bias_cols = 1;
@@ -174,6 +176,16 @@ size_t x3p_bwd_stream_ints(int M, int N);
 // part then needs x3p_bwd_stream_part_floats(M, N) floats
 bool x3p_bwd_stream_256(int M, int N, int KB, bool bf16);
 size_t x3p_bwd_stream_part_floats(int M, int N);
+// split-K tail of the 256-tile launch (X3PBwdStream::part2): the last
+// x3p_stream_tail_rows() row-tile slots of each direction, kStreamTailSplit ways
+constexpr int kStreamTailSplit = 4;
+int x3p_stream_tail_rows();
+size_t x3p_bwd_stream_part2_floats(int N);
+// test hook: the 256-tile row stream against a producer that has finished
+// (every epoch final): C = sum_d pack(E[:, d K .. d K + K)) Wt_d^T (+ bias[c]),
+// E [M][2K] row-major, Wt [2][N][K], device pointers; tail_rows as X3PBwdStream
+void x3p_row_stream_selftest(hipStream_t s, int M, int N, int KB, int forward, int tail_rows, const float *E,
+                             const float *Wt, const float *bias, float *C);
 void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a);
 // pack rows r < R of X (K values each, row stride ldx) -> out[b][r][KB][64],
 // exponent per row into eout (bound > 0: from the bound, else the row max)

@@ -20,6 +20,7 @@
 // the fragment reads (ds_read_b128, rows fr = lane & 15, chunk fq or 4 + fq)
 // are conflict-free.  Two stages in flight, one barrier per stage.
 #include <algorithm>
+#include <vector>
 
 #include "common.h"
 #include "gemm.h"
@@ -83,6 +84,11 @@ struct PParams {
   // frames ascending, direction 1 descending; bias + bias2 of column c at
   // (c / bcols) * sBias + c % bcols, added by the second partial
   int fwdp, bcols;
+  // split-K tail: the last tailr row-tile slots of each direction (ready only
+  // at the producer's last steps) run as tails K-splits each; their tiles'
+  // partials meet in part2 ([tail tile][tails + 1][256 x 256])
+  int tailr, tails;
+  float *part2;
 };
 
 
@@ -1271,8 +1277,11 @@ __global__ __launch_bounds__(NTH, 2) void x3p_bwd_stream_kernel(PParams p) {
 // (part + tile * 256 * 256: thread t's (i, j) fragment is 16 B at
 // [i * 4 + j][t]): the first to arrive stores its partial (sc1), the second
 // adds it and writes C -- part0 + part1 either way round.
+// ks / S: this job's K-split of S (S > 1: a tail slot, its tile's partials
+// meet in part2)
 template <bool BFM>
-__device__ __forceinline__ void p256_bwd_tile(const PParams &p, unsigned char *lds, int tm, int tn, int d, int *bc) {
+__device__ __forceinline__ void p256_bwd_tile(const PParams &p, unsigned char *lds, int tm, int tn, int d, int *bc,
+                                              int ks, int S) {
   const _Float16 *A = p.A + (long)d * p.sA, *B = p.B + (long)d * p.sB;
   const int m0 = tm * TB2, n0 = tn * TB2;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1283,7 +1292,8 @@ __device__ __forceinline__ void p256_bwd_tile(const PParams &p, unsigned char *l
   for (int i = 0; i < 8; i++)
 #pragma unroll
     for (int j = 0; j < 4; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  p256_kloop_spread<BFM, 16>(A, B, p.M, p.N, p.KB, m0, n0, 0, p.KB, lds, wm, wn, fr, fq, acc);
+  const int kbs = (p.KB + S - 1) / S, kb0 = ks * kbs, nk = max(0, min(p.KB, kb0 + kbs) - kb0);
+  if (nk > 0) p256_kloop_spread<BFM, 16>(A, B, p.M, p.N, p.KB, m0, n0, kb0, nk, lds, wm, wn, fr, fq, acc);
   if constexpr (!BFM) {  // to values: 2^-(eA[row] + eB[col]) (eA written by other CUs: sc1 loads)
     const int *eA = p.eA + (long)d * p.seA, *eB = p.eB + (long)d * p.seB;
     int eb[4];
@@ -1304,6 +1314,54 @@ __device__ __forceinline__ void p256_bwd_tile(const PParams &p, unsigned char *l
   }
   const long tile = (long)tm * p.gx + tn;
   int *arr = p.arrive + tile;
+  // a tail tile (one of its directions split p.tails ways): every partial
+  // goes to its slot q of [other direction's, split 0 .. tails - 1] in
+  // part2, then arrives; the last arrival adds the slots up in q order (acc
+  // is dead after the store: the tail costs the k loop no registers)
+  const bool tail = p.tailr > 0 && (tm < p.tailr || tm >= p.nrt - p.tailr);
+  if (tail) {
+    const int n = p.tails + 1, q = S > 1 ? 1 + ks : 0;
+    const int ti = tm < p.tailr ? tm : p.tailr + tm - (p.nrt - p.tailr);
+    float *base = p.part2 + ((long)(ti * p.gx + tn) * n) * (TB2 * TB2);
+    {
+      const auto rq = __builtin_amdgcn_make_buffer_rsrc(base + (long)q * (TB2 * TB2), 0, TB2 * TB2 * 4, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rq,
+                                                 ((i * 4 + j) * NTH2 + (int)threadIdx.x) * 16, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) *bc = __hip_atomic_fetch_add(arr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (__builtin_amdgcn_readfirstlane(*bc) == n - 1) {
+      const auto rb = __builtin_amdgcn_make_buffer_rsrc(base, 0, n * TB2 * TB2 * 4, 0x00020000);
+      for (int i = 0; i < 8; i++)
+        for (int j = 0; j < 4; j++) {
+          const int off = ((i * 4 + j) * NTH2 + (int)threadIdx.x) * 16;
+          floatx4 v = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, 16));
+          for (int qq = 1; qq < n; qq++)
+            v += __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rb, off + qq * TB2 * TB2 * 4, 0, 16));
+          const int col = n0 + wn + j * 16 + fr;
+          if (col >= p.N) continue;
+          float badd = 0.f;
+          if (p.bias) {
+            const long bo = (long)(col / p.bcols) * p.sBias + col % p.bcols;
+            badd += p.bias[bo];
+            if (p.bias2) badd += p.bias2[bo];
+          }
+          for (int r = 0; r < 4; r++) {
+            const int row = m0 + wm + i * 16 + fq * 4 + r;
+            if (row < p.M) p.C[(long)row * p.ldc + col] = p.bias ? v[r] + badd : v[r];
+          }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    return;
+  }
   if (threadIdx.x == 0) *bc = __hip_atomic_fetch_add(arr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   const bool first = __builtin_amdgcn_readfirstlane(*bc) == 0;
@@ -1351,7 +1409,10 @@ __global__ __launch_bounds__(NTH2, 1) void x3p_bwd_stream256_kernel(PParams p) {
   int *seen = next + 1;  // [2] producer epochs seen
   int *bc = next + 3;    // combine broadcast
   if (threadIdx.x == 0) { seen[0] = 0; seen[1] = 0; }
-  const int J = p.P + p.gx, total = 2 * p.nrt * J, rows_per = TB2 / p.P;
+  // slots of the regular ranks (P pack + gx GEMM jobs), then the tail ranks'
+  // (P pack + gx x tails GEMM jobs)
+  const int J0 = p.P + p.gx, J1 = p.P + p.gx * p.tails, nreg = 2 * (p.nrt - p.tailr);
+  const int base1 = nreg * J0, total = base1 + 2 * p.tailr * J1, rows_per = TB2 / p.P;
   if (on_pinned_xcd(p, bc)) return;  // before taking any job
   while (true) {
     if (threadIdx.x == 0) *next = atomicAdd(p.counter, 1);
@@ -1359,7 +1420,15 @@ __global__ __launch_bounds__(NTH2, 1) void x3p_bwd_stream256_kernel(PParams p) {
     const int id = __builtin_amdgcn_readfirstlane(*next);
     __syncthreads();
     if (id >= total) break;
-    const int slot = id / J, r = id - slot * J, d = slot & 1, rank = slot >> 1;
+    int slot, r;
+    if (id < base1) {
+      slot = id / J0;
+      r = id - slot * J0;
+    } else {
+      slot = nreg + (id - base1) / J1;
+      r = (id - base1) % J1;
+    }
+    const int d = slot & 1, rank = slot >> 1;
     // the producer's direction that walks the frames downwards takes the
     // row tiles from the last (a backward producer's direction 0, a forward
     // producer's direction 1)
@@ -1379,7 +1448,8 @@ __global__ __launch_bounds__(NTH2, 1) void x3p_bwd_stream256_kernel(PParams p) {
       __syncthreads();  // (see x3p_bwd_stream_kernel: reconverge after the lane-0 atomic)
     } else {
       wait_count(p.done + d * p.nrt + rt, p.P, p.serr);
-      p256_bwd_tile<BFM>(p, lds, rt, r - p.P, d, bc);
+      const int S = rank >= p.nrt - p.tailr ? p.tails : 1, gj = r - p.P;
+      p256_bwd_tile<BFM>(p, lds, rt, gj % p.gx, d, bc, gj / p.gx, S);
       __syncthreads();
     }
   }
@@ -1800,6 +1870,19 @@ bool x3p_bwd_stream_256(int M, int N, int KB, bool bf16) {
   // per-tile buffer offsets stay below 2^31 (C rows are addressed as [M][ldc])
   return on && x3p_use_256(M, N) && KB * (bf16 ? 64 : 32) <= 4096;
 }
+// off by default: at configs[1] the streams end ~200 us after their
+// producers with or without it (they run behind, not on the last jobs) and
+// the extra partial traffic cost 1.4 % (752k vs 741k frames/s, same box)
+int x3p_stream_tail_rows() {
+  static const int r = [] {
+    const char *e = getenv("KCTC_STREAM_TAIL");
+    return e ? std::max(0, atoi(e)) : 0;
+  }();
+  return r;
+}
+size_t x3p_bwd_stream_part2_floats(int N) {
+  return (size_t)2 * x3p_stream_tail_rows() * ceil_div(N, TB2) * (kStreamTailSplit + 1) * TB2 * TB2;
+}
 size_t x3p_bwd_stream_part_floats(int M, int N) {
   return std::max((size_t)M * N, (size_t)ceil_div(M, TB2) * ceil_div(N, TB2) * TB2 * TB2);
 }
@@ -1834,7 +1917,11 @@ void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a) {
     p.gx = ceil_div(a.N, TB2); p.nrt = ceil_div(a.M, TB2);
     p.tiles = p.gx * p.nrt;
     p.done = a.cnt + 1; p.arrive = a.cnt + 1 + 2 * p.nrt;  // within x3p_bwd_stream_ints (128-tile counts)
-    const int total = 2 * p.nrt * (p.P + p.gx);
+    const int tr = a.tail_rows >= 0 ? a.tail_rows : x3p_stream_tail_rows();
+    p.tailr = a.part2 && tr > 0 && p.nrt >= 2 * tr + 2 ? tr : 0;
+    p.tails = p.tailr ? kStreamTailSplit : 1;
+    p.part2 = a.part2;
+    const int total = 2 * (p.nrt - p.tailr) * (p.P + p.gx) + 2 * p.tailr * (p.P + p.gx * p.tails);
     const dim3 grid(std::min(total, a.blocks > 0 ? a.blocks : 96));
     auto go = [&](auto kern) {
       static bool attr = false;
@@ -1876,6 +1963,50 @@ void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a) {
     else if (K <= 2048) go(x3p_bwd_stream_kernel<8, false>);
     else go(x3p_bwd_stream_kernel<16, false>);
   }
+}
+
+void x3p_row_stream_selftest(hipStream_t s, int M, int N, int KB, int forward, int tail_rows, const float *E,
+                             const float *Wt, const float *bias, float *C) {
+  const int K = KB * 32, Nf = 16, T = (M + Nf - 1) / Nf;
+  if (M <= 0 || N <= 0 || KB <= 0 || M % Nf) throw std::invalid_argument("x3p_row_stream_selftest: shape");
+  if (!x3p_bwd_stream_256(M, N, KB, false)) throw std::invalid_argument("x3p_row_stream_selftest: not a 256-tile shape");
+  const int tr = tail_rows >= 0 ? tail_rows : x3p_stream_tail_rows();
+  const size_t ap = (size_t)2 * M * KB * 128, bp = (size_t)2 * N * KB * 128;
+  const size_t part = sizeof(float) * x3p_bwd_stream_part_floats(M, N);
+  const size_t part2 = sizeof(float) * (size_t)2 * tr * ceil_div(N, TB2) * (kStreamTailSplit + 1) * TB2 * TB2;
+  const size_t cnt = sizeof(int) * x3p_bwd_stream_ints(M, N), fl = 4096;
+  char *buf = nullptr;
+  const size_t total = ap + bp + part + part2 + cnt + fl + sizeof(int) * 4 * (size_t)(M + N) + 4096;
+  KCTC_HIP_CHECK(hipMalloc(&buf, total));
+  char *o = buf;
+  auto take = [&](size_t b) { char *r = o; o += (b + 255) / 256 * 256; return r; };
+  _Float16 *A = reinterpret_cast<_Float16 *>(take(ap)), *B = reinterpret_cast<_Float16 *>(take(bp));
+  float *pt = reinterpret_cast<float *>(take(part)), *pt2 = reinterpret_cast<float *>(take(part2));
+  int *cn = reinterpret_cast<int *>(take(cnt));
+  unsigned *flags = reinterpret_cast<unsigned *>(take(fl));
+  int *eA = reinterpret_cast<int *>(take(sizeof(int) * 2 * (size_t)M)), *eB = reinterpret_cast<int *>(take(sizeof(int) * 2 * (size_t)N));
+  // every epoch final: lines (d) at 32-word strides
+  std::vector<unsigned> hf(fl / 4, (unsigned)(T + 2));
+  hf[1000] = 0u;  // the error word
+  KCTC_HIP_CHECK(hipMemcpyAsync(flags, hf.data(), fl, hipMemcpyHostToDevice, s));
+  x3p_pack_rows(s, Wt, K, N, K, B, eB, 0.f, 2, (long)N * K, (long)N * KB * 64, N);
+  X3PBwdStream a;
+  a.M = M; a.N = N; a.KB = KB;
+  a.E = E; a.lde = 2L * K; a.edoff = K;
+  a.Ap = A; a.eA = eA;
+  a.B = B; a.eB = eB; a.sB = (long)N * KB * 64; a.seB = N;
+  a.C = C; a.ldc = N;
+  a.part = pt; a.part2 = tr > 0 ? pt2 : nullptr; a.tail_rows = tr; a.cnt = cn;
+  a.flags = flags; a.nwg = 1; a.T = T; a.Nf = Nf; a.err = flags + 1000; a.rg = 1;
+  a.blocks = 64;
+  a.forward = forward != 0;
+  a.bias = bias; a.bias_cols = N;
+  gemm_x3p_bwd_stream(s, a);
+  KCTC_HIP_CHECK(hipStreamSynchronize(s));
+  unsigned err = 0;
+  KCTC_HIP_CHECK(hipMemcpy(&err, flags + 1000, sizeof(unsigned), hipMemcpyDeviceToHost));
+  KCTC_HIP_CHECK(hipFree(buf));
+  if (err) throw std::runtime_error("x3p_row_stream_selftest: wait timeout");
 }
 
 }  // namespace kctc

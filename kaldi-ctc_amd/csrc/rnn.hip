@@ -159,7 +159,7 @@ static size_t xch_bytes(const RnnDesc &d, int T, int N) {
 //               shifted output^T [dirs*H][TN]
 // plus int exponents and float-bit column maxima (G = nW*H).
 struct PackLay {
-  size_t a, b, c, d, ea, eb, ec, ed, cm, part, cnt, cme, fcnt, fpart, gtf, wt, ewt, cmw, xt, yt, ext, eyt, total;
+  size_t a, b, c, d, ea, eb, ec, ed, cm, part, cnt, part2, cme, fcnt, fpart, gtf, wt, ewt, cmw, xt, yt, ext, eyt, total;
 };
 static PackLay pack_layout(const RnnDesc &d, int T, int N) {
   const long TN = (long)T * N, G = (long)d.nw() * d.H, Dm = std::max(d.D, d.dirs * d.H), dirs = d.dirs;
@@ -183,6 +183,7 @@ static PackLay pack_layout(const RnnDesc &d, int T, int N) {
   // (also the row stream of this component's projection off the previous
   // component's forward, launch_chain_rows: N = dirs * G columns)
   p.cnt = o; o = align_up(o + sizeof(int) * x3p_bwd_stream_ints((int)TN, (int)std::max(Dm, dirs * G)), 256);
+  p.part2 = o; o = align_up(o + sizeof(float) * x3p_bwd_stream_part2_floats((int)std::max(Dm, dirs * G)), 256);
   p.cme = o; o = align_up(o + sizeof(unsigned) * 2 * dirs * G, 256);  // dGates column maxima (v6 backward)
   // arrival counters of the direction-split streamed projection (this component as its consumer)
   p.fcnt = o; o = align_up(o + sizeof(int) * ((TN + 127) / 128 * dirs * ((G + 127) / 128) + 64), 256);
@@ -3550,6 +3551,7 @@ void launch_chain_rows(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
   a.bias2 = n.mode == kGru ? nullptr : wl + (n.lin_offset(0, NW, true) - pl0);
   a.bias_cols = G; a.sbias = pls;
   a.part = pk<float>(c.workspace, n, T, N, pl.fpart);
+  a.part2 = pk<float>(c.workspace, n, T, N, pl.part2);
   a.cnt = pk<int>(c.workspace, n, T, N, pl.cnt);
   a.flags = p.flags + 1024 + (p.xpd ? 256 * kFlagStride : 0);  // pinned: agg_flag6 lines
   a.nwg = p.xpd ? 1 : p.nwg; a.T = T; a.Nf = N; a.err = err; a.rg = p.rg;
@@ -3970,6 +3972,7 @@ void launch_bwd_stream(const RnnDesc &d, const RecParams &p, int l, const float 
   a.B = Bp; a.eB = bf ? nullptr : eB; a.sB = (long)Din * KB * 64; a.seB = Din;
   a.C = dxl; a.ldc = Din;
   a.part = pk<float>(workspace, d, T, N, pl.part);
+  a.part2 = pk<float>(workspace, d, T, N, pl.part2);
   a.cnt = pk<int>(workspace, d, T, N, pl.cnt);
   // XCD-pinned recurrence: its epochs' sc1 copies (the L2 flags are not
   // visible here), and no block on the recurrence's XCDs
