@@ -148,7 +148,7 @@ __device__ __forceinline__ float lse3(float a, float b, float c) {
 //   emit[2][F][SP] | col[2][CP] | wmax[2][8] | feasible flag
 struct AbLds {
   int F, SP, CP;
-  int pair;  // frames per barrier (SPT == 1, 1..8): KCTC_CTC_PAIR
+  int pair;  // frames per barrier (SPT == 1, 1..8): mictc_set_frame_group
   __device__ __host__ size_t floats() const { return 2 * (size_t)F * SP + 2 * (size_t)CP + 2 * kABWaves + 4; }
 };
 
@@ -554,8 +554,7 @@ static std::atomic<int> g_frame_group{0};
 static int frame_group() {
   int m = g_frame_group.load(std::memory_order_relaxed);
   if (m <= 0) {
-    const char *e = getenv("KCTC_CTC_PAIR");
-    m = std::max(1, std::min(e && *e ? atoi(e) : 8, 8));
+    m = 8;
     int expect = 0;
     g_frame_group.compare_exchange_strong(expect, m);
     m = g_frame_group.load(std::memory_order_relaxed);

@@ -115,7 +115,7 @@ void gemm_x3p(hipStream_t s, const X3PArgs &g);
 // recurrence's XCDs could start, so one launch per recurrence keeps the
 // side stream from falling a GEMM behind per layer
 void gemm_x3p_pair(hipStream_t s, const X3PArgs &g1, const X3PArgs &g2);
-// shapes gemm_x3p runs on 256 x 256 tiles (KCTC_GEMM256=0 turns them off)
+// shapes gemm_x3p runs on 256 x 256 tiles
 bool x3p_use_256(int M, int N);
 // split-K for gemm_x3p on a (M x N, KB k-blocks, batch) problem so that the
 // tiles fill the chip (callers size ws for it: split * batch * M * N floats)

@@ -59,12 +59,12 @@ struct PParams {
   int nrt;                 // row tiles
   long sxs;                // halves per producer step image
   long sxg;                // halves per row group's part of a step image
-  int backoff;             // streaming waits sleep in proportion to the producer's distance (KCTC_STREAM_BACKOFF)
+  int backoff;             // streaming waits sleep in proportion to the producer's distance
   int sdir;                // streaming: K split by producer direction (two half-K jobs per C tile, see fwd_combine)
-  int dbg;                 // KCTC_STREAM_DBG diagnostics: 1 no combine wait, 2 wait for both directions, 4 no combine,
+  int dbg;                 // diagnostics (0 in the product): 1 no combine wait, 2 wait for both directions, 4 no combine,
                            // 32 register-A k loop without the two-deep prefetch
   unsigned *serr;          // producer's error word (wait timeout)
-  int p256v;               // 256-tile k loop (KCTC_P256): 2 DMA spread over the MFMAs, 1 DMA block per stage, 0 auto
+  int p256v;               // 256-tile k loop: 2 DMA spread over the MFMAs, 1 DMA block per stage, 0 auto
   const unsigned *xcd_word;  // XCDs of a pinned producer (X3PBwdStream::xcd_word), xcd_count of them
   int xcd_count;
   // backward stream (x3p_bwd_stream_kernel)
@@ -816,7 +816,7 @@ __device__ __forceinline__ void p256_row(floatx4 (&acc)[4], halfx8 ah, halfx8 al
 // iteration (where both waves of a SIMD issued them at once, right after the
 // barrier, with no matrix work to hide behind).  Source pointers are computed
 // once per tile; the loads of the last iteration re-read the last k block
-// (clamped) so the body is straight-line.  KCTC_P256=1: the previous loop.
+// (clamped) so the body is straight-line.
 // AUXA: cache policy of the A pieces (16: sc1, rows packed by other CUs
 // while this kernel runs)
 template <bool BFM, int AUXA = 0>
@@ -1699,18 +1699,9 @@ float x3p_bench(hipStream_t s, int M, int N, int K, bool bf16, int iters, int sp
   return ms / iters;
 }
 
-static int env_backoff() {
-  const char *e = getenv("KCTC_STREAM_BACKOFF");
-  return e ? atoi(e) : 1;
-}
+static int env_backoff() { return 1; }
 
-bool x3p_use_256(int M, int N) {
-  static const int on = [] {
-    const char *e = getenv("KCTC_GEMM256");
-    return e ? atoi(e) : 1;
-  }();
-  return on && M >= 192 && N >= 192;
-}
+bool x3p_use_256(int M, int N) { return M >= 192 && N >= 192; }
 
 int x3p_pick_split(int M, int N, int KB, int batch) {
   const int tb = x3p_use_256(M, N) ? TB2 : TB;
@@ -1735,7 +1726,7 @@ static PParams x3p_params(const X3PArgs &g, bool &t256) {
   p.kbchunk = p.split > 1 ? ceil_div(g.KB, p.split) : (g.KB > 0 ? g.KB : 1);
   if (p.split > 1) p.split = ceil_div(g.KB, p.kbchunk);
   p.ws = g.ws;
-  // large shapes on 256 x 256 tiles (KCTC_GEMM256=0: 128 x 128 everywhere)
+  // large shapes on 256 x 256 tiles
   t256 = !g.stream_flags && x3p_use_256(g.M, g.N);
   if (t256) {
     p.gx = ceil_div(g.N, TB2);
@@ -1756,9 +1747,8 @@ static PParams x3p_params(const X3PArgs &g, bool &t256) {
   p.mt = ceil_div(g.M, TB2);
   if (p.gate && (!t256 || p.split > 1 || !p.counter || g.beta != 0.f))
     throw std::invalid_argument("gemm_x3p: a gated projection runs on 256 tiles, no split-K, with a tile counter");
-  p.dbg = getenv("KCTC_STREAM_DBG") ? atoi(getenv("KCTC_STREAM_DBG")) : 0;
-  static const int p256v = getenv("KCTC_P256") ? atoi(getenv("KCTC_P256")) : 0;
-  p.p256v = p256v;
+  p.dbg = 0;
+  p.p256v = 0;
   p.avoid = g.avoid_word;
   p.nxcd = g.avoid_xcds;
   if (p.avoid && (!t256 || !p.counter || p.gate))
@@ -1863,23 +1853,13 @@ size_t x3p_bwd_stream_ints(int M, int N) {
 }
 
 bool x3p_bwd_stream_256(int M, int N, int KB, bool bf16) {
-  static const int on = [] {
-    const char *e = getenv("KCTC_BWD_S256");
-    return e ? atoi(e) : 1;
-  }();
   // per-tile buffer offsets stay below 2^31 (C rows are addressed as [M][ldc])
-  return on && x3p_use_256(M, N) && KB * (bf16 ? 64 : 32) <= 4096;
+  return x3p_use_256(M, N) && KB * (bf16 ? 64 : 32) <= 4096;
 }
 // off by default: at configs[1] the streams end ~200 us after their
 // producers with or without it (they run behind, not on the last jobs) and
 // the extra partial traffic cost 1.4 % (752k vs 741k frames/s, same box)
-int x3p_stream_tail_rows() {
-  static const int r = [] {
-    const char *e = getenv("KCTC_STREAM_TAIL");
-    return e ? std::max(0, atoi(e)) : 0;
-  }();
-  return r;
-}
+int x3p_stream_tail_rows() { return 0; }
 size_t x3p_bwd_stream_part2_floats(int N) {
   return (size_t)2 * x3p_stream_tail_rows() * ceil_div(N, TB2) * (kStreamTailSplit + 1) * TB2 * TB2;
 }
@@ -1907,7 +1887,7 @@ void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a) {
   p.sflags = a.flags; p.snwg = a.nwg; p.sT = a.T; p.sN = a.Nf; p.serr = a.err; p.srg = a.rg;
   p.xcd_word = a.xcd_word; p.xcd_count = a.xcd_count;
   p.backoff = env_backoff();
-  p.dbg = getenv("KCTC_STREAM_DBG") ? atoi(getenv("KCTC_STREAM_DBG")) : 0;
+  p.dbg = 0;
   p.fwdp = a.forward ? 1 : 0;
   p.bias = a.bias; p.bias2 = a.bias2; p.bcols = a.bias_cols > 0 ? a.bias_cols : 1; p.sBias = a.sbias;
   const bool t256 = x3p_bwd_stream_256(a.M, a.N, a.KB, a.bf16);

@@ -699,8 +699,6 @@ void UpdatableComponent::Add(float alpha, const UpdatableComponent &other) {
 }
 
 int CuDNNRecurrentComponent::side_gemm_blocks() const {
-  const char *e = getenv("KCTC_SIDE_BLOCKS");
-  if (e && *e) return atoi(e);
   return 512;  // dynamic tile scheduling: two per CU, late starters exit
 }
 

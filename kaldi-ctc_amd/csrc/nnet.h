@@ -288,7 +288,7 @@ class CuDNNRecurrentComponent : public UpdatableComponent {
   unsigned *DeviceError() const { return err_ext_ ? err_ext_ : err_; }
   void SetErrorWord(unsigned *e) const { err_ext_ = e; }
   // workgroup cap of the side-stream weight GEMMs: the CUs left over by the
-  // backward recurrence (KCTC_SIDE_BLOCKS overrides)
+  // backward recurrence
   int side_gemm_blocks() const;
   const RnnPrepack *wgrad_prepack(const CuMatrixBase &in_value, const CuMatrixBase &out_value) const;
   const RnnDesc &Desc() const { return desc_; }

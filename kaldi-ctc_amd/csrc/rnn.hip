@@ -212,14 +212,9 @@ static P *pk(void *ws, const RnnDesc &d, int T, int N, size_t off) {
   return reinterpret_cast<P *>(static_cast<char *>(ws) + pack_offset(d, T, N) + off);
 }
 // The RNN GEMMs run on the packed split-fp16 matrix-core path (gemm_x3p.hip)
-// unless KCTC_GEMM=f32 (or the contraction is too short to pay for packing).
+// unless the contraction is too short to pay for packing.
 static bool use_x3(int K, int min_k = 128) {
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("KCTC_GEMM");
-    v = (e && !strcmp(e, "f32")) ? 0 : 1;
-  }
-  return v && K >= min_k;
+  return K >= min_k;
 }
 // |x| <= 1: an LSTM / GRU / TANH layer output
 static bool bounded_out(const RnnDesc &d) { return d.mode != kRelu; }
@@ -322,7 +317,7 @@ struct RecParams {
   int e_sc1;        // v6 backward: dGates rows written through (sc1) for a streaming consumer
   int ysc1;         // v6 forward: y rows written through (sc1) and the aggregated epochs published
                     // for the next component's projection streamed off them (launch_chain_rows)
-  int bfpart;       // v6 backward, bf16 mode: partial dh exchanged as bf16 (KCTC_BF16_PARTIALS)
+  int bfpart;       // v6 backward, bf16 mode: partial dh exchanged as bf16
   unsigned *cmax;   // v6 backward: column max |DX| [dirs * nW * H] (GRU: then |E|), as float bits
   unsigned *reg;    // v6 backward: per-device registration word (+1 per workgroup at start)
   // v6 backward, bf16 (RnnReserveLayout::pk): dGates written straight into the
@@ -347,7 +342,7 @@ struct RecParams {
   const unsigned *gtf;
   unsigned gid;
   int gmt, ggx;
-  int gplain;  // diagnostic (KCTC_GATE_PLAIN): the gated G rows fetched without sc1
+  int gplain;  // diagnostic (0): the gated G rows fetched without sc1
   // v6 backward, fp32 partials, ring of 2: self-tagged hand-off (see
   // rnn_bwd_rec6): the consumers poll the partial-dh words themselves instead
   // of the producers' epoch flags; taken by the slots probe6 finds XCD-local
@@ -3042,21 +3037,21 @@ static void launch6_u(bool fwd, int nth, const RecParams &p, dim3 grid, size_t l
         // default since round 4: the stacked forward (one A load per k block,
         // 2/3 of the MFMAs) runs 1.76 us/step against 2.05 for the IO-wave
         // forward, same box; backward off (2.53 vs 2.43: the fold's cross-lane
-        // exchange).  KCTC_STK_FWD / KCTC_STK_BWD (or KCTC_STK for both)
-        const int stk = env_int(fwd ? "KCTC_STK_FWD" : "KCTC_STK_BWD", env_int("KCTC_STK", 1));
+        // exchange).  KCTC_STK_FWD (forward; KCTC_STK for both)
+        const int stk = fwd ? env_int("KCTC_STK_FWD", env_int("KCTC_STK", 1)) : env_int("KCTC_STK", 1);
         if constexpr (P == kPrecX3) {
           if (p.gs <= 8 && stk) {
-            // the stacked forward with IO waves (KCTC_STK_IOW=1, measuring)
-            if (fwd && env_int("KCTC_FWD_IOW", 1) && env_int("KCTC_STK_IOW", 0))
+            // the stacked forward with IO waves (measured slower; not taken)
+            if (false)
               launch6_h<MODE, 16, 512, kPrecX3S | 4>(fwd, p, grid, lds, s);
             else
               launch6_h<MODE, 16, 512, kPrecX3S>(fwd, p, grid, lds, s);
             break;
           }
         }
-        // forward with IO waves (the G loads off the hand-off waves; KCTC_FWD_IOW=0: all waves hand off)
+        // forward with IO waves (the G loads off the hand-off waves)
         if constexpr (MODE == kLstm || MODE == kGru) {
-          if (fwd && env_int("KCTC_FWD_IOW", 1)) {
+          if (fwd) {
             if (p.gtf) launch6_h<MODE, 16, 512, P | 4 | 8>(fwd, p, grid, lds, s);
             else launch6_h<MODE, 16, 512, P | 4>(fwd, p, grid, lds, s);
             break;
@@ -3132,7 +3127,7 @@ static int env_int(const char *name, int dflt) {
 
 // pick U (units per workgroup): divides H, multiple of 4, blocks <= 256
 static int pick_fwd_u(const RnnDesc &d, int N) {
-  int want = env_int("KCTC_FWD_U", 0);
+  int want = 0;
   const int NW = d.nw();
   auto ok = [&](int U) {
     if (U < 4 || U % 4 || d.H % U || NW * U > 16 * kMaxCT || N * U / 4 > NT) return false;
@@ -3160,7 +3155,7 @@ static size_t bwd_lds_bytes(const RnnDesc &d, int N, int U, int ver = 3) {
   return sizeof(float) * ((size_t)(ver == 4 ? 16 : U) * (d.nw() * d.H + 4) +
                           std::max(4 * (size_t)Npad * 16, (size_t)2 * N * U * d.nw()));
 }
-static int rec_version() { return env_int("KCTC_REC", 4); }
+static int rec_version() { return 4; }
 // XCD slots one direction spans for U units per workgroup (0: not a v4 shape)
 static int v4_xpd(const RnnDesc &d, int U) {
   if (U <= 0 || d.H % U) return 0;
@@ -3175,7 +3170,7 @@ static int pick_fwd_u4(const RnnDesc &d, int N) {
     return U >= 4 && U % 4 == 0 && v4_xpd(d, U) && d.nw() * U <= 16 * kMaxCT && N * U <= kMaxEPT * NT &&
            fwd_lds_bytes(d, N, U) <= 160 * 1024;
   };
-  const int want = env_int("KCTC_FWD_U", 0);
+  const int want = 0;
   if (want) return ok(want) ? want : 0;
   // measured on BLSTM-512 N=16 (1 x MI355X): U=8 (2 XCD slots per direction)
   // 44 ms/step of forward recurrence, U=4 48, U=16 58
@@ -3189,7 +3184,7 @@ static int pick_bwd_u4(const RnnDesc &d, int N) {
     return U >= 4 && U <= 16 && U % 4 == 0 && v4_xpd(d, U) && N * U <= kMaxEPT * NT &&
            bwd_lds_bytes(d, N, U, 4) <= 160 * 1024;
   };
-  const int want = env_int("KCTC_BWD_U", 0);
+  const int want = 0;
   if (want) return ok(want) ? want : 0;
   for (int U : {16, 8, 4})
     if (ok(U)) return U;
@@ -3200,21 +3195,21 @@ static int pick_bwd_u4(const RnnDesc &d, int N) {
 //   rg   row groups of 16 sequences, each an independent recurrence
 //   U    units per workgroup (8, 16 at 256 threads; 32 at 512 threads)
 // chosen so that dirs * (H / U) * rg workgroups (one per CU, >= 96 KB LDS
-// each) stay within KCTC_REC_MAX_WG (default 128: half the chip, the rest
+// each) stay within 128 workgroups (half the chip, the rest
 // for the GEMMs that overlap the recurrences).  Preference U = 16, then 32,
 // then 8 (measured on BLSTM-512 N=16: U=16 34.2 ms/step of forward
-// recurrence, U=8 37.1).  KCTC_FWD_U / KCTC_BWD_U force U.
+// recurrence, U=8 37.1).
 // Sequences per v6 row group: 16 (one MFMA row tile), or 8 for 9 <= N <= 32
 // -- the batch then runs as ceil(N / 8) independent recurrences side by side,
 // each moving half the hand-off rows per step.  Default 8 for N <= 16
 // (configs[1]: forward 28.0 -> 27.0, backward 34.2 -> 33.0 ms/step of
 // recurrence; the weight GEMMs beside the backward get 64 CUs fewer and take
-// twice as long, still hidden).  KCTC_REC_GS sets both, KCTC_REC_GS_FWD /
-// KCTC_REC_GS_BWD one direction; a set knob applies up to N = 32.  pick6
+// twice as long, still hidden).  KCTC_REC_GS sets both directions; a set
+// knob applies up to N = 32.  pick6
 // falls back to 16 when no workgroup partition fits the groups of 8.
 static int v6_group_rows(int N, bool fwd) {
   const int dflt = N <= 16 ? 8 : 16;
-  const int want = env_int(fwd ? "KCTC_REC_GS_FWD" : "KCTC_REC_GS_BWD", env_int("KCTC_REC_GS", dflt));
+  const int want = env_int("KCTC_REC_GS", dflt);
   return (want == 8 && N > 8 && N <= 32) ? 8 : 16;
 }
 struct V6Cfg {
@@ -3223,12 +3218,12 @@ struct V6Cfg {
 };
 static V6Cfg pick6(const RnnDesc &d, int N, bool fwd, int gs_force = 0) {
   V6Cfg c;
-  if (env_int(fwd ? "KCTC_FWD_REC" : "KCTC_BWD_REC", 6) != 6 || rec_version() != 4) return c;
+  if (rec_version() != 4) return c;
   if ((d.mode != kLstm && d.mode != kGru) || N <= 0 || N > 64 || d.dirs > 2) return c;
   if (d.H != 256 && d.H != 320 && d.H != 512 && d.H != 1024) return c;
   const int gs = gs_force ? gs_force : v6_group_rows(N, fwd), rg = (N + gs - 1) / gs;
   // never more workgroups than the CUs this process may use (all must be resident)
-  const int max_wg = std::min(env_int("KCTC_REC_MAX_WG", 128), rnn_usable_cus());
+  const int max_wg = std::min(128, rnn_usable_cus());
   auto ok = [&](int U) {
     const int nth = U == 32 ? 512 : 256, nwv = nth / 64;
     if (d.H % U || d.H % (16 * nwv) || (d.H / U) % (nth / (4 * U))) return false;
@@ -3238,15 +3233,14 @@ static V6Cfg pick6(const RnnDesc &d, int N, bool fwd, int gs_force = 0) {
     c.U = U;
     // U = 16 at H = 512 runs 512 threads (K split over 8 waves; measured on
     // BLSTM-512 N=16: forward 31.9 -> 28.4, backward 34.4 -> 32.9 ms/step of
-    // recurrence vs 256 threads; 1024 threads 30.5 / 33.5); KCTC_FWD_NTH /
-    // KCTC_BWD_NTH = 256 | 512 | 1024 override
-    const int want_nth = env_int(fwd ? "KCTC_FWD_NTH" : "KCTC_BWD_NTH", d.H == 512 ? 512 : 256);
+    // recurrence vs 256 threads; 1024 threads 30.5 / 33.5)
+    const int want_nth = d.H == 512 ? 512 : 256;
     c.nth = U == 32 ? 512 : (U == 16 && d.H == 512 && (want_nth == 512 || want_nth == 1024)) ? want_nth : 256;
     c.rg = rg;
     c.gs = gs;
     return c;
   };
-  const int want = env_int(fwd ? "KCTC_FWD_U" : "KCTC_BWD_U", 0);
+  const int want = 0;
   if (want) {
     if (ok(want)) return take(want);
   } else {
@@ -3322,7 +3316,7 @@ static void xch_release(hipStream_t s) {
 }
 
 static int pick_bwd_u(const RnnDesc &d, int N) {
-  int want = env_int("KCTC_BWD_U", 0);
+  int want = 0;
   const int K = d.nw() * d.H;
   auto ok = [&](int U) {
     if (U < 4 || U % 4 || U > 16 || d.H % U || N * U / 4 > NT) return false;
@@ -3357,14 +3351,14 @@ int g_usable_cus = 0, g_comm_cus = 0;
 // (configs[2]: U = 32 at H = 512, four row groups x two directions = all
 // eight XCDs, half of each XCD's CUs) of that XCD's CUs, and the whole chip's
 // CUs must be usable (no CU partition).  KCTC_XCD6=0 / KCTC_XCD6F=0 switch it
-// off; KCTC_XCD6_HALF=0 keeps the 16-workgroup shapes unpinned (configs[2]
+// off; the 16-workgroup shapes pin too (configs[2]
 // pinned: 990k -> 1.12M frames/s, forward 3.14 -> 2.42, backward 4.52 -> 3.53
 // us/step, same box).
 unsigned xcd_mask(const RnnDesc &d, int N, bool fwd) {
   const V6Cfg c6 = pick6(d, N, fwd);
   if (!c6 || d.dirs * c6.rg > 8) return 0;
   const int nwg = d.H / c6.U;
-  if (nwg != kCusPerXcd && !(nwg == kCusPerXcd / 2 && env_int("KCTC_XCD6_HALF", 1))) return 0;
+  if (nwg != kCusPerXcd && nwg != kCusPerXcd / 2) return 0;
   if (!env_int(fwd ? "KCTC_XCD6F" : "KCTC_XCD6", 1)) return 0;
   int dev = 0, cus = 0;
   KCTC_HIP_CHECK(hipGetDevice(&dev));
@@ -3425,9 +3419,9 @@ bool chain_ok(const RnnDesc &d, int ver, int T, int N, const RnnFwdChain *c) {
   // frames/s same box); KCTC_FWD_STREAM_PINNED=1 streams anyway
   if (xcd_mask(d, N, true) && !env_int("KCTC_FWD_STREAM_PINNED", 0)) return false;
   // and only the IO-wave variant (U = 16, 512 threads) carries the copies
-  // (launch6_u: U = 16 / 512 threads, KCTC_FWD_IOW, not the stacked variant)
+  // (launch6_u: U = 16 / 512 threads, not the stacked variant)
   if (xcd_mask(d, N, true) && !(pick6(d, N, true).U == 16 && pick6(d, N, true).nth == 512 &&
-                                env_int("KCTC_FWD_IOW", 1) &&
+                                
                                 !(pick6(d, N, true).gs <= 8 && env_int("KCTC_STK_FWD", env_int("KCTC_STK", 1)))))
     return false;
   const V6Cfg c6 = pick6(d, N, true);
@@ -3487,7 +3481,7 @@ void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
   // forward pass: the updates of the previous step waited for it.
   // (blocks landing on a pinned producer's XCDs exit at once: launch enough that the budget stays)
   const int nb = stream_block_budget(d.dirs * p.nwg * p.rg, false);
-  x.max_blocks = env_int("KCTC_STREAM_BLOCKS", pinned ? nb * 8 / (8 - pinned) : nb);
+  x.max_blocks = pinned ? nb * 8 / (8 - pinned) : nb;
   {
     ProfSpan ps(c.side, "fwd_proj_stream");
     gemm_x3p(c.side, x);
@@ -3498,7 +3492,7 @@ void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
 // Can `c`'s layer-0 projection stream off this component's y rows
 // (launch_chain_rows)?  Split-fp16 into split-fp16, the 256-tile row stream.
 bool chain_rows_ok(const RnnDesc &d, int ver, int T, int N, const RnnFwdChain *c) {
-  if (!c || !c->d || !c->side || ver != 6 || d.dirs != 2 || d.prec == kPrecBf16 || !env_int("KCTC_FWD_ROWS", 1))
+  if (!c || !c->d || !c->side || ver != 6 || d.dirs != 2 || d.prec == kPrecBf16 || !env_int("KCTC_FWD_STREAM", 1))
     return false;
   const RnnDesc &n = *c->d;
   const long TN = (long)T * N;
@@ -3558,7 +3552,7 @@ void launch_chain_rows(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
   const int pinned = p.xpd ? d.dirs * p.rg : 0;
   if (pinned) { a.xcd_word = p.flags + kXcdWord; a.xcd_count = pinned; }
   // 128: every CU the recurrence leaves (configs[1]: 96 -> 128 blocks 720k -> 751k frames/s)
-  const int nb = std::min(env_int("KCTC_FWD_ROWS_BLOCKS", 128), stream_block_budget(d.dirs * p.nwg * p.rg, false));
+  const int nb = std::min(128, stream_block_budget(d.dirs * p.nwg * p.rg, false));
   a.blocks = pinned ? nb * 8 / (8 - pinned) : nb;
   {
     ProfSpan ps(c.side, "fwd_proj_rows");
@@ -3679,7 +3673,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
   // consumer-gated projection: the split-fp16 forward with IO waves
   // (launch6_u), XCD-pinned so that the GEMM keeps to the other XCDs
   const bool gate_ok = side && ver == 6 && c6.U == 16 && c6.nth == 512 && d.prec == kPrecX3 &&
-                       env_int("KCTC_FWD_IOW", 1) &&
+                       
                        !(c6.gs <= 8 && env_int("KCTC_STK_FWD", env_int("KCTC_STK", 1))) &&
                        env_int("KCTC_FWD_GATE", 0) && xcd_mask(d, N, true) != 0 &&
                        __builtin_popcount(xcd_mask(d, N, true)) <= 4 &&  // XCDs left to the GEMM
@@ -3703,12 +3697,12 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     const bool gated = gate_ok && !skip_proj && use_x3(Din, 32);
     hipEvent_t gfork = nullptr;
     std::function<void()> gated_launch;  // the deferred packs + gated GEMM
-    // diagnostic (KCTC_GATE_DIAG): 1 the gated GEMM stream-ordered before an
+    // diagnostic (0 in the product): 1 the gated GEMM stream-ordered before an
     // ungated recurrence, 2 stream-ordered before the gated recurrence
-    const int gdiag = gated ? env_int("KCTC_GATE_DIAG", 0) : 0;
-    // diagnostic: the GEMM on a stream of its own at normal priority (KCTC_GATE_STREAM=1)
+    const int gdiag = 0;
+    // diagnostic (off): the GEMM on a stream of its own at normal priority
     hipStream_t gside = side;
-    if (gated && env_int("KCTC_GATE_STREAM", 0)) {
+    if (false) {
       static hipStream_t own = nullptr;
       if (!own) KCTC_HIP_CHECK(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
       gside = own;
@@ -3806,8 +3800,8 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.ncol = (NW * U + 15) / 16 * 16; p.Npad = (N + 15) / 16 * 16;
     p.w = wl; p.pl_stride = pls; p.r_off = roff; p.bR_off = bR;
     p.G = R0 + lay.G; p.y = out; p.aux = R0 + lay.aux; p.err = err;
-    p.sync = ver == 4 ? kSyncFlag : env_int("KCTC_SYNC_FWD", env_int("KCTC_SYNC", kSyncData));
-    p.allow_local = env_int("KCTC_LOCAL", 0);
+    p.sync = ver == 4 ? kSyncFlag : kSyncData;
+    p.allow_local = 0;
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, kFlagBytes, s));
     const size_t lds = ver == 6 ? fwd6_lds_bytes(d, c6) : fwd_lds_bytes(d, N, U);
@@ -3815,14 +3809,14 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.rg = ver == 6 ? c6.rg : 1;
     p.gs = ver == 6 ? c6.gs : 16;
     p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
-    p.poll_sleep = env_int("KCTC_POLL_SLEEP", 1);
-    p.gla = env_int("KCTC_FWD_GLA", 3) == 7 && !gated ? 7 : 3;  // G rows fetched 3 or 7 steps ahead (IO waves)
+    p.poll_sleep = 1;
+    p.gla = 3;  // G rows fetched 3 steps ahead (IO waves)
     if (gated) {
       p.gtf = gdiag == 1 ? nullptr : gtf + 64;
       p.gid = gid;
       p.gmt = (int)((TN + 255) / 256);
       p.ggx = (NW * H + 255) / 256;
-      p.gplain = env_int("KCTC_GATE_PLAIN", 0);
+      p.gplain = 0;
     }
     if (ver == 6 && bf16_io(d)) {  // the output also as packed bf16 rows and columns
       p.yr = reinterpret_cast<__bf16 *>(R0 + lay.pkyr);
@@ -3842,10 +3836,10 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       p.ring = p.xpd ? 2 : 0;
       p.fcopy = p.xpd && chained;
       p.ysc1 = rowchain ? 1 : 0;
-      p.allow_local = p.xpd ? env_int("KCTC_LOCAL", 1) : 0;
+      p.allow_local = p.xpd ? 1 : 0;
       // self-tagged hand-off (the kernel takes it for split-fp16 without IO
       // waves or a write-through copy): the ring's two images start at tag 1
-      p.dtag = d.prec != kPrecBf16 && p.ring == 2 && !p.fcopy && T >= 2 && env_int("KCTC_FWD_DTAG", 1);
+      p.dtag = d.prec != kPrecBf16 && p.ring == 2 && !p.fcopy && T >= 2;
       if (p.dtag) {  // rnn_fwd_rec6's ring: after T step images of XS = 64 H rg halves (2 dirs, hi / lo, 16 rows)
         const size_t xs = sizeof(_Float16) * 64 * (size_t)d.H * p.rg;
         KCTC_HIP_CHECK(hipMemsetAsync(reinterpret_cast<char *>(p.xch) + xs * T, 0x01, 2 * xs, s));
@@ -3856,7 +3850,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     if (tr.arm("fwd", grid.x)) p.trace = tr.dev;
     // W^T of the backward's streamed dx GEMM, packed beside this recurrence
     // (rnn_backward_data's `streamed` shapes; one-layer descriptors)
-    const bool prepack = pre && pre->dx && pre->stream && pre->ev && ver == 6 && d.layers == 1 && dirs == 2 && env_int("KCTC_PREPACK", 1) &&
+    const bool prepack = pre && pre->dx && pre->stream && pre->ev && ver == 6 && d.layers == 1 && dirs == 2 &&
                          ((d.prec == kPrecX3 && N <= 16) || env_int("KCTC_STREAM_ALL", 0)) && use_x3(NW * H) &&
                          NW * H <= 4096 && (d.prec == kPrecX3 || (NW * H) % 64 == 0);
     const bool prepack_w = pre && pre->stream && pre->wev && pre->wgrad && pre->in_bound > 0.f && ver == 6 &&
@@ -3987,9 +3981,9 @@ void launch_bwd_stream(const RnnDesc &d, const RecParams &p, int l, const float 
   // 256-tile launch: 48 blocks keep up with the recurrence and leave the
   // other CUs beside it to the weight GEMMs (rnn_backward_weights beside)
   const bool t256 = x3p_bwd_stream_256(a.M, a.N, a.KB, bf);
-  const int nb = std::min(t256 ? env_int("KCTC_BWD_S256_BLOCKS", 64) : 128,
+  const int nb = std::min(t256 ? 64 : 128,
                           stream_block_budget(d.dirs * p.nwg * p.rg, true));
-  a.blocks = env_int("KCTC_BWD_STREAM_BLOCKS", pinned ? nb * 8 / (8 - pinned) : nb);
+  a.blocks = pinned ? nb * 8 / (8 - pinned) : nb;
   // not before every workgroup of the recurrence is resident: its blocks
   // wait (on_pinned_xcd) for the pinned recurrence's XCDs to register, and a
   // block parked on one of those XCDs' CUs before the recurrence's last
@@ -4169,8 +4163,8 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     p.bR_off = d.lin_offset(l * dirs, NW, true) - pl0;
     p.G = R0 + lay.G; p.y = const_cast<float *>(out); p.aux = R0 + lay.aux;
     p.dy = dcur; p.E = E; p.DX = DX; p.bias = R0 + lay.bias; p.err = err;
-    p.sync = ver >= 4 ? kSyncFlag : env_int("KCTC_SYNC_BWD", env_int("KCTC_SYNC", kSyncFlag));
-    p.allow_local = env_int("KCTC_LOCAL", 0);
+    p.sync = kSyncFlag;
+    p.allow_local = 0;
     if (ws_bytes < rnn_workspace_bytes(d, T, N)) return KRNN_BAD_PARAM;
     p.flags = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + flags_offset(d, T, N));
     KCTC_HIP_CHECK(hipMemsetAsync(p.flags, 0, kFlagBytes, s));
@@ -4185,13 +4179,13 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
       // the streamed dx GEMM beside it (2.41 without), 468k -> 511k frames/s
       p.xpd = xcd_mask(d, N, false) ? 1 : 0;
       p.ring = p.xpd ? 2 : 0;
-      p.allow_local = env_int("KCTC_LOCAL", 1);
-      p.poll_sleep = env_int("KCTC_POLL_SLEEP", 1);
-      p.bfpart = env_int("KCTC_BF16_PARTIALS", 1);
+      p.allow_local = 1;
+      p.poll_sleep = 1;
+      p.bfpart = 1;
       p.xch = xch_acquire(sizeof(float) * (size_t)T * dirs * p.nwg * (16 * H + 64) * p.rg, s);
       // self-tagged hand-off (fp32 partials through the L2 ring): the two ring
       // images start with tag 1 in every word (steps 0 and 1 publish tag 0)
-      p.dtag = d.prec != kPrecBf16 && p.ring == 2 && p.xpd && T >= 2 && env_int("KCTC_BWD_DTAG", 1);
+      p.dtag = d.prec != kPrecBf16 && p.ring == 2 && p.xpd && T >= 2;
       if (p.dtag)
         KCTC_HIP_CHECK(hipMemsetAsync(p.xch, 0x01, sizeof(float) * 2 * (size_t)dirs * p.nwg * (16 * H + 64) * p.rg, s));
     } else {
@@ -4212,7 +4206,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     // its dGates rows must be written through too
     const bool wstream = wgrad && wgrad->side && !dxl && ver == 6 && !p.xpd && d.layers == 1 &&
                          rnn_wgrad_stream_ok(d, T, N);
-    p.e_sc1 = env_int("KCTC_DIAG_ESC1", (streamed || wstream) ? 1 : 0);  // diagnostic override (0 with streaming: wrong dx)
+    p.e_sc1 = (streamed || wstream) ? 1 : 0;
     // bf16: dGates straight into the packed operands of the dx / dW / dR GEMMs
     // (no fp32 rows, no pack passes over them; KCTC_BF16_DIRECT=0: the fp32
     // rows and the pack kernels as in round 3)
@@ -4494,7 +4488,7 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       // input^T (per-dim), and for dR the output shifted by one step per direction
       ProfSpan ps(s, "x3_pack_w");
       // beside a pinned recurrence: off its XCDs (x3p_pack_cols avoid)
-      const unsigned *av = beside && env_int("KCTC_PACK_AVOID", 1) ? rnn_pinned_xcds() : nullptr;
+      const unsigned *av = beside ? rnn_pinned_xcds() : nullptr;
       const int nx = std::max(1, rnn_usable_cus() / kCusPerXcd);
       // their item counters: flag words 1010..1014 (this component's
       // recurrences, which use the flag words, are done)
@@ -4528,7 +4522,7 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     // stream fell one GEMM per layer behind, 4 ms of weight GEMMs after the
     // last recurrence)
     const bool pair = beside && x3 && !two && T > 1 && x3p_use_256((int)G4, Din) && x3p_use_256((int)G4, H) &&
-                      max_blocks > 0 && env_int("KCTC_WGRAD_PAIR", 1);
+                      max_blocks > 0;
     X3PArgs xw;
     if (x3) {
       X3PArgs &x = xw;
@@ -4544,7 +4538,7 @@ int rnn_backward_weights(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       x.ws = (two || pair) && sR > 1 ? ws + al64(sR * dirs * G4 * H) : ws;
       x.max_blocks = g.max_blocks; x.tile_counter = g.tile_counter;
       if (pair) {
-        x.max_blocks = env_int("KCTC_SIDE_BESIDE_BLOCKS", 192);
+        x.max_blocks = 192;
         x.avoid_word = rnn_pinned_xcds();
         x.avoid_xcds = std::max(1, rnn_usable_cus() / kCusPerXcd);
       } else {

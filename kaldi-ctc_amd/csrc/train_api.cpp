@@ -286,8 +286,8 @@ static std::vector<uint32_t> partition_mask(int part, int nparts, int cus) {
 }
 
 // compute stream at the highest priority (the latency-bound recurrences),
-// the weight-gradient side stream at the lowest; KCTC_OVERLAP=0 keeps
-// everything on one stream
+// the weight-gradient side stream at the lowest, and a default-priority
+// queue for the streamed GEMMs
 void kctcNnetImpl::create_streams() {
   if (g_nparts > 1) {  // ranks sharing the device: this rank's streams on its CU share only
     int cus = 0;
@@ -303,12 +303,9 @@ void kctcNnetImpl::create_streams() {
   int lo = 0, hi = 0;
   KCTC_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
   KCTC_HIP_CHECK(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, hi));
-  const char *e = getenv("KCTC_OVERLAP");
-  if (!(e && *e == '0')) {
-    KCTC_HIP_CHECK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, lo));
-    // streamed GEMMs (default priority: a queue of its own, neither the recurrences' nor the side stream's)
-    KCTC_HIP_CHECK(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
-  }
+  KCTC_HIP_CHECK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, lo));
+  // streamed GEMMs (default priority: a queue of its own, neither the recurrences' nor the side stream's)
+  KCTC_HIP_CHECK(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
 }
 
 template <typename F>
