@@ -412,26 +412,22 @@ def main():
         """K steps, pipelined host loop (each call queues a step and returns
         the stats of the step before the previous one; the flush inside the
         timed region waits for the rest).  h2d: the features are copied from
-        pinned host memory inside the timed region (SURVEY §8d's region) on the
-        trainer's copy stream, one minibatch ahead, so the next step's H2D runs
-        beside this step's tail (kctc_nnet_copy_features_async); else they are
-        resident in HBM.  HIP
+        pinned host memory on the trainer's stream at the start of each step
+        (SURVEY §8d's timed region); else they are resident in HBM.  HIP
         events on the trainer's stream mark every step's start."""
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
         staging = [torch.empty_like(batches[0][0]) for _ in range(3)] if h2d else None
         barrier()
         t0 = time.perf_counter()
         frames, stats = 0, []
-        if h2d:  # step K's features go up on the trainer's copy stream while step K-1 finishes
-            net.copy_features_async(staging[0], batches[args.warmup][4])
         for i, step in enumerate(range(args.warmup, total)):
             f, nf, fl, ll, fh = batches[step]
             evs[i].record(ext)
             if h2d:
-                f = staging[i % 3]
+                with torch.cuda.stream(ext):
+                    f = staging[i % 3]
+                    f.copy_(fh, non_blocking=True)
             r = net.train_step_async(f, T, N, nf, fl, ll)
-            if h2d and step + 1 < total:  # (the minibatch two calls back is done: its buffer is free)
-                net.copy_features_async(staging[(i + 1) % 3], batches[step + 1][4])
             if r is not None:
                 stats.append(r)
             frames += int(nf.sum())

@@ -103,16 +103,6 @@ int kctc_nnet_train_step(kctcNnet_t nnet, const float *feats_dev, int T_max, int
 int kctc_nnet_train_step_async(kctcNnet_t nnet, const float *feats_dev, int T_max, int N,
                                const int *num_frames, const int *flat_labels, const int *label_lengths,
                                int *have_stats, double *tot_objf, double *tot_accuracy, double *tot_weight);
-/* Host -> device copy of a minibatch's features on a stream of the trainer's
- * own (no reference counterpart: the reference copies inside
- * FormatNnetInput on the compute stream, nnet-cudnn-component.cc via
- * CuMatrix::CopyFromMat).  The next train_step / train_step_async /
- * compute_objf waits for it on the device; the copy itself overlaps what is
- * still queued (the previous minibatch's exchange, updates and stats).
- * dst_dev must not be in use by a queued step: with train_step_async, once a
- * call returns, the buffer of the minibatch queued two calls earlier is free.
- * src_host should be pinned for an asynchronous copy. */
-int kctc_nnet_copy_features_async(kctcNnet_t nnet, float *dst_dev, const float *src_host, size_t count);
 int kctc_nnet_train_flush(kctcNnet_t nnet, int *have_stats, double *tot_objf, double *tot_accuracy,
                           double *tot_weight);
 

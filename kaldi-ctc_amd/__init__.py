@@ -480,17 +480,6 @@ class Nnet:
                                                  ctypes.byref(a), ctypes.byref(w)), "train_step_async")
         return (o.value, a.value, w.value) if h.value else None
 
-    def copy_features_async(self, dst, src):
-        """Host -> device copy of a minibatch's features on the trainer's copy
-        stream (kctc_nnet_copy_features_async): the next train_step(_async) /
-        compute_objf waits for it on the device, the copy overlaps what is
-        still queued.  dst: device float32 tensor not used by a queued step;
-        src: contiguous float32 host tensor / array (pinned for an async copy)."""
-        n = dst.numel()
-        assert src.numel() == n if hasattr(src, "numel") else src.size == n
-        ptr = src.data_ptr() if hasattr(src, "data_ptr") else src.ctypes.data
-        _tcheck(lib().kctc_nnet_copy_features_async(self.h, dst.data_ptr(), ptr, n), "copy_features_async")
-
     def train_flush(self):
         """Stats of the queued minibatches, oldest first (kctc_nnet_train_flush)."""
         out = []

@@ -17,16 +17,6 @@ struct kctcNnetImpl {
   kctc::nnet2::NnetCtcUpdater trainer{&nnet, true};
   kctc::nnet2::NnetCtcUpdater evaluator{&nnet, false};
   hipStream_t side = nullptr, stream2 = nullptr;
-  // kctc_nnet_copy_features_async: host -> device copies on a stream of
-  // their own (the next minibatch's features go up while this one's exchange
-  // and updates finish); h2d_ev is what the next queued step waits for
-  hipStream_t copy = nullptr;
-  hipEvent_t h2d_ev = nullptr;
-  bool h2d_pending = false;
-  void wait_h2d() {
-    if (h2d_pending) KCTC_HIP_CHECK(hipStreamWaitEvent(stream, h2d_ev, 0));
-    h2d_pending = false;
-  }
   kctc::nnet2::GradExchange *dp = nullptr;
   bool dp_average = false;  // model averaging: no per-step gradient exchange
   kctc::nnet2::DevBuf egs_feats, egs_scratch;  // TrainNnetSimple staging
@@ -44,9 +34,6 @@ struct kctcNnetImpl {
     if (stream) (void)hipStreamSynchronize(stream);
     if (side) (void)hipStreamSynchronize(side);
     if (stream2) (void)hipStreamSynchronize(stream2);
-    if (copy) (void)hipStreamSynchronize(copy);
-    if (copy) (void)hipStreamDestroy(copy);
-    if (h2d_ev) (void)hipEventDestroy(h2d_ev);
     auto &d = kctc::nnet2::CuDevice::Instantiate();
     if (d.stream == stream) d.stream = nullptr;
     if (d.side == side) d.side = nullptr;

@@ -483,7 +483,6 @@ int kctc_nnet_train_step(kctcNnet_t n, const float *feats_dev, int T_max, int N,
                          double *tot_objf, double *tot_accuracy, double *tot_weight) {
   return guarded([&] {
     n->activate();
-    n->wait_h2d();
     auto st = n->trainer.ComputeForMinibatch(feats_dev, T_max, N, num_frames, flat_labels,
                                              label_lengths);
     if (tot_objf) *tot_objf = st.tot_objf;
@@ -498,7 +497,6 @@ int kctc_nnet_train_step_async(kctcNnet_t n, const float *feats_dev, int T_max, 
   return guarded([&] {
     n->activate();
     if (have_stats) *have_stats = 0;
-    n->wait_h2d();
     n->trainer.Enqueue(feats_dev, T_max, N, num_frames, flat_labels, label_lengths);
     if (n->trainer.Pending() == 2) {
       auto st = n->trainer.Finish();
@@ -507,20 +505,6 @@ int kctc_nnet_train_step_async(kctcNnet_t n, const float *feats_dev, int T_max, 
       if (tot_accuracy) *tot_accuracy = st.tot_accuracy;
       if (tot_weight) *tot_weight = st.tot_weight;
     }
-  });
-}
-
-int kctc_nnet_copy_features_async(kctcNnet_t n, float *dst_dev, const float *src_host, size_t count) {
-  return guarded([&] {
-    KCTC_REQUIRE(n && dst_dev && src_host, "null argument");
-    n->activate();
-    if (!n->copy) {
-      KCTC_HIP_CHECK(hipStreamCreateWithFlags(&n->copy, hipStreamNonBlocking));
-      KCTC_HIP_CHECK(hipEventCreateWithFlags(&n->h2d_ev, hipEventDisableTiming));
-    }
-    KCTC_HIP_CHECK(hipMemcpyAsync(dst_dev, src_host, sizeof(float) * count, hipMemcpyHostToDevice, n->copy));
-    KCTC_HIP_CHECK(hipEventRecord(n->h2d_ev, n->copy));
-    n->h2d_pending = true;
   });
 }
 
@@ -544,7 +528,6 @@ int kctc_nnet_compute_objf(kctcNnet_t n, const float *feats_dev, int T_max, int 
                            double *tot_objf, double *tot_accuracy, double *tot_weight) {
   return guarded([&] {
     n->activate();
-    n->wait_h2d();
     auto st = n->evaluator.ComputeForMinibatch(feats_dev, T_max, N, num_frames, flat_labels,
                                                label_lengths);
     if (tot_objf) *tot_objf = st.tot_objf;
