@@ -79,6 +79,8 @@ int rnn_comm_cus();
 unsigned rnn_bwd_registrations();
 void rnn_comm_gate(hipStream_t s, unsigned target);
 unsigned rnn_comm_gate_errors();
+// s waits until *word - target >= 0 (a launch's own residency count)
+void rnn_resident_gate(hipStream_t s, const unsigned *word, unsigned target);
 // device word: bit x set once an XCD-pinned backward recurrence ran on XCD x
 // (never cleared; GEMMs launched beside one avoid those XCDs, X3PArgs::avoid_word)
 const unsigned *rnn_pinned_xcds();

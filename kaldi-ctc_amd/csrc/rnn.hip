@@ -1481,6 +1481,7 @@ constexpr int kFlagStride = 32;  // words
 // word of the flag area where an XCD-pinned backward recurrence's workgroups
 // OR in 1 << XCC_ID (words 1008 / 1009: weight-gradient tile counters)
 constexpr int kXcdWord = 1016;
+constexpr int kResWord = 1017;  // pinned forward: workgroups resident so far (launch_chain_rows' gate)
 __device__ __forceinline__ unsigned *flag6(const RecParams &p, int grp, int d, int g, int nwg) {
   return p.flags + 1024 + (((long)grp * p.dirs + d) * nwg + g) * kFlagStride;
 }
@@ -2617,7 +2618,10 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // gflag = k there means rows of steps <= k - 3 are out ("epoch s + 3" as
   // the backward's rows), T + 2 at exit
   unsigned *gflag = ((fcopy || p.ysc1) && g == 0) ? agg_flag6(p, grp, d) : nullptr;
-  if (p.xpd && tid == 0) atomicOr(p.flags + kXcdWord, 1u << xcc_id());
+  if (p.xpd && tid == 0) {
+    atomicOr(p.flags + kXcdWord, 1u << xcc_id());
+    atomicAdd(p.flags + kResWord, 1u);
+  }
   // gated projection: tell the GEMM's blocks which XCDs this launch holds
   // (this call's id in the tag word of the XCD; they leave those XCDs)
   if (GATE && p.gtf && tid == 0) st_u32_sc1(const_cast<unsigned *>(p.gtf) - 56 + xcc_id(), p.gid);
@@ -3554,6 +3558,11 @@ void launch_chain_rows(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
   // 128: every CU the recurrence leaves (configs[1]: 96 -> 128 blocks 720k -> 751k frames/s)
   const int nb = std::min(128, stream_block_budget(d.dirs * p.nwg * p.rg, false));
   a.blocks = pinned ? nb * 8 / (8 - pinned) : nb;
+  // not before every workgroup of the recurrence is resident: dispatched
+  // first (another queue), 32 blocks per XCD would take every CU of an XCD
+  // the recurrence is pinned to before its first workgroup got there (seen
+  // once as a 3-s stream-wait timeout, error 0x2)
+  if (pinned) rnn_resident_gate(c.side, p.flags + kResWord, (unsigned)(d.dirs * p.nwg * p.rg));
   {
     ProfSpan ps(c.side, "fwd_proj_rows");
     gemm_x3p_bwd_stream(c.side, a);
@@ -3617,6 +3626,11 @@ __global__ __launch_bounds__(64) void comm_gate_kernel(const unsigned *word, uns
 }
 
 unsigned rnn_bwd_registrations() { return reg_of_device().expected; }
+// the same wait on a launch's own count (a timeout counts as the exchange gate's)
+void rnn_resident_gate(hipStream_t s, const unsigned *word, unsigned target) {
+  hipLaunchKernelGGL(comm_gate_kernel, dim3(1), dim3(64), 0, s, word, target, reg_of_device().word + 1);
+  KCTC_HIP_CHECK(hipGetLastError());
+}
 const unsigned *rnn_pinned_xcds() { return reg_of_device().word + 2; }
 void rnn_comm_gate(hipStream_t s, unsigned target) {
   RegWord &r = reg_of_device();
