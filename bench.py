@@ -208,7 +208,7 @@ def ctc_bytes(T_max, A, num_frames, label_lengths):
 def _committed_pmc(kind, config):
     """Newest committed rocprofv3 PMC summary of `kind` ("traffic" or "mfma")
     for `config`: profiles/rNN*_pmc_<kind>.json for configs[1],
-    profiles/rNN*_cfg<N>_pmc_<kind>.json otherwise (scripts/gpu_bench_prof.sh
+    profiles/rNN*_cfg<N>_pmc_<kind>.json otherwise (scripts/gpu_prof.sh
     and scripts/gpu_cfg_prof.sh on this workload).  bench.py cannot read
     counters itself."""
     import glob
@@ -277,14 +277,17 @@ def loss_match(k, dev, case="cfg1"):
     logits = net.last_output(T, N, A)
     table = {"costs": (float(rc.max()), tol("costs")),
              "tot_objf": (abs(objf - float(g["tot_objf"])) / abs(float(g["tot_objf"])), tol("costs"))}
-    e = S.compare(logits, S.load(g, "logits"), 500, tol("logits"))
-    table["logits"] = (max(e["norm"], e["proj"]), tol("logits"))
+    samp = {}  # sampled entries' max |diff| / rms against SAMP_FACTOR x the bar
+
+    def put(key, e, bar):
+        table[key] = (max(e["norm"], e["proj"]), bar)
+        samp[key] = (e["samp"], S.SAMP_FACTOR * bar)
+    put("logits", S.compare(logits, S.load(g, "logits"), 500, tol("logits")), tol("logits"))
     for c, i in enumerate(rnn_idx):
-        e = S.compare(np.clip(net.get_grad(i).astype(np.float64), -5.0, 5.0), S.load(g, f"g{c}"), 600 + c,
-                      tol("grad", c))
-        table[f"grad_rnn{c}"] = (max(e["norm"], e["proj"]), tol("grad", c))
-    e = S.compare(net.get_grad(aff_idx).astype(np.float64), S.load(g, "gaff"), 700, tol("affine"))
-    table["grad_affine"] = (max(e["norm"], e["proj"]), tol("affine"))
+        put(f"grad_rnn{c}", S.compare(np.clip(net.get_grad(i).astype(np.float64), -5.0, 5.0), S.load(g, f"g{c}"),
+                                      600 + c, tol("grad", c)), tol("grad", c))
+    put("grad_affine", S.compare(net.get_grad(aff_idx).astype(np.float64), S.load(g, "gaff"), 700, tol("affine")),
+        tol("affine"))
     ids = net.last_best_path(T, N)
     net.close()
     grads = [v[0] for key, v in table.items() if key.startswith("grad_")]
@@ -296,8 +299,11 @@ def loss_match(k, dev, case="cfg1"):
            "objf_per_label": objf / wt,
            "bar": "bf16 error model per output (tests/sketch_common.bf16_tol)" if bf16 else LOSS_BAR,
            "errors_vs_bar": {key: {"err": float("%.3g" % v[0]), "bar": float("%.3g" % v[1])}
-                             for key, v in table.items()}}
-    out["pass"] = bool(all(v[0] < v[1] for v in table.values()) and wt == float(g["tot_weight"]))
+                             for key, v in table.items()},
+           "sampled_entries_vs_bar": {key: {"err": float("%.3g" % v[0]), "bar": float("%.3g" % v[1])}
+                                      for key, v in samp.items()}}
+    out["pass"] = bool(all(v[0] < v[1] for v in list(table.values()) + list(samp.values())) and
+                       wt == float(g["tot_weight"]))
     return out
 
 

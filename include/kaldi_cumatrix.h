@@ -30,19 +30,6 @@ size_t kcm_add_mat_mat_x3_workspace(int M, int N, int K);
 int kcm_add_mat_mat_x3(struct ihipStream_t *stream, int transA, int transB, int M, int N, int K,
                        float alpha, const float *A, long lda, const float *B, long ldb, float beta,
                        float *C, long ldc, void *ws);
-/* Measurement helper (no reference counterpart): average ms of the packed
- * gate GEMM (the kernel under kcm_add_mat_mat_x3 and the RNN GEMMs) on random
- * packed operands, C[M][N] = A[M][K] B[N][K]^T, split-fp16 (bf16 = 0) or bf16
- * operands, split-K slices; -1 on failure. */
-float kcm_bench_gemm_packed(struct ihipStream_t *stream, int M, int N, int K, int bf16, int iters, int split);
-/* Test helper (no reference counterpart): the streamed direction-split GEMM
- * of the RNN backward (dx) and chained forward (next projection) against a
- * producer that has already finished: C[M][N] = E[:, 0:K] Wt[0]^T +
- * E[:, K:2K] Wt[1]^T (+ bias[c]), E [M][2K], Wt [2][N][K], device pointers;
- * forward: the producer's direction order of a forward recurrence; tail_rows:
- * split-K tail slots per direction (-1: default).  1 on unsupported shapes. */
-int kcm_test_row_stream(struct ihipStream_t *stream, int M, int N, int K, int forward, int tail_rows,
-                        const float *E, const float *Wt, const float *bias, float *C);
 /* ids[r] = argmax_c m[r][c].  Replaces CuMatrix::FindRowMaxId on the device
  * (src/cudamatrix/cu-matrix.cc:1612-1628 -> _find_row_max_id,
  * src/cudamatrix/cu-kernels.cu:2454-2500) with the same result bit for bit:

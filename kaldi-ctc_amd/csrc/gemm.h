@@ -86,18 +86,6 @@ struct X3PArgs {
   // blocks, no exponents): two v_mfma_f32_16x16x32_bf16 per stage, fp32
   // accumulation; streaming: A = a bf16 v6 forward's h images (eA0 = 0)
   bool bf16 = false;
-  // Consumer-gated mode (gate_flags != null; 256 x 256 tiles, no split-K,
-  // batch = the consumer's directions): C is the input projection of a v6
-  // forward recurrence that runs CONCURRENTLY and reads its rows as they are
-  // published.  Tiles are taken in the order the recurrence needs them
-  // (batch 0 row tiles ascending, batch 1 descending, all column tiles of a
-  // row tile together); C is written through (sc1) and then the tile's flag
-  // gate_flags[(b * row tiles + tm) * column tiles + tn] = gate_id.  Blocks on
-  // the XCDs in xcd_avoid (the recurrence's) exit before taking work.
-  // tile_counter is required.
-  unsigned *gate_flags = nullptr;
-  unsigned gate_id = 0;
-  unsigned xcd_avoid = 0;
   // Beside an XCD-pinned recurrence (non-gated, non-streaming 256-tile GEMMs
   // with a tile counter): blocks whose XCD has its bit set in *avoid_word
   // (rnn.hip rnn_pinned_xcds: the XCDs pinned backward recurrences ran on)
@@ -109,6 +97,8 @@ struct X3PArgs {
   int avoid_xcds = 8;
 };
 void gemm_x3p(hipStream_t s, const X3PArgs &g);
+// rnn.hip: s passed the residency gate of the recurrence in flight (or none is)
+bool rnn_side_gated(hipStream_t s);
 // two independent 256-tile problems (e.g. a layer's dW and dR) as ONE launch
 // sharing g1's tile counter, then each one's split-K reduction: beside a
 // pinned recurrence a launch completes only once its blocks on the

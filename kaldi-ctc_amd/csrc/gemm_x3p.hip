@@ -74,9 +74,6 @@ struct PParams {
   int *done;               // [2][nrt] pack jobs finished
   int *arrive;             // [nrt][gx] direction partials arrived (+1) / partial published (+2)
   float *part;             // [M][N] the first direction's partial
-  // consumer-gated projection (X3PArgs::gate_flags)
-  unsigned *gate;
-  unsigned gate_id, xcd_avoid;
   int mt;                  // row tiles
   const unsigned *avoid;   // X3PArgs::avoid_word, avoid_xcds
   int nxcd;
@@ -976,22 +973,10 @@ __device__ __forceinline__ void p256_tile(const PParams &p, unsigned char *lds, 
           float *c = C + (long)row * p.ldc + col;
           float o = p.alpha * v + badd[j];
           if (p.beta != 0.f) o += p.beta * *c;
-          if (p.gate && !(p.dbg & 0x200)) __hip_atomic_store(reinterpret_cast<unsigned *>(c), __float_as_uint(o), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);  // write-through: read by a running consumer
-          else *c = o;
+          *c = o;
         }
       }
     }
-  if (p.gate && !(p.dbg & 0x400)) {  // the tile's rows are out (every storing wave drained): publish it
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-      __hip_atomic_store(p.gate + ((long)b * p.mt + tm) * p.gx + tn, p.gate_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // reconverge: without it hipcc structured the job loop with this
-    // lane-0 store as a divergent exit and left lane 0 -- the one that takes
-    // the next job -- behind (the loop then spun on a stale job id)
-    __syncthreads();
-  }
 }
 
 // beside a pinned recurrence (X3PArgs::avoid_word): true on one of its XCDs
@@ -1014,42 +999,15 @@ __global__ __launch_bounds__(NTH2, 1) void gemm_p256_kernel(PParams p) {
   int *next = reinterpret_cast<int *>(lds + 2 * 2 * TILEB2);
   const int total = p.tiles * p.batch * p.split;
   if (avoid_here(p, next + 1)) return;
-  // consumer-gated: off the consumer's XCDs -- the static mask, and the XCDs
-  // the running consumer has tagged with this call's id (gate - 56 + XCC_ID),
-  // checked before every job, so a block that started before the consumer's
-  // workgroups arrived on its XCD leaves after its current tile
-  unsigned xcc = 0;
-  if (p.gate) {
-    if (threadIdx.x == 0) __hip_atomic_store(p.gate - 63, p.gate_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    xcc &= 0xfu;
-    if (((p.xcd_avoid >> xcc) & 1u) && !(p.dbg & 0x100)) return;
-  }
   if (p.counter) {  // dynamic scheduling (beside a persistent kernel)
     while (true) {
-      if (p.gate && !(p.dbg & 0x100)) {
-        if (threadIdx.x == 0)
-          next[1] = __hip_atomic_load(p.gate - 56 + xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.gate_id;
-        __syncthreads();
-        const int here = __builtin_amdgcn_readfirstlane(next[1]);
-        __syncthreads();
-        if (here) return;
-      }
       if (threadIdx.x == 0) *next = atomicAdd(p.counter, 1);
       __syncthreads();
       const int id = __builtin_amdgcn_readfirstlane(*next);
       __syncthreads();
       if (id >= total) break;
       int tm, tn, b, ks;
-      if (p.gate) {  // in the consumer's order: step q's row tile of every batch, all column tiles
-        const int q = id / (p.batch * p.gx), r = id - q * p.batch * p.gx;
-        b = r / p.gx;
-        tn = r - b * p.gx;
-        tm = (b & 1) ? p.mt - 1 - q : q;
-        ks = 0;
-      } else {
-        decode_tile(p, id, total, false, tm, tn, b, ks);
-      }
+      decode_tile(p, id, total, false, tm, tn, b, ks);
       p256_tile<BFM>(p, lds, tm, tn, b, ks);
     }
     return;
@@ -1743,15 +1701,12 @@ static PParams x3p_params(const X3PArgs &g, bool &t256) {
   p.xcd_word = g.stream_xcd_word; p.xcd_count = g.stream_xcd_count;
   p.sdir = 0;
   p.arrive = nullptr;
-  p.gate = g.gate_flags; p.gate_id = g.gate_id; p.xcd_avoid = g.xcd_avoid;
   p.mt = ceil_div(g.M, TB2);
-  if (p.gate && (!t256 || p.split > 1 || !p.counter || g.beta != 0.f))
-    throw std::invalid_argument("gemm_x3p: a gated projection runs on 256 tiles, no split-K, with a tile counter");
   p.dbg = 0;
   p.p256v = 0;
   p.avoid = g.avoid_word;
   p.nxcd = g.avoid_xcds;
-  if (p.avoid && (!t256 || !p.counter || p.gate))
+  if (p.avoid && (!t256 || !p.counter))
     throw std::invalid_argument("gemm_x3p: avoid_word needs a 256-tile launch with a tile counter");
   return p;
 }
@@ -1786,6 +1741,8 @@ static void x3p_reduce(hipStream_t s, const PParams &p) {
 
 void gemm_x3p(hipStream_t s, const X3PArgs &g) {
   if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return;
+  if (g.stream_flags && !rnn_side_gated(s))
+    throw std::logic_error("gemm_x3p: streaming launch beside a recurrence without its residency gate");
   bool t256 = false;
   PParams p = x3p_params(g, t256);
   const int total = p.tiles * p.batch * p.split;
@@ -1832,8 +1789,7 @@ void gemm_x3p_pair(hipStream_t s, const X3PArgs &g1, const X3PArgs &g2) {
   if (g1.M <= 0 || g1.N <= 0 || g1.batch <= 0) return gemm_x3p(s, g2);
   bool a = false, b = false;
   PParams p = x3p_params(g1, a), q = x3p_params(g2, b);
-  if (!a || !b || !p.counter || g1.bf16 != g2.bf16 || g1.stream_flags || g2.stream_flags || g1.gate_flags ||
-      g2.gate_flags)
+  if (!a || !b || !p.counter || g1.bf16 != g2.bf16 || g1.stream_flags || g2.stream_flags)
     throw std::invalid_argument("gemm_x3p_pair: two 256-tile problems with a tile counter");
   if (g1.bf16 && (p.eA || p.eB || q.eA || q.eB)) throw std::invalid_argument("gemm_x3p: bf16 operands take no exponents");
   const int total = p.tiles * p.batch * p.split + q.tiles * q.batch * q.split;
@@ -1869,6 +1825,8 @@ size_t x3p_bwd_stream_part_floats(int M, int N) {
 
 void gemm_x3p_bwd_stream(hipStream_t s, const X3PBwdStream &a) {
   if (a.M <= 0 || a.N <= 0) return;
+  if (!rnn_side_gated(s))
+    throw std::logic_error("gemm_x3p_bwd_stream: streaming launch beside a recurrence without its residency gate");
   const int K = a.KB * (a.bf16 ? 64 : 32);
   if (K > 4096 || a.Nf <= 0 || (long)a.M * a.N * 4 >= (1L << 31) || (long)a.M * a.KB * 128 >= (1L << 31) ||
       (a.lde & 3) || (a.edoff & 3))

@@ -511,8 +511,8 @@ void CuDNNRecurrentComponent::Forward(const CuMatrixBase &in, CuMatrixBase *out,
   in_tn_[0] = T;
   in_tn_[1] = N;
   ProfScope ps("layer_rnn_forward");
-  // the trainer's side stream (idle during the forward pass) for a projection
-  // computed beside the recurrence (rnn.h, consumer-gated projection)
+  // the trainer's side stream (idle during the forward pass): the W^T / x^T /
+  // y^T prepacks beside the recurrence (rnn.h RnnPrepack)
   auto &dev = CuDevice::Instantiate();
   hipStream_t side = S() == dev.stream ? dev.side : nullptr;
   RnnPrepack *pre = nullptr;
@@ -532,7 +532,7 @@ void CuDNNRecurrentComponent::Forward(const CuMatrixBase &in, CuMatrixBase *out,
   pre_y_ = out->Data();
   int st = rnn_forward_training(desc_, S(), T, N, in.Data(), params_.f(), out->Data(), workspace_.p,
                                 workspace_.bytes, reserve_.p, reserve_.bytes, DeviceError(), chain, projected, in_rows_,
-                                side, pre);
+                                pre);
   pre_ver_ = pver_;
   if (st) throw std::runtime_error("rnn_forward_training failed: " + std::to_string(st));
 }

@@ -81,6 +81,18 @@ void rnn_comm_gate(hipStream_t s, unsigned target);
 unsigned rnn_comm_gate_errors();
 // s waits until *word - target >= 0 (a launch's own residency count)
 void rnn_resident_gate(hipStream_t s, const unsigned *word, unsigned target);
+// Launches beside a running recurrence.  Every v6 recurrence counts its
+// resident workgroups in its own flag area (kResWord, zeroed with the flags
+// before the launch).  Each kernel that rnn.hip puts on another stream while
+// that recurrence runs -- the streamed GEMMs, the wgrad chunk gates, the
+// forward-time packs -- is enqueued behind a one-wave gate on that count
+// (rnn.hip beside_recurrence): nothing there can take a CU before every
+// workgroup of the recurrence holds its own, so a consumer spinning on the
+// recurrence's progress cannot keep a producer workgroup out.  The host
+// refuses a streaming launch (gemm_x3p with stream_flags,
+// gemm_x3p_bwd_stream) on a stream that has not passed the gate of the
+// recurrence this thread has in flight: rnn_side_gated(s) is false then.
+bool rnn_side_gated(hipStream_t s);
 // device word: bit x set once an XCD-pinned backward recurrence ran on XCD x
 // (never cleared; GEMMs launched beside one avoid those XCDs, X3PArgs::avoid_word)
 const unsigned *rnn_pinned_xcds();
@@ -114,12 +126,6 @@ struct RnnFwdChain {
 // in_rows (nullable): the input already packed as bf16 rows [T*N][D] (the
 // previous component's rnn_packed_output), used by a bf16 input projection
 // instead of packing x.
-// side (nullable): a stream for a consumer-gated input projection
-// (KCTC_FWD_GATE): the projection GEMM runs on `side` CONCURRENTLY with this
-// call's XCD-pinned recurrence, on the other XCDs, in the order the
-// recurrence needs its rows, and the recurrence's IO waves fetch a row tile
-// only once the GEMM has published it (gemm.h X3PArgs::gate_flags); joined
-// back into `s` before return.  Taken for the split-fp16 IO-wave forward only.
 // The backward's streamed dx GEMM reads W's columns packed (split-fp16 /
 // bf16 rows of W^T).  W does not change between a training step's forward and
 // backward, so rnn_forward_training packs them on `stream` while its own
@@ -145,8 +151,7 @@ struct RnnPrepack {
 int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *w, float *y, void *workspace, size_t ws_bytes,
                          void *reserve, size_t res_bytes, unsigned *err, RnnFwdChain *chain = nullptr,
-                         bool input_projected = false, const void *in_rows = nullptr, hipStream_t side = nullptr,
-                         RnnPrepack *pre = nullptr);
+                         bool input_projected = false, const void *in_rows = nullptr, RnnPrepack *pre = nullptr);
 // bf16 one-layer bidirectional components: the forward recurrence also writes
 // its output as packed bf16 rows [T*N][2H] and columns [2H][kbt64] into the
 // reserve (the GEMM operands the next component's projection / dW and this

@@ -159,7 +159,7 @@ static size_t xch_bytes(const RnnDesc &d, int T, int N) {
 //               shifted output^T [dirs*H][TN]
 // plus int exponents and float-bit column maxima (G = nW*H).
 struct PackLay {
-  size_t a, b, c, d, ea, eb, ec, ed, cm, part, cnt, part2, cme, fcnt, fpart, gtf, wt, ewt, cmw, xt, yt, ext, eyt, total;
+  size_t a, b, c, d, ea, eb, ec, ed, cm, part, cnt, part2, cme, fcnt, fpart, wt, ewt, cmw, xt, yt, ext, eyt, pcnt, total;
 };
 static PackLay pack_layout(const RnnDesc &d, int T, int N) {
   const long TN = (long)T * N, G = (long)d.nw() * d.H, Dm = std::max(d.D, d.dirs * d.H), dirs = d.dirs;
@@ -189,9 +189,6 @@ static PackLay pack_layout(const RnnDesc &d, int T, int N) {
   p.fcnt = o; o = align_up(o + sizeof(int) * ((TN + 127) / 128 * dirs * ((G + 127) / 128) + 64), 256);
   p.fpart = o; o = align_up(o + sizeof(float) * std::max((size_t)((TN + 127) / 128) * dirs * ((G + 127) / 128) * 128 * 128,
                                                           x3p_bwd_stream_part_floats((int)TN, (int)(dirs * G))), 256);
-  // consumer-gated projection: its tile counter (word 0), then the tile flags
-  // [dirs][row tiles][column tiles] from word 64 (never reset: a call's id)
-  p.gtf = o; o = align_up(o + sizeof(unsigned) * (64 + dirs * ((TN + 255) / 256) * ((G + 255) / 256)), 256);
   // W^T of the streamed dx GEMM, packed by the forward (RnnPrepack): kept
   // from the forward to the backward, apart from every other slot
   p.wt = o; o = align_up(o + x3p_bytes(dirs * Dm, G), 256);
@@ -202,6 +199,9 @@ static PackLay pack_layout(const RnnDesc &d, int T, int N) {
   p.yt = o; o = align_up(o + bw_c, 256);
   p.ext = o; o = align_up(o + sizeof(int) * (Dm + 64), 256);
   p.eyt = o; o = align_up(o + sizeof(int) * (dirs * d.H + 64), 256);
+  // item counters of those packs (on the prepack stream; apart from the
+  // recurrence flags, which the backward resets on the compute stream)
+  p.pcnt = o; o = align_up(o + sizeof(int) * 4, 256);
   p.total = o;
   return p;
 }
@@ -335,14 +335,6 @@ struct RecParams {
   // f + N), so that dR pairs it with the unshifted yc
   __bf16 *yr, *yc;
   int eshift;
-  // v6 forward with IO waves: the input projection G is computed CONCURRENTLY
-  // by a consumer-gated GEMM (gemm.h X3PArgs::gate_flags); before fetching a
-  // step's G rows the IO waves check that every column tile of the rows' row
-  // tile (256 rows) carries this call's id gid: gtf[(d * gmt + tile) * ggx + j]
-  const unsigned *gtf;
-  unsigned gid;
-  int gmt, ggx;
-  int gplain;  // diagnostic (0): the gated G rows fetched without sc1
   // v6 backward, fp32 partials, ring of 2: self-tagged hand-off (see
   // rnn_bwd_rec6): the consumers poll the partial-dh words themselves instead
   // of the producers' epoch flags; taken by the slots probe6 finds XCD-local
@@ -1481,7 +1473,7 @@ constexpr int kFlagStride = 32;  // words
 // word of the flag area where an XCD-pinned backward recurrence's workgroups
 // OR in 1 << XCC_ID (words 1008 / 1009: weight-gradient tile counters)
 constexpr int kXcdWord = 1016;
-constexpr int kResWord = 1017;  // pinned forward: workgroups resident so far (launch_chain_rows' gate)
+constexpr int kResWord = 1017;  // v6 recurrence: workgroups resident so far (beside_recurrence)
 __device__ __forceinline__ unsigned *flag6(const RecParams &p, int grp, int d, int g, int nwg) {
   return p.flags + 1024 + (((long)grp * p.dirs + d) * nwg + g) * kFlagStride;
 }
@@ -1664,10 +1656,14 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   const int g = p.xpd ? (blockIdx.x >> 3) : (blockIdx.x / dirs) % NWG;
   const int grp = p.xpd ? (blockIdx.x & 7) / dirs : blockIdx.x / (dirs * NWG);
   if (d >= dirs || g >= NWG || grp >= p.rg) return;
-  // resident: counted for the exchange's residency gate (rnn_comm_gate)
-  if (p.reg && threadIdx.x == 0) {
-    __hip_atomic_fetch_add(p.reg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (p.xpd) __hip_atomic_fetch_or(p.reg + 2, 1u << xcc_id(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // rnn_pinned_xcds
+  // resident: counted for the exchange's residency gate (rnn_comm_gate) and
+  // in the launch's own word for the side launches beside it (beside_recurrence)
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(p.flags + kResWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (p.reg) {
+      __hip_atomic_fetch_add(p.reg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (p.xpd) __hip_atomic_fetch_or(p.reg + 2, 1u << xcc_id(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // rnn_pinned_xcds
+    }
   }
   // rows n0 .. nend-1 of the batch (p.gs <= 16 of the 16 MFMA rows)
   const int N = p.N, T = p.T, n0 = grp * p.gs, nend = min(N, n0 + p.gs);
@@ -2314,9 +2310,6 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // held up that wave's next flag poll / hand-off loads / publish drain
   // (measured: forward 2.38 -> 1.89 us/step with the G loads left out)
   constexpr bool IOW = (P & 4) != 0;
-  // P & 8: the consumer-gated input projection (p.gtf), a variant of its own
-  // so that the plain IO-wave kernel compiles exactly as before
-  constexpr bool GATE = IOW && (P & 8) != 0;
   // the row-major outputs through the IO waves too: measured slower (forward
   // 2.46 -> 2.52 us/step; the IO waves' waits then delay the post-cell barrier)
   constexpr bool IO_OUT = false;
@@ -2361,7 +2354,6 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // filled by LDS-DMA p.gla (3 or 7) steps ahead
   float *ginl = smem + kStgOff + (NP * 16 * U + 7) / 8 * 4;  // 16-B aligned
   float *outl = ginl + 8 * NW * 16 * U;  // (IO_OUT) [2][NW + 2][16 U]
-  unsigned *pollbuf = reinterpret_cast<unsigned *>(outl + 2 * (NW + 2) * 16 * U);  // (gated) [IO waves][64]
   const float *Wd = p.w + d * p.pl_stride;
   const float *R = Wd + p.r_off;
   AT *xch = reinterpret_cast<AT *>(p.xch);
@@ -2481,72 +2473,14 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // by LDS-DMA (lane l of IO wave v writes element 64 v + l); NW DMAs per
   // call whatever kk, so that the waits can count them (rows past N and
   // steps past T read a valid row and are never used)
-  // Consumer-gated G (p.gtf): an IO wave checks the row tile(s) of a step's
-  // rows before fetching them.  gvt = last verified row tile in this
-  // direction's order; the flags of the next tile are fetched by LDS-DMA into
-  // pollbuf right after a tile is verified (gpt, gpd steps ago) and read when
-  // that tile is first needed, >= 3 steps later (landed by then: see io_wait);
-  // otherwise, or if they do not all hold this call's id yet, the wave polls
-  // the flags itself (gate_spin, compiler-counted loads: a full drain).
-  const bool gate = GATE && p.gtf != nullptr;
-  int gvt = d == 0 ? -1 : p.gmt, gpt = -1, gpd = 3;
-  int gnext = 0;  // first forward-order step whose rows need a tile past gvt
-  auto gate_spin = [&](int tile) {  // (asm loads only: see ld_u32_sc1_now)
-    const unsigned *f = p.gtf + ((long)d * p.gmt + tile) * p.ggx + (lane < p.ggx ? lane : 0);
-    int spins = 0;
-    while (true) {
-      const unsigned v = ld_u32_sc1_now(f);
-      if (__all(v == p.gid)) return;
-      if (++spins > kSpinLimit || ((spins & 255) == 0 && ld_u32_sc1_now(p.err))) {
-        // timeout: the error word gets 0x10 if the GEMM had started (its tag), 0x20 if not
-        if (lane == 0) bad_lds = ld_u32_sc1_now(p.gtf - 63) == p.gid ? 0x11 : 0x21;
-        return;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  };
-  auto gate_rows = [&](int kk) {  // before the G fetch of forward-order step kk
-    if (kk < gnext) return;  // (one compare on most steps)
-    const int tt = d == 0 ? min(kk, T - 1) : max(T - 1 - kk, 0);
-    const int lo = (int)(((long)tt * N + n0) >> 8), hi = (int)(((long)tt * N + nend - 1) >> 8);
-    bool moved = false;
-    while (d == 0 ? gvt < hi : gvt > lo) {
-      const int nt = d == 0 ? gvt + 1 : gvt - 1;
-      const unsigned *pb = pollbuf + (w - CW) * 64;
-      const bool have = gpt == nt && gpd >= 3 && __all(lane >= p.ggx || pb[lane] == p.gid);
-      if (!have) gate_spin(nt);
-      gvt = nt;
-      moved = true;
-    }
-    // the first step past the verified tiles: direction 0 rows reach tile
-    // gvt + 1 at frame ceil(((gvt + 1) 256 - (nend - 1)) / N), direction 1
-    // rows reach below tile gvt at frame floor((gvt 256 - n0 - 1) / N)
-    if (d == 0) {
-      const long num = (long)(gvt + 1) * 256 - (nend - 1);
-      gnext = num <= 0 ? kk + 1 : (int)min((num + N - 1) / N, (long)T + 64);
-    } else {
-      const long num = (long)gvt * 256 - n0 - 1;
-      gnext = num < 0 ? T + 64 : T - 1 - (int)(num / N);
-    }
-    gnext = max(gnext, kk + 1);
-    const int nx = d == 0 ? gvt + 1 : gvt - 1;
-    if (moved && nx >= 0 && nx < p.gmt) {  // the next tile's flags, checked when it is first needed
-      const unsigned *f = p.gtf + ((long)d * p.gmt + nx) * p.ggx + (lane < p.ggx ? lane : 0);
-      dma_lds_dword_sc1(f, __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(pollbuf + (w - CW) * 64)));
-      gpt = nx;
-      gpd = 0;
-    }
-  };
   auto io_dma = [&](int kk) {
-    if (gate) gate_rows(kk);
     const int tt = d == 0 ? min(kk, T - 1) : max(T - 1 - kk, 0);
     const long gr = ((long)tt * N + n0 + (io_live ? ion : 0)) * ldg + (long)d * NW * H + u0 + iou;
 #pragma unroll
     for (int q = 0; q < NW; q++) {
       const unsigned dst = __builtin_amdgcn_readfirstlane(
           (unsigned)reinterpret_cast<uintptr_t>(ginl + ((kk & 7) * NW + q) * 16 * U + (w - CW) * 64));
-      if (gate && !p.gplain) dma_lds_dword_sc1(p.G + gr + q * H, dst);  // written by the GEMM's XCDs during this kernel
-      else dma_lds_dword(p.G + gr + q * H, dst);
+      dma_lds_dword(p.G + gr + q * H, dst);
     }
   };
   auto io_out = [&](int kk) {  // row-major outputs of step kk from outl[kk & 1]
@@ -2564,15 +2498,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // steps after it) still in flight
   const bool gla7 = p.gla == 7;
   auto io_wait = [&]() {
-    if (gate) {  // gla 3; a flag fetch issued this step or the last one sits among the G fetches
-      if constexpr (NW == 4) {
-        if (gpd <= 1) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      } else {
-        if (gpd <= 1) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      }
-    } else if (gla7) {
+    if (gla7) {
       if constexpr (NW == 4) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
     } else {
@@ -2583,13 +2509,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   if constexpr (IOW) {
     if (w >= CW) {  // steps 0 .. gla - 1; step 0's in place before the loop's first barrier
       for (int kk = 0; kk < (gla7 ? 7 : 3); kk++) io_dma(kk);
-      if (gate) {  // a flag fetch here is older than every G fetch: the plain count holds
-        if constexpr (NW == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        gpd = 3;
-      } else {
-        io_wait();
-      }
+      io_wait();
     }
     __syncthreads();
   } else {
@@ -2618,13 +2538,10 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
   // gflag = k there means rows of steps <= k - 3 are out ("epoch s + 3" as
   // the backward's rows), T + 2 at exit
   unsigned *gflag = ((fcopy || p.ysc1) && g == 0) ? agg_flag6(p, grp, d) : nullptr;
-  if (p.xpd && tid == 0) {
-    atomicOr(p.flags + kXcdWord, 1u << xcc_id());
+  if (tid == 0) {  // (the side launches' residency gate: beside_recurrence)
+    if (p.xpd) atomicOr(p.flags + kXcdWord, 1u << xcc_id());
     atomicAdd(p.flags + kResWord, 1u);
   }
-  // gated projection: tell the GEMM's blocks which XCDs this launch holds
-  // (this call's id in the tag word of the XCD; they leave those XCDs)
-  if (GATE && p.gtf && tid == 0) st_u32_sc1(const_cast<unsigned *>(p.gtf) - 56 + xcc_id(), p.gid);
   if (tid == 0) loc_lds = 0;
   const int local = (p.xpd && p.allow_local) ? probe6(p, grp, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
   if (trc_ && tid == 0) trc_[9] = (unsigned long long)(local + 1);  // step 0, slot 9
@@ -2899,7 +2816,6 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
         // gla - 1 steps after it was asked for
         io_dma(k + (gla7 ? 7 : 3));
         io_wait();
-        gpd++;
       }
       if (IO_OUT && k > 0) io_out(k - 1);
     }
@@ -2954,7 +2870,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_fwd_rec6(RecParams p) {
     }
   }
   asm volatile("" ::"v"(pv));
-  if (bad && tid == 0) atomicOr(p.err, 1u | ((unsigned)bad_lds & 0x30u));  // (gated: 0x10 / 0x20 diagnosis)
+  if (bad && tid == 0) atomicOr(p.err, 1u);
 }
 
 template <typename F>
@@ -3037,27 +2953,23 @@ static void launch6_u(bool fwd, int nth, const RecParams &p, dim3 grid, size_t l
       if (nth == 1024) launch6_h<MODE, 16, 1024, P>(fwd, p, grid, lds, s);
       else if (nth == 512) {
         // row groups of <= 8 sequences: hi / lo stacked in one MFMA operand
-        // (all four products: equally accurate or better).  Forward on by
-        // default since round 4: the stacked forward (one A load per k block,
-        // 2/3 of the MFMAs) runs 1.76 us/step against 2.05 for the IO-wave
-        // forward, same box; backward off (2.53 vs 2.43: the fold's cross-lane
-        // exchange).  KCTC_STK_FWD (forward; KCTC_STK for both)
+        // (all four products: equally accurate or better), on by default in
+        // both directions: the stacked forward (one A load per k block, 2/3
+        // of the MFMAs) runs 1.76 us/step against 2.05 for the IO-wave
+        // forward (round 4); the transposed stacked backward with its DPP row
+        // fold 1.91 against 2.43 (round 5).  KCTC_STK_FWD (forward; KCTC_STK
+        // for both)
         const int stk = fwd ? env_int("KCTC_STK_FWD", env_int("KCTC_STK", 1)) : env_int("KCTC_STK", 1);
         if constexpr (P == kPrecX3) {
           if (p.gs <= 8 && stk) {
-            // the stacked forward with IO waves (measured slower; not taken)
-            if (false)
-              launch6_h<MODE, 16, 512, kPrecX3S | 4>(fwd, p, grid, lds, s);
-            else
-              launch6_h<MODE, 16, 512, kPrecX3S>(fwd, p, grid, lds, s);
+            launch6_h<MODE, 16, 512, kPrecX3S>(fwd, p, grid, lds, s);
             break;
           }
         }
         // forward with IO waves (the G loads off the hand-off waves)
         if constexpr (MODE == kLstm || MODE == kGru) {
           if (fwd) {
-            if (p.gtf) launch6_h<MODE, 16, 512, P | 4 | 8>(fwd, p, grid, lds, s);
-            else launch6_h<MODE, 16, 512, P | 4>(fwd, p, grid, lds, s);
+            launch6_h<MODE, 16, 512, P | 4>(fwd, p, grid, lds, s);
             break;
           }
         }
@@ -3131,7 +3043,6 @@ static int env_int(const char *name, int dflt) {
 
 // pick U (units per workgroup): divides H, multiple of 4, blocks <= 256
 static int pick_fwd_u(const RnnDesc &d, int N) {
-  int want = 0;
   const int NW = d.nw();
   auto ok = [&](int U) {
     if (U < 4 || U % 4 || d.H % U || NW * U > 16 * kMaxCT || N * U / 4 > NT) return false;
@@ -3140,7 +3051,6 @@ static int pick_fwd_u(const RnnDesc &d, int N) {
     const size_t lds = sizeof(float) * ((size_t)ncol * (d.H + 4) + 4 * (size_t)Npad * ncol);
     return lds <= 160 * 1024;
   };
-  if (want && ok(want)) return want;
   // smallest U that keeps every workgroup resident (<= 256 = one per CU):
   // per-step MFMA latency falls with U (measured: U=4 < 8 < 16 on BLSTM-512)
   for (int U : {4, 8, 16})
@@ -3174,8 +3084,6 @@ static int pick_fwd_u4(const RnnDesc &d, int N) {
     return U >= 4 && U % 4 == 0 && v4_xpd(d, U) && d.nw() * U <= 16 * kMaxCT && N * U <= kMaxEPT * NT &&
            fwd_lds_bytes(d, N, U) <= 160 * 1024;
   };
-  const int want = 0;
-  if (want) return ok(want) ? want : 0;
   // measured on BLSTM-512 N=16 (1 x MI355X): U=8 (2 XCD slots per direction)
   // 44 ms/step of forward recurrence, U=4 48, U=16 58
   for (int U : {8, 16, 4, 32})
@@ -3188,8 +3096,6 @@ static int pick_bwd_u4(const RnnDesc &d, int N) {
     return U >= 4 && U <= 16 && U % 4 == 0 && v4_xpd(d, U) && N * U <= kMaxEPT * NT &&
            bwd_lds_bytes(d, N, U, 4) <= 160 * 1024;
   };
-  const int want = 0;
-  if (want) return ok(want) ? want : 0;
   for (int U : {16, 8, 4})
     if (ok(U)) return U;
   return 0;
@@ -3244,16 +3150,11 @@ static V6Cfg pick6(const RnnDesc &d, int N, bool fwd, int gs_force = 0) {
     c.gs = gs;
     return c;
   };
-  const int want = 0;
-  if (want) {
-    if (ok(want)) return take(want);
-  } else {
-    for (int U : {16, 32, 8})
-      if (ok(U)) {
-        // rg = 1 keeps the measured N <= 16 choice even above the budget
-        if (rg == 1 || (long)d.dirs * (d.H / U) * rg <= max_wg) return take(U);
-      }
-  }
+  for (int U : {16, 32, 8})
+    if (ok(U)) {
+      // rg = 1 keeps the measured N <= 16 choice even above the budget
+      if (rg == 1 || (long)d.dirs * (d.H / U) * rg <= max_wg) return take(U);
+    }
   return gs == 8 ? pick6(d, N, fwd, 16) : c;
 }
 static int pick_fwd_u6(const RnnDesc &d, int N) { return pick6(d, N, true).U; }
@@ -3320,7 +3221,6 @@ static void xch_release(hipStream_t s) {
 }
 
 static int pick_bwd_u(const RnnDesc &d, int N) {
-  int want = 0;
   const int K = d.nw() * d.H;
   auto ok = [&](int U) {
     if (U < 4 || U % 4 || U > 16 || d.H % U || N * U / 4 > NT) return false;
@@ -3330,13 +3230,52 @@ static int pick_bwd_u(const RnnDesc &d, int N) {
                                                                         (size_t)2 * N * U * d.nw()));
     return lds <= 160 * 1024;
   };
-  if (want && ok(want)) return want;
   for (int U : {16, 8, 4})
     if (ok(U)) return U;
   return 0;
 }
 
 }  // namespace
+
+// ---- launches beside a running recurrence (rnn.h rnn_side_gated) ----
+namespace {
+// the v6 recurrence this host thread enqueued last, while the host function
+// that enqueued it runs (RecScope), and the side streams gated on it
+struct RecInFlight {
+  const unsigned *res = nullptr;  // its residency word (p.flags + kResWord)
+  unsigned target = 0;            // its workgroups
+  hipStream_t gated[4] = {};
+  int ngated = 0;
+};
+thread_local RecInFlight g_rec;
+// from a recurrence's launch to the end of the enclosing host call
+struct RecScope {
+  ~RecScope() { g_rec = RecInFlight{}; }
+  void enqueued(const RecParams &p) {
+    g_rec = RecInFlight{};
+    g_rec.res = p.flags + kResWord;
+    g_rec.target = (unsigned)(p.dirs * p.nwg * p.rg);
+  }
+  void none() { g_rec = RecInFlight{}; }  // (a v3 / v4 recurrence: no side launches)
+};
+// `side` waits until every workgroup of the recurrence in flight is resident;
+// whatever is enqueued on it afterwards may run beside that recurrence
+void beside_recurrence(hipStream_t side) {
+  if (!g_rec.res) throw std::logic_error("beside_recurrence: no recurrence in flight");
+  for (int i = 0; i < g_rec.ngated; i++)
+    if (g_rec.gated[i] == side) return;  // (already behind this recurrence's gate)
+  if (g_rec.ngated == 4) throw std::logic_error("beside_recurrence: too many side streams");
+  rnn_resident_gate(side, g_rec.res, g_rec.target);
+  g_rec.gated[g_rec.ngated++] = side;
+}
+}  // namespace
+
+bool rnn_side_gated(hipStream_t s) {
+  if (!g_rec.res) return true;
+  for (int i = 0; i < g_rec.ngated; i++)
+    if (g_rec.gated[i] == s) return true;
+  return false;
+}
 
 // ---------------------------------------------------------------------------
 // host: forward training
@@ -3391,6 +3330,20 @@ int stream_block_budget(int rec_wgs, bool backward) {
   return left >= 8 ? left : 0;
 }
 
+// Is the dx of layer l streamed off its v6 backward recurrence
+// (launch_bwd_stream, given a dx buffer and an overlap stream)?  The
+// forward's W^T prepack (RnnPrepack) asks the same question.
+bool bwd_dx_stream_ok(const RnnDesc &d, int l, int T, int N) {
+  const V6Cfg c6 = pick6(d, N, false);
+  if (!c6 || d.dirs != 2 || !env_int("KCTC_BWD_STREAM", 1)) return false;
+  // split-fp16 at N <= 16 by default (KCTC_STREAM_ALL: bf16 and N > 16 too)
+  if (!((d.prec == kPrecX3 && N <= 16) || env_int("KCTC_STREAM_ALL", 0))) return false;
+  const int G4 = d.nw() * d.H;
+  if (!use_x3(G4) || G4 > 4096 || (d.prec != kPrecX3 && G4 % 64)) return false;
+  if ((long)T * N * d.din(l) * 4 >= (1L << 31)) return false;
+  return stream_block_budget(d.dirs * (d.H / c6.U) * c6.rg, true) > 0;
+}
+
 hipEvent_t fork_event(hipStream_t s) {
   static thread_local hipEvent_t ev = nullptr;
   if (!ev) KCTC_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -3425,7 +3378,6 @@ bool chain_ok(const RnnDesc &d, int ver, int T, int N, const RnnFwdChain *c) {
   // and only the IO-wave variant (U = 16, 512 threads) carries the copies
   // (launch6_u: U = 16 / 512 threads, not the stacked variant)
   if (xcd_mask(d, N, true) && !(pick6(d, N, true).U == 16 && pick6(d, N, true).nth == 512 &&
-                                
                                 !(pick6(d, N, true).gs <= 8 && env_int("KCTC_STK_FWD", env_int("KCTC_STK", 1)))))
     return false;
   const V6Cfg c6 = pick6(d, N, true);
@@ -3440,6 +3392,7 @@ bool chain_ok(const RnnDesc &d, int ver, int T, int N, const RnnFwdChain *c) {
 void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipEvent_t fork, int T, int N, RnnFwdChain &c,
                        unsigned *err) {
   KCTC_HIP_CHECK(hipStreamWaitEvent(c.side, fork, 0));  // after the producer's flag reset
+  beside_recurrence(c.side);
   const RnnDesc &n = *c.d;
   const bool bf = n.prec == kPrecBf16;
   const int NW = n.nw(), G = NW * n.H, Din = n.D, KB = Din / (bf ? 64 : 32);
@@ -3522,6 +3475,11 @@ bool chain_rows_ok(const RnnDesc &d, int ver, int T, int N, const RnnFwdChain *c
 void launch_chain_rows(const RnnDesc &d, const RecParams &p, hipEvent_t fork, int T, int N, RnnFwdChain &c,
                        unsigned *err) {
   KCTC_HIP_CHECK(hipStreamWaitEvent(c.side, fork, 0));  // after the producer's flag reset
+  // not before every workgroup of the recurrence is resident: dispatched
+  // first (another queue), 32 blocks per XCD would take every CU of an XCD
+  // the recurrence is pinned to before its first workgroup got there (seen
+  // once as a 3-s stream-wait timeout, error 0x2)
+  beside_recurrence(c.side);
   const RnnDesc &n = *c.d;
   const int NW = n.nw(), G = NW * n.H, H = d.H, KBh = H / 32, Din = n.D;
   const long TN = (long)T * N;
@@ -3558,11 +3516,6 @@ void launch_chain_rows(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
   // 128: every CU the recurrence leaves (configs[1]: 96 -> 128 blocks 720k -> 751k frames/s)
   const int nb = std::min(128, stream_block_budget(d.dirs * p.nwg * p.rg, false));
   a.blocks = pinned ? nb * 8 / (8 - pinned) : nb;
-  // not before every workgroup of the recurrence is resident: dispatched
-  // first (another queue), 32 blocks per XCD would take every CU of an XCD
-  // the recurrence is pinned to before its first workgroup got there (seen
-  // once as a 3-s stream-wait timeout, error 0x2)
-  if (pinned) rnn_resident_gate(c.side, p.flags + kResWord, (unsigned)(d.dirs * p.nwg * p.rg));
   {
     ProfSpan ps(c.side, "fwd_proj_rows");
     gemm_x3p_bwd_stream(c.side, a);
@@ -3632,6 +3585,7 @@ void rnn_resident_gate(hipStream_t s, const unsigned *word, unsigned target) {
   KCTC_HIP_CHECK(hipGetLastError());
 }
 const unsigned *rnn_pinned_xcds() { return reg_of_device().word + 2; }
+
 void rnn_comm_gate(hipStream_t s, unsigned target) {
   RegWord &r = reg_of_device();
   hipLaunchKernelGGL(comm_gate_kernel, dim3(1), dim3(64), 0, s, r.word, target, r.word + 1);
@@ -3666,7 +3620,8 @@ void pack_dx_weights(const RnnDesc &d, int l, const float *w, void *workspace, i
 int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const float *x,
                          const float *w, float *y, void *workspace, size_t ws_bytes,
                          void *reserve, size_t res_bytes, unsigned *err, RnnFwdChain *chain,
-                         bool input_projected, const void *in_rows, hipStream_t side, RnnPrepack *pre) {
+                         bool input_projected, const void *in_rows, RnnPrepack *pre) {
+  RecScope rec_scope;  // the side launches' residency gates (beside_recurrence)
   if (chain) chain->done = false;
   if (pre) pre->done = pre->wdone = false;
   if (T <= 0 || N <= 0 || N > 16 * kMaxRT || d.H % 16) return KRNN_NOT_SUPPORTED;
@@ -3684,15 +3639,6 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
   const long TN = (long)T * N;
   float *res = static_cast<float *>(reserve);
   const float *in = x;
-  // consumer-gated projection: the split-fp16 forward with IO waves
-  // (launch6_u), XCD-pinned so that the GEMM keeps to the other XCDs
-  const bool gate_ok = side && ver == 6 && c6.U == 16 && c6.nth == 512 && d.prec == kPrecX3 &&
-                       
-                       !(c6.gs <= 8 && env_int("KCTC_STK_FWD", env_int("KCTC_STK", 1))) &&
-                       env_int("KCTC_FWD_GATE", 0) && xcd_mask(d, N, true) != 0 &&
-                       __builtin_popcount(xcd_mask(d, N, true)) <= 4 &&  // XCDs left to the GEMM
-                       x3p_use_256((int)TN, d.nw() * d.H);
-  static unsigned gate_calls = 0x5eed0000u;  // a projection's id (never 0, never repeated in practice)
   for (int l = 0; l < d.layers; l++) {
     float *R0 = res + lay.per_layer * l;
     float *out = (l == d.layers - 1) ? y : R0 + lay.out;
@@ -3708,21 +3654,6 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     g.transA = false; g.transB = true;
     g.M = (int)TN; g.N = NW * H; g.K = Din;
     const bool skip_proj = l == 0 && input_projected;  // streamed by the previous component
-    const bool gated = gate_ok && !skip_proj && use_x3(Din, 32);
-    hipEvent_t gfork = nullptr;
-    std::function<void()> gated_launch;  // the deferred packs + gated GEMM
-    // diagnostic (0 in the product): 1 the gated GEMM stream-ordered before an
-    // ungated recurrence, 2 stream-ordered before the gated recurrence
-    const int gdiag = 0;
-    // diagnostic (off): the GEMM on a stream of its own at normal priority
-    hipStream_t gside = side;
-    if (false) {
-      static hipStream_t own = nullptr;
-      if (!own) KCTC_HIP_CHECK(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
-      gside = own;
-    }
-    const unsigned gid = gated ? ++gate_calls : 0u;
-    unsigned *gtf = gated ? pk<unsigned>(workspace, d, T, N, pack_layout(d, T, N).gtf) : nullptr;
     g.A = in; g.lda = Din;
     g.B = wl; g.ldb = Din;
     g.C = R0 + lay.G; g.ldc = (long)dirs * NW * H;
@@ -3759,26 +3690,10 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       _Float16 *Ap = pk<_Float16>(workspace, d, T, N, pl.a), *Bp = pk<_Float16>(workspace, d, T, N, pl.b);
       int *eA = pk<int>(workspace, d, T, N, pl.ea), *eB = pk<int>(workspace, d, T, N, pl.eb);
       const int KB = (Din + 31) / 32;
-      // gated: the packs stay on s before the recurrence, the GEMM goes on
-      // `gside` right AFTER the recurrence launch (forked at an event recorded
-      // before it, like the streamed GEMMs).  A kernel's workgroups are dealt
-      // to the XCDs round-robin whatever is free, so a kernel launched beside
-      // the pinned recurrence has blocks that cannot start on its XCDs until
-      // it ends: fine for the GEMM (its jobs come from a counter, the blocks
-      // elsewhere take them all), a deadlock for a static-grid pack kernel
-      // the GEMM would wait for -- measured before the packs moved here
-      const hipStream_t ps_ = gated && !gdiag ? gside : s;
-      const bool defer = gated && !gdiag;
       {
         ProfSpan ps(s, "x3_pack");
         x3p_pack_rows(s, in, Din, (int)TN, Din, Ap, eA, (l > 0 && bounded_out(d)) ? 1.f : 0.f);
         x3p_pack_rows(s, wl, Din, NW * H, Din, Bp, eB, 0.f, dirs, pls, (long)NW * H * KB * 64, (long)NW * H);
-      }
-      if (defer) {
-        static thread_local hipEvent_t ev = nullptr;
-        if (!ev) KCTC_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        KCTC_HIP_CHECK(hipEventRecord(ev, s));
-        gfork = ev;
       }
       X3PArgs x;
       x.M = (int)TN; x.N = NW * H; x.KB = KB;
@@ -3786,25 +3701,8 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       x.C = g.C; x.ldc = g.ldc; x.bias = g.bias; x.bias2 = g.bias2;
       x.batch = dirs; x.sA = 0; x.seA = 0; x.sB = (long)NW * H * KB * 64; x.seB = (long)NW * H;
       x.sC = g.strideC; x.sBias = g.strideBias;
-      if (gated) {
-        x.gate_flags = gtf + 64;
-        x.gate_id = gid;
-        x.xcd_avoid = 0;  // (the recurrence's XCDs come from its tags at run time)
-        x.tile_counter = reinterpret_cast<int *>(gtf);
-        // one block per CU: those dealt to the recurrence's XCDs start only
-        // after it (or leave at once if they get there first: its XCD tags)
-        x.max_blocks = 8 * kCusPerXcd;
-      }
-      if (defer) {
-        gated_launch = [=]() {
-          KCTC_HIP_CHECK(hipStreamWaitEvent(ps_, gfork, 0));
-          ProfSpan ps(ps_, "gemm_fwd_proj");
-          gemm_x3p(ps_, x);
-        };
-      } else {
-        ProfSpan ps(ps_, "gemm_fwd_proj");
-        gemm_x3p(ps_, x);
-      }
+      ProfSpan ps(s, "gemm_fwd_proj");
+      gemm_x3p(s, x);
     } else {
       ProfSpan ps(s, "gemm_fwd_proj");
       gemm_f32(s, g);
@@ -3825,13 +3723,6 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     p.xch = reinterpret_cast<float *>(static_cast<char *>(workspace) + xch_offset(d, T, N));
     p.poll_sleep = 1;
     p.gla = 3;  // G rows fetched 3 steps ahead (IO waves)
-    if (gated) {
-      p.gtf = gdiag == 1 ? nullptr : gtf + 64;
-      p.gid = gid;
-      p.gmt = (int)((TN + 255) / 256);
-      p.ggx = (NW * H + 255) / 256;
-      p.gplain = 0;
-    }
     if (ver == 6 && bf16_io(d)) {  // the output also as packed bf16 rows and columns
       p.yr = reinterpret_cast<__bf16 *>(R0 + lay.pkyr);
       p.yc = reinterpret_cast<__bf16 *>(R0 + lay.pkyc);
@@ -3864,9 +3755,8 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     if (tr.arm("fwd", grid.x)) p.trace = tr.dev;
     // W^T of the backward's streamed dx GEMM, packed beside this recurrence
     // (rnn_backward_data's `streamed` shapes; one-layer descriptors)
-    const bool prepack = pre && pre->dx && pre->stream && pre->ev && ver == 6 && d.layers == 1 && dirs == 2 &&
-                         ((d.prec == kPrecX3 && N <= 16) || env_int("KCTC_STREAM_ALL", 0)) && use_x3(NW * H) &&
-                         NW * H <= 4096 && (d.prec == kPrecX3 || (NW * H) % 64 == 0);
+    const bool prepack = pre && pre->dx && pre->stream && pre->ev && ver == 6 && d.layers == 1 &&
+                         bwd_dx_stream_ok(d, 0, T, N);
     const bool prepack_w = pre && pre->stream && pre->wev && pre->wgrad && pre->in_bound > 0.f && ver == 6 &&
                            d.layers == 1 && d.prec != kPrecBf16 && T > 1 && bounded_out(d) && use_x3((int)TN);
     const hipEvent_t fork = (chained || prepack || prepack_w || rowchain) ? fork_event(s) : nullptr;
@@ -3876,8 +3766,11 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       else launch_rec(true, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
-    if (prepack) {  // launched after the recurrence: its workgroups are placed first
+    if (ver == 6) rec_scope.enqueued(p);
+    else rec_scope.none();
+    if (prepack) {  // beside the recurrence, once it is resident
       KCTC_HIP_CHECK(hipStreamWaitEvent(pre->stream, fork, 0));
+      beside_recurrence(pre->stream);
       pack_dx_weights(d, 0, w, workspace, T, N, pre->stream);
       KCTC_HIP_CHECK(hipEventRecord(pre->ev, pre->stream));
       pre->done = true;
@@ -3885,19 +3778,16 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     if (prepack_w) {  // x^T beside the recurrence, y^T after it, off its XCDs (rnn_backward_weights' packs)
       hipStream_t ss = pre->stream;
       if (!prepack) KCTC_HIP_CHECK(hipStreamWaitEvent(ss, fork, 0));
+      beside_recurrence(ss);
       const PackLay pl = pack_layout(d, T, N);
       const int Din = d.din(0);
-      int *pc = reinterpret_cast<int *>(p.flags + 1010);  // item counters (the recurrence's flags are after them)
+      int *pc = pk<int>(workspace, d, T, N, pl.pcnt);  // item counters
       KCTC_HIP_CHECK(hipMemsetAsync(pc, 0, sizeof(int) * 3, ss));
       const unsigned *av = rnn_pinned_xcds();
       const int nx = std::max(1, rnn_usable_cus() / kCusPerXcd);
       ProfSpan ps(ss, "x3_pack_w_fwd");
       x3p_pack_cols(ss, in, Din, (int)TN, Din, 0, pk<_Float16>(workspace, d, T, N, pl.xt),
                     pk<int>(workspace, d, T, N, pl.ext), nullptr, pre->in_bound, 1, 0, 0, 0, 0, av, nx, pc);
-    }
-    if (gated_launch) {
-      gated_launch();
-      join_stream(s, gside);  // (complete by the recurrence's end: it read every row)
     }
     if (chained) {
       launch_chain_proj(d, p, fork, T, N, *chain, err);
@@ -3912,7 +3802,7 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
       KCTC_HIP_CHECK(hipStreamWaitEvent(ss, fork_event(s), 0));
       const PackLay pl = pack_layout(d, T, N);
       const long KBt = (TN + 31) / 32;
-      int *pc = reinterpret_cast<int *>(p.flags + 1010);
+      int *pc = pk<int>(workspace, d, T, N, pl.pcnt);
       const unsigned *av = rnn_pinned_xcds();
       const int nx = std::max(1, rnn_usable_cus() / kCusPerXcd);
       const long ldy = (long)dirs * H;
@@ -3963,6 +3853,12 @@ void pack_dx_weights(const RnnDesc &d, int l, const float *w, void *workspace, i
 void launch_bwd_stream(const RnnDesc &d, const RecParams &p, int l, const float *w, float *dxl, void *workspace,
                        int T, int N, hipStream_t ov, hipEvent_t fork, unsigned *err, const RnnPrepack *pre) {
   KCTC_HIP_CHECK(hipStreamWaitEvent(ov, fork, 0));  // after the flag reset, not after the recurrence
+  // not before every workgroup of the recurrence is resident: its blocks
+  // wait (on_pinned_xcd) for the pinned recurrence's XCDs to register, and a
+  // block parked on one of those XCDs' CUs before the recurrence's last
+  // workgroup got there would keep it out (with W^T packed by the forward
+  // the GEMM starts together with the recurrence)
+  beside_recurrence(ov);
   const bool bf = d.prec == kPrecBf16;
   const int NW = d.nw(), H = d.H, G4 = NW * H, KB = G4 / (bf ? 64 : 32), Din = d.din(l);
   const long TN = (long)T * N;
@@ -3998,12 +3894,6 @@ void launch_bwd_stream(const RnnDesc &d, const RecParams &p, int l, const float 
   const int nb = std::min(t256 ? 64 : 128,
                           stream_block_budget(d.dirs * p.nwg * p.rg, true));
   a.blocks = pinned ? nb * 8 / (8 - pinned) : nb;
-  // not before every workgroup of the recurrence is resident: its blocks
-  // wait (on_pinned_xcd) for the pinned recurrence's XCDs to register, and a
-  // block parked on one of those XCDs' CUs before the recurrence's last
-  // workgroup got there would keep it out (with W^T packed by the forward
-  // the GEMM starts together with the recurrence)
-  rnn_comm_gate(ov, rnn_bwd_registrations());
   ProfSpan ps(ov, "bwd_data_stream");
   gemm_x3p_bwd_stream(ov, a);
 }
@@ -4145,6 +4035,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
                       const float *dy, const float *w, float *dx, void *workspace,
                       size_t ws_bytes, void *reserve, size_t res_bytes, unsigned *err,
                       hipStream_t overlap, RnnWgradStream *wgrad, const RnnPrepack *pre) {
+  RecScope rec_scope;  // the side launches' residency gates (beside_recurrence)
   if (wgrad) wgrad->done = false;
   if (T <= 0 || N <= 0 || N > 16 * kMaxRT || d.H % 16) return KRNN_NOT_SUPPORTED;
   const RnnReserveLayout lay = rnn_reserve_layout(d, T, N);
@@ -4211,11 +4102,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     // dx_l = sum_dir DX_dir W_dir   (lower layer's dy, or the caller's dx)
     float *dxl = (l == 0) ? dx : res + lay.per_layer * (l - 1) + lay.dout;
     // streamed: computed on `overlap` while the recurrence runs, from its rows as they appear
-    const bool streamed = dxl && overlap && ver == 6 && dirs == 2 &&
-                          ((d.prec == kPrecX3 && N <= 16) || env_int("KCTC_STREAM_ALL", 0)) && use_x3(NW * H) &&
-                          NW * H <= 4096 &&
-                          (d.prec == kPrecX3 || (NW * H) % 64 == 0) && (long)TN * Din * 4 < (1L << 31) &&
-                          stream_block_budget(dirs * p.nwg * p.rg, true) && env_int("KCTC_BWD_STREAM", 1);
+    const bool streamed = dxl && overlap && ver == 6 && bwd_dx_stream_ok(d, l, T, N);
     // weight gradients streamed off this recurrence (the bottom component):
     // its dGates rows must be written through too
     const bool wstream = wgrad && wgrad->side && !dxl && ver == 6 && !p.xpd && d.layers == 1 &&
@@ -4251,17 +4138,21 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
         KCTC_HIP_CHECK(hipMemsetAsync(p.cmax, 0, sizeof(unsigned) * 2 * dirs * NW * H, s));
     }
     const hipEvent_t fork = (streamed || wstream) ? fork_event(s) : nullptr;
-    if (ver == 6) {  // registration for the exchange's residency gate
-      RegWord &rw = reg_of_device();
-      p.reg = rw.word;
-      rw.expected += (unsigned)(dirs * p.nwg * p.rg);
-    }
+    RegWord &rw = reg_of_device();
+    if (ver == 6) p.reg = rw.word;  // registration for the exchange's residency gate
     {
       ProfSpan ps(s, "rnn_bwd_rec");
       if (ver == 6) launch6(false, d.mode, d.prec, c6.nth, p, grid, lds, s);
       else launch_rec(false, d.mode, p, grid, lds, s, ver);
     }
     KCTC_HIP_CHECK(hipGetLastError());
+    if (ver == 6) {
+      // counted once the launch is enqueued (a failed launch never raises the target)
+      rw.expected += (unsigned)(dirs * p.nwg * p.rg);
+      rec_scope.enqueued(p);
+    } else {
+      rec_scope.none();
+    }
     if (streamed) {
       launch_bwd_stream(d, p, l, w, dxl, workspace, T, N, overlap, fork, err, d.layers == 1 ? pre : nullptr);
       join_stream(s, overlap);
@@ -4272,6 +4163,7 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
       // epoch b(c+1) + 2 (rows of step k are out at epoch k + 3)
       hipStream_t ws2 = wgrad->side;
       KCTC_HIP_CHECK(hipStreamWaitEvent(ws2, fork, 0));  // after the flag reset
+      beside_recurrence(ws2);
       const int C = std::max(1, std::min(wgrad->chunks, T / 4));
       const unsigned *lines = p.flags + 1024;
       const int nlines = p.rg * dirs * p.nwg;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-5 measurement, configs[1]: smoke, default bench, rocprofv3 stats +
+# round measurement, configs[1]: smoke, default bench, rocprofv3 stats +
 # timeline, PMC traffic (FETCH_SIZE / WRITE_SIZE) and MFMA-utilisation
 # (SQ_VALU_MFMA_BUSY_CYCLES, SQ_BUSY_CYCLES, GRBM_GUI_ACTIVE) passes, and the
 # recurrence phase trace.  Large raw outputs are summarised and removed.

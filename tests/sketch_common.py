@@ -17,6 +17,12 @@ import numpy as np
 
 NPROJ = 4
 NSAMP = 256
+# sampled entries: max |diff| / rms(ref) over NSAMP entries may exceed the
+# norm-wise bar by this factor -- an entry's error scales with its own
+# magnitude, and the largest of 256 sampled |entries| of a gradient runs to
+# several times the rms (measured on the fp32 configs[1] step: the sampled
+# error at most 0.56x the norm-wise bar, profiles/r02b_fullsize_parity.log)
+SAMP_FACTOR = 10.0
 
 
 def proj_vectors(n, seed):
@@ -49,8 +55,9 @@ def load(g, prefix):
 
 def compare(a, ref, seed, tol):
     """Max relative sketch error of tensor a vs the committed sketch ref:
-    max(|norm diff|, max_k |proj diff|) / |ref|, and the sampled entries'
-    max |diff| / rms(ref)."""
+    max(|norm diff|, max_k |proj diff|) / |ref| (bar: tol), and the sampled
+    entries' max |diff| / rms(ref) (bar: SAMP_FACTOR * tol); ok = all three
+    below their bars."""
     s = sketch(a, seed)
     n = np.asarray(a).size
     den = float(ref["norm"]) or 1.0
@@ -58,7 +65,8 @@ def compare(a, ref, seed, tol):
     e_proj = float(np.max(np.abs(s["proj"] - ref["proj"]))) / den
     rms = den / np.sqrt(n)
     e_samp = float(np.max(np.abs(s["val"] - ref["val"]))) / rms
-    return {"norm": e_norm, "proj": e_proj, "samp": e_samp, "ok": e_norm < tol and e_proj < tol}
+    return {"norm": e_norm, "proj": e_proj, "samp": e_samp,
+            "ok": e_norm < tol and e_proj < tol and e_samp < SAMP_FACTOR * tol}
 
 
 # ---- the two workloads --------------------------------------------------------

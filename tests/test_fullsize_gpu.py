@@ -71,13 +71,19 @@ def test_layer_full_length_matches_oracle(kctc, gpu, oracle, case):
                                atol=1e-6 if not bf16 else 8e-3)
 
 
-@pytest.mark.parametrize("case", sorted(S.STEPS))
-def test_train_step_full_size_matches_oracle(kctc, gpu, oracle, case):
+@pytest.mark.parametrize("case", sorted(S.STEPS) + ["cfg2+stream_all", "cfg4+stream_all"])
+def test_train_step_full_size_matches_oracle(kctc, gpu, oracle, case, monkeypatch):
     """One whole train step per BASELINE config at full size: configs[1]
     (5 x BLSTM-512, N=16, T=2000), configs[2] (N=64, T=667) at the fp32 bar,
     configs[4] (5 x BGRU-1024 bf16, N=32, T=2000) at the bf16 error model's
-    tolerance per output (sketch_common.bf16_tol / step_stages)."""
+    tolerance per output (sketch_common.bf16_tol / step_stages).  "+stream_all":
+    the same step with KCTC_STREAM_ALL=1 -- the dx GEMMs streamed off the
+    row-grouped / bf16 backward recurrences, W^T packed beside the forward
+    ones, every side launch behind its recurrence's residency gate."""
     import torch
+    case, _, variant = case.partition("+")
+    if variant == "stream_all":
+        monkeypatch.setenv("KCTC_STREAM_ALL", "1")
     s = S.STEPS[case]
     g = golden(s["file"])
     T, N, D, H, A, R = s["T"], s["N"], s["D"], s["H"], s["A"], s["R"]

@@ -435,3 +435,41 @@ def test_multistep_trajectory_matches_oracle(kctc, gpu, oracle):
     print("gpu", [round(x, 4) for x in got], "oracle fp64", [round(x, 4) for x in ref])
     np.testing.assert_allclose(got, ref, rtol=1e-4)
     assert max(ref) > 2 * ref[0]  # the over-shooting first steps
+
+
+def test_two_nets_interleaved_on_one_device(kctc, gpu):
+    """Two trainers on one device, their steps interleaved (A B A B), each
+    bit-identical to its own run alone.  The streamed GEMMs and packs beside
+    a recurrence wait on that launch's own residency count (rnn.hip
+    beside_recurrence), so one net's launches never hold up the other's side
+    streams (the round-5 gate waited on a device-wide registration count
+    that every net's backward raised)."""
+    import torch
+    T, N, D, A, H = 300, 16, 40, 41, 512
+    cfg = kctc.recipe_config(num_rnn=2, input_dim=D, hidden=H, num_targets=A, learning_rate=1e-3)
+    batches = []
+    for s in range(4):
+        feats, nf, fl, ll = kctc.synth_minibatch(40 + s, T, N, D, A, 0.125)
+        batches.append((torch.from_numpy(feats).to(gpu), nf, fl, ll))
+
+    def params(net):
+        return [net.get_params(c) for c in range(net.num_components) if net.num_params(c) > 0]
+
+    alone = []
+    for seed, idx in ((3, (0, 1)), (4, (2, 3))):
+        net = kctc.Nnet(cfg, seed=seed)
+        for i in idx:
+            f, nf, fl, ll = batches[i]
+            net.train_step(f, T, N, nf, fl, ll)
+        alone.append(params(net))
+        net.close()
+    a, b = kctc.Nnet(cfg, seed=3), kctc.Nnet(cfg, seed=4)
+    for ia, ib in ((0, 2), (1, 3)):
+        for net, i in ((a, ia), (b, ib)):
+            f, nf, fl, ll = batches[i]
+            net.train_step(f, T, N, nf, fl, ll)
+    for net, ref in ((a, alone[0]), (b, alone[1])):
+        for p, r in zip(params(net), ref):
+            np.testing.assert_array_equal(p, r)
+    a.close()
+    b.close()
