@@ -194,11 +194,18 @@ __device__ __forceinline__ unsigned wave_flags_min(const unsigned *f, int nwg) {
     m = min(m, __hip_atomic_load(f + 32L * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   return wave_min_u32(m);
 }
-__device__ __forceinline__ bool wave_timed_out(unsigned *err, int spins, unsigned long long t0) {
+// A wait that runs out of time itself (no error posted yet) also sets bit
+// 8 + site of err: which wait it was (0 producer rows, 1 pack jobs / tile
+// arrivals, 2 pinned-XCD registrations, 3 producer epochs) -- the other
+// bits are set by whoever saw the error first.
+__device__ __forceinline__ bool wave_timed_out(unsigned *err, int spins, unsigned long long t0, int site) {
   if ((spins & 255) != 255) return false;
   const unsigned e = err ? __builtin_amdgcn_readfirstlane(__hip_atomic_load(err, __ATOMIC_RELAXED,
                                                                             __HIP_MEMORY_SCOPE_AGENT)) : 0u;
-  return e != 0u || __builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks;
+  if (e != 0u) return true;
+  const bool late = __builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks;
+  if (late && err && (threadIdx.x & 63) == 0) atomicOr(err, 0x100u << site);
+  return late;
 }
 __device__ __forceinline__ void wave_fail(unsigned *err) {
   if ((threadIdx.x & 63) == 0 && err) atomicOr(err, 2u);
@@ -242,7 +249,7 @@ __device__ void x3p_wait_rows(const PParams &p, int m0, int *prog, int pd) {
         s1 = min(s1, (int)wave_flags_min(p.sflags + 32L * (2 * gi + 1) * p.snwg, p.snwg) - 2);
       }
       if (s0 >= need0 && s1 >= need1) break;
-      failed = wave_timed_out(p.serr, spins++, ts);
+      failed = wave_timed_out(p.serr, spins++, ts, 0);
       if (failed) break;  // the producer stopped: flag it, finish on whatever is there
       backoff(p.backoff ? max(need0 - s0, need1 - s1) : 0);
     }
@@ -263,7 +270,7 @@ __device__ __forceinline__ void wait_count(const int *a, int v, unsigned *err) {
     while (true) {
       const int x = __builtin_amdgcn_readfirstlane(__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       if (x >= v) break;
-      failed = wave_timed_out(err, i++, t0);
+      failed = wave_timed_out(err, i++, t0, 1);
       if (failed) break;
       __builtin_amdgcn_s_sleep(4);
     }
@@ -287,7 +294,7 @@ __device__ bool on_pinned_xcd(const PParams &p, int *bc) {
     while (true) {
       m = __builtin_amdgcn_readfirstlane(__hip_atomic_load(p.xcd_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       if (__builtin_popcount(m) >= p.xcd_count) break;
-      failed = wave_timed_out(p.serr, i++, t0);
+      failed = wave_timed_out(p.serr, i++, t0, 2);
       if (failed) break;
       __builtin_amdgcn_s_sleep(4);
     }
@@ -315,7 +322,7 @@ __device__ void wait_epoch(const PParams &p, int d, int need, int *seen) {
       for (int gi = 0; gi < p.srg; gi++)
         m = min(m, (int)wave_flags_min(p.sflags + 32L * (2 * gi + d) * p.snwg, p.snwg));
       if (m >= need) break;
-      failed = wave_timed_out(p.serr, spins++, t0);
+      failed = wave_timed_out(p.serr, spins++, t0, 3);
       if (failed) break;
       backoff(p.backoff ? need - m : 0);
     }

@@ -48,6 +48,7 @@
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
+#include <map>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -1494,7 +1495,10 @@ __device__ __forceinline__ void wait_flags6(const unsigned *f0, int nwg, unsigne
       if (++spins > kSpinLimit ||
           ((spins & 255) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
         bad = 1;
-        if (threadIdx.x == 0) *bad_lds = 1;
+        if (threadIdx.x == 0) {
+          *bad_lds = 1;
+          if (spins > kSpinLimit) atomicOr(err, 0x10000u);  // this wait ran out of time itself
+        }
         break;
       }
       if (sleep) __builtin_amdgcn_s_sleep(1);
@@ -1661,7 +1665,8 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   if (threadIdx.x == 0) {
     __hip_atomic_fetch_add(p.flags + kResWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (p.reg) {
-      __hip_atomic_fetch_add(p.reg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(p.reg + 4), 1ull, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
       if (p.xpd) __hip_atomic_fetch_or(p.reg + 2, 1u << xcc_id(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // rnn_pinned_xcds
     }
   }
@@ -2918,9 +2923,23 @@ constexpr bool v6_shape_ok() {
   return (NTH == (U == 32 ? 512 : 256) || (U == 16 && (NTH == 512 || NTH == 1024) && H == 512)) && H % (16 * (NTH / 64)) == 0 &&
          (H / U) % (NTH / (4 * U)) == 0;
 }
+// rec6_scratch_bytes: launch6 with this set names the kernel it would launch
+// (its private segment size lands here) instead of launching it
+thread_local size_t *g_rec6_probe = nullptr;
+static size_t kernel_scratch(const void *f) {
+  hipFuncAttributes a{};
+  KCTC_HIP_CHECK(hipFuncGetAttributes(&a, f));
+  return a.localSizeBytes;
+}
 template <int MODE, int U, int H, int NTH, int P>
 static void launch6_shape(bool fwd, const RecParams &p, dim3 grid, size_t lds, hipStream_t s) {
   if constexpr (v6_shape_ok<U, H, NTH>()) {
+    if (g_rec6_probe) {
+      if (fwd) *g_rec6_probe = kernel_scratch(reinterpret_cast<const void *>(rnn_fwd_rec6<MODE, U, H, NTH, P>));
+      else if constexpr ((P & 4) == 0)
+        *g_rec6_probe = kernel_scratch(reinterpret_cast<const void *>(rnn_bwd_rec6<MODE, U, H, NTH, P>));
+      return;
+    }
     if (fwd) {
       set_lds(rnn_fwd_rec6<MODE, U, H, NTH, P>, lds);
       hipLaunchKernelGGL((rnn_fwd_rec6<MODE, U, H, NTH, P>), grid, dim3(NTH), lds, s, p);
@@ -3270,6 +3289,9 @@ void beside_recurrence(hipStream_t side) {
 }
 }  // namespace
 
+thread_local bool g_last_bwd_scratch_free = true;
+bool rnn_last_bwd_scratch_free() { return g_last_bwd_scratch_free; }
+
 bool rnn_side_gated(hipStream_t s) {
   if (!g_rec.res) return true;
   for (int i = 0; i < g_rec.ngated; i++)
@@ -3287,6 +3309,37 @@ namespace {
 // two streams share a hardware queue, the GEMM then merely runs after the
 // recurrence instead of blocking it (its blocks only wait for recurrence flags).
 int g_usable_cus = 0, g_comm_cus = 0;
+
+// Does the v6 recurrence of (d, N) run without scratch (no register
+// spills)?  Nothing runs beside one that does: a workgroup of a kernel that
+// uses scratch was not dispatched onto an XCD where a wave of another
+// queue's kernel was resident -- configs[4]'s bf16 GRU backward (124 B of
+// spills per lane) stayed short of its 32 workgroups on one XCD for 0.4 s
+// behind the one-wave residency wait of its dx stream, measured
+// (tests/test_fullsize_gpu.py cfg4+stream_all) -- and a
+// persistent recurrence needs every workgroup resident.
+bool rec6_scratch_free(const RnnDesc &d, int N, bool fwd) {
+  const V6Cfg c6 = pick6(d, N, fwd);
+  if (!c6) return false;
+  static thread_local std::map<long, bool> memo;
+  const int stk = fwd ? env_int("KCTC_STK_FWD", env_int("KCTC_STK", 1)) : env_int("KCTC_STK", 1);
+  const long key = ((((long)fwd * 4 + d.mode) * 4 + d.prec) * 64 + c6.U) * 2048 * 2048 + (long)c6.nth * 2048 * 2 +
+                   (long)d.H * 2 + (c6.gs <= 8 && stk ? 1 : 0);
+  auto it = memo.find(key);
+  if (it != memo.end()) return it->second;
+  RecParams q{};
+  q.H = d.H; q.U = c6.U; q.gs = c6.gs; q.rg = c6.rg; q.dirs = d.dirs; q.nwg = d.H / c6.U;
+  size_t bytes = 0;
+  g_rec6_probe = &bytes;
+  try {
+    launch6(fwd, d.mode, d.prec, c6.nth, q, dim3(1), 0, nullptr);
+  } catch (...) {
+    g_rec6_probe = nullptr;
+    throw;
+  }
+  g_rec6_probe = nullptr;
+  return memo[key] = bytes == 0;
+}
 
 // XCDs an XCD-pinned v6 recurrence of (d, N) occupies (bit x: XCD x), 0
 // when it is not pinned: every (row group, direction) runs on one XCD, its
@@ -3330,12 +3383,23 @@ int stream_block_budget(int rec_wgs, bool backward) {
   return left >= 8 ? left : 0;
 }
 
+// XCDs whose every CU an XCD-pinned recurrence holds: a streamed GEMM's
+// blocks landing there leave at once (xcd_word / xcd_count), and the launch
+// has 8 / (8 - pinned) times the blocks so that its budget stays.  0 when the
+// recurrence is not pinned or its slots take half an XCD each (configs[2]:
+// all eight XCDs, 16 of each XCD's CUs left to the stream: there its blocks
+// stay, on the CUs the recurrence leaves).
+int whole_pinned_xcds(const RecParams &p) {
+  const int n = p.xpd && p.nwg == kCusPerXcd ? p.dirs * p.rg : 0;
+  return n < 8 ? n : 0;
+}
+
 // Is the dx of layer l streamed off its v6 backward recurrence
 // (launch_bwd_stream, given a dx buffer and an overlap stream)?  The
 // forward's W^T prepack (RnnPrepack) asks the same question.
 bool bwd_dx_stream_ok(const RnnDesc &d, int l, int T, int N) {
   const V6Cfg c6 = pick6(d, N, false);
-  if (!c6 || d.dirs != 2 || !env_int("KCTC_BWD_STREAM", 1)) return false;
+  if (!c6 || d.dirs != 2 || !env_int("KCTC_BWD_STREAM", 1) || !rec6_scratch_free(d, N, false)) return false;
   // split-fp16 at N <= 16 by default (KCTC_STREAM_ALL: bf16 and N > 16 too)
   if (!((d.prec == kPrecX3 && N <= 16) || env_int("KCTC_STREAM_ALL", 0))) return false;
   const int G4 = d.nw() * d.H;
@@ -3361,6 +3425,7 @@ void join_stream(hipStream_t s, hipStream_t other) {
 // recurrence (v6, bidirectional) as its layer-0 projection input?
 bool chain_ok(const RnnDesc &d, int ver, int T, int N, const RnnFwdChain *c) {
   if (!c || !c->d || !c->side || ver != 6 || d.dirs != 2 || !env_int("KCTC_FWD_STREAM", 1)) return false;
+  if (!rec6_scratch_free(d, N, true)) return false;
   const RnnDesc &n = *c->d;
   // split-fp16 into split-fp16, or bf16 images into a bf16 projection
   if (n.D != d.dirs * d.H || !use_x3(n.D) || N > 64 || d.prec != n.prec) return false;
@@ -3422,7 +3487,7 @@ void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
   // XCD-pinned producer: the sc1 copies of its epochs, no block on its XCDs
   x.stream_flags = p.flags + 1024 + (p.xpd ? 256 * kFlagStride : 0);  // pinned: agg_flag6 lines
   x.stream_nwg = p.xpd ? 1 : p.nwg; x.stream_T = T; x.stream_N = N;
-  const int pinned = p.xpd ? d.dirs * p.rg : 0;
+  const int pinned = whole_pinned_xcds(p);
   if (pinned) { x.stream_xcd_word = p.flags + kXcdWord; x.stream_xcd_count = pinned; }
   x.stream_group_step = 2L * (d.H / 32) * (bf ? 1 : 2) * 16 * 32;  // rnn_fwd_rec6's XG
   x.stream_rg = p.rg; x.stream_gs = p.gs; x.stream_step = x.stream_group_step * p.rg; x.stream_err = err;
@@ -3451,6 +3516,7 @@ void launch_chain_proj(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
 bool chain_rows_ok(const RnnDesc &d, int ver, int T, int N, const RnnFwdChain *c) {
   if (!c || !c->d || !c->side || ver != 6 || d.dirs != 2 || d.prec == kPrecBf16 || !env_int("KCTC_FWD_STREAM", 1))
     return false;
+  if (!rec6_scratch_free(d, N, true)) return false;
   const RnnDesc &n = *c->d;
   const long TN = (long)T * N;
   if (n.D != d.dirs * d.H || n.prec != d.prec || !use_x3(n.D) || d.H % 32 || d.H > 4096 || T < 2) return false;
@@ -3511,7 +3577,7 @@ void launch_chain_rows(const RnnDesc &d, const RecParams &p, hipEvent_t fork, in
   a.cnt = pk<int>(c.workspace, n, T, N, pl.cnt);
   a.flags = p.flags + 1024 + (p.xpd ? 256 * kFlagStride : 0);  // pinned: agg_flag6 lines
   a.nwg = p.xpd ? 1 : p.nwg; a.T = T; a.Nf = N; a.err = err; a.rg = p.rg;
-  const int pinned = p.xpd ? d.dirs * p.rg : 0;
+  const int pinned = whole_pinned_xcds(p);
   if (pinned) { a.xcd_word = p.flags + kXcdWord; a.xcd_count = pinned; }
   // 128: every CU the recurrence leaves (configs[1]: 96 -> 128 blocks 720k -> 751k frames/s)
   const int nb = std::min(128, stream_block_budget(d.dirs * p.nwg * p.rg, false));
@@ -3542,8 +3608,8 @@ int rnn_comm_cus() { return g_comm_cus; }
 // ---- residency gate of the gradient exchange (rnn.h) ----
 namespace {
 struct RegWord {
-  unsigned *word = nullptr;  // [0]: registrations, [1]: gate timeouts
-  unsigned expected = 0;     // host: registrations once every enqueued launch is resident
+  unsigned *word = nullptr;          // [2]: pinned XCDs, [4..5]: registrations (64-bit: never wraps)
+  unsigned long long expected = 0;   // host: registrations once every enqueued launch is resident
 };
 RegWord g_reg[64];
 int g_comm_gated[64] = {0};  // per device: live gated exchanges (at most one, GatedExchange)
@@ -3564,38 +3630,20 @@ RegWord &reg_of_device() {
 }
 }  // namespace
 
-// one wave: wait until *word - target >= 0 (wrap-safe), at most 10 s
-__global__ __launch_bounds__(64) void comm_gate_kernel(const unsigned *word, unsigned target, unsigned *gerr) {
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  bool late = false;
-  while (true) {
-    const unsigned v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    if ((int)(v - target) >= 0) break;
-    late = __builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull;  // 100 MHz clock
-    if (late) break;
-    __builtin_amdgcn_s_sleep(8);
-  }
-  if (late && threadIdx.x == 0) atomicOr(gerr, 1u);
-}
-
-unsigned rnn_bwd_registrations() { return reg_of_device().expected; }
-// the same wait on a launch's own count (a timeout counts as the exchange gate's)
+// The gates are stream memory waits: the command processor of the waiting
+// queue polls the word, no wave is placed anywhere.  (A one-wave gate
+// kernel, dispatched from its queue before the recurrence's workgroups were,
+// kept a pinned XCD from taking any of them: configs[4] with the dx stream
+// timed out that way, tests/test_fullsize_gpu.py cfg4+stream_all.)
+unsigned long long rnn_bwd_registrations() { return reg_of_device().expected; }
 void rnn_resident_gate(hipStream_t s, const unsigned *word, unsigned target) {
-  hipLaunchKernelGGL(comm_gate_kernel, dim3(1), dim3(64), 0, s, word, target, reg_of_device().word + 1);
-  KCTC_HIP_CHECK(hipGetLastError());
+  KCTC_HIP_CHECK(hipStreamWaitValue32(s, const_cast<unsigned *>(word), target, hipStreamWaitValueGte, 0xFFFFFFFFu));
 }
 const unsigned *rnn_pinned_xcds() { return reg_of_device().word + 2; }
 
-void rnn_comm_gate(hipStream_t s, unsigned target) {
+void rnn_comm_gate(hipStream_t s, unsigned long long target) {
   RegWord &r = reg_of_device();
-  hipLaunchKernelGGL(comm_gate_kernel, dim3(1), dim3(64), 0, s, r.word, target, r.word + 1);
-  KCTC_HIP_CHECK(hipGetLastError());
-}
-unsigned rnn_comm_gate_errors() {
-  RegWord &r = reg_of_device();
-  unsigned h = 0;
-  KCTC_HIP_CHECK(hipMemcpy(&h, r.word + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
-  return h;
+  KCTC_HIP_CHECK(hipStreamWaitValue64(s, r.word + 4, target, hipStreamWaitValueGte, ~0ull));
 }
 void rnn_set_comm_gated(bool on) {
   int &c = g_comm_gated[current_device()];
@@ -3758,7 +3806,8 @@ int rnn_forward_training(const RnnDesc &d, hipStream_t s, int T, int N, const fl
     const bool prepack = pre && pre->dx && pre->stream && pre->ev && ver == 6 && d.layers == 1 &&
                          bwd_dx_stream_ok(d, 0, T, N);
     const bool prepack_w = pre && pre->stream && pre->wev && pre->wgrad && pre->in_bound > 0.f && ver == 6 &&
-                           d.layers == 1 && d.prec != kPrecBf16 && T > 1 && bounded_out(d) && use_x3((int)TN);
+                           d.layers == 1 && d.prec != kPrecBf16 && T > 1 && bounded_out(d) && use_x3((int)TN) &&
+                           rec6_scratch_free(d, N, true);
     const hipEvent_t fork = (chained || prepack || prepack_w || rowchain) ? fork_event(s) : nullptr;
     {
       ProfSpan ps(s, "rnn_fwd_rec");
@@ -3882,7 +3931,7 @@ void launch_bwd_stream(const RnnDesc &d, const RecParams &p, int l, const float 
   // visible here), and no block on the recurrence's XCDs
   a.flags = p.flags + 1024 + (p.xpd ? 256 * kFlagStride : 0);  // pinned: agg_flag6 lines
   a.nwg = p.xpd ? 1 : p.nwg; a.T = T; a.Nf = N; a.err = err; a.rg = p.rg;
-  const int pinned = p.xpd ? d.dirs * p.rg : 0;
+  const int pinned = whole_pinned_xcds(p);
   if (pinned) { a.xcd_word = p.flags + kXcdWord; a.xcd_count = pinned; }
   // 128 measured best at configs[1] since the self-tagged recurrences (96
   // before: 655.7k -> 670.7k frames/s); never more than the CU budget leaves
@@ -4024,7 +4073,8 @@ bool rnn_wgrad_stream_ok(const RnnDesc &d, int T, int N) {
   if (!env_int("KCTC_WGRAD_STREAM", 0) || d.layers != 1 || d.dirs != 2 || d.mode != kLstm ||
       d.prec != kPrecX3 || T < 8 || N > 16)
     return false;
-  if (!pick6(d, N, false) || !use_x3((int)((long)T * N)) || !use_x3(d.nw() * d.H)) return false;
+  if (!pick6(d, N, false) || !use_x3((int)((long)T * N)) || !use_x3(d.nw() * d.H) || !rec6_scratch_free(d, N, false))
+    return false;
   return (long)T * N * d.din(0) * 4 < (1L << 31);
 }
 
@@ -4148,10 +4198,12 @@ int rnn_backward_data(const RnnDesc &d, hipStream_t s, int T, int N, const float
     KCTC_HIP_CHECK(hipGetLastError());
     if (ver == 6) {
       // counted once the launch is enqueued (a failed launch never raises the target)
-      rw.expected += (unsigned)(dirs * p.nwg * p.rg);
+      rw.expected += (unsigned long long)(dirs * p.nwg * p.rg);
       rec_scope.enqueued(p);
+      g_last_bwd_scratch_free = rec6_scratch_free(d, N, false);
     } else {
       rec_scope.none();
+      g_last_bwd_scratch_free = true;
     }
     if (streamed) {
       launch_bwd_stream(d, p, l, w, dxl, workspace, T, N, overlap, fork, err, d.layers == 1 ? pre : nullptr);

@@ -52,8 +52,9 @@ int kctc_comm_ctas() {
 
 // Residency-gated exchange: a bucket's reduction is queued on
 // the comm stream only behind the NEXT backward recurrence's launch, after a
-// one-wave gate kernel that waits until every workgroup of that recurrence is
-// resident (rnn_comm_gate), and the launch of the recurrence after that waits
+// stream memory wait until every workgroup of that recurrence is resident
+// (rnn_comm_gate; after its end instead when it uses scratch, rnn.h
+// rnn_last_bwd_scratch_free), and the launch of the recurrence after that waits
 // for it.  So no exchange kernel holds a CU while a recurrence's workgroups
 // are being placed -- the condition under which an XCD-pinned recurrence
 // (which needs all CUs of its XCDs) could wait on an all-reduce that waits on
@@ -76,6 +77,7 @@ class GatedExchange : public kctc::nnet2::GradExchange {
     if (gated_) kctc::rnn_set_comm_gated(true);
     KCTC_HIP_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
     KCTC_HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+    KCTC_HIP_CHECK(hipEventCreateWithFlags(&after_, hipEventDisableTiming));
   }
   ~GatedExchange() override {
     kctc::rnn_set_cu_budget(kctc_usable_cus_override(), 0);
@@ -83,6 +85,7 @@ class GatedExchange : public kctc::nnet2::GradExchange {
     (void)hipStreamSynchronize(comm_stream_);
     (void)hipStreamDestroy(comm_stream_);
     (void)hipEventDestroy(done_);
+    (void)hipEventDestroy(after_);
     for (auto ev : pool_) (void)hipEventDestroy(ev);
   }
   void GradReady(int, float *grad, long n, hipStream_t producer) override {
@@ -104,7 +107,12 @@ class GatedExchange : public kctc::nnet2::GradExchange {
   }
   void AfterRecurrence() override {
     if (!gated_ || pending_.empty()) return;
-    kctc::rnn_comm_gate(comm_stream_, kctc::rnn_bwd_registrations());
+    if (kctc::rnn_last_bwd_scratch_free()) {
+      kctc::rnn_comm_gate(comm_stream_, kctc::rnn_bwd_registrations());
+    } else {  // nothing beside a recurrence that uses scratch: after its end
+      KCTC_HIP_CHECK(hipEventRecord(after_, compute_));
+      KCTC_HIP_CHECK(hipStreamWaitEvent(comm_stream_, after_, 0));
+    }
     Launch();
   }
   void Finish() override {
@@ -144,6 +152,7 @@ class GatedExchange : public kctc::nnet2::GradExchange {
   };
   bool gated_ = true, launched_ = false;
   hipEvent_t done_ = nullptr;
+  hipEvent_t after_ = nullptr;  // the end of a recurrence that uses scratch
   std::vector<hipEvent_t> pool_;
   size_t next_ev_ = 0;
   std::vector<Bucket> pending_;
