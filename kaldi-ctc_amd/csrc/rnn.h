@@ -69,8 +69,9 @@ int rnn_comm_cus();
 // of a v6 backward recurrence adds 1 to a per-device 64-bit registration
 // counter when it starts; rnn_bwd_registrations() is the value it reaches
 // once all backward recurrences enqueued so far on this device are resident.
-// rnn_comm_gate(s, target) makes s wait (a stream memory wait: no kernel,
-// no CU) until the counter has reached `target`.  An exchange
+// rnn_comm_gate(s, target) enqueues on s a one-wave kernel that returns once
+// the counter has reached `target` (after 10 s it gives up and flags a gate
+// timeout in the device word).  An exchange
 // that runs its kernels only behind such a gate -- i.e. only while the
 // backward recurrence launched last is fully resident -- and makes the next
 // recurrence launch wait for them declares rnn_set_comm_gated(true): the
@@ -81,15 +82,15 @@ unsigned long long rnn_bwd_registrations();
 // exchange waits for its end instead of its residency
 bool rnn_last_bwd_scratch_free();
 void rnn_comm_gate(hipStream_t s, unsigned long long target);
-// s waits until *word >= target (a launch's own residency count; a stream
-// memory wait as well)
+// s waits until *word >= target (a launch's own residency count; the same
+// one-wave kernel)
 void rnn_resident_gate(hipStream_t s, const unsigned *word, unsigned target);
 // Launches beside a running recurrence.  Every v6 recurrence counts its
 // resident workgroups in its own flag area (kResWord, zeroed with the flags
 // before the launch).  Each kernel that rnn.hip puts on another stream while
 // that recurrence runs -- the streamed GEMMs, the wgrad chunk gates, the
-// forward-time packs -- is enqueued behind a stream memory wait on that
-// count (rnn.hip beside_recurrence): nothing there can take a CU before every
+// forward-time packs -- is enqueued behind a one-wave wait on that count
+// (rnn.hip beside_recurrence): nothing there can take a CU before every
 // workgroup of the recurrence holds its own, so a consumer spinning on the
 // recurrence's progress cannot keep a producer workgroup out.  The host
 // refuses a streaming launch (gemm_x3p with stream_flags,

@@ -3608,7 +3608,7 @@ int rnn_comm_cus() { return g_comm_cus; }
 // ---- residency gate of the gradient exchange (rnn.h) ----
 namespace {
 struct RegWord {
-  unsigned *word = nullptr;          // [2]: pinned XCDs, [4..5]: registrations (64-bit: never wraps)
+  unsigned *word = nullptr;          // [1]: gate timeouts, [2]: pinned XCDs, [4..5]: registrations (64-bit: never wraps)
   unsigned long long expected = 0;   // host: registrations once every enqueued launch is resident
 };
 RegWord g_reg[64];
@@ -3630,20 +3630,38 @@ RegWord &reg_of_device() {
 }
 }  // namespace
 
-// The gates are stream memory waits: the command processor of the waiting
-// queue polls the word, no wave is placed anywhere.  (A one-wave gate
-// kernel, dispatched from its queue before the recurrence's workgroups were,
-// kept a pinned XCD from taking any of them: configs[4] with the dx stream
-// timed out that way, tests/test_fullsize_gpu.py cfg4+stream_all.)
+// The gates are one-wave kernels that poll the word (10 s at most, then
+// they give up and set bit 0 of the device word's [1]).  hipStreamWaitValue
+// is no alternative: ROCclr runs it as a one-thread kernel too
+// (__amd_rocclr_streamOpsWait), without a timeout -- under rocprofv3's
+// counter collection, which serialises dispatches, a gate dispatched before
+// its recurrence then never returns.
+template <typename W>
+__global__ __launch_bounds__(64) void gate_kernel(const W *word, W target, unsigned *gerr) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  bool late = false;
+  while (true) {
+    const W v = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__builtin_amdgcn_readfirstlane((int)(v >= target))) break;
+    late = __builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull;  // 100 MHz clock
+    if (late) break;
+    __builtin_amdgcn_s_sleep(8);
+  }
+  if (late && threadIdx.x == 0) atomicOr(gerr, 1u);
+}
+
 unsigned long long rnn_bwd_registrations() { return reg_of_device().expected; }
 void rnn_resident_gate(hipStream_t s, const unsigned *word, unsigned target) {
-  KCTC_HIP_CHECK(hipStreamWaitValue32(s, const_cast<unsigned *>(word), target, hipStreamWaitValueGte, 0xFFFFFFFFu));
+  hipLaunchKernelGGL(gate_kernel<unsigned>, dim3(1), dim3(64), 0, s, word, target, reg_of_device().word + 1);
+  KCTC_HIP_CHECK(hipGetLastError());
 }
 const unsigned *rnn_pinned_xcds() { return reg_of_device().word + 2; }
 
 void rnn_comm_gate(hipStream_t s, unsigned long long target) {
   RegWord &r = reg_of_device();
-  KCTC_HIP_CHECK(hipStreamWaitValue64(s, r.word + 4, target, hipStreamWaitValueGte, ~0ull));
+  hipLaunchKernelGGL(gate_kernel<unsigned long long>, dim3(1), dim3(64), 0, s,
+                     reinterpret_cast<const unsigned long long *>(r.word + 4), target, r.word + 1);
+  KCTC_HIP_CHECK(hipGetLastError());
 }
 void rnn_set_comm_gated(bool on) {
   int &c = g_comm_gated[current_device()];

@@ -16,8 +16,11 @@ f=$(find gpurun_out/prof -name "*kernel_trace.csv" | head -1)
 python scripts/timeline.py $f 30 > gpurun_out/keep/timeline.txt 2>&1 || true
 find gpurun_out/prof -name "*kernel_stats*" -exec cp {} gpurun_out/keep/kernel_stats.csv \;
 rm -rf gpurun_out/prof
+echo "stats + timeline done"
 timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- $B --steps 1 --warmup 1 --no-profile > gpurun_out/pmc_fetch.log 2>&1 || { echo PMC_FETCH_FAILED; tail -5 gpurun_out/pmc_fetch.log; exit 1; }
+echo "FETCH_SIZE pass done"
 timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- $B --steps 1 --warmup 1 --no-profile > gpurun_out/pmc_write.log 2>&1 || { echo PMC_WRITE_FAILED; tail -5 gpurun_out/pmc_write.log; exit 1; }
+echo "WRITE_SIZE pass done"
 python - <<'PY'
 import json, subprocess
 out = {}
@@ -36,6 +39,7 @@ rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
 timeout -s KILL 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_mfma -o run --output-format csv -- $B --steps 1 --warmup 1 --no-profile > gpurun_out/pmc_mfma.log 2>&1 || { echo PMC_MFMA_FAILED; tail -5 gpurun_out/pmc_mfma.log; exit 1; }
 python3 scripts/pmc_mfma.py gpurun_out/pmc_mfma gpurun_out/keep/pmc_mfma.json 256 rnn_fwd_rec=rnn_fwd_rec6@128 rnn_bwd_rec=rnn_bwd_rec6@128 gemm_p256=gemm_p256_kernel gemm_p256_pair=gemm_p256_pair_kernel dx_stream=x3p_bwd_stream256_kernel\<8 fwd_row_stream=x3p_bwd_stream256_kernel\<4 > /dev/null
 rm -rf gpurun_out/pmc_mfma
+echo "MFMA pass done"
 TRACES="base:X=0" timeout -k 10 150 bash scripts/gpu_trace_diag.sh > gpurun_out/keep/trace_summary.txt 2>&1 || { echo TRACE_FAILED; tail -5 gpurun_out/keep/trace_summary.txt; exit 1; }
 rm -rf gpurun_out/tr_base
 ls gpurun_out/keep
