@@ -2,6 +2,7 @@
 // nnet2 components (the Component plug-in point, nnet-component.h:157-348)
 // and the nnet-am-average component loops.
 #include "kaldi_nnet2_component.h"
+#include "test_hooks.h"
 
 #include <hip/hip_runtime.h>
 
@@ -31,6 +32,9 @@ using kctc::nnet2::UpdatableComponent;
 struct kctcComponentImpl {
   int device = 0;
   hipStream_t stream = nullptr;
+  // test hook (kctc_test_component_side_streams): the trainer's side and
+  // dx-stream queues, so that the component streams and prepacks as in training
+  hipStream_t side = nullptr, stream2 = nullptr;
   std::unique_ptr<Component> c;
   kctc::GlibcRand rng{0};  // ClipGradient self-repair draws (srand(0))
   explicit kctcComponentImpl(int dev) : device(dev) {
@@ -44,18 +48,31 @@ struct kctcComponentImpl {
       if (d.stream == stream) d.stream = nullptr;
     }
     c.reset();
+    for (hipStream_t s2 : {side, stream2})
+      if (s2) {
+        (void)hipStreamSynchronize(s2);
+        auto &d = CuDevice::Instantiate();
+        if (d.side == s2) d.side = nullptr;
+        if (d.stream2 == s2) d.stream2 = nullptr;
+        (void)hipStreamDestroy(s2);
+      }
     if (stream) (void)hipStreamDestroy(stream);
   }
-  // everything of a standalone component on its one stream (no side streams)
+  // everything of a standalone component on its one stream (no side streams
+  // unless the test hook gave it the trainer's two)
   void activate() {
     KCTC_HIP_CHECK(hipSetDevice(device));
     auto &d = CuDevice::Instantiate();
     d.device = device;
     d.stream = stream;
-    d.side = nullptr;
-    d.stream2 = nullptr;
+    d.side = side;
+    d.stream2 = stream2;
   }
-  void sync() { KCTC_HIP_CHECK(hipStreamSynchronize(stream)); }
+  void sync() {
+    for (hipStream_t s2 : {side, stream2})
+      if (s2) KCTC_HIP_CHECK(hipStreamSynchronize(s2));
+    KCTC_HIP_CHECK(hipStreamSynchronize(stream));
+  }
   UpdatableComponent &u() {
     if (!c->IsUpdatable()) throw std::invalid_argument(c->Type() + " is not an UpdatableComponent");
     return static_cast<UpdatableComponent &>(*c);
@@ -316,6 +333,7 @@ int kctc_component_backprop(kctcComponent_t h, int T, int N, const float *in_val
     Component *tu = to_update ? to_update->c.get() : nullptr;
     if (auto *cg = dynamic_cast<ClipGradientComponent *>(&c)) cg->rng_ = &h->rng;
     c.Backprop(ii, oi, x, y, dy, tu, in_deriv ? &dx : nullptr);
+    CuDevice::Instantiate().Join();  // (the test hook's side stream: the weight GEMMs)
     // the reference updates inside Backprop (CuDNNRecurrentComponent::Update,
     // AffineComponent::UpdateSimple); the mirror defers it to ApplyUpdate
     if (tu && tu->IsUpdatable()) static_cast<UpdatableComponent *>(tu)->ApplyUpdate();
@@ -502,6 +520,23 @@ int kctc_nnet_average_models(kctcNnet_t *nnets, const float *weights, int num, i
     nnet_scale(avg, w[0], skip_last_layer != 0);
     for (int i = 1; i < num; i++) nnet_add(avg, w[i], nnets[i], skip_last_layer != 0);
     KCTC_HIP_CHECK(hipStreamSynchronize(avg->stream));
+  });
+}
+
+// test hook (csrc/test_hooks.h): a CuDNNRecurrentComponent with the trainer's
+// side streams and the forward-time prepacks of W^T (dx) and x^T / y^T (weights)
+int kctc_test_component_side_streams(kctcComponent_t h, int on) {
+  return kctc_guarded([&] {
+    KCTC_REQUIRE(h, "kctc_test_component_side_streams: bad handle");
+    auto *r = dynamic_cast<CuDNNRecurrentComponent *>(h->c.get());
+    KCTC_REQUIRE(r, "kctc_test_component_side_streams: not a CuDNNRecurrentComponent");
+    KCTC_HIP_CHECK(hipSetDevice(h->device));
+    if (on && !h->side) {
+      KCTC_HIP_CHECK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+      KCTC_HIP_CHECK(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
+    }
+    r->SetPrepackDx(on != 0);
+    r->SetPrepackW(on != 0);
   });
 }
 

@@ -23,6 +23,12 @@ float kcm_bench_gemm_packed(struct ihipStream_t *stream, int M, int N, int K, in
  * split-K tail slots per direction (-1: default).  1 on unsupported shapes. */
 int kcm_test_row_stream(struct ihipStream_t *stream, int M, int N, int K, int forward, int tail_rows,
                         const float *E, const float *Wt, const float *bias, float *C);
+/* A CuDNNRecurrentComponent handle (include/kaldi_nnet2_component.h) with
+ * the trainer's side streams and forward-time prepacks on (on = 1): its
+ * Propagate packs W^T and x^T / y^T beside the recurrence, its Backprop
+ * streams dx and runs the weight GEMMs on the side stream, as in training. */
+struct kctcComponentImpl;
+int kctc_test_component_side_streams(struct kctcComponentImpl *h, int on);
 #ifdef __cplusplus
 }
 #endif

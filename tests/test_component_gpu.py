@@ -401,3 +401,58 @@ def test_gradient_outlives_backprop_handle(kctc, gpu):
     assert np.isfinite(ref.DotProduct(grad))
     grad.close()
     ref.close()
+
+
+@pytest.mark.parametrize("case", ["params_written", "other_buffers"])
+def test_forward_prepacks_not_reused_when_stale(kctc, gpu, case):
+    """The forward packs W^T (for the streamed dx) and x^T / y^T (for the
+    weight GEMMs) beside its recurrence; Backprop reuses them only while the
+    parameters are the ones packed (a parameter-version counter) and the
+    in / out buffers are the ones propagated (nnet.cpp wgrad_prepack).
+    params_written: Propagate, then UnVectorize new parameters, then Backprop
+    -- dx and the gradient must be those of the new parameters (a reused W^T
+    would give the old ones'); other_buffers: Backprop given copies of the
+    propagated in / out tensors.  Reference: the same calls on a component
+    without side streams (no prepack, dx after the recurrence)."""
+    import torch
+    T, N, D, H = 48, 16, 1024, 512
+    line = (f"CuDNNRecurrentComponent input-dim={D} output-dim={H} bidirectional=true max-seq-length=200 "
+            "learning-rate=0.0005 rnn-mode=2 num-layers=1 param-stddev=0.02 bias-stddev=0.2")
+    g = torch.Generator().manual_seed(5)
+    x = torch.tanh(torch.randn(T * N, D, generator=g)).to(gpu)
+    dy = (torch.randn(T * N, 2 * H, generator=g) * 1e-2).to(gpu)
+
+    def run(side):
+        c = kctc.Component(line, seed=11)
+        p1 = c.Vectorize()
+        if side:
+            assert kctc.lib().kctc_test_component_side_streams(c.h, 1) == 0
+        y = c.Propagate(T, N, x)
+        if case == "params_written":
+            c.UnVectorize((p1 * 1.5).astype(np.float32))
+            xin, yout = x, y
+        else:
+            xin, yout = x.clone(), y.clone()
+        grad = c.Copy()
+        grad.SetZero(True)
+        dx = torch.empty_like(x)
+        c.Backprop(T, N, xin, yout, dy, to_update=grad, in_deriv=dx)
+        torch.cuda.synchronize()
+        out = (dx.cpu().numpy().astype(np.float64), grad.Vectorize().astype(np.float64))
+        grad.close()
+        c.close()
+        return out
+
+    dx_s, g_s = run(True)
+    dx_r, g_r = run(False)
+    rel = lambda a, b: np.linalg.norm(a - b) / np.linalg.norm(b)
+    assert rel(dx_s, dx_r) < 1e-6, rel(dx_s, dx_r)
+    assert rel(g_s, g_r) < 1e-6, rel(g_s, g_r)
+    if case == "params_written":  # the check can tell: dx at 1.5 x W is far from dx at W
+        c = kctc.Component(line, seed=11)
+        y = c.Propagate(T, N, x)
+        dx0 = torch.empty_like(x)
+        c.Backprop(T, N, x, y, dy, in_deriv=dx0)
+        torch.cuda.synchronize()
+        assert rel(dx0.cpu().numpy().astype(np.float64), dx_r) > 0.1
+        c.close()
