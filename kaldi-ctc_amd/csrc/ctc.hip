@@ -116,13 +116,13 @@ __global__ __launch_bounds__(256) void ctc_logz(const float *__restrict__ acts, 
 // log(e^a + e^b + e^c) as max + log1p(sum of the two smaller terms): the
 // dominant term contributes exactly 1, so log1p keeps full relative precision
 // of the small ones (logf(1 + x) would round x to the ulp of 1).  log1p(x) is
-// evaluated as log(u) * x / (u - 1) with u = fl(1 + x) (the rounding of u
-// cancels to first order), on the hardware v_log_f32 / v_exp_f32.
-// (u in [1, 3]: the raw v_log_f32 / v_rcp_f32 need no range reduction)
+// evaluated as log(u) - ((u - 1) - x) with u = fl(1 + x): (u - 1) - x is
+// u's rounding error, exact in fp32, and log(u) - c differs from log(u - c) by
+// c (u - 1) / u, below 2^-24 of the result (u == 1 gives x exactly).  One
+// hardware v_log_f32 (u in [1, 3]: no range reduction) and no reciprocal.
 __device__ __forceinline__ float fast_log1p(float x) {
   const float u = 1.f + x;
-  const float r = __builtin_amdgcn_logf(u) * 0.693147180559945309f * (x * __builtin_amdgcn_rcpf(u - 1.f));
-  return u == 1.f ? x : r;
+  return __builtin_fmaf(__builtin_amdgcn_logf(u), 0.693147180559945309f, x - (u - 1.f));
 }
 // branch-free: -inf in, -inf out (all three -inf gives m = -inf, and
 // -inf - -inf = NaN is selected away)

@@ -710,7 +710,18 @@ __device__ __forceinline__ void decode_tile(const PParams &p, int id, int total,
   const int q = total >> 3, rr = total & 7, xcd = id & 7, loc = id >> 3;
   const int wl = remap ? (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc : id;
   const int bz = wl / p.tiles, wg = wl - bz * p.tiles;
-  tn = wg % p.gx; tm = wg / p.gx;
+  if (remap) {
+    // groups of 8 tile rows, column by column inside a group: the 32 blocks
+    // an XCD runs at once cover 8 row x 4 column tiles (12 panels of A and B
+    // in its L2) instead of one row of tiles (1 + gx panels); 8192^3 bf16
+    // 0.42 -> 0.45 of peak, the train step's shapes unchanged (±1 %)
+    const int rows = p.tiles / p.gx, per = 8 * p.gx;
+    const int grp = wg / per, first = grp * 8, w = wg - grp * per;
+    const int gsz = min(8, rows - first);
+    tm = first + w % gsz; tn = w / gsz;
+  } else {
+    tn = wg % p.gx; tm = wg / p.gx;
+  }
   b = bz % p.batch; ks = bz / p.batch;
 }
 

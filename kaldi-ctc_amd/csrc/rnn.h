@@ -69,9 +69,13 @@ int rnn_comm_cus();
 // of a v6 backward recurrence adds 1 to a per-device 64-bit registration
 // counter when it starts; rnn_bwd_registrations() is the value it reaches
 // once all backward recurrences enqueued so far on this device are resident.
-// rnn_comm_gate(s, target) enqueues on s a one-wave kernel that returns once
-// the counter has reached `target` (after 10 s it gives up and flags a gate
-// timeout in the device word).  An exchange
+// rnn_comm_gate(s, target) enqueues on s a gate kernel that returns once the
+// counter has reached `target` (after 10 s it gives up and flags a gate
+// timeout in the device word).  A gate is 8 one-wave blocks, one per XCD;
+// a block on an XCD a recurrence is pinned to leaves (unless it is the last
+// one waiting), so that no gate wave holds a CU a workgroup of that
+// recurrence needs -- a workgroup that takes a CU's whole register file
+// cannot be placed beside one (rnn.hip gate_kernel).  An exchange
 // that runs its kernels only behind such a gate -- i.e. only while the
 // backward recurrence launched last is fully resident -- and makes the next
 // recurrence launch wait for them declares rnn_set_comm_gated(true): the
@@ -82,14 +86,15 @@ unsigned long long rnn_bwd_registrations();
 // exchange waits for its end instead of its residency
 bool rnn_last_bwd_scratch_free();
 void rnn_comm_gate(hipStream_t s, unsigned long long target);
-// s waits until *word >= target (a launch's own residency count; the same
-// one-wave kernel)
-void rnn_resident_gate(hipStream_t s, const unsigned *word, unsigned target);
+// s waits until the v6 launch whose flag area is `flags` has `target`
+// workgroups resident (its own residency count; the same gate kernel, its
+// blocks leaving on the XCDs that launch runs on)
+void rnn_resident_gate(hipStream_t s, const unsigned *flags, unsigned target);
 // Launches beside a running recurrence.  Every v6 recurrence counts its
 // resident workgroups in its own flag area (kResWord, zeroed with the flags
 // before the launch).  Each kernel that rnn.hip puts on another stream while
 // that recurrence runs -- the streamed GEMMs, the wgrad chunk gates, the
-// forward-time packs -- is enqueued behind a one-wave wait on that count
+// forward-time packs -- is enqueued behind a gate kernel waiting for that count
 // (rnn.hip beside_recurrence): nothing there can take a CU before every
 // workgroup of the recurrence holds its own, so a consumer spinning on the
 // recurrence's progress cannot keep a producer workgroup out.  The host

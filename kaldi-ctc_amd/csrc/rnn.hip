@@ -1475,6 +1475,7 @@ constexpr int kFlagStride = 32;  // words
 // OR in 1 << XCC_ID (words 1008 / 1009: weight-gradient tile counters)
 constexpr int kXcdWord = 1016;
 constexpr int kResWord = 1017;  // v6 recurrence: workgroups resident so far (beside_recurrence)
+constexpr int kGateWord = 1018;  // blocks of its residency gate that left (rnn_resident_gate)
 __device__ __forceinline__ unsigned *flag6(const RecParams &p, int grp, int d, int g, int nwg) {
   return p.flags + 1024 + (((long)grp * p.dirs + d) * nwg + g) * kFlagStride;
 }
@@ -1628,7 +1629,7 @@ __device__ __forceinline__ void split16(float x, _Float16 &hi, _Float16 &lo) {
 // dGates by a bf16 R slice instead of the split-fp16 pair (one MFMA per
 // block, no scaling; partial dh stay fp32).
 template <int MODE, int U, int H, int NTH, int P>
-__global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
+__global__ __launch_bounds__(NTH, 1) __attribute__((amdgpu_num_vgpr(248))) void rnn_bwd_rec6(RecParams p) {
   REC_TRACE_INIT;
   constexpr int NW = MODE == kLstm ? 4 : 3;
   constexpr int NWV = NTH / 64;
@@ -1663,6 +1664,8 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   // resident: counted for the exchange's residency gate (rnn_comm_gate) and
   // in the launch's own word for the side launches beside it (beside_recurrence)
   if (threadIdx.x == 0) {
+    // the XCD first (a residency gate block there leaves on it: rnn_resident_gate)
+    if (p.xpd) atomicOr(p.flags + kXcdWord, 1u << xcc_id());
     __hip_atomic_fetch_add(p.flags + kResWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (p.reg) {
       __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(p.reg + 4), 1ull, __ATOMIC_RELAXED,
@@ -1723,22 +1726,23 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
     sB = split_exp(m4);
   }
   AV bhi[CTW][KB], blo[BF ? 1 : CTW][BF ? 1 : KB];
+  if constexpr (!BF) {
 #pragma unroll
-  for (int c = 0; c < CTW; c++)
+    for (int c = 0; c < CTW; c++)
 #pragma unroll
-    for (int kb = 0; kb < KB; kb++)
+      for (int kb = 0; kb < KB; kb++)
 #pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const float v = rval(kb * 32 + fq * 8 + j, (w * CTW + c) * 16 + fr);
-        if constexpr (BF) {
-          bhi[c][kb][j] = (__bf16)v;
-        } else {
+        for (int j = 0; j < 8; j++) {
           _Float16 h, l;
-          split16(ldexpf(v, sB), h, l);
+          split16(ldexpf(rval(kb * 32 + fq * 8 + j, (w * CTW + c) * 16 + fr), sB), h, l);
           bhi[c][kb][j] = h;
           blo[c][kb][j] = l;
         }
-      }
+  }
+  // bf16: filled after the start-up wait (probe6) below -- filled here, hipcc
+  // sank the conversions past that wait loop with all 8 x KB x CTW fp32
+  // values live and spilled the 512-thread GRU kernel to scratch (before the
+  // step loop, but a kernel with scratch must run alone: rec6_scratch_free)
   // ---- per-element state: thread tid <-> (row n0 + en, unit u0 + eu) ----
   const bool has_e = tid < 16 * U;
   const int en = tid / U, eu = tid - en * U;
@@ -1914,9 +1918,19 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   // per direction instead of 32 for up to ~100 polling GEMM blocks.
   unsigned *gflag = (p.xpd && p.e_sc1 && g == 0) ? agg_flag6(p, grp, d) : nullptr;
   // and where it runs, for the streamed GEMM's blocks (on_pinned_xcd)
-  if (p.xpd && tid == 0) atomicOr(p.flags + kXcdWord, 1u << xcc_id());
   if (tid == 0) loc_lds = 0;
   const int local = (p.xpd && p.allow_local) ? probe6(p, grp, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
+  if constexpr (BF) {
+    auto fill = [&]() {
+#pragma unroll
+      for (int c = 0; c < CTW; c++)
+#pragma unroll
+        for (int kb = 0; kb < KB; kb++)
+#pragma unroll
+          for (int j = 0; j < 8; j++) bhi[c][kb][j] = (__bf16)rval(kb * 32 + fq * 8 + j, (w * CTW + c) * 16 + fr);
+    };
+    fill();
+  }
   if (trc_ && tid == 0) trc_[9] = (unsigned long long)(local + 1);  // step 0, slot 9
   // Self-tagged hand-off (fp32 partials, XCD-local slot, ring of two step
   // images set to tag 1 before the launch): the producer's partial-dh words
@@ -3261,8 +3275,9 @@ namespace {
 // the v6 recurrence this host thread enqueued last, while the host function
 // that enqueued it runs (RecScope), and the side streams gated on it
 struct RecInFlight {
-  const unsigned *res = nullptr;  // its residency word (p.flags + kResWord)
-  unsigned target = 0;            // its workgroups
+  const unsigned *res = nullptr;    // its residency word (p.flags + kResWord)
+  const unsigned *flags = nullptr;  // its flag area
+  unsigned target = 0;              // its workgroups
   hipStream_t gated[4] = {};
   int ngated = 0;
 };
@@ -3273,6 +3288,7 @@ struct RecScope {
   void enqueued(const RecParams &p) {
     g_rec = RecInFlight{};
     g_rec.res = p.flags + kResWord;
+    g_rec.flags = p.flags;
     g_rec.target = (unsigned)(p.dirs * p.nwg * p.rg);
   }
   void none() { g_rec = RecInFlight{}; }  // (a v3 / v4 recurrence: no side launches)
@@ -3284,7 +3300,7 @@ void beside_recurrence(hipStream_t side) {
   for (int i = 0; i < g_rec.ngated; i++)
     if (g_rec.gated[i] == side) return;  // (already behind this recurrence's gate)
   if (g_rec.ngated == 4) throw std::logic_error("beside_recurrence: too many side streams");
-  rnn_resident_gate(side, g_rec.res, g_rec.target);
+  rnn_resident_gate(side, g_rec.flags, g_rec.target);
   g_rec.gated[g_rec.ngated++] = side;
 }
 }  // namespace
@@ -3311,13 +3327,15 @@ namespace {
 int g_usable_cus = 0, g_comm_cus = 0;
 
 // Does the v6 recurrence of (d, N) run without scratch (no register
-// spills)?  Nothing runs beside one that does: a workgroup of a kernel that
-// uses scratch was not dispatched onto an XCD where a wave of another
-// queue's kernel was resident -- configs[4]'s bf16 GRU backward (124 B of
-// spills per lane) stayed short of its 32 workgroups on one XCD for 0.4 s
-// behind the one-wave residency wait of its dx stream, measured
-// (tests/test_fullsize_gpu.py cfg4+stream_all) -- and a
-// persistent recurrence needs every workgroup resident.
+// spills)?  Nothing runs beside one that does.  Round 6 first blamed scratch
+// for configs[4]'s KCTC_STREAM_ALL hang (the bf16 GRU backward, then 124 B of
+// spills per lane, stayed short of its 32 workgroups on one XCD for 0.4 s
+// behind the one-wave residency wait of its dx stream); with the spills gone
+// it hung the same way: the cause is its 256 VGPRs x 2 waves per SIMD, a
+// whole CU's register file, which no workgroup gets on a CU where a gate wave
+// sits -- gate_kernel's blocks now leave the recurrence's XCDs
+// (tests/test_fullsize_gpu.py cfg4+stream_all).  The scratch
+// condition stays as a precaution (no recipe-shape recurrence uses scratch).
 bool rec6_scratch_free(const RnnDesc &d, int N, bool fwd) {
   const V6Cfg c6 = pick6(d, N, fwd);
   if (!c6) return false;
@@ -3608,7 +3626,8 @@ int rnn_comm_cus() { return g_comm_cus; }
 // ---- residency gate of the gradient exchange (rnn.h) ----
 namespace {
 struct RegWord {
-  unsigned *word = nullptr;          // [1]: gate timeouts, [2]: pinned XCDs, [4..5]: registrations (64-bit: never wraps)
+  unsigned *word = nullptr;          // [1]: gate timeouts, [2]: pinned XCDs, [4..5]: registrations (64-bit: never wraps),
+                                     // [6]: exchange gate blocks gone (rnn_comm_gate)
   unsigned long long expected = 0;   // host: registrations once every enqueued launch is resident
 };
 RegWord g_reg[64];
@@ -3630,19 +3649,38 @@ RegWord &reg_of_device() {
 }
 }  // namespace
 
-// The gates are one-wave kernels that poll the word (10 s at most, then
-// they give up and set bit 0 of the device word's [1]).  hipStreamWaitValue
-// is no alternative: ROCclr runs it as a one-thread kernel too
-// (__amd_rocclr_streamOpsWait), without a timeout -- under rocprofv3's
-// counter collection, which serialises dispatches, a gate dispatched before
-// its recurrence then never returns.
+// The gates poll the word (10 s at most, then they give up and set bit 0 of
+// the device word's [1]).  hipStreamWaitValue is no alternative: ROCclr runs
+// it as a one-thread kernel too (__amd_rocclr_streamOpsWait), without a
+// timeout -- under rocprofv3's counter collection, which serialises
+// dispatches, a gate dispatched before its recurrence then never returns.
+// A gate is kGateBlocks one-wave blocks, one per XCD (round-robin dispatch).
+// A wave of it holds a CU, and a recurrence workgroup that needs a CU's whole
+// register file (configs[4]'s bf16 GRU backward: 256 VGPRs x 2 waves per
+// SIMD) cannot be placed beside it: a gate on one of the 32 CUs of an XCD the
+// recurrence is pinned to kept that XCD's last workgroup out until the gate
+// timed out (error 0x10003 at configs[4] with KCTC_STREAM_ALL=1).  So a block
+// leaves as soon as the recurrence has a workgroup on its own XCD (xw: the
+// XCD bits its workgroups OR in first thing), unless it is the last block
+// still waiting (leave counts the ones gone): the blocks on XCDs the
+// recurrence does not use do the waiting.
+constexpr int kGateBlocks = 8;
 template <typename W>
-__global__ __launch_bounds__(64) void gate_kernel(const W *word, W target, unsigned *gerr) {
+__global__ __launch_bounds__(64) void gate_kernel(const W *word, W target, unsigned *gerr, const unsigned *xw,
+                                                  unsigned *leave) {
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned me = 1u << xcc_id();
   bool late = false;
   while (true) {
     const W v = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (__builtin_amdgcn_readfirstlane((int)(v >= target))) break;
+    if (xw && __builtin_amdgcn_readfirstlane((int)(__hip_atomic_load(xw, __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_AGENT) & me))) {
+      unsigned gone = 0;
+      if (threadIdx.x == 0) gone = atomicAdd(leave, 1u);
+      if (__builtin_amdgcn_readfirstlane((int)gone) < kGateBlocks - 1) return;
+      xw = nullptr;  // the last one: it stays
+    }
     late = __builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull;  // 100 MHz clock
     if (late) break;
     __builtin_amdgcn_s_sleep(8);
@@ -3651,16 +3689,21 @@ __global__ __launch_bounds__(64) void gate_kernel(const W *word, W target, unsig
 }
 
 unsigned long long rnn_bwd_registrations() { return reg_of_device().expected; }
-void rnn_resident_gate(hipStream_t s, const unsigned *word, unsigned target) {
-  hipLaunchKernelGGL(gate_kernel<unsigned>, dim3(1), dim3(64), 0, s, word, target, reg_of_device().word + 1);
+void rnn_resident_gate(hipStream_t s, const unsigned *flags, unsigned target) {
+  hipLaunchKernelGGL(gate_kernel<unsigned>, dim3(kGateBlocks), dim3(64), 0, s, flags + kResWord, target,
+                     reg_of_device().word + 1, flags + kXcdWord, const_cast<unsigned *>(flags) + kGateWord);
   KCTC_HIP_CHECK(hipGetLastError());
 }
 const unsigned *rnn_pinned_xcds() { return reg_of_device().word + 2; }
 
 void rnn_comm_gate(hipStream_t s, unsigned long long target) {
   RegWord &r = reg_of_device();
-  hipLaunchKernelGGL(gate_kernel<unsigned long long>, dim3(1), dim3(64), 0, s,
-                     reinterpret_cast<const unsigned long long *>(r.word + 4), target, r.word + 1);
+  // XCDs of the pinned backward recurrences (word [2], never cleared); the
+  // blocks gone counted in word [6], zeroed per gate on its own stream
+  KCTC_HIP_CHECK(hipMemsetAsync(r.word + 6, 0, sizeof(unsigned), s));
+  hipLaunchKernelGGL(gate_kernel<unsigned long long>, dim3(kGateBlocks), dim3(64), 0, s,
+                     reinterpret_cast<const unsigned long long *>(r.word + 4), target, r.word + 1, r.word + 2,
+                     r.word + 6);
   KCTC_HIP_CHECK(hipGetLastError());
 }
 void rnn_set_comm_gated(bool on) {

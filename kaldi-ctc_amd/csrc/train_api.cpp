@@ -52,9 +52,9 @@ int kctc_comm_ctas() {
 
 // Residency-gated exchange: a bucket's reduction is queued on
 // the comm stream only behind the NEXT backward recurrence's launch, after a
-// one-wave wait until every workgroup of that recurrence is resident
-// (rnn_comm_gate; after its end instead when it uses scratch, rnn.h
-// rnn_last_bwd_scratch_free), and the launch of the recurrence after that waits
+// gate kernel's wait until every workgroup of that recurrence is resident
+// (rnn_comm_gate, its blocks off the recurrence's XCDs; after its end instead
+// when it uses scratch, rnn.h rnn_last_bwd_scratch_free), and the launch of the recurrence after that waits
 // for it.  So no exchange kernel holds a CU while a recurrence's workgroups
 // are being placed -- the condition under which an XCD-pinned recurrence
 // (which needs all CUs of its XCDs) could wait on an all-reduce that waits on

@@ -1,6 +1,7 @@
 """CTC alpha/beta timing probe at the configs[1] shape (T=2000, N=16, A=41,
 L = T/8): compute_ctc_loss with and without gradients (alpha+beta with the
-column spill vs alpha alone), for rocprofv3 --kernel-trace --stats."""
+column spill vs alpha alone), for rocprofv3 --kernel-trace --stats; also
+prints the event-timed mean per call."""
 import os
 import sys
 
@@ -19,7 +20,14 @@ fl = np.concatenate([rng.integers(1, A, size=l) for l in ll]).astype(np.int32)
 acts = torch.randn(T, N, A, device="cuda")
 ws = torch.empty(pkg.ctc_workspace_size(ll, lens, A), dtype=torch.uint8, device="cuda")
 for want in (True, False):
-    for _ in range(10):
+    for _ in range(3):
         pkg.compute_ctc_loss(acts, fl, ll, lens, want_grad=want, workspace=ws)
-torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        pkg.compute_ctc_loss(acts, fl, ll, lens, want_grad=want, workspace=ws)
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"compute_ctc_loss want_grad={want}: {e0.elapsed_time(e1) / 20:.4f} ms per call (host launch gaps included)")
 print("ctc probe done")

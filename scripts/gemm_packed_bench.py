@@ -22,7 +22,10 @@ SHAPES = [  # (name, M, N, K, bf16, split)
     ("sq8192_bf16", 8192, 8192, 8192, 1, 1),
     ("sq8192_x3", 8192, 8192, 8192, 0, 1),
 ]
+pick = sys.argv[1:]  # shape names (default: all)
 for name, M, N, K, bf, sp in SHAPES:
+    if pick and name not in pick:
+        continue
     ms = L.kcm_bench_gemm_packed(None, M, N, K, bf, 10, sp)
     tf = 2.0 * M * N * K / ms / 1e9 if ms > 0 else 0.0
     f16 = tf * (1 if bf else 3)

@@ -259,11 +259,14 @@ def test_gemm_matches_numpy(kctc, gpu, ta, tb, M, N, K):
     assert rel_err(C.cpu().numpy(), ref) < 1e-6
 
 
-@pytest.mark.parametrize("ta,tb,M,N,K", [(0, 0, 77, 41, 40), (0, 1, 300, 130, 257), (1, 0, 64, 96, 1000),
-                                         (1, 1, 33, 17, 9), (0, 1, 1024, 1024, 1024), (1, 0, 512, 256, 4000),
-                                         # 256 x 256 tiles with ragged edges in both dimensions
-                                         (0, 1, 300, 260, 257), (1, 0, 700, 450, 3000)])
-def test_gemm_x3_matches_numpy(kctc, gpu, ta, tb, M, N, K):
+@pytest.mark.parametrize("ta,tb,M,N,K,beta", [(0, 0, 77, 41, 40, 0.0), (0, 1, 300, 130, 257, 0.0),
+                                              (1, 0, 64, 96, 1000, 0.0), (1, 1, 33, 17, 9, 0.0),
+                                              (0, 1, 1024, 1024, 1024, 0.0), (1, 0, 512, 256, 4000, 0.0),
+                                              # 256 x 256 tiles with ragged edges in both dimensions
+                                              # (16-B row pieces where ldc allows, element stores otherwise)
+                                              (0, 1, 300, 260, 257, 0.0), (1, 0, 700, 450, 3000, 0.0),
+                                              (0, 1, 520, 300, 700, -1.5), (0, 0, 700, 451, 300, 0.75)])
+def test_gemm_x3_matches_numpy(kctc, gpu, ta, tb, M, N, K, beta):
     """Split-fp16 GEMM: fp32-class accuracy, also for rows / columns whose
     magnitudes differ by many orders (per-row / per-column power-of-two scaling)."""
     import torch
@@ -278,11 +281,12 @@ def test_gemm_x3_matches_numpy(kctc, gpu, ta, tb, M, N, K):
     C0 = rng.standard_normal((M, N)).astype(np.float32)
     C = torch.from_numpy(C0).to(gpu)
     kctc.add_mat_mat_x3(C, torch.from_numpy(A).to(gpu), torch.from_numpy(B).to(gpu), bool(ta), bool(tb),
-                        alpha=0.5, beta=0.0)
+                        alpha=0.5, beta=beta)
     torch.cuda.synchronize()
-    ref = 0.5 * ((A.T if ta else A).astype(np.float64) @ (B.T if tb else B).astype(np.float64))
+    ref = 0.5 * ((A.T if ta else A).astype(np.float64) @ (B.T if tb else B).astype(np.float64)) + beta * C0
     out = C.cpu().numpy().astype(np.float64)
     # element-wise, relative to the scale of the row of op(A) times the column of op(B)
     scale = np.abs(A.T if ta else A).max(axis=1)[:, None] * np.abs(B.T if tb else B).max(axis=0)[None, :] * K
+    scale = scale + 4 * np.abs(beta * C0)
     assert np.max(np.abs(out - ref) / scale) < 2e-7
     assert rel_err(out, ref) < 1e-6
