@@ -89,6 +89,14 @@ ctcStatus_t mictc_compute_ctc_loss_async(const float *activations, float *gradie
  * results for every m (tests/test_ctc_gpu.py). */
 int mictc_set_frame_group(int m);
 
+/* TEST KNOB, not part of the warp-ctc contract: 1 (default) runs the
+ * alpha/beta recursion on overlapping per-wave state windows (one
+ * log-sum-exp per lane and frame, up to 12 waves), 0 on the 512-thread kernel
+ * with halo log-sum-exps.  Process-global like mictc_set_frame_group; same
+ * results either way (tests/test_ctc_gpu.py).  Returns the previous value;
+ * on < 0 only queries. */
+int mictc_set_win(int on);
+
 #ifdef __cplusplus
 }
 #endif

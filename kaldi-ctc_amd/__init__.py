@@ -78,6 +78,8 @@ def lib():
     L.mictc_compute_ctc_loss_async.restype = ctypes.c_int
     L.mictc_set_frame_group.argtypes = [ctypes.c_int]
     L.mictc_set_frame_group.restype = ctypes.c_int
+    L.mictc_set_win.argtypes = [ctypes.c_int]
+    L.mictc_set_win.restype = ctypes.c_int
     _bind_optional(L)
     _lib = L
     return L
@@ -127,6 +129,12 @@ def ctc_frame_group(m=0):
     """Frames per barrier of the alpha/beta kernel (mictc_set_frame_group):
     sets it when m > 0; returns the previous value."""
     return lib().mictc_set_frame_group(int(m))
+
+
+def ctc_window_kernel(on=-1):
+    """Overlapping-window alpha/beta kernel on (1, default) / off (0)
+    (mictc_set_win); returns the previous value (on < 0: query only)."""
+    return lib().mictc_set_win(int(on))
 
 
 def ctc_workspace_size(label_lengths, input_lengths, alphabet_size):

@@ -6,9 +6,12 @@
 //   K1 ctc_logz        one wave per frame row: logZ[t,n] = logsumexp_a act[t,n,a]
 //                      and lp[t,n,a] = act - logZ (fully parallel, HBM-bound:
 //                      4*A B read + 4*A B written per row).
-//   K2 ctc_alpha_beta  one 256-thread workgroup per (utterance, direction):
-//                      log-space alpha (forward) or beta (backward) recursion,
-//                      serial over T with ONE workgroup barrier per frame.  The
+//   K2 ctc_alpha_beta  one workgroup per (utterance, direction): log-space
+//                      alpha (forward) or beta (backward) recursion, serial
+//                      over T with ONE workgroup barrier per group of 8 frames
+//                      (ctc_alpha_beta_win: overlapping per-wave state windows,
+//                      the default up to 600 extended labels; ab_body: 512
+//                      threads with halo lanes, 1..3 states per thread).  The
 //                      extended (blank-interleaved) label sequence lives in
 //                      registers, the previous frame's column in double-buffered
 //                      LDS, the emission log-probs (normalised by K1) are
@@ -430,6 +433,175 @@ __device__ __forceinline__ void ab_body(
   }
 }
 
+// ---------------------------------------------------------------------------
+// K2, overlapping windows (S <= kWinWaves x own states; the default path).
+// Frames go in groups of m per barrier as in ab_body, but instead of a second
+// log-sum-exp per lane for the halo, each wave's 64 lanes hold a WINDOW of 64
+// consecutive states: `own` = 64 - 2 (m - 1) of them its own, the other
+// 2 (m - 1) the neighbour's edge (alpha: the states below, beta: above).
+// Within a group the previous frame's s - 1 / s - 2 (beta: s + 1 / s + 2) come
+// from the neighbouring lanes by whole-wave DPP shifts; the lanes a shift
+// cannot feed (the window's far edge) go stale by two per frame, which after
+// m - 1 frames reaches exactly the halo, so every own state stays exact and
+// every lane computes ONE log-sum-exp per frame.  The group's first frame
+// reads the whole previous column from LDS (own states written by their
+// waves at the group's end) and carries the renormalisation.  Same spill,
+// offsets and costs as ab_body; more waves (ceil(S / own), up to 12 at m = 8).
+constexpr int kWinWaves = 12;
+template <bool SPILL, bool is_beta>
+__device__ __forceinline__ void win_body(const float *__restrict__ lp, int N, int A, int blank,
+                                         UttDesc *__restrict__ descs, const int *__restrict__ labels,
+                                         float *__restrict__ spill, double *__restrict__ offs,
+                                         double *__restrict__ costs, AbLds lay) {
+  const int n = is_beta ? blockIdx.x - N : blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nwv = blockDim.x >> 6;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int F = lay.F, SP = lay.SP, CP = lay.CP;
+  float *emit = lds;                        // [2][F][SP]
+  float *colb = emit + 2 * (size_t)F * SP;  // [2][CP]
+  float *wmax = colb + 2 * CP;              // [2][kWinWaves]
+  int *sh_feasible = reinterpret_cast<int *>(wmax + 2 * kWinWaves);
+
+  UttDesc d = descs[n];
+  const int T = d.T, L = d.L, S = d.S;
+  const int *lab = labels + d.lab_off;
+  if (tid == 0) {
+    int rep = 0;
+    for (int i = 1; i < L; i++) rep += (lab[i] == lab[i - 1]);
+    *sh_feasible = (T > 0 && L + rep <= T);
+  }
+  __syncthreads();
+  const int feasible = *sh_feasible;
+  if (!is_beta && tid == 0) {
+    descs[n].feasible = feasible;
+    if (!feasible) costs[n] = 0.0;
+  }
+  if (!feasible) return;
+
+  const int gm = max(1, min(lay.pair, 8)), nh = 2 * (gm - 1), own = 64 - nh;
+  const int s = is_beta ? own * wid + lane : own * wid - nh + lane;  // this lane's state
+  const bool mine = is_beta ? lane < own : lane >= nh;
+  const bool live = s >= 0 && s < S;
+  bool skip = false;  // alpha: s - 2 -> s allowed; beta: s + 2 -> s (see ab_body)
+  if (live && (s & 1)) {
+    if (!is_beta) skip = (s >= 2) && (lab[(s - 1) >> 1] != lab[(s - 3) >> 1]);
+    else skip = (s + 2 < S) && (lab[(s + 1) >> 1] != lab[(s - 1) >> 1]);
+  }
+  const int sc = min(max(s, 0), CP - 1);  // clamped LDS index
+  auto at = [&](int x) { return min(max(x, 0), CP - 1); };
+  // emission gather: wave w fills state block w (nwv >= ceil(S / 64) blocks)
+  const int nblk = (S + 63) / 64, gs = wid * 64 + lane;
+  const int gext = gs < S ? ((gs & 1) ? lab[(gs - 1) >> 1] : blank) : blank;
+  const long tstride = (long)N * A;
+  const float *lrow = lp + (long)n * A;
+  float *sp = spill + d.ab_off + (is_beta ? (long long)T * S : 0);
+  double *op = offs + d.off_off + (is_beta ? T : 0);
+  auto tframe = [&](int k) { return is_beta ? T - 1 - k : k; };
+  auto issue = [&](int c, int b) {
+    if (wid >= nblk) return;
+    float *dst = emit + (size_t)b * F * SP + wid * 64;
+    for (int f = 0; f < F; f++) {
+      const int k = c * F + f;
+      if (k >= T) break;
+      __builtin_amdgcn_global_load_lds(lrow + (long)tframe(k) * tstride + gext, dst + (size_t)f * SP, 4, 0, 0);
+    }
+  };
+  const int ems = min(max(s, 0), SP - 1);
+  auto publish = [&](int cur, float q) {  // own states of the column, the wave's max, barrier
+    if (mine && s < CP) colb[cur * CP + s] = q;
+    const float lm = wave_max_l63(mine && live ? q : -INFINITY);
+    if (lane == 63) wmax[cur * kWinWaves + wid] = lm;
+    lds_barrier();
+  };
+
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+  double off = 0.0;
+  int cur = 0;
+  float q = -INFINITY;
+  const int nchunk = (T + F - 1) / F;
+  for (int c = 0; c < nchunk; c++) {
+    if (c + 1 < nchunk) issue(c + 1, (c + 1) & 1);
+    const float *em = emit + (size_t)(c & 1) * F * SP;
+    const int fend = min(F, T - c * F);
+    int f = 0;
+    if (c == 0) {
+      // init: alpha_0(0) = ly(blank), alpha_0(1) = ly(l1); beta_{T-1}(S-1) =
+      // beta(S-2) = 0, kept as q = beta + ly (the next step's input)
+      const int t = tframe(0);
+      const float ly = em[ems];
+      const float v = !live ? -INFINITY : !is_beta ? (s <= 1 ? ly : -INFINITY) : (s >= S - 2 ? 0.f : -INFINITY);
+      q = live ? (is_beta ? v + ly : v) : -INFINITY;
+      if (SPILL && mine && live) sp[(long)t * S + s] = v;
+      if (SPILL && tid == 0) op[t] = off;
+      publish(cur, q);
+      cur ^= 1;
+      f = 1;
+    }
+    while (f < fend) {
+      const int g = min(gm, fend - f), k = c * F + f;
+      const float *pv = colb + (cur ^ 1) * CP;
+      const float *wm = wmax + (cur ^ 1) * kWinWaves;
+      float pa = pv[sc], pb, pc;
+      if (!is_beta) {
+        pb = s >= 1 ? pv[at(s - 1)] : -INFINITY;
+        pc = skip ? pv[at(s - 2)] : -INFINITY;
+      } else {
+        pb = s + 1 < S ? pv[at(s + 1)] : -INFINITY;
+        pc = skip ? pv[at(s + 2)] : -INFINITY;
+      }
+      float mu = wm[0];
+      for (int w = 1; w < nwv; w++) mu = fmaxf(mu, wm[w]);
+      off += (double)mu;
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        if (j >= g) break;
+        const int t = tframe(k + j);
+        const float ly = em[(size_t)(f + j) * SP + ems];
+        if (j > 0) {
+          // whole-wave DPP shifts: alpha wave_shr:1 (lane l <- q[l - 1]),
+          // beta wave_shl:1 (lane l <- q[l + 1]); the edge lane gets -inf
+          constexpr int ctrl = is_beta ? 0x130 : 0x138;
+          const int ninf = __float_as_int(-INFINITY);
+          const float b1 = __int_as_float(__builtin_amdgcn_update_dpp(ninf, __float_as_int(q), ctrl, 0xf, 0xf, false));
+          const float c1 = __int_as_float(__builtin_amdgcn_update_dpp(ninf, __float_as_int(b1), ctrl, 0xf, 0xf, false));
+          pa = q;
+          pb = (is_beta ? s + 1 < S : s >= 1) ? b1 : -INFINITY;
+          pc = skip ? c1 : -INFINITY;
+        }
+        const float v = lse3(pa, pb, pc) - (j == 0 ? mu : 0.f);
+        q = live ? v + ly : -INFINITY;
+        if (SPILL && mine && live) sp[(long)t * S + s] = is_beta ? v : q;
+        if (SPILL && tid == 0) op[t] = off;
+      }
+      publish(cur, q);
+      cur ^= 1;
+      f += g;
+    }
+    // the next chunk's gathers have landed; every wave is done with this chunk's buffer
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+  }
+  if (!is_beta && tid == 0) {
+    // log p = O_{T-1} + lse(alpha~_{T-1}(S-1), alpha~_{T-1}(S-2))
+    const float *pv = colb + (cur ^ 1) * CP;
+    float a = pv[S - 1], b = S > 1 ? pv[S - 2] : -INFINITY;
+    float m = fmaxf(a, b);
+    double lpv = off + (double)m + log((double)expf(a - m) + (double)expf(b - m));
+    costs[n] = -lpv;
+  }
+}
+
+template <bool SPILL>
+__global__ __launch_bounds__(64 * kWinWaves) void ctc_alpha_beta_win(
+    const float *__restrict__ lp, int N, int A, int blank, UttDesc *__restrict__ descs,
+    const int *__restrict__ labels, float *__restrict__ spill, double *__restrict__ offs,
+    double *__restrict__ costs, AbLds lay) {
+  if (blockIdx.x >= (unsigned)N) win_body<SPILL, true>(lp, N, A, blank, descs, labels, spill, offs, costs, lay);
+  else win_body<SPILL, false>(lp, N, A, blank, descs, labels, spill, offs, costs, lay);
+}
+
 template <bool SPILL, int SPT>
 __global__ __launch_bounds__(kABThreads) void ctc_alpha_beta(
     const float *__restrict__ lp, int N, int A, int blank, UttDesc *__restrict__ descs,
@@ -562,6 +734,11 @@ static int frame_group() {
   return m;
 }
 
+// the overlapping-window alpha / beta kernel (default; mictc_set_win(0): the
+// 512-thread ab_body kernel with halo log-sum-exps, as before round 6)
+static std::atomic<int> g_win{1};
+static bool win_enabled() { return g_win.load(std::memory_order_relaxed) != 0; }
+
 static ctcStatus_t launch(const float *acts, float *grads, const int *flat_labels,
                           const int *label_lengths, const int *input_lengths, int A, int N,
                           double *costs_dev, void *workspace, hipStream_t stream, int blank) {
@@ -622,25 +799,41 @@ static ctcStatus_t launch(const float *acts, float *grads, const int *flat_label
     AbLds al;
     al.pair = frame_group();  // measured: 8 < 6 < 4 < 3 < 1 < 2 (ms)
     al.SP = (Smax + 63) / 64 * 64;
-    al.CP = std::max((Smax + 4 + 3) / 4 * 4, (Smax <= kABThreads ? 1 : kSPT) * kABThreads);
-    // chunk depth: as many frames as fit 96 KB of double-buffered emissions (4..32)
-    al.F = (int)std::min<size_t>(32, std::max<size_t>(4, (size_t)96 * 1024 / (2 * sizeof(float) * al.SP)));
-    const size_t shm = sizeof(float) * al.floats();
-    if (shm > 160 * 1024) return CTC_STATUS_INVALID_VALUE;
-    ProfSpan ps(stream, "ctc_alpha_beta");
-    auto go = [&](auto kern, int grid) {
+    // overlapping windows (ctc_alpha_beta_win) up to kWinWaves waves
+    const int own = 64 - 2 * (std::max(1, std::min(al.pair, 8)) - 1);
+    const int nwv = std::max(1, (Smax + own - 1) / own);
+    if (nwv <= kWinWaves && win_enabled()) {
+      al.CP = std::max((Smax + 4 + 3) / 4 * 4, own * nwv);
+      al.F = (int)std::min<size_t>(32, std::max<size_t>(4, (size_t)96 * 1024 / (2 * sizeof(float) * al.SP)));
+      const size_t shm = sizeof(float) * (2 * (size_t)al.F * al.SP + 2 * (size_t)al.CP + 2 * kWinWaves + 4);
+      if (shm > 160 * 1024) return CTC_STATUS_INVALID_VALUE;
+      ProfSpan ps(stream, "ctc_alpha_beta");
+      auto kern = want ? ctc_alpha_beta_win<true> : ctc_alpha_beta_win<false>;
       (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)shm);
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(kABThreads), shm, stream, d_lp, N, A, blank, d_desc, d_lab,
+      hipLaunchKernelGGL(kern, dim3(want ? 2 * N : N), dim3(64 * nwv), shm, stream, d_lp, N, A, blank, d_desc, d_lab,
                          d_spill, d_offs, costs_dev, al);
-    };
-    // one state per thread up to 512 extended labels (L <= 255), else three
-    if (Smax <= kABThreads) {
-      if (want) go(ctc_alpha_beta<true, 1>, 2 * N);
-      else go(ctc_alpha_beta<false, 1>, N);
     } else {
-      if (want) go(ctc_alpha_beta<true, kSPT>, 2 * N);
-      else go(ctc_alpha_beta<false, kSPT>, N);
+      al.CP = std::max((Smax + 4 + 3) / 4 * 4, (Smax <= kABThreads ? 1 : kSPT) * kABThreads);
+      // chunk depth: as many frames as fit 96 KB of double-buffered emissions (4..32)
+      al.F = (int)std::min<size_t>(32, std::max<size_t>(4, (size_t)96 * 1024 / (2 * sizeof(float) * al.SP)));
+      const size_t shm = sizeof(float) * al.floats();
+      if (shm > 160 * 1024) return CTC_STATUS_INVALID_VALUE;
+      ProfSpan ps(stream, "ctc_alpha_beta");
+      auto go = [&](auto kern, int grid) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)shm);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kABThreads), shm, stream, d_lp, N, A, blank, d_desc, d_lab,
+                           d_spill, d_offs, costs_dev, al);
+      };
+      // one state per thread up to 512 extended labels (L <= 255), else three
+      if (Smax <= kABThreads) {
+        if (want) go(ctc_alpha_beta<true, 1>, 2 * N);
+        else go(ctc_alpha_beta<false, 1>, N);
+      } else {
+        if (want) go(ctc_alpha_beta<true, kSPT>, 2 * N);
+        else go(ctc_alpha_beta<false, kSPT>, N);
+      }
     }
   }
   if (want && lay.T_max > 0) {
@@ -672,6 +865,12 @@ int get_warpctc_version(void) { return 2; }
 int mictc_set_frame_group(int m) {
   const int prev = frame_group();
   if (m > 0) g_frame_group.store(std::max(1, std::min(m, 8)));
+  return prev;
+}
+
+int mictc_set_win(int on) {
+  const int prev = g_win.load();
+  if (on >= 0) g_win.store(on ? 1 : 0);
   return prev;
 }
 

@@ -19,7 +19,8 @@ ll = (lens // 8).astype(np.int32)
 fl = np.concatenate([rng.integers(1, A, size=l) for l in ll]).astype(np.int32)
 acts = torch.randn(T, N, A, device="cuda")
 ws = torch.empty(pkg.ctc_workspace_size(ll, lens, A), dtype=torch.uint8, device="cuda")
-for want in (True, False):
+for win, want in ((1, True), (0, True), (1, False), (0, False)):
+    pkg.ctc_window_kernel(win)
     for _ in range(3):
         pkg.compute_ctc_loss(acts, fl, ll, lens, want_grad=want, workspace=ws)
     torch.cuda.synchronize()
@@ -29,5 +30,6 @@ for want in (True, False):
         pkg.compute_ctc_loss(acts, fl, ll, lens, want_grad=want, workspace=ws)
     e1.record()
     torch.cuda.synchronize()
-    print(f"compute_ctc_loss want_grad={want}: {e0.elapsed_time(e1) / 20:.4f} ms per call (host launch gaps included)")
+    print(f"compute_ctc_loss {'window' if win else 'halo'} kernel, want_grad={want}: "
+          f"{e0.elapsed_time(e1) / 20:.4f} ms per call (host launch gaps included)")
 print("ctc probe done")

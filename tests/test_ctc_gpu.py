@@ -49,6 +49,15 @@ def frame_group(kctc, request):
     kctc.ctc_frame_group(prev)
 
 
+@pytest.fixture(params=[1, 0], ids=lambda w: "win" if w else "halo")
+def window(kctc, request):
+    """alpha/beta on overlapping per-wave state windows (default, S <= 600 at
+    8 frames per barrier) or on the 512-thread kernel with halo lanes."""
+    prev = kctc.ctc_window_kernel(request.param)
+    yield request.param
+    kctc.ctc_window_kernel(prev)
+
+
 @pytest.mark.parametrize("seed,T,N,L,A,rep", [
     (1, 2000, 16, 237, 41, False),     # configs[1] shape: T_max=2000, N=16, L=T/8
     (2, 667, 8, 250, 41, False),       # configs[2] (fs=3): L = 3T/8
@@ -56,9 +65,10 @@ def frame_group(kctc, request):
     (4, 1300, 2, 639, 41, False),      # maximum label length (MAX_WARPCTC_LABEL_LENGTH)
     (5, 50, 3, 5, 300, False),         # large alphabet
     (6, 37, 5, 9, 41, True),           # T not a multiple of any group depth, short utterances
+    (7, 900, 3, 290, 41, True),        # 512 < S <= 600: the window kernel's 12 waves (halo: 3 states per thread)
 ])
-def test_ctc_matches_oracle(kctc, gpu, oracle, frame_group, seed, T, N, L, A, rep):
-    assert kctc.ctc_frame_group() == frame_group
+def test_ctc_matches_oracle(kctc, gpu, oracle, window, frame_group, seed, T, N, L, A, rep):
+    assert kctc.ctc_frame_group() == frame_group and kctc.ctc_window_kernel() == window
     rng = np.random.default_rng(seed)
     acts = (rng.standard_normal((T, N, A)) * 3).astype(np.float32)
     lens = [T - int(rng.integers(0, T // 10 + 1)) if n else T for n in range(N)]
