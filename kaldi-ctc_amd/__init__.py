@@ -78,8 +78,9 @@ def lib():
     L.mictc_compute_ctc_loss_async.restype = ctypes.c_int
     L.mictc_set_frame_group.argtypes = [ctypes.c_int]
     L.mictc_set_frame_group.restype = ctypes.c_int
-    L.mictc_set_win.argtypes = [ctypes.c_int]
-    L.mictc_set_win.restype = ctypes.c_int
+    if hasattr(L, "mictc_set_win"):  # (absent from pre-round-6 builds run in A/B comparisons)
+        L.mictc_set_win.argtypes = [ctypes.c_int]
+        L.mictc_set_win.restype = ctypes.c_int
     _bind_optional(L)
     _lib = L
     return L

@@ -1664,8 +1664,6 @@ __global__ __launch_bounds__(NTH, 1) __attribute__((amdgpu_num_vgpr(248))) void 
   // resident: counted for the exchange's residency gate (rnn_comm_gate) and
   // in the launch's own word for the side launches beside it (beside_recurrence)
   if (threadIdx.x == 0) {
-    // the XCD first (a residency gate block there leaves on it: rnn_resident_gate)
-    if (p.xpd) atomicOr(p.flags + kXcdWord, 1u << xcc_id());
     __hip_atomic_fetch_add(p.flags + kResWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (p.reg) {
       __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(p.reg + 4), 1ull, __ATOMIC_RELAXED,
@@ -1918,6 +1916,9 @@ __global__ __launch_bounds__(NTH, 1) __attribute__((amdgpu_num_vgpr(248))) void 
   // per direction instead of 32 for up to ~100 polling GEMM blocks.
   unsigned *gflag = (p.xpd && p.e_sc1 && g == 0) ? agg_flag6(p, grp, d) : nullptr;
   // and where it runs, for the streamed GEMM's blocks (on_pinned_xcd)
+  // (before any wait on another workgroup: a residency gate block on this XCD
+  // leaves on it, rnn_resident_gate)
+  if (p.xpd && tid == 0) atomicOr(p.flags + kXcdWord, 1u << xcc_id());
   if (tid == 0) loc_lds = 0;
   const int local = (p.xpd && p.allow_local) ? probe6(p, grp, d, g, NWG, bad, &bad_lds, &loc_lds) : 0;
   if constexpr (BF) {
