@@ -801,26 +801,35 @@ __device__ __forceinline__ void issue_tile256(const _Float16 *__restrict__ P, in
 }
 
 // one row block (16 rows of the wave's 128) of a k block: 4 (bf16: 2 x 4)
-// or 12 (split-fp16) MFMAs against the wave's B fragments
-template <bool BFM>
+// or 12 (split-fp16) MFMAs against the wave's B fragments.  TR: operands
+// swapped, the accumulators hold C^T (lane (fr, fq): row fr, columns
+// 4 fq .. 4 fq + 3 of the 16 x 16 block -- 16-B row pieces for the epilogue)
+template <bool BFM, bool TR = false>
 __device__ __forceinline__ void p256_row(floatx4 (&acc)[4], halfx8 ah, halfx8 al, const halfx8 (&bh)[4],
                                          const halfx8 (&bl)[4]) {
+  auto mm = [](halfx8 a, halfx8 b, floatx4 c) {
+    if constexpr (BFM) {
+      return TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, b), __builtin_bit_cast(bf16x8, a),
+                                                          c, 0, 0, 0)
+                : __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
+                                                          c, 0, 0, 0);
+    } else {
+      return TR ? __builtin_amdgcn_mfma_f32_16x16x32_f16(b, a, c, 0, 0, 0)
+                : __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+    }
+  };
   if constexpr (BFM) {
 #pragma unroll
-    for (int j = 0; j < 4; j++)
-      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ah), __builtin_bit_cast(bf16x8, bh[j]),
-                                                       acc[j], 0, 0, 0);
+    for (int j = 0; j < 4; j++) acc[j] = mm(ah, bh[j], acc[j]);
 #pragma unroll
-    for (int j = 0; j < 4; j++)
-      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al), __builtin_bit_cast(bf16x8, bl[j]),
-                                                       acc[j], 0, 0, 0);
+    for (int j = 0; j < 4; j++) acc[j] = mm(al, bl[j], acc[j]);
   } else {
 #pragma unroll
-    for (int j = 0; j < 4; j++) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[j], acc[j], 0, 0, 0);
+    for (int j = 0; j < 4; j++) acc[j] = mm(ah, bh[j], acc[j]);
 #pragma unroll
-    for (int j = 0; j < 4; j++) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[j], acc[j], 0, 0, 0);
+    for (int j = 0; j < 4; j++) acc[j] = mm(ah, bl[j], acc[j]);
 #pragma unroll
-    for (int j = 0; j < 4; j++) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acc[j], 0, 0, 0);
+    for (int j = 0; j < 4; j++) acc[j] = mm(al, bh[j], acc[j]);
   }
 }
 
@@ -834,7 +843,7 @@ __device__ __forceinline__ void p256_row(floatx4 (&acc)[4], halfx8 ah, halfx8 al
 // (clamped) so the body is straight-line.
 // AUXA: cache policy of the A pieces (16: sc1, rows packed by other CUs
 // while this kernel runs)
-template <bool BFM, int AUXA = 0>
+template <bool BFM, int AUXA = 0, bool TR = false>
 __device__ __forceinline__ void p256_kloop_spread(const _Float16 *A, const _Float16 *B, int M, int N, int KB, int m0,
                                                   int n0, int kb0, int nk, unsigned char *lds, int wm, int wn, int fr,
                                                   int fq, floatx4 (&acc)[8][4]) {
@@ -876,7 +885,7 @@ __device__ __forceinline__ void p256_kloop_spread(const _Float16 *A, const _Floa
       }
       const halfx8 ah = frag(cur, wm + i * 16 + fr, fq);
       const halfx8 al = frag(cur, wm + i * 16 + fr, 4 + fq);
-      p256_row<BFM>(acc[i], ah, al, bh, bl);
+      p256_row<BFM, TR>(acc[i], ah, al, bh, bl);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -903,7 +912,7 @@ __device__ __forceinline__ void p256_tile(const PParams &p, unsigned char *lds, 
   // for bf16 (equal or 1-3 % faster there: fewer MFMAs per stage to hide the
   // DMA issue behind)
   if (p.p256v == 2 || (p.p256v == 0 && !BFM)) {
-    if (nk > 0) p256_kloop_spread<BFM>(A, B, p.M, p.N, p.KB, m0, n0, kb0, nk, lds, wm, wn, fr, fq, acc);
+    if (nk > 0) p256_kloop_spread<BFM, 0, true>(A, B, p.M, p.N, p.KB, m0, n0, kb0, nk, lds, wm, wn, fr, fq, acc);
   } else {
   if (nk > 0) {
     issue_tile256(A, p.M, m0, p.KB, kb0, lds);
@@ -928,73 +937,69 @@ __device__ __forceinline__ void p256_tile(const PParams &p, unsigned char *lds, 
     for (int i = 0; i < 8; i++) {
       const halfx8 ah = frag(cur, wm + i * 16 + fr, fq);
       const halfx8 al = frag(cur, wm + i * 16 + fr, 4 + fq);
-      if constexpr (BFM) {
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ah),
-                                                              __builtin_bit_cast(bf16x8, bh[j]), acc[i][j], 0, 0, 0);
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al),
-                                                              __builtin_bit_cast(bf16x8, bl[j]), acc[i][j], 0, 0, 0);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[j], acc[i][j], 0, 0, 0);
-#pragma unroll
-        for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[j], acc[i][j], 0, 0, 0);
-#pragma unroll
-        for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acc[i][j], 0, 0, 0);
-      }
+      p256_row<BFM, true>(acc[i], ah, al, bh, bl);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
   }
-  // epilogue: acc[i][j][r] -> C[m0+wm+16i+4fq+r][n0+wn+16j+fr], times 2^-(eA + eB)
+  // epilogue, transposed accumulators: acc[i][j][c] -> C[m0+wm+16i+fr][n0+wn+16j+4fq+c],
+  // times 2^-(eA + eB); one 16-B store per (i, j) where the row piece is aligned
   const int *eA = p.eA ? p.eA + (long)b * p.seA : nullptr;
   const int *eB = p.eB ? p.eB + (long)b * p.seB : nullptr;
-  int eb[4];
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const int col = n0 + wn + j * 16 + fr;
-    eb[j] = col < p.N ? (eB ? eB[col] : p.eB0) : 0;
-  }
   float *W = p.split > 1 ? p.ws + ((long)ks * p.batch + b) * (long)p.M * p.N : nullptr;
   float *C = p.C + (long)b * p.sC;
   const float *bias = p.bias ? p.bias + (long)b * p.sBias : nullptr;
   const float *bias2 = p.bias2 ? p.bias2 + (long)b * p.sBias : nullptr;
-  float badd[4];
+  float *const O = W ? W : C;
+  const long ldo = W ? p.N : p.ldc;
+  const bool vec = ((reinterpret_cast<unsigned long>(O) & 15) == 0) && (ldo & 3) == 0;
 #pragma unroll
   for (int j = 0; j < 4; j++) {
-    const int col = n0 + wn + j * 16 + fr;
-    badd[j] = 0.f;
-    if (!W && col < p.N) {
-      if (bias) badd[j] += bias[col];
-      if (bias2) badd[j] += bias2[col];
+    const int col0 = n0 + wn + j * 16 + fq * 4;
+    int eb[4];
+    float badd[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int col = col0 + c;
+      eb[c] = col < p.N ? (eB ? eB[col] : p.eB0) : 0;
+      badd[c] = 0.f;
+      if (!W && col < p.N) {
+        if (bias) badd[c] += bias[col];
+        if (bias2) badd[c] += bias2[col];
+      }
     }
-  }
 #pragma unroll
-  for (int i = 0; i < 8; i++)
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int row = m0 + wm + i * 16 + fq * 4 + r;
-      if (row >= p.M) continue;
+    for (int i = 0; i < 8; i++) {
+      const int row = m0 + wm + i * 16 + fr;
+      if (row >= p.M || col0 >= p.N) continue;
       const int ea = eA ? eA[row] : p.eA0;
+      float *o = O + (long)row * ldo + col0;
+      floatx4 v;
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const int col = n0 + wn + j * 16 + fr;
-        if (col >= p.N) continue;
-        const float v = ldexpf(acc[i][j][r], -(ea + eb[j]));
-        if (W) {
-          W[(long)row * p.N + col] = v;
-        } else {
-          float *c = C + (long)row * p.ldc + col;
-          float o = p.alpha * v + badd[j];
-          if (p.beta != 0.f) o += p.beta * *c;
-          *c = o;
+      for (int c = 0; c < 4; c++) {
+        v[c] = ldexpf(acc[i][j][c], -(ea + eb[c]));
+        if (!W) v[c] = p.alpha * v[c] + badd[c];
+      }
+      if (vec && col0 + 3 < p.N) {
+        if (!W && p.beta != 0.f) {
+          const floatx4 old = *reinterpret_cast<const floatx4 *>(o);
+#pragma unroll
+          for (int c = 0; c < 4; c++) v[c] += p.beta * old[c];
+        }
+        *reinterpret_cast<floatx4 *>(o) = v;
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          if (col0 + c < p.N) {
+            float x = v[c];
+            if (!W && p.beta != 0.f) x += p.beta * o[c];
+            o[c] = x;
+          }
         }
       }
     }
+  }
 }
 
 // beside a pinned recurrence (X3PArgs::avoid_word): true on one of its XCDs

@@ -11,10 +11,12 @@ k = ge.load_package()
 L = k.lib()
 torch.zeros(1, device="cuda:0")
 SHAPES = [  # (name, M, N, K, bf16, split)
+    ("c1_proj0", 32000, 4096, 40, 0, 1),     # layer 0 (D = 40): output-bound
     ("c1_fwd_proj", 32000, 2048, 1024, 0, 1),
     ("c1_bwd_data", 32000, 1024, 2048, 0, 1),
     ("c1_bwd_w", 2048, 1024, 32000, 0, 8),
     ("c1_bwd_r", 2048, 512, 32000, 0, 16),
+    ("c4_proj0", 64000, 6144, 40, 1, 1),
     ("c4_fwd_proj", 64000, 3072, 2048, 1, 1),
     ("c4_bwd_data", 64000, 2048, 3072, 1, 1),
     ("c4_bwd_w", 3072, 2048, 64000, 1, 4),
