@@ -1447,14 +1447,35 @@ __device__ __forceinline__ void pack_cols_item(const float *__restrict__ X, long
   const int c0 = bx * 64, kb0 = kq * KPI;
   const float *x = X + (long)b * sX;
   const int t = threadIdx.x;
-  // load KPI * 32 rows x 64 columns (each row: 64 consecutive floats)
+  // load KPI * 32 rows x 64 columns (each row: 64 consecutive floats), 16 B
+  // per lane where the rows are 16-B aligned (4 rows per wave instruction)
+  if (((reinterpret_cast<unsigned long>(x) & 15) | (ldx & 3)) == 0) {
 #pragma unroll
-  for (int i = 0; i < 8 * KPI; i++) {
-    const int kr = (t >> 6) + 4 * i, cc = t & 63;
-    const int k = kb0 * 32 + kr, src = k - shift;
-    float v = 0.f;
-    if (k < R && src >= 0 && src < R && c0 + cc < Cn) v = x[(long)src * ldx + c0 + cc];
-    tile[kr][cc] = v;
+    for (int i = 0; i < 2 * KPI; i++) {
+      const int kr = (t >> 4) + 16 * i, cc = (t & 15) * 4;
+      const int k = kb0 * 32 + kr, src = k - shift;
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if (k < R && src >= 0 && src < R) {
+        const float *xr = x + (long)src * ldx + c0 + cc;
+        if (c0 + cc + 3 < Cn) {
+          v = *reinterpret_cast<const floatx4 *>(xr);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; e++) v[e] = c0 + cc + e < Cn ? xr[e] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; e++) tile[kr][cc + e] = v[e];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8 * KPI; i++) {
+      const int kr = (t >> 6) + 4 * i, cc = t & 63;
+      const int k = kb0 * 32 + kr, src = k - shift;
+      float v = 0.f;
+      if (k < R && src >= 0 && src < R && c0 + cc < Cn) v = x[(long)src * ldx + c0 + cc];
+      tile[kr][cc] = v;
+    }
   }
   __syncthreads();
   const int c = t >> 2, part = t & 3;
