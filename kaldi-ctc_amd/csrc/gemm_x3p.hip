@@ -1274,25 +1274,62 @@ __device__ __forceinline__ void p256_bwd_tile(const PParams &p, unsigned char *l
 #pragma unroll
     for (int j = 0; j < 4; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   const int kbs = (p.KB + S - 1) / S, kb0 = ks * kbs, nk = max(0, min(p.KB, kb0 + kbs) - kb0);
-  if (nk > 0) p256_kloop_spread<BFM, 16>(A, B, p.M, p.N, p.KB, m0, n0, kb0, nk, lds, wm, wn, fr, fq, acc);
+  // transposed accumulators (p256_row TR): lane (fr, fq) holds row
+  // m0 + wm + 16 i + fr, columns n0 + wn + 16 j + 4 fq .. + 3 of C
+  if (nk > 0) p256_kloop_spread<BFM, 16, true>(A, B, p.M, p.N, p.KB, m0, n0, kb0, nk, lds, wm, wn, fr, fq, acc);
   if constexpr (!BFM) {  // to values: 2^-(eA[row] + eB[col]) (eA written by other CUs: sc1 loads)
     const int *eA = p.eA + (long)d * p.seA, *eB = p.eB + (long)d * p.seB;
-    int eb[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const int col = n0 + wn + j * 16 + fr;
-      eb[j] = col < p.N ? eB[col] : 0;
-    }
+      int eb[4];
 #pragma unroll
-    for (int i = 0; i < 8; i++)
+      for (int c = 0; c < 4; c++) {
+        const int col = n0 + wn + j * 16 + fq * 4 + c;
+        eb[c] = col < p.N ? eB[col] : 0;
+      }
 #pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int row = m0 + wm + i * 16 + fq * 4 + r;
+      for (int i = 0; i < 8; i++) {
+        const int row = m0 + wm + i * 16 + fr;
         const int ea = row < p.M ? __hip_atomic_load(eA + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
 #pragma unroll
-        for (int j = 0; j < 4; j++) acc[i][j][r] = ldexpf(acc[i][j][r], -(ea + eb[j]));
+        for (int c = 0; c < 4; c++) acc[i][j][c] = ldexpf(acc[i][j][c], -(ea + eb[c]));
+      }
+    }
+  }
+  // C row piece (i, j) of this lane: + bias + bias2 of each column (gemm_x3p's
+  // order), one 16-B store where the piece is whole and aligned
+  const bool vec = ((reinterpret_cast<unsigned long>(p.C) & 15) | (p.ldc & 3)) == 0;
+  // the biases of this lane's 16 columns (a column's only: computed once)
+  float bsum[4][4];
+  if (p.bias) {
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const int col = min(n0 + wn + j * 16 + fq * 4 + c, p.N - 1);
+        const long bo = (long)(col / p.bcols) * p.sBias + col % p.bcols;
+        float badd = 0.f;
+        badd += p.bias[bo];
+        if (p.bias2) badd += p.bias2[bo];
+        bsum[j][c] = badd;
       }
   }
+  auto put = [&](int i, int j, floatx4 v) {
+    const int row = m0 + wm + i * 16 + fr, col0 = n0 + wn + j * 16 + fq * 4;
+    if (row >= p.M || col0 >= p.N) return;
+    if (p.bias) {
+#pragma unroll
+      for (int c = 0; c < 4; c++) v[c] = v[c] + bsum[j][c];
+    }
+    float *o = p.C + (long)row * p.ldc + col0;
+    if (vec && col0 + 3 < p.N) {
+      *reinterpret_cast<floatx4 *>(o) = v;
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; c++)
+        if (col0 + c < p.N) o[c] = v[c];
+    }
+  };
   const long tile = (long)tm * p.gx + tn;
   int *arr = p.arrive + tile;
   // a tail tile (one of its directions split p.tails ways): every partial
@@ -1325,18 +1362,7 @@ __device__ __forceinline__ void p256_bwd_tile(const PParams &p, unsigned char *l
           floatx4 v = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, 16));
           for (int qq = 1; qq < n; qq++)
             v += __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rb, off + qq * TB2 * TB2 * 4, 0, 16));
-          const int col = n0 + wn + j * 16 + fr;
-          if (col >= p.N) continue;
-          float badd = 0.f;
-          if (p.bias) {
-            const long bo = (long)(col / p.bcols) * p.sBias + col % p.bcols;
-            badd += p.bias[bo];
-            if (p.bias2) badd += p.bias2[bo];
-          }
-          for (int r = 0; r < 4; r++) {
-            const int row = m0 + wm + i * 16 + fq * 4 + r;
-            if (row < p.M) p.C[(long)row * p.ldc + col] = p.bias ? v[r] + badd : v[r];
-          }
+          put(i, j, v);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1362,19 +1388,7 @@ __device__ __forceinline__ void p256_bwd_tile(const PParams &p, unsigned char *l
       for (int j = 0; j < 4; j++) {
         const floatx4 o = __builtin_bit_cast(
             floatx4, __builtin_amdgcn_raw_buffer_load_b128(rp, ((i * 4 + j) * NTH2 + (int)threadIdx.x) * 16, 0, 16));
-        const int col = n0 + wn + j * 16 + fr;
-        if (col >= p.N) continue;
-        float badd = 0.f;  // (as gemm_x3p's epilogue: bias, then bias2)
-        if (p.bias) {
-          const long bo = (long)(col / p.bcols) * p.sBias + col % p.bcols;
-          badd += p.bias[bo];
-          if (p.bias2) badd += p.bias2[bo];
-        }
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int row = m0 + wm + i * 16 + fq * 4 + r;
-          if (row < p.M) p.C[(long)row * p.ldc + col] = p.bias ? (acc[i][j][r] + o[r]) + badd : acc[i][j][r] + o[r];
-        }
+        put(i, j, acc[i][j] + o);
       }
   }
   // unconditional barrier (see fwd_combine)
@@ -1578,13 +1592,33 @@ __global__ __launch_bounds__(256) void bf16_pack_cols_kernel(const float *__rest
   const int b = blockIdx.z, c0 = blockIdx.x * 64, kb = blockIdx.y;
   const float *x = X + (long)b * sX;
   const int t = threadIdx.x;
+  if (((reinterpret_cast<unsigned long>(x) & 15) | (ldx & 3)) == 0) {  // 16 B per lane (as pack_cols_item)
 #pragma unroll
-  for (int i = 0; i < 16; i++) {
-    const int kr = (t >> 6) + 4 * i, cc = t & 63;
-    const int src = kb * 64 + kr - shift;
-    float v = 0.f;
-    if (kb * 64 + kr < R && src >= 0 && src < R && c0 + cc < Cn) v = x[(long)src * ldx + c0 + cc];
-    tile[kr][cc] = v;
+    for (int i = 0; i < 4; i++) {
+      const int kr = (t >> 4) + 16 * i, cc = (t & 15) * 4;
+      const int src = kb * 64 + kr - shift;
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if (kb * 64 + kr < R && src >= 0 && src < R) {
+        const float *xr = x + (long)src * ldx + c0 + cc;
+        if (c0 + cc + 3 < Cn) {
+          v = *reinterpret_cast<const floatx4 *>(xr);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; e++) v[e] = c0 + cc + e < Cn ? xr[e] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; e++) tile[kr][cc + e] = v[e];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int kr = (t >> 6) + 4 * i, cc = t & 63;
+      const int src = kb * 64 + kr - shift;
+      float v = 0.f;
+      if (kb * 64 + kr < R && src >= 0 && src < R && c0 + cc < Cn) v = x[(long)src * ldx + c0 + cc];
+      tile[kr][cc] = v;
+    }
   }
   __syncthreads();
   const int c = t >> 2, part = t & 3;
