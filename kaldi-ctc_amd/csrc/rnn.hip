@@ -1628,8 +1628,13 @@ __device__ __forceinline__ void split16(float x, _Float16 &hi, _Float16 &lo) {
 // H / (16 NTH / 64) output column tiles).  P = kPrecBf16 multiplies bf16
 // dGates by a bf16 R slice instead of the split-fp16 pair (one MFMA per
 // block, no scaling; partial dh stay fp32).
+#ifndef KCTC_PIPE_STK
+#define KCTC_PIPE_STK 1
+#endif
+// stacked backward: partial-dh stores pipelined behind the next tile's MFMAs
+constexpr bool kPipeStk = KCTC_PIPE_STK != 0;
 template <int MODE, int U, int H, int NTH, int P>
-__global__ __launch_bounds__(NTH, 1) __attribute__((amdgpu_num_vgpr(248))) void rnn_bwd_rec6(RecParams p) {
+__global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   REC_TRACE_INIT;
   constexpr int NW = MODE == kLstm ? 4 : 3;
   constexpr int NWV = NTH / 64;
@@ -2152,7 +2157,59 @@ __global__ __launch_bounds__(NTH, 1) __attribute__((amdgpu_num_vgpr(248))) void 
     REC_TRACE(ks, 12);
     __syncthreads();
     REC_TRACE(ks, 3);
-    if (k > 0) {  // partial dh of all units for the next step
+    if (STK && k > 0 && kPipeStk) {
+      // partial dh of all units for the next step, stacked hi / lo: tile c's
+      // four MFMAs, then -- while tile c + 1's run -- its fold, scaling, tag
+      // and 16-B store, as one straight-line block per cache policy (the
+      // store of a dead lane goes past the buffer's end and is dropped)
+      const auto ro = rsrc(p.xch + (long)(p.ring ? ks & 1 : ks) * xstep, (unsigned)(xstep * 4));
+      const long obase = (long)grp * xgrp + (long)(d * NWG + g) * PSTR;
+      const unsigned tg = (unsigned)(ks >> 1) & 1u;
+      const int e1 = -rowexp[fr & 7];
+      AV ah[KB];
+#pragma unroll
+      for (int kb = 0; kb < KB; kb++) ah[kb] = *reinterpret_cast<const AV *>(Ahi + fr * AP + kb * 32 + fq * 8);
+      auto phase = [&](auto aux_c) {
+        constexpr int aux = decltype(aux_c)::value;
+        floatx4 acc[CTW];
+#pragma unroll
+        for (int c = 0; c < CTW; c++) {
+          acc[c] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kb = 0; kb < KB; kb++) {  // the order of the interleaved version: hi, lo per k block
+            acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bhi[c][kb], ah[kb], acc[c], 0, 0, 0);
+            acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(blo[c][kb], ah[kb], acc[c], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < CTW; c++) {
+          floatx4 o;
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            float v = acc[c][i] + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(acc[c][i]), 0x128, 0xF, 0xF, true));
+            v = ldexpf(v, e1);
+            o[i] = __uint_as_float((__float_as_uint(v) & ~1u) | tg);
+          }
+          const int slot = fq * 8 + (fr & 7);
+          const int off = prow_live ? (int)((obase + ((long)(w * CTW + c) * 64 + slot) * LW) * 4) : 0x7ffffff0;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ro, off, 0, aux);
+        }
+        // pipeline: MFMAs of tiles 0 and 1, then per tile c the fold + store
+        // of tile c - 1 ... interleaved with tile c + 1's MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * KB, 0);  // tile 0 (2 KB MFMAs a tile)
+#pragma unroll
+        for (int c = 1; c < CTW; c++) {
+          __builtin_amdgcn_sched_group_barrier(0x008, KB, 0);  // tile c (first half)
+          __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);  // tile c - 1: fold, scale, tag
+          __builtin_amdgcn_sched_group_barrier(0x008, KB, 0);  // tile c (second half)
+          __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);   // tile c - 1: store
+        }
+        __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);  // last tile
+        __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);
+      };
+      if (local) phase(std::integral_constant<int, 0>{});
+      else phase(std::integral_constant<int, 16>{});
+    } else if (k > 0) {  // partial dh of all units for the next step
       floatx4 acc[CTW];
 #pragma unroll
       for (int c = 0; c < CTW; c++) acc[c] = floatx4{0.f, 0.f, 0.f, 0.f};
