@@ -2209,6 +2209,44 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
       };
       if (local) phase(std::integral_constant<int, 0>{});
       else phase(std::integral_constant<int, 16>{});
+    } else if (BF && k > 0 && kPipeStk && bfp) {
+      // bf16 with bf16 partials (configs[4]): the same pipeline -- tile c's KB
+      // MFMAs, then its bf16 pack and 8-B store behind tile c + 1's
+      const auto ro = rsrc(p.xch + (long)(p.ring ? ks & 1 : ks) * xstep, (unsigned)(xstep * 4));
+      const long obase = (long)grp * xgrp + (long)(d * NWG + g) * PSTR;
+      AV ah[KB];
+#pragma unroll
+      for (int kb = 0; kb < KB; kb++) ah[kb] = *reinterpret_cast<const AV *>(Ahi + fr * AP + kb * 32 + fq * 8);
+      auto phase = [&](auto aux_c) {
+        constexpr int aux = decltype(aux_c)::value;
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        floatx4 acc[CTW];
+#pragma unroll
+        for (int c = 0; c < CTW; c++) {
+          acc[c] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kb = 0; kb < KB; kb++) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[kb], bhi[c][kb], acc[c], 0, 0, 0);
+        }
+#pragma unroll
+        for (int c = 0; c < CTW; c++) {
+          bf16x4 b;
+#pragma unroll
+          for (int i = 0; i < 4; i++) b[i] = (__bf16)acc[c][i];
+          const int off = prow_live ? (int)((obase + ((long)(w * CTW + c) * 64 + lane) * LW) * 4) : 0x7ffffff0;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, b), ro, off, 0, aux);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, KB, 0);  // tile 0
+#pragma unroll
+        for (int c = 1; c < CTW; c++) {
+          __builtin_amdgcn_sched_group_barrier(0x008, KB, 0);  // tile c
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // tile c - 1: bf16 pack
+          __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);   // tile c - 1: store
+        }
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // last tile
+        __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);
+      };
+      if (local) phase(std::integral_constant<int, 0>{});
+      else phase(std::integral_constant<int, 16>{});
     } else if (k > 0) {  // partial dh of all units for the next step
       floatx4 acc[CTW];
 #pragma unroll
