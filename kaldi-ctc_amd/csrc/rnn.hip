@@ -1633,6 +1633,11 @@ __device__ __forceinline__ void split16(float x, _Float16 &hi, _Float16 &lo) {
 #endif
 // stacked backward: partial-dh stores pipelined behind the next tile's MFMAs
 constexpr bool kPipeStk = KCTC_PIPE_STK != 0;
+#ifndef KCTC_EARLY_E
+#define KCTC_EARLY_E 1
+#endif
+// bf16 backward: the previous step's dGates stores under the hand-off loads
+constexpr bool kEarlyE = KCTC_EARLY_E != 0;
 template <int MODE, int U, int H, int NTH, int P>
 __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
   REC_TRACE_INIT;
@@ -1983,14 +1988,22 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
       if (bfp) {
         typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
         u32x2 v[PER];
+        // unconditional (a dead row quad past the buffer: zeros), so that the
+        // work below overlaps them
 #pragma unroll
         for (int i = 0; i < PER; i++)
-          v[i] = crow_live ? __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
-                                 rs, (int)((coff + (long)i * NGRP * PSTR) * 4), 0, 16 /* sc1 */))
-                           : u32x2{0u, 0u};
+          v[i] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                     rs, crow_live ? (int)((coff + (long)i * NGRP * PSTR) * 4) : 0x7fff0000, 0, 16 /* sc1 */));
         if constexpr (PRE) {
           __builtin_amdgcn_sched_barrier(0);
           coef();  // while the hand-off loads are in flight
+          __builtin_amdgcn_sched_barrier(0);
+        } else if (kEarlyE) {
+          // bf16: the previous step's dGates rows / packed operands (its
+          // cell's estg stage, complete since the MFMA phase's barrier) while
+          // the hand-off loads are in flight, instead of after them
+          __builtin_amdgcn_sched_barrier(0);
+          e_store(t_prev);
           __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
@@ -2060,7 +2073,7 @@ __global__ __launch_bounds__(NTH, 1) void rnn_bwd_rec6(RecParams p) {
     }
     asm volatile("" ::: "memory");
     // behind the hand-off loads: next step's operands, last step's row-major dGates
-    if (t_prev >= 0) e_store(t_prev);
+    if (t_prev >= 0 && !(kEarlyE && !PRE && bfp && ks > 0)) e_store(t_prev);
     if (k > 0) prefetch(k - 1);
     __syncthreads();
     REC_TRACE(ks, 8);
