@@ -3772,7 +3772,10 @@ RegWord &reg_of_device() {
 // leaves as soon as the recurrence has a workgroup on its own XCD (xw: the
 // XCD bits its workgroups OR in first thing), unless it is the last block
 // still waiting (leave counts the ones gone): the blocks on XCDs the
-// recurrence does not use do the waiting.
+// recurrence does not use do the waiting.  (A full-register recurrence on all
+// eight XCDs would keep the last block's CU; no recipe shape is one -- with
+// every CU taken nothing streams beside it either -- and the gate's timeout
+// would flag it.)
 constexpr int kGateBlocks = 8;
 template <typename W>
 __global__ __launch_bounds__(64) void gate_kernel(const W *word, W target, unsigned *gerr, const unsigned *xw,
